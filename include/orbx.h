@@ -1,0 +1,131 @@
+/* orbx.h — C ABI of the MI355X-native ORB front-end (liborbx.so).
+ *
+ * Drop-in boundary for the hot path of the reference (zackLiuzz/MY_ORB_SLAM2).  Each entry
+ * point names the reference interface it replaces (file:line relative to the reference
+ * root).  Plain pointers and sizes only; no OpenCV, no torch types.  All functions return
+ * an orbx_status (0 = ok, < 0 = error) and are safe to call from several host threads as
+ * long as each thread uses its own extractor handle (an ORBextractor is not re-entrant in
+ * the reference either: its pyramid is mutable state, include/ORBextractor.h:85).
+ *
+ * Numerics: bit-exact with the CPU restatement in oracle/ (same keypoints, angles,
+ * descriptors, pyramid bytes, stereo outputs); see DESIGN.md for the OpenCV 3.2 conventions.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    ORBX_OK = 0,
+    ORBX_ERR_INVALID = -1,      /* bad argument (null pointer, size, level ...) */
+    ORBX_ERR_DEVICE = -2,       /* HIP runtime error / no GPU */
+    ORBX_ERR_CAPACITY = -3,     /* output buffer too small (n_out holds the needed size) */
+    ORBX_ERR_UNSUPPORTED = -4,  /* configuration outside the kernels' design limits */
+    ORBX_ERR_STATE = -5         /* call order (e.g. stereo before extraction) */
+} orbx_status;
+
+/* cv::KeyPoint field order and size (28 bytes), so a std::vector<cv::KeyPoint> buffer can
+ * be filled directly. */
+typedef struct {
+    float x, y;       /* pt (level-0 pixel coordinates)          */
+    float size;       /* (int)(31 * scale[octave])               */
+    float angle;      /* degrees, fastAtan2 of the intensity centroid */
+    float response;   /* FAST score                              */
+    int32_t octave;   /* pyramid level                           */
+    int32_t class_id; /* -1                                      */
+} orbx_keypoint;
+
+typedef struct {
+    int nfeatures;       /* ORBextractor.nFeatures                  */
+    float scale_factor;  /* ORBextractor.scaleFactor                */
+    int nlevels;         /* ORBextractor.nLevels (<= 16)            */
+    int ini_th_fast;     /* ORBextractor.iniThFAST                  */
+    int min_th_fast;     /* ORBextractor.minThFAST                  */
+    int cv_simd;         /* 1: OpenCV 3.2 x86-64 SSE2 rounding in resize/GaussianBlur
+                            (default); 0: OpenCV scalar formulas      */
+    int max_batch;       /* images per batched call (device workspace sizing), >= 1 */
+    int device;          /* HIP device ordinal                       */
+} orbx_extractor_params;
+
+typedef struct orbx_extractor orbx_extractor;
+
+/* Replaces ORB_SLAM2::ORBextractor::ORBextractor (src/ORBextractor.cc:410-470).
+ * Device workspace is allocated lazily on the first call for a given image size. */
+orbx_status orbx_extractor_create(const orbx_extractor_params* params, orbx_extractor** out);
+orbx_status orbx_extractor_destroy(orbx_extractor* h);
+
+/* ORBextractor getters (include/ORBextractor.h:63-83); arrays hold nlevels floats. */
+orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* inv_scale,
+                                  float* sigma2, float* inv_sigma2, int* features_per_level);
+
+/* Replaces ORBextractor::operator() (src/ORBextractor.cc:1065-1127) for one host image.
+ * img: 8-bit gray, `stride` bytes per row.  Writes min(n, kp_cap) keypoints and rows of
+ * 32-byte descriptors; *n_out = n.  An empty image (w or h == 0) returns ORBX_OK with
+ * *n_out = -1 and leaves the outputs untouched, like the reference's silent return. */
+orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
+                         size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
+                         int* n_out);
+
+/* mvImagePyramid[level] (include/ORBextractor.h:85) of image `index` of the last call,
+ * copied to host (w*h bytes, tightly packed). */
+orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out,
+                               int* width, int* height);
+
+/* ---- batched, device-resident API (throughput path) -------------------------------------
+ * d_imgs: `batch` images in device memory, image i at d_imgs + i*batch_stride, rows
+ * `stride` bytes apart.  Results stay in the handle's workspace; orbx_batch_view exposes
+ * them as device pointers.  `stream` is the hipStream_t every kernel of the call is
+ * launched on (0 = the null stream).  Calls that consume another call's results (stereo
+ * after both extractions) must be on the same stream or ordered by the caller. */
+orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int batch,
+                                      int width, int height, size_t stride,
+                                      size_t batch_stride, void* stream);
+
+typedef struct {
+    int batch;              /* images in the last call                        */
+    int kp_cap;             /* keypoint slots per image                       */
+    orbx_keypoint* kps;     /* device [batch][kp_cap]                         */
+    uint8_t* desc;          /* device [batch][kp_cap][32]                     */
+    int32_t* nkp;           /* device [batch]                                 */
+    uint8_t* pyramid;       /* device [batch][pyr_bytes]                      */
+    size_t pyr_bytes;       /* bytes per image pyramid block                  */
+    int level_w[16], level_h[16], level_pitch[16];
+    size_t level_off[16];   /* byte offset of each level inside the block      */
+} orbx_batch_view;
+
+orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* view);
+
+/* Replaces Frame::ComputeStereoMatches (src/Frame.cc:496-686) for the last orbx_extract
+ * calls on `left` and `right` (same image size, same params).  mb is the baseline term the
+ * reference reads at Frame.cc:534 (normally mbf/fx).  uRight/depth: n_left floats
+ * (-1 = no match).  *n_valid = accepted matches. */
+orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float mbf, float mb,
+                              float* uRight, float* depth, int n_left, int* n_valid);
+
+/* Batched stereo over the last orbx_extract_batch_device calls of both handles (pair i =
+ * image i of each).  d_uRight/d_depth: device [batch][kp_cap] floats; d_nvalid: device
+ * [batch] (may be NULL). */
+orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor* right,
+                                           float mbf, float mb, float* d_uRight,
+                                           float* d_depth, int32_t* d_nvalid, void* stream);
+
+/* ---- descriptor matching (src/ORBmatcher.cc) ---------------------------------------------- */
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1715-1731) on host memory. */
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Library / device information. */
+const char* orbx_version(void);
+/* Text of the last failing HIP call on this thread ("" if none). */
+const char* orbx_last_error(void);
+orbx_status orbx_device_count(int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

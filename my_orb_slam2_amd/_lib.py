@@ -1,0 +1,114 @@
+"""ctypes binding of liborbx.so (include/orbx.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is present,
+constructing an extractor raises.  Loading the library itself needs no GPU (the CPU test
+suite checks that every symbol of include/orbx.h is exported).
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+
+import numpy as np
+
+PKG = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG / "liborbx.so"
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
+          -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_STATE"}
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__(f"{fn} failed: {STATUS.get(code, code)}")
+        self.code = code
+
+
+class ExtractorParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float),
+                ("nlevels", ctypes.c_int), ("ini_th_fast", ctypes.c_int),
+                ("min_th_fast", ctypes.c_int), ("cv_simd", ctypes.c_int),
+                ("max_batch", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+class BatchView(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int), ("kp_cap", ctypes.c_int), ("kps", ctypes.c_void_p),
+                ("desc", ctypes.c_void_p), ("nkp", ctypes.c_void_p),
+                ("pyramid", ctypes.c_void_p), ("pyr_bytes", ctypes.c_size_t),
+                ("level_w", ctypes.c_int * 16), ("level_h", ctypes.c_int * 16),
+                ("level_pitch", ctypes.c_int * 16), ("level_off", ctypes.c_size_t * 16)]
+
+
+# name -> (restype, argtypes); the exported C ABI (include/orbx.h)
+_vp, _i, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+SIGNATURES = {
+    "orbx_extractor_create": (_i, [ctypes.POINTER(ExtractorParams), ctypes.POINTER(_vp)]),
+    "orbx_extractor_destroy": (_i, [_vp]),
+    "orbx_extractor_tables": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbx_extract": (_i, [_vp, _vp, _i, _i, _sz, _vp, _i, _vp, ctypes.POINTER(_i)]),
+    "orbx_pyramid_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "orbx_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp]),
+    "orbx_batch_view_get": (_i, [_vp, ctypes.POINTER(BatchView)]),
+    "orbx_stereo_match": (_i, [_vp, _vp, _f, _f, _vp, _vp, _i, ctypes.POINTER(_i)]),
+    "orbx_stereo_match_batch_device": (_i, [_vp, _vp, _f, _f, _vp, _vp, _vp, _vp]),
+    "orbx_descriptor_distance": (_i, [_vp, _vp]),
+    "orbx_version": (ctypes.c_char_p, []),
+    "orbx_last_error": (ctypes.c_char_p, []),
+    "orbx_device_count": (_i, [ctypes.POINTER(_i)]),
+}
+
+_lib = None
+
+
+def load(path: pathlib.Path | str | None = None):
+    """Load liborbx.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is None or path is not None:
+        p = pathlib.Path(path) if path else LIB_PATH
+        # One HIP runtime per process: torch wheels bundle their own libamdhip64 (same
+        # soname).  Loading torch first makes liborbx bind to that copy instead of pulling
+        # in /opt/rocm's second runtime next to it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not p.exists():
+            raise OSError(f"{p} not found: build it with `python -m my_orb_slam2_amd.build`")
+        L = ctypes.CDLL(str(p))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        if path is not None:
+            return L
+        _lib = L
+    return _lib
+
+
+def check(fn: str, code: int):
+    if code != 0:
+        err = OrbxError(fn, code)
+        try:
+            detail = load().orbx_last_error()
+            if detail:
+                err.args = (err.args[0] + " [" + detail.decode() + "]",)
+        except Exception:
+            pass
+        raise err
+    return code
+
+
+def ptr(a) -> ctypes.c_void_p:
+    """Address of a numpy array or a torch tensor (device or host)."""
+    if isinstance(a, np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    if a is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(int(a))

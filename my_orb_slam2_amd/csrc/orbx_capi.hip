@@ -1,0 +1,634 @@
+// orbx_capi.hip — the extern "C" boundary (include/orbx.h) over the gfx950 kernels.
+//
+// Host responsibilities: the ORBextractor constructor tables (src/ORBextractor.cc:410-470),
+// the per-image-size geometry (pyramid sizes :1134, FAST cell grid :793-818, octree roots
+// :543-545, OpenCV resize coefficient tables), the HBM workspace, and the launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/orbx.h"
+#include "orbx_internal.h"
+#include "orbx_kernels.h"
+
+#define ORBX_VERSION "orbx 0.1.0 (gfx950)"
+
+namespace orbx {
+hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds);
+}
+
+using namespace orbx;
+
+static thread_local char g_err[256] = "";
+// Records the first failing HIP call for orbx_last_error().
+static bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    return false;
+}
+#define HIPOK(call) hip_ok((call), #call)
+
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    bool ensure(size_t bytes) {
+        if (bytes <= n && p) return true;
+        release();
+        if (bytes == 0) bytes = 16;
+        if (!HIPOK(hipMalloc(&p, bytes))) { p = nullptr; return false; }
+        n = bytes;
+        return true;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+struct orbx_extractor {
+    orbx_extractor_params prm;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // ORBextractor tables
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nfeat;
+    int umax[16];
+    int taps[7];
+    // geometry of the current image size
+    bool have_geom = false;
+    Geometry hg;
+    std::vector<CellDesc> cells;
+    std::vector<int16_t> rtab;
+    int ncap = 0, kcap = 0;
+    size_t octree_lds = 0, stereo_lds = 0;
+    int cap_batch = 0;
+    DevBuf d_geom, d_cells, d_rtab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
+        d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
+    long long kscratch_per_image = 0;
+    // last extraction
+    int last_batch = 0;
+    bool last_valid = false;
+    std::mutex mu;
+};
+
+namespace {
+
+
+inline int cvRound(float v) { return (int)lrintf(v); }
+inline int cvRound(double v) { return (int)lrint(v); }
+inline int cvFloor(float v) { int i = cvRound(v); float d = (float)(v - i); return i - (d < 0); }
+inline int cvCeil(float v) { int i = cvRound(v); float d = (float)(i - v); return i + (d < 0); }
+inline short sat_short(float v) {
+    int i = cvRound(v);
+    return (short)std::min(std::max(i, (int)SHRT_MIN), (int)SHRT_MAX);
+}
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+void compute_tables(orbx_extractor* h) {
+    const int L = h->prm.nlevels;
+    const double scaleFactor = (double)h->prm.scale_factor;   // ORBextractor::scaleFactor is double
+    h->scale.assign(L, 0.f);
+    h->sigma2.assign(L, 0.f);
+    h->inv_scale.assign(L, 0.f);
+    h->inv_sigma2.assign(L, 0.f);
+    h->nfeat.assign(L, 0);
+    h->scale[0] = 1.0f;
+    h->sigma2[0] = 1.0f;
+    for (int i = 1; i < L; i++) {
+        h->scale[i] = (float)(h->scale[i - 1] * scaleFactor);
+        h->sigma2[i] = h->scale[i] * h->scale[i];
+    }
+    for (int i = 0; i < L; i++) {
+        h->inv_scale[i] = 1.0f / h->scale[i];
+        h->inv_sigma2[i] = 1.0f / h->sigma2[i];
+    }
+    const int nfeatures = h->prm.nfeatures;
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)L));
+    int sum = 0;
+    for (int level = 0; level < L - 1; level++) {
+        h->nfeat[level] = cvRound(nDesired);
+        sum += h->nfeat[level];
+        nDesired *= factor;
+    }
+    h->nfeat[L - 1] = std::max(nfeatures - sum, 0);
+    // umax (src/ORBextractor.cc:454-469)
+    const int HP = 15;
+    int v, v0, vmax = cvFloor((float)(HP * std::sqrt(2.f) / 2 + 1));
+    int vmin = cvCeil((float)(HP * std::sqrt(2.f) / 2));
+    const double hp2 = HP * HP;
+    for (v = 0; v <= vmax; ++v) h->umax[v] = cvRound(std::sqrt(hp2 - v * v));
+    for (v = HP, v0 = 0; v >= vmin; --v) {
+        while (h->umax[v0] == h->umax[v0 + 1]) ++v0;
+        h->umax[v] = v0;
+        ++v0;
+    }
+    // getGaussianKernel(7, 2, CV_32F) -> x256 fixed point (FilterEngine 8U path)
+    float cf[7];
+    double s2 = -0.5 / (2.0 * 2.0), ksum = 0;
+    for (int i = 0; i < 7; ++i) {
+        double x = i - 3.0;
+        cf[i] = (float)std::exp(s2 * x * x);
+        ksum += cf[i];
+    }
+    ksum = 1. / ksum;
+    for (int i = 0; i < 7; ++i) cf[i] = (float)(cf[i] * ksum);
+    for (int i = 0; i < 7; ++i) h->taps[i] = cvRound(cf[i] * 256.f);
+}
+
+int vresize_simd_end(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x < width - 4; x += 4) {}
+    return x;
+}
+
+// Per-size geometry.  Returns ORBX_OK or ORBX_ERR_UNSUPPORTED.
+orbx_status build_geometry(orbx_extractor* h, int W, int H) {
+    Geometry& G = h->hg;
+    memset(&G, 0, sizeof(G));
+    h->cells.clear();
+    h->rtab.clear();
+    const int L = h->prm.nlevels;
+    G.width = W;
+    G.height = H;
+    G.nlevels = L;
+    G.ini_th = std::min(std::max(h->prm.ini_th_fast, 0), 255);
+    G.min_th = std::min(std::max(h->prm.min_th_fast, 0), 255);
+    memcpy(G.taps, h->taps, sizeof(G.taps));
+    memcpy(G.umax, h->umax, sizeof(G.umax));
+    G.stereo_win = (int)std::ceil(2.0f * h->scale[L - 1]) + 2;
+    long long off = 0, cand = 0;
+    int out = 0, blur_tiles = 0, oblocks = 0;
+    for (int l = 0; l < L; ++l) {
+        LevelGeom& lv = G.lv[l];
+        lv.w = cvRound((float)W * h->inv_scale[l]);
+        lv.h = cvRound((float)H * h->inv_scale[l]);
+        if (lv.w <= 0 || lv.h <= 0) return ORBX_ERR_UNSUPPORTED;
+        if (lv.w > 4096 + 32 || lv.h > 4096 + 32) return ORBX_ERR_UNSUPPORTED;   // 12-bit packing
+        lv.pitch = (int)align_up(lv.w, 64);
+        lv.off = off;
+        off += (long long)align_up((size_t)lv.pitch * lv.h, 256);
+        lv.scale = h->scale[l];
+        lv.inv_scale = h->inv_scale[l];
+        lv.nfeat = h->nfeat[l];
+        lv.patch_size = (int)(31 * h->scale[l]);
+        // FAST cell grid (src/ORBextractor.cc:785-818)
+        const int minB = ORBX_MIN_BORDER;
+        const int maxBX = lv.w - ORBX_EDGE + 3, maxBY = lv.h - ORBX_EDGE + 3;
+        const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+        const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+        lv.ncols = nCols;
+        lv.nrows = nRows;
+        lv.cell_begin = (int)h->cells.size();
+        lv.cand_off = cand;
+        int lcap = 0;
+        if (nCols > 0 && nRows > 0) {
+            const int wCell = (int)std::ceil(width / nCols);
+            const int hCell = (int)std::ceil(height / nRows);
+            lv.wcell = wCell;
+            lv.hcell = hCell;
+            for (int i = 0; i < nRows; i++) {
+                const float iniY = (float)(minB + i * hCell);
+                float maxY = iniY + hCell + 6;
+                if (iniY >= maxBY - 3) continue;
+                if (maxY > maxBY) maxY = (float)maxBY;
+                for (int j = 0; j < nCols; j++) {
+                    const float iniX = (float)(minB + j * wCell);
+                    float maxX = iniX + wCell + 6;
+                    if (iniX >= maxBX - 6) continue;
+                    if (maxX > maxBX) maxX = (float)maxBX;
+                    CellDesc c;
+                    memset(&c, 0, sizeof(c));
+                    c.level = (int16_t)l;
+                    c.ini_x = (int16_t)(int)iniX;
+                    c.ini_y = (int16_t)(int)iniY;
+                    c.cols = (int16_t)((int)maxX - (int)iniX);
+                    c.rows = (int16_t)((int)maxY - (int)iniY);
+                    const int dh = c.rows - 6, dw = c.cols - 6;
+                    c.cap = (dh > 0 && dw > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
+                    c.slot = (int32_t)cand;
+                    cand += c.cap;
+                    lcap += c.cap;
+                    G.max_roi_bytes = std::max(G.max_roi_bytes, (int)c.rows * c.cols);
+                    if (dh > 0 && dw > 0)
+                        G.max_mbuf_bytes = std::max(G.max_mbuf_bytes, (dh + 2) * (dw + 2));
+                    h->cells.push_back(c);
+                }
+            }
+        }
+        lv.ncells = (int)h->cells.size() - lv.cell_begin;
+        lv.cand_cap = lcap;
+        G.max_ncand_level = std::max(G.max_ncand_level, lcap);
+        // octree roots (src/ORBextractor.cc:543-545)
+        lv.n_ini = 0;
+        lv.hx = 0.f;
+        if (maxBY - minB > 0) {
+            const float r = std::round(static_cast<float>(maxBX - minB) / (maxBY - minB));
+            if (r >= 1.f && r < 4096.f) {
+                lv.n_ini = (int)r;
+                lv.hx = static_cast<float>(maxBX - minB) / lv.n_ini;
+            }
+        }
+        lv.out_cap = std::max(std::max(lv.nfeat + 3, 4 * lv.n_ini), 4);
+        lv.kp_level_cap = lv.out_cap;
+        lv.out_off = out;
+        out += lv.out_cap;
+        G.max_out_cap = std::max(G.max_out_cap, lv.out_cap);
+        G.blur_tile_begin[l] = blur_tiles;
+        blur_tiles += ((lv.w + 63) / 64) * ((lv.h + 15) / 16);
+        G.orient_block_begin[l] = oblocks;
+        oblocks += (lv.out_cap + 3) / 4;
+        lv.bsimd_end = h->prm.cv_simd ? (lv.w / 4) * 4 : 0;
+        // resize tables (cv::resize INTER_LINEAR 8U, imgwarp.cpp)
+        lv.copy = lv.area2 = 0;
+        lv.rtab_off = 0;
+        lv.xmax = lv.w;
+        lv.rsimd_end = 0;
+        if (l > 0) {
+            const LevelGeom& S = G.lv[l - 1];
+            const int sw = S.w, sh = S.h, dw = lv.w, dh = lv.h;
+            if (sw == dw && sh == dh) {
+                lv.copy = 1;
+            } else {
+                const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+                const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+                const int isx = cvRound(scale_x), isy = cvRound(scale_y);
+                const bool area_fast = std::abs(scale_x - isx) < DBL_EPSILON &&
+                                       std::abs(scale_y - isy) < DBL_EPSILON;
+                if (area_fast && isx == 2 && isy == 2) {
+                    lv.area2 = 1;
+                } else {
+                    lv.rtab_off = (int)h->rtab.size();
+                    std::vector<int16_t> xofs(dw), alpha(2 * dw), yofs(dh), beta(2 * dh);
+                    int xmax = dw;
+                    for (int dx = 0; dx < dw; ++dx) {
+                        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                        int sx = cvFloor(fx);
+                        fx -= sx;
+                        if (sx < 0) { fx = 0, sx = 0; }
+                        if (sx + 1 >= sw) {
+                            xmax = std::min(xmax, dx);
+                            if (sx >= sw - 1) fx = 0, sx = sw - 1;
+                        }
+                        xofs[dx] = (int16_t)sx;
+                        alpha[2 * dx] = sat_short((1.f - fx) * 2048);
+                        alpha[2 * dx + 1] = sat_short(fx * 2048);
+                    }
+                    for (int dy = 0; dy < dh; ++dy) {
+                        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                        int sy = cvFloor(fy);
+                        fy -= sy;
+                        yofs[dy] = (int16_t)sy;
+                        beta[2 * dy] = sat_short((1.f - fy) * 2048);
+                        beta[2 * dy + 1] = sat_short(fy * 2048);
+                    }
+                    h->rtab.insert(h->rtab.end(), xofs.begin(), xofs.end());
+                    h->rtab.insert(h->rtab.end(), alpha.begin(), alpha.end());
+                    h->rtab.insert(h->rtab.end(), yofs.begin(), yofs.end());
+                    h->rtab.insert(h->rtab.end(), beta.begin(), beta.end());
+                    lv.xmax = xmax;
+                    lv.rsimd_end = h->prm.cv_simd ? vresize_simd_end(dw) : 0;
+                }
+            }
+        }
+    }
+    G.blur_tile_begin[L] = blur_tiles;
+    G.orient_block_begin[L] = oblocks;
+    G.blur_tiles = blur_tiles;
+    G.orient_blocks = oblocks;
+    G.n_cells = (int)h->cells.size();
+    G.kp_cap = out;
+    G.out_words = out;
+    G.pyr_bytes = off;
+    G.cand_words = std::max(cand, 1LL);
+    if (G.max_roi_bytes == 0) G.max_roi_bytes = 16;
+    if (G.max_mbuf_bytes == 0) G.max_mbuf_bytes = 16;
+    if (G.max_out_cap > 8192) return ORBX_ERR_UNSUPPORTED;
+    h->kscratch_per_image = 0;
+    for (int l = 0; l < L; ++l) h->kscratch_per_image += (long long)G.lv[l].cand_cap * 8;
+    h->kscratch_per_image = (long long)align_up((size_t)std::max(h->kscratch_per_image, 16LL), 256);
+    // octree LDS: node arrays for the largest list, candidate arrays up to kcap in LDS
+    h->ncap = (int)align_up((size_t)G.max_out_cap, 16);
+    int kcap = std::min(std::max(G.max_ncand_level, 64), 8192);
+    while (kcap > 64 && octree_lds_bytes(h->ncap, kcap) > 96 * 1024) kcap -= 64;
+    h->kcap = kcap;
+    h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
+    h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h);
+    if (h->octree_lds > 160 * 1024 || h->stereo_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
+    if (G.kp_cap > 32767) return ORBX_ERR_UNSUPPORTED;   // 16-bit keypoint indices in stereo
+    return ORBX_OK;
+}
+
+orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
+    if (batch < 1) return ORBX_ERR_INVALID;
+    if (!HIPOK(hipSetDevice(h->device))) return ORBX_ERR_DEVICE;
+    const bool same = h->have_geom && h->hg.width == W && h->hg.height == H;
+    if (!same) {
+        orbx_status s = build_geometry(h, W, H);
+        if (s != ORBX_OK) { h->have_geom = false; return s; }
+        if (!h->d_geom.ensure(sizeof(Geometry))) return ORBX_ERR_DEVICE;
+        if (!h->d_cells.ensure(std::max<size_t>(h->cells.size(), 1) * sizeof(CellDesc))) return ORBX_ERR_DEVICE;
+        if (!h->d_rtab.ensure(std::max<size_t>(h->rtab.size(), 1) * 2)) return ORBX_ERR_DEVICE;
+        if (!HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
+            return ORBX_ERR_DEVICE;
+        if (!h->cells.empty() &&
+            !HIPOK(hipMemcpy(h->d_cells.p, h->cells.data(), h->cells.size() * sizeof(CellDesc),
+                      hipMemcpyHostToDevice)))
+            return ORBX_ERR_DEVICE;
+        if (!h->rtab.empty() &&
+            !HIPOK(hipMemcpy(h->d_rtab.p, h->rtab.data(), h->rtab.size() * 2, hipMemcpyHostToDevice)))
+            return ORBX_ERR_DEVICE;
+        if (!HIPOK(prepare_kernels(h->octree_lds, h->stereo_lds))) return ORBX_ERR_DEVICE;
+        h->have_geom = true;
+        h->cap_batch = 0;
+    }
+    if (batch > h->cap_batch) {
+        const Geometry& G = h->hg;
+        const size_t B = (size_t)batch;
+        bool ok = h->d_pyr.ensure(B * G.pyr_bytes) && h->d_blur.ensure(B * G.pyr_bytes) &&
+                  h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
+                  h->d_cand.ensure(B * G.cand_words * 4) &&
+                  h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
+                  h->d_kscr.ensure(B * h->kscratch_per_image) &&
+                  h->d_kps.ensure(B * G.kp_cap * sizeof(orbx_keypoint)) &&
+                  h->d_desc.ensure(B * G.kp_cap * 32) && h->d_nkp.ensure(B * 4) &&
+                  h->d_in.ensure((size_t)W * H);
+        if (!ok) return ORBX_ERR_DEVICE;
+        h->cap_batch = batch;
+    }
+    return ORBX_OK;
+}
+
+orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, int batch, size_t stride,
+                        size_t batch_stride, hipStream_t st) {
+    ExtractLaunch a;
+    a.hg = &h->hg;
+    a.dg = h->d_geom.as<Geometry>();
+    a.cells = h->d_cells.as<CellDesc>();
+    a.rtab = h->d_rtab.as<int16_t>();
+    a.d_imgs = d_imgs;
+    a.stride = stride;
+    a.batch_stride = batch_stride;
+    a.batch = batch;
+    a.pyr = h->d_pyr.as<uint8_t>();
+    a.blur = h->d_blur.as<uint8_t>();
+    a.ccnt = h->d_ccnt.as<int>();
+    a.cand = h->d_cand.as<uint32_t>();
+    a.ocnt = h->d_ocnt.as<int>();
+    a.okp = h->d_okp.as<uint32_t>();
+    a.kscratch = h->d_kscr.as<uint8_t>();
+    a.kscratch_per_image = h->kscratch_per_image;
+    a.ncap = h->ncap;
+    a.kcap = h->kcap;
+    a.octree_lds = h->octree_lds;
+    a.kps = h->d_kps.as<float>();
+    a.desc = h->d_desc.as<uint8_t>();
+    a.nkp = h->d_nkp.as<int>();
+    if (!HIPOK(launch_extract(a, st))) return ORBX_ERR_DEVICE;
+    h->last_batch = batch;
+    h->last_valid = true;
+    return ORBX_OK;
+}
+
+// Batched calls run on exactly the stream the caller names; 0 is the null (legacy default)
+// stream, which orders them with the caller's other default-stream work.
+hipStream_t pick_stream(orbx_extractor*, void* s) { return (hipStream_t)s; }
+
+orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, float mbf, float mb, float* d_uR,
+                       float* d_dep, int* d_nv, hipStream_t st) {
+    if (!L->last_valid || !R->last_valid) return ORBX_ERR_STATE;
+    if (L->hg.width != R->hg.width || L->hg.height != R->hg.height || L->last_batch != R->last_batch ||
+        L->hg.nlevels != R->hg.nlevels || L->hg.kp_cap != R->hg.kp_cap)
+        return ORBX_ERR_INVALID;
+    StereoLaunch a;
+    a.dg = L->d_geom.as<Geometry>();
+    a.batch = L->last_batch;
+    a.kpsL = L->d_kps.as<float>();
+    a.descL = L->d_desc.as<uint8_t>();
+    a.nkpL = L->d_nkp.as<int>();
+    a.pyrL = L->d_pyr.as<uint8_t>();
+    a.kpsR = R->d_kps.as<float>();
+    a.descR = R->d_desc.as<uint8_t>();
+    a.nkpR = R->d_nkp.as<int>();
+    a.pyrR = R->d_pyr.as<uint8_t>();
+    a.mbf = mbf;
+    a.mb = mb;
+    a.uR = d_uR;
+    a.depth = d_dep;
+    a.nvalid = d_nv;
+    a.lds = L->stereo_lds;
+    return HIPOK(launch_stereo(a, st)) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* orbx_version(void) { return ORBX_VERSION; }
+
+const char* orbx_last_error(void) { return g_err; }
+
+orbx_status orbx_device_count(int* n) {
+    if (!n) return ORBX_ERR_INVALID;
+    int c = 0;
+    if (!HIPOK(hipGetDeviceCount(&c))) { *n = 0; return ORBX_ERR_DEVICE; }
+    *n = c;
+    return ORBX_OK;
+}
+
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    for (int i = 0; i < 32; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor** out) {
+    if (!p || !out) return ORBX_ERR_INVALID;
+    *out = nullptr;
+    if (p->nlevels < 1 || p->nlevels > ORBX_MAX_LEVELS || p->nfeatures < 0 ||
+        !(p->scale_factor > 0.f) || p->max_batch < 0)
+        return ORBX_ERR_INVALID;
+    int ndev = 0;
+    if (!HIPOK(hipGetDeviceCount(&ndev)) || ndev <= 0) return ORBX_ERR_DEVICE;
+    if (p->device < 0 || p->device >= ndev) return ORBX_ERR_INVALID;
+    orbx_extractor* h = new orbx_extractor();
+    h->prm = *p;
+    if (h->prm.max_batch < 1) h->prm.max_batch = 1;
+    h->device = p->device;
+    compute_tables(h);
+    if (!HIPOK(hipSetDevice(h->device)) ||
+        !HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) ||
+        !HIPOK(hipEventCreateWithFlags(&h->done, hipEventDisableTiming))) {
+        delete h;
+        return ORBX_ERR_DEVICE;
+    }
+    *out = h;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extractor_destroy(orbx_extractor* h) {
+    if (!h) return ORBX_ERR_INVALID;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_in, &h->d_pyr, &h->d_blur,
+                      &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
+                      &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv};
+    for (DevBuf* b : bufs) b->release();
+    if (h->done) (void)hipEventDestroy(h->done);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* inv_scale,
+                                  float* sigma2, float* inv_sigma2, int* features_per_level) {
+    if (!h) return ORBX_ERR_INVALID;
+    for (int i = 0; i < h->prm.nlevels; ++i) {
+        if (scale) scale[i] = h->scale[i];
+        if (inv_scale) inv_scale[i] = h->inv_scale[i];
+        if (sigma2) sigma2[i] = h->sigma2[i];
+        if (inv_sigma2) inv_sigma2[i] = h->inv_sigma2[i];
+        if (features_per_level) features_per_level[i] = h->nfeat[i];
+    }
+    return ORBX_OK;
+}
+
+orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
+                         size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
+                         int* n_out) {
+    if (!h || !n_out) return ORBX_ERR_INVALID;
+    if (width <= 0 || height <= 0 || !img) {   // cv::Mat::empty(): silent return
+        *n_out = -1;
+        return ORBX_OK;
+    }
+    if (stride < (size_t)width) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, 1);
+    if (s != ORBX_OK) return s;
+    hipStream_t st = h->stream;
+    if (!HIPOK(hipMemcpy2DAsync(h->d_in.p, width, img, stride, width, height, hipMemcpyHostToDevice, st)))
+        return ORBX_ERR_DEVICE;
+    s = run_extract(h, h->d_in.as<uint8_t>(), 1, width, (size_t)width * height, st);
+    if (s != ORBX_OK) return s;
+    int n = 0;
+    if (!HIPOK(hipMemcpyAsync(&n, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipStreamSynchronize(st)))
+        return ORBX_ERR_DEVICE;
+    *n_out = n;
+    const int m = std::min(n, kp_cap);
+    if (m > 0) {
+        if (kps && !HIPOK(hipMemcpyAsync(kps, h->d_kps.p, (size_t)m * sizeof(orbx_keypoint),
+                                  hipMemcpyDeviceToHost, st)))
+            return ORBX_ERR_DEVICE;
+        if (desc && !HIPOK(hipMemcpyAsync(desc, h->d_desc.p, (size_t)m * 32, hipMemcpyDeviceToHost, st)))
+            return ORBX_ERR_DEVICE;
+        if (!HIPOK(hipStreamSynchronize(st))) return ORBX_ERR_DEVICE;
+    }
+    return n > kp_cap ? ORBX_ERR_CAPACITY : ORBX_OK;
+}
+
+orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
+                               int* height) {
+    if (!h || !h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
+        index >= h->last_batch)
+        return ORBX_ERR_INVALID;
+    const LevelGeom& lv = h->hg.lv[level];
+    if (width) *width = lv.w;
+    if (height) *height = lv.h;
+    if (!out) return ORBX_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    (void)hipSetDevice(h->device);
+    const uint8_t* src = h->d_pyr.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
+    if (!HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
+        !HIPOK(hipStreamSynchronize(h->stream)))
+        return ORBX_ERR_DEVICE;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int batch,
+                                      int width, int height, size_t stride, size_t batch_stride,
+                                      void* stream) {
+    if (!h || !d_imgs || batch < 1 || width <= 0 || height <= 0 || stride < (size_t)width)
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, batch);
+    if (s != ORBX_OK) return s;
+    return run_extract(h, d_imgs, batch, stride, batch_stride, pick_stream(h, stream));
+}
+
+orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {
+    if (!h || !v || !h->last_valid) return ORBX_ERR_STATE;
+    memset(v, 0, sizeof(*v));
+    v->batch = h->last_batch;
+    v->kp_cap = h->hg.kp_cap;
+    v->kps = h->d_kps.as<orbx_keypoint>();
+    v->desc = h->d_desc.as<uint8_t>();
+    v->nkp = h->d_nkp.as<int32_t>();
+    v->pyramid = h->d_pyr.as<uint8_t>();
+    v->pyr_bytes = (size_t)h->hg.pyr_bytes;
+    for (int l = 0; l < h->hg.nlevels && l < 16; ++l) {
+        v->level_w[l] = h->hg.lv[l].w;
+        v->level_h[l] = h->hg.lv[l].h;
+        v->level_pitch[l] = h->hg.lv[l].pitch;
+        v->level_off[l] = (size_t)h->hg.lv[l].off;
+    }
+    return ORBX_OK;
+}
+
+orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float mbf, float mb,
+                              float* uRight, float* depth, int n_left, int* n_valid) {
+    if (!left || !right || left == right) return ORBX_ERR_INVALID;
+    if (!left->last_valid || !right->last_valid || left->last_batch != 1 || right->last_batch != 1)
+        return ORBX_ERR_STATE;
+    std::lock_guard<std::mutex> lk(left->mu);
+    (void)hipSetDevice(left->device);
+    const size_t KC = (size_t)left->hg.kp_cap;
+    if (!left->d_uR.ensure(KC * 4) || !left->d_dep.ensure(KC * 4) || !left->d_nv.ensure(16))
+        return ORBX_ERR_DEVICE;
+    hipStream_t st = left->stream;
+    if (!HIPOK(hipEventRecord(right->done, right->stream)) ||
+        !HIPOK(hipStreamWaitEvent(st, right->done, 0)))
+        return ORBX_ERR_DEVICE;
+    orbx_status s = run_stereo(left, right, mbf, mb, left->d_uR.as<float>(), left->d_dep.as<float>(),
+                               left->d_nv.as<int>(), st);
+    if (s != ORBX_OK) return s;
+    int n = 0, nv = 0;
+    if (!HIPOK(hipMemcpyAsync(&n, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(&nv, left->d_nv.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipStreamSynchronize(st)))
+        return ORBX_ERR_DEVICE;
+    const int m = std::min(n, n_left);
+    if (m > 0) {
+        if ((uRight && !HIPOK(hipMemcpyAsync(uRight, left->d_uR.p, (size_t)m * 4, hipMemcpyDeviceToHost,
+                                      st))) ||
+            (depth && !HIPOK(hipMemcpyAsync(depth, left->d_dep.p, (size_t)m * 4, hipMemcpyDeviceToHost,
+                                     st))) ||
+            !HIPOK(hipStreamSynchronize(st)))
+            return ORBX_ERR_DEVICE;
+    }
+    if (n_valid) *n_valid = nv;
+    return n > n_left ? ORBX_ERR_CAPACITY : ORBX_OK;
+}
+
+orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor* right, float mbf,
+                                           float mb, float* d_uRight, float* d_depth,
+                                           int32_t* d_nvalid, void* stream) {
+    if (!left || !right || left == right || !d_uRight || !d_depth) return ORBX_ERR_INVALID;
+    (void)hipSetDevice(left->device);
+    return run_stereo(left, right, mbf, mb, d_uRight, d_depth, d_nvalid,
+                      pick_stream(left, stream));
+}
+
+}  // extern "C"

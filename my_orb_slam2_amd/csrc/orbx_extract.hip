@@ -1,0 +1,835 @@
+// orbx_extract.hip — the ORB extractor as gfx950 kernels, batched over B images.
+//
+// Replaces ORB_SLAM2::ORBextractor::operator() (src/ORBextractor.cc:1065-1127).  Stages:
+//   k_copy_level0  input -> pyramid level 0                     (ComputePyramid :1148-1150)
+//   k_resize       level l-1 -> level l, INTER_LINEAR 8U         (ComputePyramid :1140-1146)
+//   k_blur         7x7 Gaussian sigma 2 of every level           (operator() :1106-1108)
+//   k_fast         FAST-9 + cell-local NMS per 30px cell         (ComputeKeyPointsOctTree :801-850)
+//   k_octree       quadtree distribution, one workgroup/level    (DistributeOctTree :539-765)
+//   k_orient_desc  IC angle + rBRIEF + level-major assembly      (:872-874, :77-147, :1097-1126)
+// Every kernel is integer work except three float formulas that the reference evaluates in
+// float (fastAtan2, the BRIEF rotation, the blur's SSE2 column pass); the library is built
+// with -ffp-contract=off so each of those is a separately rounded v_mul/v_add, as on x86.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_math.h"
+#include "orbx_kernels.h"
+
+namespace orbx {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "orbx_pattern.inc"
+};
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
+
+// ----------------------------------------------------------------------------------------
+// Pyramid
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_copy_level0(const Geometry* __restrict__ g,
+                                                     const uint8_t* __restrict__ src,
+                                                     size_t stride, size_t batch_stride,
+                                                     uint8_t* __restrict__ pyr) {
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const LevelGeom& L = g->lv[0];
+    if (x0 >= L.w) return;
+    const uint8_t* s = src + b * batch_stride + (size_t)y * stride + x0;
+    uint8_t* d = pyr + b * g->pyr_bytes + L.off + (size_t)y * L.pitch + x0;
+    if (x0 + 3 < L.w) {
+        uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) |
+                     ((uint32_t)s[3] << 24);
+        *(uint32_t*)d = v;
+    } else {
+        for (int j = 0; x0 + j < L.w; ++j) d[j] = s[j];
+    }
+}
+
+// cv::resize INTER_LINEAR 8U restated over precomputed OpenCV coefficient tables
+// (xofs/alpha/yofs/beta, built on the host exactly as imgwarp.cpp builds them).
+__global__ __launch_bounds__(256) void k_resize(const Geometry* __restrict__ g,
+                                                const int16_t* __restrict__ rtab,
+                                                uint8_t* __restrict__ pyr, int level) {
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const LevelGeom& L = g->lv[level];
+    const LevelGeom& S = g->lv[level - 1];
+    if (x0 >= L.w) return;
+    const uint8_t* src = pyr + b * g->pyr_bytes + S.off;
+    uint8_t* dst = pyr + b * g->pyr_bytes + L.off + (size_t)y * L.pitch;
+    uint32_t out = 0;
+    const int nx = min(4, L.w - x0);
+    if (L.copy) {
+        for (int j = 0; j < nx; ++j) out |= (uint32_t)src[(size_t)y * S.pitch + x0 + j] << (8 * j);
+    } else if (L.area2) {
+        const uint8_t* s0 = src + (size_t)(2 * y) * S.pitch;
+        const uint8_t* s1 = s0 + S.pitch;
+        for (int j = 0; j < nx; ++j) {
+            int x = 2 * (x0 + j);
+            out |= (uint32_t)((s0[x] + s0[x + 1] + s1[x] + s1[x + 1] + 2) >> 2) << (8 * j);
+        }
+    } else {
+        const int16_t* xofs = rtab + L.rtab_off;
+        const int16_t* alpha = xofs + L.w;
+        const int16_t* yofs = alpha + 2 * L.w;
+        const int16_t* beta = yofs + L.h;
+        const int sy0 = yofs[y];
+        const int r0 = min(max(sy0, 0), S.h - 1), r1 = min(max(sy0 + 1, 0), S.h - 1);
+        const uint8_t* s0 = src + (size_t)r0 * S.pitch;
+        const uint8_t* s1 = src + (size_t)r1 * S.pitch;
+        const int b0 = beta[2 * y], b1 = beta[2 * y + 1];
+        for (int j = 0; j < nx; ++j) {
+            const int x = x0 + j;
+            const int sx = xofs[x];
+            int h0, h1;
+            if (x < L.xmax) {
+                const int a0 = alpha[2 * x], a1 = alpha[2 * x + 1];
+                h0 = s0[sx] * a0 + s0[sx + 1] * a1;
+                h1 = s1[sx] * a0 + s1[sx + 1] * a1;
+            } else {
+                h0 = s0[sx] * 2048;
+                h1 = s1[sx] * 2048;
+            }
+            int v;
+            if (x < L.rsimd_end) {
+                // VResizeLinearVec_32s8u: packs(>>4), mulhi, adds, (+2)>>2, packus
+                int t0 = min(max(h0 >> 4, -32768), 32767);
+                int t1 = min(max(h1 >> 4, -32768), 32767);
+                int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
+                m = min(max(m, -32768), 32767);
+                m = min(max(m + 2, -32768), 32767);
+                v = sat_u8(m >> 2);
+            } else {
+                v = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);   // FixedPtCast<int,uchar,22>
+            }
+            out |= (uint32_t)v << (8 * j);
+        }
+    }
+    if (nx == 4) {
+        *(uint32_t*)(dst + x0) = out;
+    } else {
+        for (int j = 0; j < nx; ++j) dst[x0 + j] = (uint8_t)(out >> (8 * j));
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of every level: 64x16 output tile per
+// workgroup, source tile + row pass staged in LDS.
+// ----------------------------------------------------------------------------------------
+#define BT_W 64
+#define BT_H 16
+__global__ __launch_bounds__(256) void k_blur(const Geometry* __restrict__ g,
+                                              const uint8_t* __restrict__ pyr,
+                                              uint8_t* __restrict__ blur) {
+    __shared__ uint8_t tin[BT_H + 6][BT_W + 8];
+    __shared__ int trow[BT_H + 6][BT_W + 1];
+    const int b = blockIdx.y;
+    const int t = blockIdx.x;
+    int level = 0;
+    while (level + 1 < g->nlevels && t >= g->blur_tile_begin[level + 1]) ++level;
+    const LevelGeom& L = g->lv[level];
+    const int tl = t - g->blur_tile_begin[level];
+    const int ntx = (L.w + BT_W - 1) / BT_W;
+    const int X0 = (tl % ntx) * BT_W, Y0 = (tl / ntx) * BT_H;
+    const uint8_t* src = pyr + b * g->pyr_bytes + L.off;
+    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
+        const int r = i / (BT_W + 6), c = i % (BT_W + 6);
+        const int yy = reflect101(Y0 + r - 3, L.h), xx = reflect101(X0 + c - 3, L.w);
+        tin[r][c] = src[(size_t)yy * L.pitch + xx];
+    }
+    __syncthreads();
+    const int k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3];
+    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
+        const int r = i / BT_W, c = i % BT_W;
+        const uint8_t* p = &tin[r][c];
+        trow[r][c] = k0 * p[0] + k1 * p[1] + k2 * p[2] + k3 * p[3] + g->taps[4] * p[4] +
+                     g->taps[5] * p[5] + g->taps[6] * p[6];
+    }
+    __syncthreads();
+    const float f0 = (float)k3 * (1.f / 65536.f), f1 = (float)g->taps[4] * (1.f / 65536.f),
+                f2 = (float)g->taps[5] * (1.f / 65536.f), f3 = (float)g->taps[6] * (1.f / 65536.f);
+    uint8_t* dst = blur + b * g->pyr_bytes + L.off;
+    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
+        const int r = i / BT_W, c = i % BT_W;
+        const int x = X0 + c, y = Y0 + r;
+        if (x >= L.w || y >= L.h) continue;
+        const int c0 = trow[r + 3][c];
+        const int p1 = trow[r + 4][c] + trow[r + 2][c];
+        const int p2 = trow[r + 5][c] + trow[r + 1][c];
+        const int p3 = trow[r + 6][c] + trow[r][c];
+        int v;
+        if (x < L.bsimd_end) {
+            // SymmColumnVec_32s8u: float accumulate, cvtps2dq (half-even), packs, packus
+            float s = (float)c0 * f0;
+            s = s + 0.0f;
+            s = s + (float)p1 * f1;
+            s = s + (float)p2 * f2;
+            s = s + (float)p3 * f3;
+            v = (int)rintf(s);
+            v = min(max(v, -32768), 32767);
+        } else {
+            const int s0 = k3 * c0 + g->taps[4] * p1 + g->taps[5] * p2 + g->taps[6] * p3;
+            v = (s0 + (1 << 15)) >> 16;   // FixedPtCastEx<int,uchar>(16)
+        }
+        dst[(size_t)y * L.pitch + x] = sat_u8(v);
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// FAST-9 per cell: one wave per 30px cell.  The reference calls cv::FAST on every cell ROI
+// with iniThFAST and, if the cell yields nothing, again with minThFAST; NMS is local to the
+// ROI.  Here the ROI is staged in LDS once, the threshold-free arc score M (max over the 16
+// 9-pixel arcs of the min |difference|, signed per polarity) is computed once per pixel,
+// and both thresholds are derived from it: corner at t <=> M > t, cornerScore = M - 1.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ int fast_arc_score(const uint8_t* roi, int cols, int r, int c) {
+    const int v = roi[r * cols + c];
+    int d[16];
+    // Bresenham circle of radius 3 in cv::FAST order (makeOffsets, patternSize 16): (dx, dy)
+    d[0] = v - roi[(r + 3) * cols + c];
+    d[1] = v - roi[(r + 3) * cols + c + 1];
+    d[2] = v - roi[(r + 2) * cols + c + 2];
+    d[3] = v - roi[(r + 1) * cols + c + 3];
+    d[4] = v - roi[(r)*cols + c + 3];
+    d[5] = v - roi[(r - 1) * cols + c + 3];
+    d[6] = v - roi[(r - 2) * cols + c + 2];
+    d[7] = v - roi[(r - 3) * cols + c + 1];
+    d[8] = v - roi[(r - 3) * cols + c];
+    d[9] = v - roi[(r - 3) * cols + c - 1];
+    d[10] = v - roi[(r - 2) * cols + c - 2];
+    d[11] = v - roi[(r - 1) * cols + c - 3];
+    d[12] = v - roi[(r)*cols + c - 3];
+    d[13] = v - roi[(r + 1) * cols + c - 3];
+    d[14] = v - roi[(r + 2) * cols + c - 2];
+    d[15] = v - roi[(r + 3) * cols + c - 1];
+    // sliding min / max over 9 cyclic neighbours by doubling
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        mn2[i] = min(d[i], d[(i + 1) & 15]);
+        mx2[i] = max(d[i], d[(i + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        mn4[i] = min(mn2[i], mn2[(i + 2) & 15]);
+        mx4[i] = max(mx2[i], mx2[(i + 2) & 15]);
+    }
+    int best_dark = -1000, best_min_max = 1000;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int mn8 = min(mn4[i], mn4[(i + 4) & 15]);
+        const int mx8 = max(mx4[i], mx4[(i + 4) & 15]);
+        const int mn9 = min(mn8, d[(i + 8) & 15]);
+        const int mx9 = max(mx8, d[(i + 8) & 15]);
+        best_dark = max(best_dark, mn9);       // 9 pixels all darker than v by > t
+        best_min_max = min(best_min_max, mx9); // 9 pixels all brighter: -max(d) > t
+    }
+    return max(best_dark, -best_min_max);
+}
+
+// Keypoint test at threshold t on the M map (mb: (dh+2) x (dw+2), zero ring).
+__device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, int cc, int t,
+                                            int& score) {
+    const uint8_t* p = mb + (rr + 1) * mw + (cc + 1);
+    const int m = p[0];
+    if (m <= t) return false;
+    const int s = m - 1;
+    score = s;
+#define ORBX_NB(o) { const int q = p[o]; if (q > t && q - 1 >= s) return false; }
+    ORBX_NB(-mw - 1) ORBX_NB(-mw) ORBX_NB(-mw + 1) ORBX_NB(-1) ORBX_NB(1)
+    ORBX_NB(mw - 1) ORBX_NB(mw) ORBX_NB(mw + 1)
+#undef ORBX_NB
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
+                                              const CellDesc* __restrict__ cells,
+                                              const uint8_t* __restrict__ pyr,
+                                              int* __restrict__ ccnt,
+                                              uint32_t* __restrict__ cand) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int ci = blockIdx.x * 4 + wid;
+    const bool active = ci < g->n_cells;
+    const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
+    uint8_t* roi = smem + wid * (roi_cap + mb_cap);
+    uint8_t* mb = roi + roi_cap;
+    CellDesc c;
+    int rows = 0, cols = 0, dh = 0, dw = 0;
+    if (active) {
+        c = cells[ci];
+        rows = c.rows; cols = c.cols;
+        dh = rows - 6; dw = cols - 6;
+        const LevelGeom& L = g->lv[c.level];
+        const uint8_t* src = pyr + b * g->pyr_bytes + L.off + (size_t)c.ini_y * L.pitch + c.ini_x;
+        for (int i = lane; i < rows * cols; i += 64) {
+            const int r = i / cols, cc = i - r * cols;
+            roi[i] = src[(size_t)r * L.pitch + cc];
+        }
+        if (dh > 0 && dw > 0)
+            for (int i = lane; i < (dh + 2) * (dw + 2); i += 64) mb[i] = 0;
+    }
+    __syncthreads();
+    const int mw = dw + 2;
+    const int npx = (dh > 0 && dw > 0) ? dh * dw : 0;
+    for (int p = lane; p < npx; p += 64) {
+        const int rr = p / dw, cc = p - rr * dw;
+        const int m = fast_arc_score(roi, cols, rr + 3, cc + 3);
+        mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
+    }
+    __syncthreads();
+    if (!active) return;
+    int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
+    if (npx == 0) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    // pass 1: any corner at iniThFAST in this cell?
+    int t = g->ini_th;
+    int found = 0;
+    for (int p0 = 0; p0 < npx && !found; p0 += 64) {
+        const int p = p0 + lane;
+        int s;
+        bool k = false;
+        if (p < npx) {
+            const int rr = p / dw, cc = p - rr * dw;
+            k = fast_nms_kp(mb, mw, rr, cc, t, s);
+        }
+        found = __ballot(k) != 0;
+    }
+    if (!found) t = g->min_th;
+    // pass 2: ordered compaction (raster order inside the cell, as cv::FAST emits)
+    uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
+    const LevelGeom& L = g->lv[c.level];
+    (void)L;
+    int base = 0;
+    for (int p0 = 0; p0 < npx; p0 += 64) {
+        const int p = p0 + lane;
+        int s = 0, rr = 0, cc = 0;
+        bool k = false;
+        if (p < npx) {
+            rr = p / dw; cc = p - rr * dw;
+            k = fast_nms_kp(mb, mw, rr, cc, t, s);
+        }
+        const uint64_t m = __ballot(k);
+        if (k) {
+            const int idx = base + lanes_below(m);
+            const int x = c.ini_x + cc + 3 - ORBX_MIN_BORDER;
+            const int y = c.ini_y + rr + 3 - ORBX_MIN_BORDER;
+            if (idx < c.cap) slot[idx] = pack_cand(x, y, s);
+        }
+        base += __popcll(m);
+    }
+    if (lane == 0) *cnt_out = min(base, c.cap);
+}
+
+// ----------------------------------------------------------------------------------------
+// DistributeOctTree — one workgroup per (image, level).
+//
+// The reference keeps a std::list of nodes, each owning a vector of keypoints.  Its output
+// depends only on (a) the rectangles of the final nodes, (b) their list order, and (c) in
+// each node the first max-response keypoint in candidate order.  This kernel keeps the
+// list as arrays (double-buffered per round) and gives every candidate the index of its
+// node; a round of splits is one pass over the candidates (quadrant + LDS atomic counts)
+// and one pass over the nodes (prefix sums place the children exactly where push_front
+// would put them: children of the last expanded node first, n4..n1).  Phase 2's
+// sort by (size, node) uses the push sequence number as the tie-break.
+// ----------------------------------------------------------------------------------------
+struct NodeArrays {
+    int16_t *x0, *y0, *x1, *y1;
+    int32_t *cnt, *seq;
+};
+
+struct OctreeSmem {
+    NodeArrays A, B;
+    int32_t* cc;      // [NCAP][4] child counts
+    int16_t* cpos;    // [NCAP][4] new position of each child
+    int16_t* npos;    // [NCAP] new position of a surviving node
+    int16_t* pord;    // [NCAP] processing order in a phase-2 round (-1: not processed)
+    int32_t* pre;     // [NCAP] scratch prefix (children before)
+    int32_t* pre2;    // [NCAP] scratch prefix (survivors before)
+    uint64_t* sortb;  // [NCAP_POW2]
+    int* tmp;         // [16] scan scratch + scalars
+};
+
+__device__ __forceinline__ void split_lines(int x0, int y0, int x1, int y1, int& sx, int& sy) {
+    const int halfX = (int)ceilf((float)(x1 - x0) / 2.0f);
+    const int halfY = (int)ceilf((float)(y1 - y0) / 2.0f);
+    sx = x0 + halfX;
+    sy = y0 + halfY;
+}
+
+__device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1, int sx, int sy,
+                                           int& cx0, int& cy0, int& cx1, int& cy1) {
+    cx0 = (q & 1) ? sx : x0;
+    cx1 = (q & 1) ? x1 : sx;
+    cy0 = (q & 2) ? sy : y0;
+    cy1 = (q & 2) ? y1 : sy;
+}
+
+// Chunked exclusive scan over n items (n may exceed 256).  f(i) gives the value; g(i, excl)
+// consumes the exclusive prefix.  Returns the total.  All threads must call.
+template <class F, class G>
+__device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
+    int carry = 0;
+    for (int c0 = 0; c0 < n; c0 += 256) {
+        const int i = c0 + threadIdx.x;
+        const int v = (i < n) ? f(i) : 0;
+        int tot;
+        const int ex = block_excl_scan(v, tmp, tot);
+        if (i < n) gcb(i, carry + ex);
+        carry += tot;
+    }
+    return carry;
+}
+
+template <bool KEYS_LDS>
+__device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
+                             int level, int ncand, uint32_t* kdata, int16_t* knode, uint8_t* kq,
+                             OctreeSmem& sm, int* __restrict__ ocnt, uint32_t* __restrict__ okp) {
+    const int tid = threadIdx.x;
+    const int N = L.nfeat;
+    int* tmp = sm.tmp;
+    const int nIni = L.n_ini;
+    const float hX = L.hx;
+    const int Hh = L.h - 2 * ORBX_MIN_BORDER;
+
+    // ---- roots (src/ORBextractor.cc:552-587) ----
+    for (int i = tid; i < nIni; i += 256) sm.cc[i * 4] = 0;
+    __syncthreads();
+    for (int k = tid; k < ncand; k += 256) {
+        const int x = cand_x(kdata[k]);
+        int r = (int)((float)x / hX);
+        r = min(r, nIni - 1);
+        knode[k] = (int16_t)r;
+        atomicAdd(&sm.cc[r * 4], 1);
+    }
+    __syncthreads();
+    int S = chunked_scan(
+        nIni, tmp, [&](int i) { return sm.cc[i * 4] > 0 ? 1 : 0; },
+        [&](int i, int ex) {
+            const int c = sm.cc[i * 4];
+            if (c > 0) {
+                sm.A.x0[ex] = (int16_t)(int)(hX * (float)i);
+                sm.A.x1[ex] = (int16_t)(int)(hX * (float)(i + 1));
+                sm.A.y0[ex] = 0;
+                sm.A.y1[ex] = (int16_t)Hh;
+                sm.A.cnt[ex] = c;
+                sm.A.seq[ex] = 0;
+            }
+            sm.npos[i] = (int16_t)ex;
+        });
+    __syncthreads();
+    for (int k = tid; k < ncand; k += 256) knode[k] = sm.npos[knode[k]];
+    __syncthreads();
+
+    int seq_base = 1;
+    bool phase2 = false;
+    NodeArrays cur = sm.A, nxt = sm.B;
+    for (int guard = 0; guard < 100000; ++guard) {
+        const int prevS = S;
+        // ---- split every multi-key node: quadrant of each of its keys ----
+        for (int i = tid; i < S; i += 256) {
+            sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
+            sm.cc[i * 4 + 2] = 0; sm.cc[i * 4 + 3] = 0;
+            sm.pord[i] = -1;
+        }
+        __syncthreads();
+        for (int k = tid; k < ncand; k += 256) {
+            const int n = knode[k];
+            if (cur.cnt[n] > 1) {
+                int sx, sy;
+                split_lines(cur.x0[n], cur.y0[n], cur.x1[n], cur.y1[n], sx, sy);
+                const uint32_t kd = kdata[k];
+                const int x = cand_x(kd), y = cand_y(kd);
+                const int q = (x < sx) ? (y < sy ? 0 : 2) : (y < sy ? 1 : 3);
+                kq[k] = (uint8_t)q;
+                atomicAdd(&sm.cc[n * 4 + q], 1);
+            }
+        }
+        __syncthreads();
+        auto nonempty = [&](int n) {
+            return (sm.cc[n * 4] > 0) + (sm.cc[n * 4 + 1] > 0) + (sm.cc[n * 4 + 2] > 0) +
+                   (sm.cc[n * 4 + 3] > 0);
+        };
+        auto multi = [&](int n) {
+            return (sm.cc[n * 4] > 1) + (sm.cc[n * 4 + 1] > 1) + (sm.cc[n * 4 + 2] > 1) +
+                   (sm.cc[n * 4 + 3] > 1);
+        };
+        int Ctot, Stot, nToExpand = 0;
+        if (!phase2) {
+            // ---- phase 1 (src/ORBextractor.cc:608-667): expand every multi-key node ----
+            for (int i = tid; i < S; i += 256) sm.pord[i] = cur.cnt[i] > 1 ? (int16_t)i : (int16_t)-1;
+            __syncthreads();
+            Ctot = chunked_scan(
+                S, tmp, [&](int i) { return sm.pord[i] >= 0 ? nonempty(i) : 0; },
+                [&](int i, int ex) { sm.pre[i] = ex; });
+            Stot = chunked_scan(
+                S, tmp, [&](int i) { return sm.pord[i] >= 0 ? 0 : 1; },
+                [&](int i, int ex) { sm.pre2[i] = ex; });
+            // nToExpand: children with more than one key
+            int e = 0;
+            for (int i = tid; i < S; i += 256) e += sm.pord[i] >= 0 ? multi(i) : 0;
+            nToExpand = block_sum(e, tmp);
+            for (int i = tid; i < S; i += 256) {
+                if (sm.pord[i] >= 0) {
+                    const int c = nonempty(i);
+                    const int start = Ctot - sm.pre[i] - c;
+                    int sx, sy;
+                    const int x0 = cur.x0[i], y0 = cur.y0[i], x1 = cur.x1[i], y1 = cur.y1[i];
+                    split_lines(x0, y0, x1, y1, sx, sy);
+                    int rank_asc = 0;
+                    for (int q = 0; q < 4; ++q) {
+                        const int cq = sm.cc[i * 4 + q];
+                        if (cq > 0) {
+                            const int pos = start + (c - 1 - rank_asc);   // n4..n1 from the front
+                            int cx0, cy0, cx1, cy1;
+                            child_rect(q, x0, y0, x1, y1, sx, sy, cx0, cy0, cx1, cy1);
+                            nxt.x0[pos] = (int16_t)cx0; nxt.y0[pos] = (int16_t)cy0;
+                            nxt.x1[pos] = (int16_t)cx1; nxt.y1[pos] = (int16_t)cy1;
+                            nxt.cnt[pos] = cq;
+                            nxt.seq[pos] = seq_base + sm.pre[i] + rank_asc;
+                            sm.cpos[i * 4 + q] = (int16_t)pos;
+                            ++rank_asc;
+                        }
+                    }
+                } else {
+                    const int pos = Ctot + sm.pre2[i];
+                    nxt.x0[pos] = cur.x0[i]; nxt.y0[pos] = cur.y0[i];
+                    nxt.x1[pos] = cur.x1[i]; nxt.y1[pos] = cur.y1[i];
+                    nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+                    sm.npos[i] = (int16_t)pos;
+                }
+            }
+        } else {
+            // ---- phase 2 (src/ORBextractor.cc:675-740): split largest (size, seq) first ----
+            const int nV = chunked_scan(
+                S, tmp, [&](int i) { return cur.cnt[i] > 1 ? 1 : 0; },
+                [&](int i, int ex) {
+                    if (cur.cnt[i] > 1)
+                        sm.sortb[ex] = ((uint64_t)cur.cnt[i] << 40) |
+                                       ((uint64_t)(uint32_t)cur.seq[i] << 16) | (uint64_t)i;
+                });
+            int P = 1;
+            while (P < nV) P <<= 1;
+            for (int i = nV + tid; i < P; i += 256) sm.sortb[i] = 0;
+            __syncthreads();
+            for (int k2 = 2; k2 <= P; k2 <<= 1) {
+                for (int j = k2 >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < P; i += 256) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const uint64_t a = sm.sortb[i], c = sm.sortb[ixj];
+                            const bool desc = (i & k2) == 0;
+                            if (desc ? (a < c) : (a > c)) { sm.sortb[i] = c; sm.sortb[ixj] = a; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // running size after processing j (descending order); stop once >= N
+            if (tid == 0) tmp[8] = nV - 1;
+            __syncthreads();
+            chunked_scan(
+                nV, tmp,
+                [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1; },
+                [&](int j, int ex) {
+                    const int delta = nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1;
+                    if (S + ex + delta >= N) atomicMin(&tmp[8], j);
+                });
+            __syncthreads();
+            const int J = tmp[8];
+            __syncthreads();
+            const int nP = J + 1;
+            // children-before prefix in processing order, over processed nodes only
+            Ctot = chunked_scan(
+                nP, tmp, [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)); },
+                [&](int j, int ex) {
+                    const int n = (int)(sm.sortb[j] & 0xFFFF);
+                    sm.pre[n] = ex;
+                    sm.pord[n] = (int16_t)j;
+                });
+            __syncthreads();
+            Stot = chunked_scan(
+                S, tmp, [&](int i) { return sm.pord[i] >= 0 ? 0 : 1; },
+                [&](int i, int ex) { sm.pre2[i] = ex; });
+            for (int i = tid; i < S; i += 256) {
+                if (sm.pord[i] >= 0) {
+                    const int c = nonempty(i);
+                    const int start = Ctot - sm.pre[i] - c;
+                    int sx, sy;
+                    const int x0 = cur.x0[i], y0 = cur.y0[i], x1 = cur.x1[i], y1 = cur.y1[i];
+                    split_lines(x0, y0, x1, y1, sx, sy);
+                    int rank_asc = 0;
+                    for (int q = 0; q < 4; ++q) {
+                        const int cq = sm.cc[i * 4 + q];
+                        if (cq > 0) {
+                            const int pos = start + (c - 1 - rank_asc);
+                            int cx0, cy0, cx1, cy1;
+                            child_rect(q, x0, y0, x1, y1, sx, sy, cx0, cy0, cx1, cy1);
+                            nxt.x0[pos] = (int16_t)cx0; nxt.y0[pos] = (int16_t)cy0;
+                            nxt.x1[pos] = (int16_t)cx1; nxt.y1[pos] = (int16_t)cy1;
+                            nxt.cnt[pos] = cq;
+                            nxt.seq[pos] = seq_base + sm.pre[i] + rank_asc;
+                            sm.cpos[i * 4 + q] = (int16_t)pos;
+                            ++rank_asc;
+                        }
+                    }
+                } else {
+                    const int pos = Ctot + sm.pre2[i];
+                    nxt.x0[pos] = cur.x0[i]; nxt.y0[pos] = cur.y0[i];
+                    nxt.x1[pos] = cur.x1[i]; nxt.y1[pos] = cur.y1[i];
+                    nxt.cnt[pos] = cur.cnt[i]; nxt.seq[pos] = cur.seq[i];
+                    sm.npos[i] = (int16_t)pos;
+                }
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < ncand; k += 256) {
+            const int n = knode[k];
+            knode[k] = sm.pord[n] >= 0 ? sm.cpos[n * 4 + kq[k]] : sm.npos[n];
+        }
+        __syncthreads();
+        NodeArrays t2 = cur; cur = nxt; nxt = t2;
+        S = Ctot + Stot;
+        seq_base += Ctot;
+        if (S >= N || S == prevS) break;
+        if (!phase2 && S + nToExpand * 3 > N) phase2 = true;
+    }
+
+    // ---- retain the best keypoint of each node (src/ORBextractor.cc:743-762) ----
+    uint32_t* best = (uint32_t*)sm.cc;
+    for (int i = tid; i < S; i += 256) best[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < ncand; k += 256)
+        atomicMax(&best[knode[k]], ((uint32_t)cand_s(kdata[k]) << 24) | (uint32_t)(0xFFFFFF - k));
+    __syncthreads();
+    uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
+    for (int i = tid; i < S; i += 256) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
+    if (tid == 0) ocnt[b * g->nlevels + level] = S;
+}
+
+__global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
+                                                const CellDesc* __restrict__ cells,
+                                                const int* __restrict__ ccnt,
+                                                const uint32_t* __restrict__ cand,
+                                                int* __restrict__ ocnt, uint32_t* __restrict__ okp,
+                                                uint8_t* __restrict__ kscratch,
+                                                long long kscratch_per_image, int NCAP, int KCAP) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int level = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom& L = g->lv[level];
+    // carve LDS
+    uint8_t* p = smem;
+    auto take = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
+    OctreeSmem sm;
+    int NP2 = 1;
+    while (NP2 < NCAP) NP2 <<= 1;
+    sm.tmp = (int*)take(16 * sizeof(int));
+    sm.sortb = (uint64_t*)take((size_t)NP2 * 8);
+    sm.A.x0 = (int16_t*)take(NCAP * 2); sm.A.y0 = (int16_t*)take(NCAP * 2);
+    sm.A.x1 = (int16_t*)take(NCAP * 2); sm.A.y1 = (int16_t*)take(NCAP * 2);
+    sm.A.cnt = (int32_t*)take(NCAP * 4); sm.A.seq = (int32_t*)take(NCAP * 4);
+    sm.B.x0 = (int16_t*)take(NCAP * 2); sm.B.y0 = (int16_t*)take(NCAP * 2);
+    sm.B.x1 = (int16_t*)take(NCAP * 2); sm.B.y1 = (int16_t*)take(NCAP * 2);
+    sm.B.cnt = (int32_t*)take(NCAP * 4); sm.B.seq = (int32_t*)take(NCAP * 4);
+    sm.cc = (int32_t*)take((size_t)NCAP * 16);
+    sm.cpos = (int16_t*)take((size_t)NCAP * 8);
+    sm.npos = (int16_t*)take(NCAP * 2);
+    sm.pord = (int16_t*)take(NCAP * 2);
+    sm.pre = (int32_t*)take(NCAP * 4);
+    sm.pre2 = (int32_t*)take(NCAP * 4);
+    uint32_t* l_kdata = (uint32_t*)take((size_t)KCAP * 4);
+    int16_t* l_knode = (int16_t*)take((size_t)KCAP * 2);
+    uint8_t* l_kq = (uint8_t*)take((size_t)KCAP);
+
+    // count the level's candidates
+    const int* cc = ccnt + (size_t)b * g->n_cells + L.cell_begin;
+    int part = 0;
+    for (int c = tid; c < L.ncells; c += 256) part += cc[c];
+    const int ncand = block_sum(part, sm.tmp);
+    if (ncand == 0 || L.n_ini < 1 || L.nfeat <= 0) {
+        if (tid == 0) ocnt[b * g->nlevels + level] = 0;
+        return;
+    }
+    const bool in_lds = ncand <= KCAP;
+    uint8_t* gs = kscratch + (size_t)b * kscratch_per_image;
+    // global fallback region of this level: [kdata u32][knode i16][kq u8]
+    long long lvl_off = 0;
+    for (int l = 0; l < level; ++l) lvl_off += (long long)g->lv[l].cand_cap * 8;
+    uint32_t* kdata = in_lds ? l_kdata : (uint32_t*)(gs + lvl_off);
+    int16_t* knode = in_lds ? l_knode : (int16_t*)(gs + lvl_off + (long long)L.cand_cap * 4);
+    uint8_t* kq = in_lds ? l_kq : (gs + lvl_off + (long long)L.cand_cap * 6);
+    // gather candidates in cell order (cell-major, raster inside a cell)
+    const uint32_t* cbase = cand + (size_t)b * g->cand_words;
+    const CellDesc* lc = cells + L.cell_begin;
+    chunked_scan(
+        L.ncells, sm.tmp, [&](int c) { return cc[c]; },
+        [&](int c, int ex) {
+            const int n = cc[c];
+            const uint32_t* s = cbase + lc[c].slot;
+            for (int e = 0; e < n; ++e) kdata[ex + e] = s[e];
+        });
+    __syncthreads();
+    if (in_lds)
+        octree_level<true>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+    else
+        octree_level<false>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+}
+
+// ----------------------------------------------------------------------------------------
+// Orientation + rBRIEF + assembly: one wave per keypoint.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict__ g,
+                                                     const uint8_t* __restrict__ pyr,
+                                                     const uint8_t* __restrict__ blur,
+                                                     const int* __restrict__ ocnt,
+                                                     const uint32_t* __restrict__ okp,
+                                                     float* __restrict__ kps,
+                                                     uint8_t* __restrict__ desc,
+                                                     int* __restrict__ nkp) {
+    const int b = blockIdx.y, blk = blockIdx.x;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int level = 0;
+    while (level + 1 < g->nlevels && blk >= g->orient_block_begin[level + 1]) ++level;
+    const int i = (blk - g->orient_block_begin[level]) * 4 + wid;
+    const int* oc = ocnt + b * g->nlevels;
+    if (level == 0 && i == 0 && lane == 0) {
+        int tot = 0;
+        for (int l = 0; l < g->nlevels; ++l) tot += oc[l];
+        nkp[b] = tot;
+    }
+    const int n = oc[level];
+    if (i >= n) return;
+    int off = 0;
+    for (int l = 0; l < level; ++l) off += oc[l];
+    const LevelGeom& L = g->lv[level];
+    const uint32_t c = okp[(size_t)b * g->out_words + L.out_off + i];
+    const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
+    const int pitch = L.pitch;
+
+    // IC_Angle (src/ORBextractor.cc:77-104) on the unblurred level; exact integer moments.
+    const uint8_t* center = pyr + b * g->pyr_bytes + L.off + (size_t)y * pitch + x;
+    int m10 = 0, m01 = 0;
+    {
+        const int half = lane >> 5, l31 = lane & 31;
+        if (l31 < 31) {
+            const int u = l31 - 15;
+            const int au = u < 0 ? -u : u;
+            if (!half) m10 += u * center[u];
+            const int vb = half ? 8 : 1, ve = half ? 16 : 8;
+            for (int v = vb; v < ve; ++v) {
+                if (au <= g->umax[v]) {
+                    const int vp = center[u + v * pitch], vm = center[u - v * pitch];
+                    m10 += u * (vp + vm);
+                    m01 += v * (vp - vm);
+                }
+            }
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = cv_fast_atan2((float)m01, (float)m10);
+
+    // computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level.
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
+    const uint8_t* bc = blur + b * g->pyr_bytes + L.off + (size_t)y * pitch + x;
+    uint64_t words[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int k = w * 64 + lane;
+        const float x1 = (float)c_pattern[4 * k], y1 = (float)c_pattern[4 * k + 1];
+        const float x2 = (float)c_pattern[4 * k + 2], y2 = (float)c_pattern[4 * k + 3];
+        const float r1a = x1 * sb, r1b = y1 * ca, c1a = x1 * ca, c1b = y1 * sb;
+        const float r2a = x2 * sb, r2b = y2 * ca, c2a = x2 * ca, c2b = y2 * sb;
+        const int t0 = bc[cv_round(r1a + r1b) * pitch + cv_round(c1a - c1b)];
+        const int t1 = bc[cv_round(r2a + r2b) * pitch + cv_round(c2a - c2b)];
+        words[w] = __ballot(t0 < t1);
+    }
+    const size_t o = (size_t)b * g->kp_cap + off + i;
+    if (lane == 0) {
+        float* kp = kps + o * 7;
+        const float sc = L.scale;
+        kp[0] = level ? (float)x * sc : (float)x;
+        kp[1] = level ? (float)y * sc : (float)y;
+        kp[2] = (float)L.patch_size;
+        kp[3] = angle;
+        kp[4] = (float)s;
+        ((int*)kp)[5] = level;
+        ((int*)kp)[6] = -1;
+    }
+    if (lane < 4) {
+        uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        *(uint64_t*)(desc + o * 32 + lane * 8) = wv;
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// launch sequence
+// ----------------------------------------------------------------------------------------
+hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
+    const Geometry& G = *a.hg;
+    {
+        dim3 grid((G.lv[0].w + 1023) / 1024, G.lv[0].h, a.batch);
+        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, st, a.dg, a.d_imgs, a.stride,
+                           a.batch_stride, a.pyr);
+    }
+    for (int l = 1; l < G.nlevels; ++l) {
+        dim3 grid((G.lv[l].w + 1023) / 1024, G.lv[l].h, a.batch);
+        hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, a.dg, a.rtab, a.pyr, l);
+    }
+    hipLaunchKernelGGL(k_blur, dim3(G.blur_tiles, a.batch), dim3(256), 0, st, a.dg, a.pyr, a.blur);
+    {
+        const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
+        const size_t lds = (size_t)4 * (roi_cap + mb_cap);
+        hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 3) / 4, a.batch), dim3(256), lds, st, a.dg,
+                           a.cells, a.pyr, a.ccnt, a.cand);
+    }
+    hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
+                       a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
+                       a.ncap, a.kcap);
+    hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,
+                       a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp);
+    return hipGetLastError();
+}
+
+size_t octree_lds_bytes(int ncap, int kcap) {
+    auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    int np2 = 1;
+    while (np2 < ncap) np2 <<= 1;
+    size_t s = r(16 * 4) + r((size_t)np2 * 8);
+    s += 2 * (4 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4));
+    s += r((size_t)ncap * 16) + r((size_t)ncap * 8) + 2 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4);
+    s += r((size_t)kcap * 4) + r((size_t)kcap * 2) + r((size_t)kcap);
+    return s;
+}
+
+}  // namespace orbx
+
+namespace orbx {
+hipError_t prepare_stereo(size_t lds);
+// Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).
+hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_octree,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
+    if (e != hipSuccess) return e;
+    return prepare_stereo(stereo_lds);
+}
+}  // namespace orbx

@@ -1,0 +1,81 @@
+// orbx_internal.h — host/device shared layout of the MI355X ORB front-end.
+//
+// HBM layout (one extractor handle, batch of B same-sized images):
+//   pyr   [B][Σ_l pitch_l*h_l] u8    image pyramid (mvImagePyramid), level 0 = input copy
+//   blur  [B][Σ_l pitch_l*h_l] u8    7x7 Gaussian of every level (descriptor sampling)
+//   ccnt  [B][n_cells]         i32   FAST candidates per cell
+//   cand  [B][Σ cells cap_c]   u32   packed candidates (x:12 | y:12 | score:8), raster order
+//   ocnt  [B][L]               i32   keypoints per level after the octree
+//   okp   [B][Σ_l out_cap_l]   u32   packed octree survivors in list order
+//   kps   [B][kp_cap]          orbx_keypoint (cv::KeyPoint layout), level-major
+//   desc  [B][kp_cap][32]      u8
+//   nkp   [B]                  i32
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#define ORBX_MAX_LEVELS 16
+#define ORBX_EDGE 19
+#define ORBX_MIN_BORDER 16   // EDGE_THRESHOLD - 3, src/ORBextractor.cc:785
+
+namespace orbx {
+
+struct LevelGeom {
+    int w, h, pitch;
+    long long off;          // byte offset of the level inside one image's pyramid block
+    float scale, inv_scale;
+    int nfeat;              // mnFeaturesPerLevel
+    int ncols, nrows, wcell, hcell;
+    int cell_begin, ncells; // range in the cell table
+    long long cand_off;     // u32 offset of the level's first cell slot in one image's block
+    int cand_cap;           // Σ cell caps of the level
+    int n_ini;              // DistributeOctTree root count (0: level yields nothing)
+    float hx;               // root width (float, as the reference)
+    int out_off, out_cap;   // octree output slots
+    int kp_level_cap;       // == out_cap
+    int rtab_off;           // resize tables (level>0): offset into the i16 table buffer
+    int xmax;               // resize: first dx whose right tap is out of range
+    int rsimd_end;          // resize: SSE2 vertical loop end (0 in scalar mode)
+    int bsimd_end;          // blur: SSE2 column loop end (0 in scalar mode)
+    int area2;              // resize at exactly 1/2: INTER_AREA 2x2 fast path
+    int copy;               // resize to the same size: plain copy
+    int patch_size;         // (int)(31*scale)
+};
+
+struct CellDesc {
+    int16_t level, ini_x, ini_y, cols, rows, pad;
+    int32_t slot;           // u32 offset of this cell's candidate slot (per image block)
+    int32_t cap;            // slot capacity
+};
+
+struct Geometry {
+    int width, height, nlevels;
+    int n_cells;            // cells over all levels
+    int kp_cap;             // Σ_l out_cap
+    long long pyr_bytes;    // per image
+    long long cand_words;   // per image
+    int out_words;          // per image (Σ out_cap)
+    int max_ncand_level;    // max cand_cap over levels
+    int max_out_cap;
+    int max_roi_bytes;      // largest FAST cell ROI (rows*cols)
+    int max_mbuf_bytes;     // largest FAST score buffer ((dh+2)*(dw+2))
+    int blur_tiles;         // Σ_l ceil(w/64)*ceil(h/16)
+    int orient_blocks;      // Σ_l ceil(out_cap/4)
+    int blur_tile_begin[ORBX_MAX_LEVELS + 1];
+    int orient_block_begin[ORBX_MAX_LEVELS + 1];
+    int taps[7];            // cvRound(getGaussianKernel(7, 2, CV_32F) * 256)
+    int umax[16];           // src/ORBextractor.cc:454-469
+    int ini_th, min_th;     // FAST thresholds, clamped to [0, 255]
+    int stereo_win;         // row-bucket search half-window: ceil(2*max scale) + 2
+    LevelGeom lv[ORBX_MAX_LEVELS];
+};
+
+// Packed candidate / octree survivor: x, y relative to (minBorderX, minBorderY).
+__host__ __device__ inline uint32_t pack_cand(int x, int y, int score) {
+    return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)score << 24);
+}
+__host__ __device__ inline int cand_x(uint32_t c) { return (int)(c & 0xFFF); }
+__host__ __device__ inline int cand_y(uint32_t c) { return (int)((c >> 12) & 0xFFF); }
+__host__ __device__ inline int cand_s(uint32_t c) { return (int)(c >> 24); }
+
+}  // namespace orbx

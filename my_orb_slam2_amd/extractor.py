@@ -1,0 +1,187 @@
+"""ORBextractor / stereo front-end over liborbx.so.
+
+Mirrors the reference's operator interface:
+  ORB_SLAM2::ORBextractor (include/ORBextractor.h:45-111, src/ORBextractor.cc:410-1154)
+  Frame::ComputeStereoMatches (src/Frame.cc:496-686)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import BatchView, ExtractorParams, KEYPOINT_DTYPE, check, load, ptr
+
+
+class ORBextractor:
+    """ORB_SLAM2::ORBextractor on the GPU.
+
+    ``extractor(image, mask)`` returns ``(keypoints, descriptors)`` like the reference's
+    ``operator()(image, mask, keypoints, descriptors)``: keypoints as a structured array with
+    cv::KeyPoint fields, descriptors as an (N, 32) uint8 array (None when N == 0, as the
+    reference releases the Mat).  An empty image returns ``(None, None)`` (the reference
+    returns without touching its outputs).  The mask is ignored, as in the reference.
+    """
+
+    def __init__(self, nfeatures: int = 1000, scaleFactor: float = 1.2, nlevels: int = 8,
+                 iniThFAST: int = 20, minThFAST: int = 7, *, cv_simd: int = 1,
+                 max_batch: int = 1, device: int = 0):
+        self._L = load()
+        self.params = ExtractorParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                      cv_simd, max_batch, device)
+        h = ctypes.c_void_p()
+        check("orbx_extractor_create",
+              self._L.orbx_extractor_create(ctypes.byref(self.params), ctypes.byref(h)))
+        self._h = h
+        self.nlevels = nlevels
+        n = nlevels
+        self._tab = [np.zeros(n, np.float32) for _ in range(4)] + [np.zeros(n, np.int32)]
+        check("orbx_extractor_tables", self._L.orbx_extractor_tables(self._h, *map(ptr, self._tab)))
+        self._last_size = None
+        self._nkp = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.orbx_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- getters of include/ORBextractor.h:63-83 ----
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return float(self.params.scale_factor)
+
+    def GetScaleFactors(self):
+        return self._tab[0].copy()
+
+    def GetInverseScaleFactors(self):
+        return self._tab[1].copy()
+
+    def GetScaleSigmaSquares(self):
+        return self._tab[2].copy()
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._tab[3].copy()
+
+    @property
+    def features_per_level(self):
+        return self._tab[4].copy()
+
+    # ---- operator() ----
+    def __call__(self, image: np.ndarray, mask=None):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        if img.size == 0:
+            return None, None
+        if img.ndim != 2:
+            raise ValueError("ORBextractor expects a single-channel 8-bit image (CV_8UC1)")
+        h, w = img.shape
+        n = ctypes.c_int(0)
+        cap = 1
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        code = self._L.orbx_extract(self._h, ptr(img), w, h, w, ptr(kps), cap, ptr(desc),
+                                    ctypes.byref(n))
+        if code == -3 or n.value > cap:   # capacity: fetch with the exact size
+            cap = n.value
+            kps = np.zeros(cap, KEYPOINT_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            code = self._L.orbx_extract(self._h, ptr(img), w, h, w, ptr(kps), cap, ptr(desc),
+                                        ctypes.byref(n))
+        check("orbx_extract", code)
+        self._last_size = (w, h)
+        self._nkp = n.value
+        kps = kps[: n.value]
+        return kps, (desc[: n.value] if n.value > 0 else None)
+
+    @property
+    def mvImagePyramid(self):
+        """Pyramid of the last call (include/ORBextractor.h:85), copied to host."""
+        return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+    def pyramid_level(self, level: int, index: int = 0) -> np.ndarray:
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check("orbx_pyramid_level", self._L.orbx_pyramid_level(
+            self._h, index, level, None, ctypes.byref(w), ctypes.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        check("orbx_pyramid_level", self._L.orbx_pyramid_level(
+            self._h, index, level, ptr(out), ctypes.byref(w), ctypes.byref(h)))
+        return out
+
+    # ---- batched device path ----
+    def extract_batch_device(self, images, stream=None):
+        """Extract a [B, H, W] uint8 CUDA/HIP tensor already resident in HBM."""
+        B, H, W = images.shape
+        stride = images.stride(1) * images.element_size()
+        bstride = images.stride(0) * images.element_size()
+        check("orbx_extract_batch_device", self._L.orbx_extract_batch_device(
+            self._h, ptr(images), B, W, H, stride, bstride, ptr(stream)))
+
+    def batch_view(self) -> BatchView:
+        v = BatchView()
+        check("orbx_batch_view_get", self._L.orbx_batch_view_get(self._h, ctypes.byref(v)))
+        return v
+
+
+def compute_stereo_matches(left: ORBextractor, right: ORBextractor, mbf: float, mb: float):
+    """Frame::ComputeStereoMatches over the last extraction of `left` and `right`.
+
+    Returns (mvuRight, mvDepth, n_valid); -1 marks a left keypoint without a match.  `mb` is
+    the term the reference reads at src/Frame.cc:534 (normally mbf / fx).
+    """
+    n = left._nkp
+    u = np.zeros(max(n, 1), np.float32)
+    d = np.zeros(max(n, 1), np.float32)
+    nv = ctypes.c_int(0)
+    check("orbx_stereo_match", left._L.orbx_stereo_match(
+        left._h, right._h, mbf, mb, ptr(u), ptr(d), n, ctypes.byref(nv)))
+    return u[:n], d[:n], nv.value
+
+
+class StereoBatch:
+    """Batched stereo front-end: B rectified pairs per call, all on one HIP stream.
+
+    Runs ORBextractor on the B left and the B right images (two handles, as the reference's
+    Frame holds two extractors, src/Frame.cc:89-92) and ComputeStereoMatches per pair.
+    Outputs stay in HBM (torch tensors / the handles' workspaces).
+    """
+
+    def __init__(self, batch: int, nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20,
+                 minThFAST=7, cv_simd=1, device=0):
+        import torch
+        self.batch = batch
+        self.left = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                 cv_simd=cv_simd, max_batch=batch, device=device)
+        self.right = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                  cv_simd=cv_simd, max_batch=batch, device=device)
+        self.device = torch.device("cuda", device)
+        self.uR = self.depth = self.nvalid = None
+
+    def __call__(self, left_imgs, right_imgs, mbf: float, mb: float, stream=None):
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        self.left.extract_batch_device(left_imgs, st)
+        self.right.extract_batch_device(right_imgs, st)
+        kc = self.left.batch_view().kp_cap
+        B = left_imgs.shape[0]
+        if self.uR is None or self.uR.shape != (B, kc):
+            self.uR = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+            self.depth = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+            self.nvalid = torch.empty((B,), dtype=torch.int32, device=self.device)
+        check("orbx_stereo_match_batch_device", self.left._L.orbx_stereo_match_batch_device(
+            self.left._h, self.right._h, mbf, mb, ptr(self.uR), ptr(self.depth),
+            ptr(self.nvalid), ctypes.c_void_p(st)))
+        return self.uR, self.depth, self.nvalid
+
+    def outputs(self, side: str = "left"):
+        """(keypoints [B,kp_cap] structured-view tensor bytes, desc, nkp) device tensors."""
+        import torch
+        ext = self.left if side == "left" else self.right
+        v = ext.batch_view()
+        return v

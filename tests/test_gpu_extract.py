@@ -1,0 +1,124 @@
+"""GPU parity: ORBextractor / ComputeStereoMatches on the HIP path vs the CPU restatement.
+
+Bit-exact bar: keypoints (every cv::KeyPoint field, bitwise), descriptors, pyramid bytes,
+stereo uRight/depth (bitwise float) and the valid-match count.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_bytes_equal, assert_f32_bits_equal, assert_kps_equal
+from my_orb_slam2_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+KITTI_MBF, KITTI_FX = 386.1448, 718.856
+
+
+def _pair(oracle_mod, nf, sf, nl, ini, mn, simd=1):
+    import my_orb_slam2_amd as m
+    return (m.ORBextractor(nf, sf, nl, ini, mn, cv_simd=simd),
+            oracle_mod.OracleExtractor(nf, sf, nl, ini, mn, simd=simd))
+
+
+def _check_extract(gpu_ext, ora_ext, img, what):
+    k_g, d_g = gpu_ext(img)
+    k_o, d_o = ora_ext(img)
+    for l in range(ora_ext.nlevels):
+        assert_bytes_equal(gpu_ext.pyramid_level(l), ora_ext.level(l), f"{what} pyramid L{l}")
+    assert_kps_equal(k_g, k_o, what)
+    assert_bytes_equal(d_g, d_o, what + " descriptors")
+    return k_g, d_g
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_kitti_extract_parity(oracle_mod, orbx_lib, gpu, seed):
+    g, o = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
+    img = synth.frame(seed, 1241, 376)
+    k, _ = _check_extract(g, o, img, f"kitti seed {seed}")
+    assert 1500 < len(k) <= 2000 + 3 * 8
+
+
+@pytest.mark.parametrize("size,nf", [((640, 480), 1000), ((752, 480), 1000)])
+def test_tum_euroc_extract_parity(oracle_mod, orbx_lib, gpu, size, nf):
+    g, o = _pair(oracle_mod, nf, 1.2, 8, 20, 7)
+    _check_extract(g, o, synth.frame(11, *size), f"{size}")
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_opencv_rounding_modes(oracle_mod, orbx_lib, gpu, simd):
+    g, o = _pair(oracle_mod, 1000, 1.2, 8, 20, 7, simd=simd)
+    _check_extract(g, o, synth.frame(5, 640, 480), f"simd={simd}")
+
+
+@pytest.mark.parametrize("params", [(500, 1.2, 8, 20, 7), (3000, 1.2, 8, 20, 7),
+                                    (1000, 1.3, 6, 25, 10), (1500, 1.1, 12, 20, 7),
+                                    (1000, 2.0, 3, 20, 7)])
+def test_param_sweep(oracle_mod, orbx_lib, gpu, params):
+    g, o = _pair(oracle_mod, *params)
+    _check_extract(g, o, synth.frame(21, 800, 600), f"params {params}")
+
+
+@pytest.mark.parametrize("name", ["zeros", "white", "checker8", "tiny64"])
+def test_edge_images(oracle_mod, orbx_lib, gpu, name):
+    g, o = _pair(oracle_mod, 1000, 1.2, 8, 20, 7)
+    img = synth.edge_cases()[name]
+    _check_extract(g, o, img, name)
+
+
+def test_empty_image(orbx_lib, gpu):
+    import my_orb_slam2_amd as m
+    g = m.ORBextractor(1000, 1.2, 8, 20, 7)
+    assert g(np.zeros((0, 0), np.uint8)) == (None, None)
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_kitti_stereo_parity(oracle_mod, orbx_lib, gpu, seed):
+    import my_orb_slam2_amd as m
+    L, R = synth.stereo_pair(seed)
+    gl, ol = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
+    gr, orr = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
+    kl, _ = _check_extract(gl, ol, L, "left")
+    _check_extract(gr, orr, R, "right")
+    mb = np.float32(KITTI_MBF) / np.float32(KITTI_FX)
+    u_g, d_g, n_g = m.compute_stereo_matches(gl, gr, KITTI_MBF, float(mb))
+    u_o, d_o, n_o = oracle_mod.stereo_match(ol, orr, len(kl), KITTI_MBF, float(mb))
+    assert_f32_bits_equal(u_g, u_o, "uRight")
+    assert_f32_bits_equal(d_g, d_o, "depth")
+    assert n_g == n_o
+    assert n_g > 100
+
+
+def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
+    import torch
+    import my_orb_slam2_amd as m
+    B = 4
+    pairs = [synth.stereo_pair(100 + i) for i in range(B)]
+    Ls = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    sb = m.StereoBatch(B, 2000)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    uR, dep, nv = sb(Ls, Rs, KITTI_MBF, mb)
+    torch.cuda.synchronize()
+    view = sb.left.batch_view()
+    kc = view.kp_cap
+    import ctypes
+    nkp = np.zeros(B, np.int32)
+    kps = np.zeros(B * kc, m.KEYPOINT_DTYPE)
+    desc = np.zeros((B * kc, 32), np.uint8)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy(ctypes.c_void_p(nkp.ctypes.data), ctypes.c_void_p(view.nkp), B * 4, 2)
+    hip.hipMemcpy(ctypes.c_void_p(kps.ctypes.data), ctypes.c_void_p(view.kps), B * kc * 28, 2)
+    hip.hipMemcpy(ctypes.c_void_p(desc.ctypes.data), ctypes.c_void_p(view.desc), B * kc * 32, 2)
+    uRh, deph, nvh = uR.cpu().numpy(), dep.cpu().numpy(), nv.cpu().numpy()
+    for i in range(B):
+        ol = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
+        orr = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
+        k_o, d_o = ol(pairs[i][0])
+        orr(pairs[i][1])
+        n = nkp[i]
+        assert_kps_equal(kps[i * kc: i * kc + n], k_o, f"batch item {i}")
+        assert_bytes_equal(desc[i * kc: i * kc + n], d_o, f"batch item {i} desc")
+        u_o, d_oo, n_o = oracle_mod.stereo_match(ol, orr, len(k_o), KITTI_MBF, mb)
+        assert_f32_bits_equal(uRh[i, :n], u_o, f"batch item {i} uRight")
+        assert_f32_bits_equal(deph[i, :n], d_oo, f"batch item {i} depth")
+        assert nvh[i] == n_o
