@@ -100,6 +100,11 @@ typedef struct {
 
 orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* view);
 
+/* Copy outputs of images [first, first+count) of the last batched call to host (waits for
+ * the device): nkp[count], kps[count][kp_cap], desc[count][kp_cap][32]; any may be NULL. */
+orbx_status orbx_batch_fetch(orbx_extractor* h, int first, int count, int32_t* nkp,
+                             orbx_keypoint* kps, uint8_t* desc);
+
 /* Replaces Frame::ComputeStereoMatches (src/Frame.cc:496-686) for the last orbx_extract
  * calls on `left` and `right` (same image size, same params).  mb is the baseline term the
  * reference reads at Frame.cc:534 (normally mbf/fx).  uRight/depth: n_left floats
@@ -118,6 +123,18 @@ orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor*
 
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1715-1731) on host memory. */
 int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ---- per-kernel timing (HIP events around each launch, on the launch stream) ------------ */
+typedef enum {
+    ORBX_K_COPY_LEVEL0 = 0, ORBX_K_RESIZE, ORBX_K_BLUR, ORBX_K_FAST, ORBX_K_OCTREE,
+    ORBX_K_ORIENT_DESC, ORBX_K_STEREO, ORBX_K_COUNT
+} orbx_kernel_id;
+orbx_status orbx_profile_enable(orbx_extractor* h, int on);
+/* Waits for the recorded launches, returns per-kernel total ms and launch counts since the
+ * last collect (arrays of ORBX_K_COUNT), and resets them.  Stereo launches are attributed
+ * to the left handle. */
+orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* launches);
+const char* orbx_kernel_name(int id);
 
 /* Library / device information. */
 const char* orbx_version(void);

@@ -17,6 +17,9 @@ LIB_PATH = PKG / "liborbx.so"
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
+KERNELS = ["k_copy_level0", "k_resize", "k_blur", "k_fast", "k_octree", "k_orient_desc",
+           "k_stereo"]
+
 STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
           -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_STATE"}
 
@@ -52,12 +55,16 @@ SIGNATURES = {
     "orbx_pyramid_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orbx_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp]),
     "orbx_batch_view_get": (_i, [_vp, ctypes.POINTER(BatchView)]),
+    "orbx_batch_fetch": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "orbx_stereo_match": (_i, [_vp, _vp, _f, _f, _vp, _vp, _i, ctypes.POINTER(_i)]),
     "orbx_stereo_match_batch_device": (_i, [_vp, _vp, _f, _f, _vp, _vp, _vp, _vp]),
     "orbx_descriptor_distance": (_i, [_vp, _vp]),
     "orbx_version": (ctypes.c_char_p, []),
     "orbx_last_error": (ctypes.c_char_p, []),
     "orbx_device_count": (_i, [ctypes.POINTER(_i)]),
+    "orbx_profile_enable": (_i, [_vp, _i]),
+    "orbx_profile_collect": (_i, [_vp, _vp, _vp]),
+    "orbx_kernel_name": (ctypes.c_char_p, [_i]),
 }
 
 _lib = None

@@ -76,6 +76,7 @@ struct orbx_extractor {
     DevBuf d_geom, d_cells, d_rtab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
     long long kscratch_per_image = 0;
+    KernelTimer timer;
     // last extraction
     int last_batch = 0;
     bool last_valid = false;
@@ -396,6 +397,7 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, int batch, siz
     a.kps = h->d_kps.as<float>();
     a.desc = h->d_desc.as<uint8_t>();
     a.nkp = h->d_nkp.as<int>();
+    a.timer = &h->timer;
     if (!HIPOK(launch_extract(a, st))) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
     h->last_valid = true;
@@ -429,6 +431,7 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, float mbf, float mb
     a.depth = d_dep;
     a.nvalid = d_nv;
     a.lds = L->stereo_lds;
+    a.timer = &L->timer;
     return HIPOK(launch_stereo(a, st)) ? ORBX_OK : ORBX_ERR_DEVICE;
 }
 
@@ -439,6 +442,30 @@ extern "C" {
 const char* orbx_version(void) { return ORBX_VERSION; }
 
 const char* orbx_last_error(void) { return g_err; }
+
+const char* orbx_kernel_name(int id) {
+    static const char* names[K_COUNT] = {"k_copy_level0", "k_resize", "k_blur", "k_fast",
+                                         "k_octree", "k_orient_desc", "k_stereo"};
+    return (id >= 0 && id < K_COUNT) ? names[id] : "";
+}
+
+orbx_status orbx_profile_enable(orbx_extractor* h, int on) {
+    if (!h) return ORBX_ERR_INVALID;
+    h->timer.on = on != 0;
+    return ORBX_OK;
+}
+
+orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* launches) {
+    if (!h) return ORBX_ERR_INVALID;
+    h->timer.collect();
+    for (int k = 0; k < K_COUNT; ++k) {
+        if (total_ms) total_ms[k] = h->timer.ms[k];
+        if (launches) launches[k] = h->timer.n[k];
+        h->timer.ms[k] = 0;
+        h->timer.n[k] = 0;
+    }
+    return ORBX_OK;
+}
 
 orbx_status orbx_device_count(int* n) {
     if (!n) return ORBX_ERR_INVALID;
@@ -486,6 +513,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv};
     for (DevBuf* b : bufs) b->release();
+    h->timer.destroy();
     if (h->done) (void)hipEventDestroy(h->done);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -584,6 +612,26 @@ orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {
         v->level_pitch[l] = h->hg.lv[l].pitch;
         v->level_off[l] = (size_t)h->hg.lv[l].off;
     }
+    return ORBX_OK;
+}
+
+orbx_status orbx_batch_fetch(orbx_extractor* h, int first, int count, int32_t* nkp,
+                             orbx_keypoint* kps, uint8_t* desc) {
+    if (!h || !h->last_valid || first < 0 || count < 0 || first + count > h->last_batch)
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    (void)hipSetDevice(h->device);
+    if (!HIPOK(hipDeviceSynchronize())) return ORBX_ERR_DEVICE;
+    const size_t KC = (size_t)h->hg.kp_cap;
+    if (nkp && !HIPOK(hipMemcpy(nkp, h->d_nkp.as<int32_t>() + first, (size_t)count * 4,
+                                hipMemcpyDeviceToHost)))
+        return ORBX_ERR_DEVICE;
+    if (kps && !HIPOK(hipMemcpy(kps, h->d_kps.as<orbx_keypoint>() + first * KC,
+                                (size_t)count * KC * sizeof(orbx_keypoint), hipMemcpyDeviceToHost)))
+        return ORBX_ERR_DEVICE;
+    if (desc && !HIPOK(hipMemcpy(desc, h->d_desc.as<uint8_t>() + first * KC * 32,
+                                 (size_t)count * KC * 32, hipMemcpyDeviceToHost)))
+        return ORBX_ERR_DEVICE;
     return ORBX_OK;
 }
 

@@ -786,27 +786,42 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
 // ----------------------------------------------------------------------------------------
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const Geometry& G = *a.hg;
+    KernelTimer dummy;
+    KernelTimer& T = a.timer ? *a.timer : dummy;
+    hipEvent_t e;
     {
         dim3 grid((G.lv[0].w + 1023) / 1024, G.lv[0].h, a.batch);
+        e = T.start(st);
         hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, st, a.dg, a.d_imgs, a.stride,
                            a.batch_stride, a.pyr);
+        T.stop(K_COPY0, e, st);
     }
     for (int l = 1; l < G.nlevels; ++l) {
         dim3 grid((G.lv[l].w + 1023) / 1024, G.lv[l].h, a.batch);
+        e = T.start(st);
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, a.dg, a.rtab, a.pyr, l);
+        T.stop(K_RESIZE, e, st);
     }
+    e = T.start(st);
     hipLaunchKernelGGL(k_blur, dim3(G.blur_tiles, a.batch), dim3(256), 0, st, a.dg, a.pyr, a.blur);
+    T.stop(K_BLUR, e, st);
     {
         const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
         const size_t lds = (size_t)4 * (roi_cap + mb_cap);
+        e = T.start(st);
         hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 3) / 4, a.batch), dim3(256), lds, st, a.dg,
                            a.cells, a.pyr, a.ccnt, a.cand);
+        T.stop(K_FAST, e, st);
     }
+    e = T.start(st);
     hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
                        a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
                        a.ncap, a.kcap);
+    T.stop(K_OCTREE, e, st);
+    e = T.start(st);
     hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,
                        a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp);
+    T.stop(K_ORIENT, e, st);
     return hipGetLastError();
 }
 

@@ -6,7 +6,60 @@
 
 #include "orbx_internal.h"
 
+#include <vector>
+
 namespace orbx {
+
+enum KernelId { K_COPY0 = 0, K_RESIZE, K_BLUR, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_COUNT };
+
+// Optional per-kernel HIP-event timing (orbx_profile_*): events bracket each launch on the
+// stream it is launched on; durations are read back by collect().
+struct KernelTimer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    struct Rec { int id; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    double ms[K_COUNT] = {0};
+    long long n[K_COUNT] = {0};
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    hipEvent_t start(hipStream_t st) {
+        if (!on) return nullptr;
+        hipEvent_t e = get();
+        if (e) (void)hipEventRecord(e, st);
+        return e;
+    }
+    void stop(int id, hipEvent_t a, hipStream_t st) {
+        if (!on || !a) return;
+        hipEvent_t b = get();
+        if (!b) return;
+        (void)hipEventRecord(b, st);
+        pending.push_back(Rec{id, a, b});
+    }
+    void collect() {
+        for (auto& r : pending) {
+            float t = 0.f;
+            if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+                ms[r.id] += t;
+                n[r.id] += 1;
+            }
+        }
+        pending.clear();
+        used = 0;
+    }
+    void destroy() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+        pool.clear();
+        used = 0;
+    }
+};
 
 struct ExtractLaunch {
     const Geometry* hg;        // host copy of the geometry
@@ -29,6 +82,7 @@ struct ExtractLaunch {
     float* kps;
     uint8_t* desc;
     int* nkp;
+    KernelTimer* timer;
 };
 
 struct StereoLaunch {
@@ -47,6 +101,7 @@ struct StereoLaunch {
     float* depth;
     int* nvalid;
     size_t lds;
+    KernelTimer* timer;
 };
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);

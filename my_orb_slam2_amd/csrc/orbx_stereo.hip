@@ -283,9 +283,11 @@ hipError_t prepare_stereo(size_t lds) {
 }
 
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {
+    hipEvent_t e = a.timer ? a.timer->start(st) : nullptr;
     hipLaunchKernelGGL(k_stereo, dim3(a.batch), dim3(256), a.lds, st, a.dg, a.kpsL, a.descL,
                        a.nkpL, a.pyrL, a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb, a.uR,
                        a.depth, a.nvalid);
+    if (a.timer) a.timer->stop(K_STEREO, e, st);
     return hipGetLastError();
 }
 

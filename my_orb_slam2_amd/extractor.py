@@ -10,7 +10,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import BatchView, ExtractorParams, KEYPOINT_DTYPE, check, load, ptr
+from ._lib import BatchView, ExtractorParams, KERNELS, KEYPOINT_DTYPE, check, load, ptr
 
 
 class ORBextractor:
@@ -122,6 +122,29 @@ class ORBextractor:
         bstride = images.stride(0) * images.element_size()
         check("orbx_extract_batch_device", self._L.orbx_extract_batch_device(
             self._h, ptr(images), B, W, H, stride, bstride, ptr(stream)))
+
+    def profile(self, on: bool = True):
+        """Bracket every kernel launch with HIP events (on its launch stream)."""
+        check("orbx_profile_enable", self._L.orbx_profile_enable(self._h, 1 if on else 0))
+
+    def collect_profile(self) -> dict:
+        """{kernel: (total_ms, launches)} since the last collect (waits for the launches)."""
+        ms = np.zeros(len(KERNELS), np.float64)
+        n = np.zeros(len(KERNELS), np.int64)
+        check("orbx_profile_collect", self._L.orbx_profile_collect(self._h, ptr(ms), ptr(n)))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(KERNELS)}
+
+    def batch_fetch(self, first: int = 0, count: int | None = None):
+        """Host copies (nkp, keypoints, descriptors) of images [first, first+count) of the last
+        batched call; keypoints/descriptors are [count, kp_cap] arrays (rows >= nkp unused)."""
+        v = self.batch_view()
+        count = v.batch - first if count is None else count
+        nkp = np.zeros(count, np.int32)
+        kps = np.zeros((count, v.kp_cap), KEYPOINT_DTYPE)
+        desc = np.zeros((count, v.kp_cap, 32), np.uint8)
+        check("orbx_batch_fetch", self._L.orbx_batch_fetch(self._h, first, count, ptr(nkp),
+                                                            ptr(kps), ptr(desc)))
+        return nkp, kps, desc
 
     def batch_view(self) -> BatchView:
         v = BatchView()

@@ -99,16 +99,7 @@ def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
     mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
     uR, dep, nv = sb(Ls, Rs, KITTI_MBF, mb)
     torch.cuda.synchronize()
-    view = sb.left.batch_view()
-    kc = view.kp_cap
-    import ctypes
-    nkp = np.zeros(B, np.int32)
-    kps = np.zeros(B * kc, m.KEYPOINT_DTYPE)
-    desc = np.zeros((B * kc, 32), np.uint8)
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy(ctypes.c_void_p(nkp.ctypes.data), ctypes.c_void_p(view.nkp), B * 4, 2)
-    hip.hipMemcpy(ctypes.c_void_p(kps.ctypes.data), ctypes.c_void_p(view.kps), B * kc * 28, 2)
-    hip.hipMemcpy(ctypes.c_void_p(desc.ctypes.data), ctypes.c_void_p(view.desc), B * kc * 32, 2)
+    nkp, kps, desc = sb.left.batch_fetch()
     uRh, deph, nvh = uR.cpu().numpy(), dep.cpu().numpy(), nv.cpu().numpy()
     for i in range(B):
         ol = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
@@ -116,8 +107,8 @@ def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
         k_o, d_o = ol(pairs[i][0])
         orr(pairs[i][1])
         n = nkp[i]
-        assert_kps_equal(kps[i * kc: i * kc + n], k_o, f"batch item {i}")
-        assert_bytes_equal(desc[i * kc: i * kc + n], d_o, f"batch item {i} desc")
+        assert_kps_equal(kps[i, :n], k_o, f"batch item {i}")
+        assert_bytes_equal(desc[i, :n], d_o, f"batch item {i} desc")
         u_o, d_oo, n_o = oracle_mod.stereo_match(ol, orr, len(k_o), KITTI_MBF, mb)
         assert_f32_bits_equal(uRh[i, :n], u_o, f"batch item {i} uRight")
         assert_f32_bits_equal(deph[i, :n], d_oo, f"batch item {i} depth")
