@@ -29,8 +29,10 @@ _lib = None
 
 def build(force: bool = False) -> pathlib.Path:
     """Compile the restatement with its Makefile (g++; no GPU needed)."""
-    if force or not LIB_PATH.exists():
-        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    srcs = list(HERE.glob("*.cpp")) + list(HERE.glob("*.h"))
+    stale = not LIB_PATH.exists() or any(p.stat().st_mtime > LIB_PATH.stat().st_mtime for p in srcs)
+    if force or stale:
+        subprocess.run(["make", "-s", "-B" if force else "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
 
 
@@ -60,6 +62,8 @@ def lib():
         L.oracle_fast.argtypes = [vp, i32, i32, i32, i32, vp, i32]
         L.oracle_fast_atan2.restype = f32
         L.oracle_fast_atan2.argtypes = [f32, f32]
+        L.oracle_gaussian_taps.argtypes = [vp]
+        L.oracle_descriptor_distance.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -159,3 +163,15 @@ def fast(img: np.ndarray, threshold: int) -> np.ndarray:
 
 def fast_atan2(y: float, x: float) -> float:
     return lib().oracle_fast_atan2(y, x)
+
+
+def gaussian_taps():
+    t = np.zeros(7, np.int32)
+    lib().oracle_gaussian_taps(_p(t))
+    return t
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(_p(a), _p(b))

@@ -978,5 +978,7 @@ int oracle_fast(const uint8_t* img, int stride, int rows, int cols, int threshol
     return (int)k.size();
 }
 float oracle_fast_atan2(float y, float x) { return fastAtan2(y, x); }
+void oracle_gaussian_taps(int* taps7) { gaussian_taps(taps7); }
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return DescriptorDistance(a, b); }
 
 }  // extern "C"

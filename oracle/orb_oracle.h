@@ -72,6 +72,8 @@ void oracle_gaussian7(const uint8_t* src, int w, int h, int stride, uint8_t* dst
 int oracle_fast(const uint8_t* img, int stride, int rows, int cols, int threshold, okp_t* out,
                 int cap);
 float oracle_fast_atan2(float y, float x);
+void oracle_gaussian_taps(int* taps7);
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,102 @@
+"""CPU: pin the oracle against the known answers the reference itself carries or implies.
+
+The reference has no tests and no golden vectors.  What it does carry:
+the rBRIEF pattern (src/ORBextractor.cc:150-408), the umax table it computes
+(:454-469), the per-level feature quotas (:436-446), the pyramid sizes (:1134), the
+matcher thresholds (src/ORBmatcher.cc:37-39) and the Gaussian kernel it asks OpenCV for
+(:1108).  glibc cosf/sinf are the real library in this image and are pinned exhaustively.
+"""
+import hashlib
+import json
+import math
+import pathlib
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+GOLD = ROOT / "tests" / "golden"
+
+
+def test_pattern_table_matches_reference_hash():
+    vals = []
+    for line in (ROOT / "my_orb_slam2_amd/csrc/orbx_pattern.inc").read_text().splitlines():
+        if line.startswith("//") or not line.strip():
+            continue
+        vals += [int(v) for v in line.replace(",", " ").split()]
+    assert len(vals) == 1024
+    digest = hashlib.sha256(bytes(v & 0xFF for v in vals)).hexdigest()
+    assert digest == json.loads((GOLD / "pattern.json").read_text())["sha256_int8"]
+    assert max(vals) <= 12 and min(vals) >= -13
+
+
+@pytest.mark.parametrize("nf,quotas", [(2000, [434, 362, 302, 251, 209, 175, 145, 122]),
+                                       (1000, [217, 181, 151, 126, 105, 87, 73, 60])])
+def test_feature_quotas(oracle_mod, nf, quotas):
+    t = oracle_mod.OracleExtractor(nf, 1.2, 8, 20, 7).tables()
+    assert list(t["features_per_level"]) == quotas
+    assert sum(quotas) == nf
+
+
+def test_scale_tables_and_umax(oracle_mod):
+    t = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7).tables()
+    exp = np.float32([1, 1.2000000477, 1.4400000572, 1.7280001640, 2.0736002922,
+                      2.4883203506, 2.9859845638, 3.5831816196])
+    np.testing.assert_allclose(t["scale"], exp, rtol=0, atol=2e-7)
+    assert np.all(t["sigma2"] == t["scale"] * t["scale"])
+    assert np.all(t["inv_scale"] == np.float32(1.0) / t["scale"])
+    assert list(t["umax"]) == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+
+
+@pytest.mark.parametrize("size,levels", [
+    ((1241, 376), [(1241, 376), (1034, 313), (862, 261), (718, 218), (598, 181), (499, 151),
+                   (416, 126), (346, 105)]),
+    ((640, 480), None), ((752, 480), None)])
+def test_pyramid_sizes(oracle_mod, size, levels):
+    e = oracle_mod.OracleExtractor(1000, 1.2, 8, 20, 7)
+    e(np.zeros(size[::-1], np.uint8))
+    got = [e.level_size(l) for l in range(8)]
+    if levels:
+        assert got == levels
+    area = sum(w * h for w, h in got)
+    assert area == {(1241, 376): 1444097, (640, 480): 950532, (752, 480): 1117367}[size]
+
+
+def test_gaussian_taps(oracle_mod):
+    # getGaussianKernel(7, 2, CV_32F) * 256, rounded: the 8U fixed-point kernel, sum 257
+    assert list(oracle_mod.gaussian_taps()) == [18, 34, 49, 55, 49, 34, 18]
+
+
+def test_fast_atan2_accuracy_and_quadrants(oracle_mod):
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        y, x = rng.integers(-20000, 20000, 2).astype(np.float32)
+        a = oracle_mod.fast_atan2(float(y), float(x))
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.3, (x, y, a, ref)
+        assert 0.0 <= a <= 360.0
+    assert oracle_mod.fast_atan2(0.0, 1.0) == 0.0
+    assert oracle_mod.fast_atan2(0.0, 0.0) == 0.0
+    assert abs(oracle_mod.fast_atan2(1.0, 0.0) - 90.0) < 1e-4
+    assert abs(oracle_mod.fast_atan2(0.0, -1.0) - 180.0) < 1e-4
+
+
+def test_descriptor_distance_is_popcount(oracle_mod):
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+        assert oracle_mod.descriptor_distance(a, b) == int(np.unpackbits(a ^ b).sum())
+
+
+def test_glibc_sincosf_port_exhaustive(tmp_path):
+    """orbx_math.h's sinf/cosf == the host glibc on every float in [0, 2*pi)."""
+    exe = tmp_path / "lpc"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-pthread",
+                    str(ROOT / "tests/native/libm_port_check.cpp"), "-o", str(exe), "-lm"],
+                   check=True)
+    r = subprocess.run([str(exe), "0", "6.2831855", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sin_mismatch=0 cos_mismatch=0" in r.stdout
