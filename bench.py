@@ -89,10 +89,8 @@ def main():
         sb(Ls, Rs, MBF, mb, stream=st)
     torch.cuda.synchronize(dev)
     if not args.no_kernel_timing:
-        sb.left.profile(True)
-        sb.right.profile(True)
-        sb.left.collect_profile()
-        sb.right.collect_profile()
+        sb.profile(True)
+        sb.collect_profile()
 
     if world > 1:
         dist.barrier()
@@ -109,15 +107,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    prof = {}
-    if not args.no_kernel_timing:
-        pl, pr = sb.left.collect_profile(), sb.right.collect_profile()
-        for k in pl:
-            prof[k] = (pl[k][0] + pr[k][0], pl[k][1] + pr[k][1])
+    prof = sb.collect_profile() if not args.no_kernel_timing else {}
 
     # sanity on the produced work (outside the timed region)
     nv = sb.nvalid.cpu().numpy()
-    nkp, _, _ = sb.left.batch_fetch(0, B)
+    nkp, _, _ = sb.fetch("left")
 
     total_pairs = B * args.steps * world
     fps = total_pairs / elapsed
@@ -161,28 +155,24 @@ def main():
 
 
 def kernel_bytes(sb, B):
-    """Algorithmic HBM bytes per launch of each kernel, both images."""
-    import ctypes
-    v = sb.left.batch_view()
-    area = sum(v.level_w[l] * v.level_h[l] for l in range(8))
-    a0 = v.level_w[0] * v.level_h[0]
+    """Algorithmic HBM bytes per launch of each kernel.  One launch
+    covers the 2B views (k_level: one level of them)."""
+    v = sb.ext.batch_view()
+    L = 8
+    area = [v.level_w[l] * v.level_h[l] for l in range(L)]
+    n = 2 * B
     kc = v.kp_cap
-    # per image
     return {
-        # level-0 copy: read + write
-        "k_copy_level0": B * 2 * a0,
-        # 7 cascaded levels read l-1 and write l: averaged per launch
-        "k_resize": B * (area - a0 + (area - v.level_w[7] * v.level_h[7])) / 7.0,
-        # blur: read every level once, write every level once
-        "k_blur": B * 2 * area,
-        # FAST: read every level once (cell ROIs), write counts + ~candidates
-        "k_fast": B * area,
-        # octree: read candidates (<= 4 B each) and write survivors
-        "k_octree": B * 4 * kc * 2,
-        # orient+desc: 31x31 patch + 37x37 blurred patch + 28+32 B out per keypoint
-        "k_orient_desc": B * kc * (31 * 31 + 37 * 37 + 60),
-        # stereo: keypoints + descriptors of both views, 11x21 windows, outputs
-        "k_stereo": B * kc * (2 * (28 + 32) + 11 * 11 + 11 * 21 + 8) / 2.0,
+        # per level: read level l-1 (level 0: the input), write level l and its blur
+        "k_level": n * (sum(area[:-1]) + area[0] + 2 * sum(area)) / L,
+        # every level byte read once
+        "k_fast": n * sum(area),
+        # candidates in (<= 4 B each, bounded by 2 x kp slots here) and survivors out
+        "k_octree": n * 4 * kc * 2,
+        # 31x31 raw + 37x37 blurred patch in, 28 + 32 B out per keypoint
+        "k_orient_desc": n * kc * (31 * 31 + 37 * 37 + 60),
+        # both views' keypoints + descriptors in, 11x11 + 11x21 SAD windows, 8 B out
+        "k_stereo": B * kc * (2 * (28 + 32) + 11 * 11 + 11 * 21 + 8),
     }
 
 

@@ -71,6 +71,12 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
                          size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
                          int* n_out);
 
+/* Build the geometry and device workspace for width x height images and up to `batch`
+ * images per call (otherwise done lazily by the first call); *kp_cap = keypoint slots per
+ * image in the batched outputs. */
+orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int batch,
+                                   int* kp_cap);
+
 /* mvImagePyramid[level] (include/ORBextractor.h:85) of image `index` of the last call,
  * copied to host (w*h bytes, tightly packed). */
 orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out,
@@ -119,6 +125,18 @@ orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor*
                                            float mbf, float mb, float* d_uRight,
                                            float* d_depth, int32_t* d_nvalid, void* stream);
 
+/* The batched stereo Frame front-end (src/Frame.cc:72-102) on ONE handle: extracts the B
+ * left and B right views as one batch of 2B images (images [0,B) left, [B,2B) right; both
+ * views use the same ORBextractor parameters, as in the reference's Tracking.cc:136-139)
+ * and runs ComputeStereoMatches on each pair.  Outputs: d_uRight/d_depth [batch][kp_cap],
+ * d_nvalid [batch] (may be NULL); keypoints/descriptors via orbx_batch_view_get /
+ * orbx_batch_fetch (left view = image i, right view = image B+i). */
+orbx_status orbx_stereo_frames_device(orbx_extractor* h, const uint8_t* d_left,
+                                      const uint8_t* d_right, int batch, int width, int height,
+                                      size_t stride, size_t batch_stride, float mbf, float mb,
+                                      float* d_uRight, float* d_depth, int32_t* d_nvalid,
+                                      void* stream);
+
 /* ---- descriptor matching (src/ORBmatcher.cc) ---------------------------------------------- */
 
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1715-1731) on host memory. */
@@ -126,8 +144,7 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 /* ---- per-kernel timing (HIP events around each launch, on the launch stream) ------------ */
 typedef enum {
-    ORBX_K_COPY_LEVEL0 = 0, ORBX_K_RESIZE, ORBX_K_BLUR, ORBX_K_FAST, ORBX_K_OCTREE,
-    ORBX_K_ORIENT_DESC, ORBX_K_STEREO, ORBX_K_COUNT
+    ORBX_K_LEVEL = 0, ORBX_K_FAST, ORBX_K_OCTREE, ORBX_K_ORIENT_DESC, ORBX_K_STEREO, ORBX_K_COUNT
 } orbx_kernel_id;
 orbx_status orbx_profile_enable(orbx_extractor* h, int on);
 /* Waits for the recorded launches, returns per-kernel total ms and launch counts since the

@@ -17,8 +17,7 @@ LIB_PATH = PKG / "liborbx.so"
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
-KERNELS = ["k_copy_level0", "k_resize", "k_blur", "k_fast", "k_octree", "k_orient_desc",
-           "k_stereo"]
+KERNELS = ["k_level", "k_fast", "k_octree", "k_orient_desc", "k_stereo"]
 
 STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
           -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_STATE"}
@@ -51,6 +50,7 @@ SIGNATURES = {
     "orbx_extractor_create": (_i, [ctypes.POINTER(ExtractorParams), ctypes.POINTER(_vp)]),
     "orbx_extractor_destroy": (_i, [_vp]),
     "orbx_extractor_tables": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbx_extractor_prepare": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i)]),
     "orbx_extract": (_i, [_vp, _vp, _i, _i, _sz, _vp, _i, _vp, ctypes.POINTER(_i)]),
     "orbx_pyramid_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orbx_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp]),
@@ -58,6 +58,8 @@ SIGNATURES = {
     "orbx_batch_fetch": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "orbx_stereo_match": (_i, [_vp, _vp, _f, _f, _vp, _vp, _i, ctypes.POINTER(_i)]),
     "orbx_stereo_match_batch_device": (_i, [_vp, _vp, _f, _f, _vp, _vp, _vp, _vp]),
+    "orbx_stereo_frames_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _sz, _sz, _f, _f, _vp, _vp,
+                                       _vp, _vp]),
     "orbx_descriptor_distance": (_i, [_vp, _vp]),
     "orbx_version": (ctypes.c_char_p, []),
     "orbx_last_error": (ctypes.c_char_p, []),

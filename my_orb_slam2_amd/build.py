@@ -15,7 +15,8 @@ import sys
 PKG = pathlib.Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "liborbx.so"
-SOURCES = ["orbx_extract.hip", "orbx_stereo.hip", "orbx_match.hip", "orbx_capi.hip"]
+SOURCES = ["orbx_pyramid.hip", "orbx_extract.hip", "orbx_stereo.hip", "orbx_match.hip",
+           "orbx_capi.hip"]
 HEADERS = ["orbx_internal.h", "orbx_device.h", "orbx_math.h", "orbx_kernels.h",
            "orbx_pattern.inc", "../../include/orbx.h"]
 

@@ -21,7 +21,8 @@
 #define ORBX_VERSION "orbx 0.1.0 (gfx950)"
 
 namespace orbx {
-hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds);
+hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
+                           size_t fast_lds);
 }
 
 using namespace orbx;
@@ -71,7 +72,7 @@ struct orbx_extractor {
     std::vector<CellDesc> cells;
     std::vector<int16_t> rtab;
     int ncap = 0, kcap = 0;
-    size_t octree_lds = 0, stereo_lds = 0;
+    size_t octree_lds = 0, stereo_lds = 0, level_lds = 0;
     int cap_batch = 0;
     DevBuf d_geom, d_cells, d_rtab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
@@ -148,6 +149,26 @@ void compute_tables(orbx_extractor* h) {
     for (int i = 0; i < 7; ++i) h->taps[i] = cvRound(cf[i] * 256.f);
 }
 
+int reflect101_h(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+void reflected_range_h(int lo, int hi, int len, int& mn, int& mx) {
+    mn = 1 << 30;
+    mx = -1;
+    for (int p = lo; p <= hi; ++p) {
+        const int r = reflect101_h(p, len);
+        mn = std::min(mn, r);
+        mx = std::max(mx, r);
+    }
+}
+
 int vresize_simd_end(int width) {
     int x = 0;
     for (; x <= width - 16; x += 16) {}
@@ -178,7 +199,7 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         lv.h = cvRound((float)H * h->inv_scale[l]);
         if (lv.w <= 0 || lv.h <= 0) return ORBX_ERR_UNSUPPORTED;
         if (lv.w > 4096 + 32 || lv.h > 4096 + 32) return ORBX_ERR_UNSUPPORTED;   // 12-bit packing
-        lv.pitch = (int)align_up(lv.w, 64);
+        lv.pitch = (int)align_up(lv.w + 4, 64);   // >= 4 bytes of slack for dword staging
         lv.off = off;
         off += (long long)align_up((size_t)lv.pitch * lv.h, 256);
         lv.scale = h->scale[l];
@@ -222,7 +243,9 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                     c.slot = (int32_t)cand;
                     cand += c.cap;
                     lcap += c.cap;
-                    G.max_roi_bytes = std::max(G.max_roi_bytes, (int)c.rows * c.cols);
+                    // k_fast stages the ROI as aligned dwords: <= cols + 6 bytes per row
+                    G.max_roi_bytes = std::max(G.max_roi_bytes,
+                                               (int)c.rows * ((c.cols + 6 + 3) / 4) * 4);
                     if (dh > 0 && dw > 0)
                         G.max_mbuf_bytes = std::max(G.max_mbuf_bytes, (dh + 2) * (dw + 2));
                     h->cells.push_back(c);
@@ -305,6 +328,42 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
             }
         }
     }
+    // k_level tiles (128 x 32) and the largest source window it stages (as the kernel does)
+    G.ltw = 128;
+    G.lth = 32;
+    G.win_cap = 16;
+    for (int l = 0; l < L; ++l) {
+        LevelGeom& lv = G.lv[l];
+        lv.ntx = (lv.w + G.ltw - 1) / G.ltw;
+        lv.nty = (lv.h + G.lth - 1) / G.lth;
+        const int mode = l == 0 ? 0 : (lv.copy ? 1 : (lv.area2 ? 2 : 3));
+        const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
+        const int16_t* xofs = h->rtab.data() + lv.rtab_off;
+        const int16_t* yofs = xofs + 3 * lv.w;
+        for (int ty = 0; ty < lv.nty; ++ty) {
+            const int Y0 = ty * G.lth, vh = std::min(G.lth, lv.h - Y0);
+            int mny, mxy;
+            reflected_range_h(Y0 - 3, Y0 + vh + 2, lv.h, mny, mxy);
+            for (int tx = 0; tx < lv.ntx; ++tx) {
+                const int X0 = tx * G.ltw, vw = std::min(G.ltw, lv.w - X0);
+                int bytes = 0;
+                if (mode == 0 || mode == 1) {
+                    const int y0 = std::max(Y0 - 3, 0), y1 = std::min(Y0 + G.lth + 2, lv.h - 1);
+                    bytes = (G.ltw + 8) * (y1 - y0 + 1);
+                } else if (mode == 3) {
+                    int mnx, mxx;
+                    reflected_range_h(X0 - 3, X0 + vw + 2, lv.w, mnx, mxx);
+                    const int x0 = xofs[mnx] & ~3, x1 = std::min((int)xofs[mxx] + 1, S.w - 1);
+                    const int y0 = std::min(std::max((int)yofs[mny], 0), S.h - 1);
+                    const int y1 = std::min(std::max((int)yofs[mxy] + 1, 0), S.h - 1);
+                    bytes = (((x1 - x0 + 1) + 3) & ~3) * (y1 - y0 + 1);
+                }
+                G.win_cap = std::max(G.win_cap, bytes);
+            }
+        }
+    }
+    h->level_lds = level_lds_bytes(G.ltw, G.lth, G.win_cap);
+    if (h->level_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     G.blur_tile_begin[L] = blur_tiles;
     G.orient_block_begin[L] = oblocks;
     G.blur_tiles = blur_tiles;
@@ -351,7 +410,8 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         if (!h->rtab.empty() &&
             !HIPOK(hipMemcpy(h->d_rtab.p, h->rtab.data(), h->rtab.size() * 2, hipMemcpyHostToDevice)))
             return ORBX_ERR_DEVICE;
-        if (!HIPOK(prepare_kernels(h->octree_lds, h->stereo_lds))) return ORBX_ERR_DEVICE;
+        if (!HIPOK(prepare_kernels(h->octree_lds, h->stereo_lds, h->level_lds, fast_lds_bytes(h->hg))))
+            return ORBX_ERR_DEVICE;
         h->have_geom = true;
         h->cap_batch = 0;
     }
@@ -372,14 +432,17 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     return ORBX_OK;
 }
 
-orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, int batch, size_t stride,
-                        size_t batch_stride, hipStream_t st) {
+orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
+                        int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
     ExtractLaunch a;
     a.hg = &h->hg;
     a.dg = h->d_geom.as<Geometry>();
     a.cells = h->d_cells.as<CellDesc>();
     a.rtab = h->d_rtab.as<int16_t>();
     a.d_imgs = d_imgs;
+    a.d_imgs2 = d_imgs2 ? d_imgs2 : d_imgs;
+    a.split = d_imgs2 ? split : batch;
+    a.level_lds = h->level_lds;
     a.stride = stride;
     a.batch_stride = batch_stride;
     a.batch = batch;
@@ -408,23 +471,26 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, int batch, siz
 // stream, which orders them with the caller's other default-stream work.
 hipStream_t pick_stream(orbx_extractor*, void* s) { return (hipStream_t)s; }
 
-orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, float mbf, float mb, float* d_uR,
-                       float* d_dep, int* d_nv, hipStream_t st) {
+// Stereo over pairs (image i of L at offset offL, image i of R at offset offR).
+orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL, int offR,
+                       float mbf, float mb, float* d_uR, float* d_dep, int* d_nv, hipStream_t st) {
     if (!L->last_valid || !R->last_valid) return ORBX_ERR_STATE;
-    if (L->hg.width != R->hg.width || L->hg.height != R->hg.height || L->last_batch != R->last_batch ||
-        L->hg.nlevels != R->hg.nlevels || L->hg.kp_cap != R->hg.kp_cap)
+    if (L->hg.width != R->hg.width || L->hg.height != R->hg.height ||
+        L->hg.nlevels != R->hg.nlevels || L->hg.kp_cap != R->hg.kp_cap ||
+        offL + batch > L->last_batch || offR + batch > R->last_batch)
         return ORBX_ERR_INVALID;
+    const size_t KC = (size_t)L->hg.kp_cap;
     StereoLaunch a;
     a.dg = L->d_geom.as<Geometry>();
-    a.batch = L->last_batch;
-    a.kpsL = L->d_kps.as<float>();
-    a.descL = L->d_desc.as<uint8_t>();
-    a.nkpL = L->d_nkp.as<int>();
-    a.pyrL = L->d_pyr.as<uint8_t>();
-    a.kpsR = R->d_kps.as<float>();
-    a.descR = R->d_desc.as<uint8_t>();
-    a.nkpR = R->d_nkp.as<int>();
-    a.pyrR = R->d_pyr.as<uint8_t>();
+    a.batch = batch;
+    a.kpsL = L->d_kps.as<float>() + offL * KC * 7;
+    a.descL = L->d_desc.as<uint8_t>() + offL * KC * 32;
+    a.nkpL = L->d_nkp.as<int>() + offL;
+    a.pyrL = L->d_pyr.as<uint8_t>() + offL * (size_t)L->hg.pyr_bytes;
+    a.kpsR = R->d_kps.as<float>() + offR * KC * 7;
+    a.descR = R->d_desc.as<uint8_t>() + offR * KC * 32;
+    a.nkpR = R->d_nkp.as<int>() + offR;
+    a.pyrR = R->d_pyr.as<uint8_t>() + offR * (size_t)R->hg.pyr_bytes;
     a.mbf = mbf;
     a.mb = mb;
     a.uR = d_uR;
@@ -444,8 +510,8 @@ const char* orbx_version(void) { return ORBX_VERSION; }
 const char* orbx_last_error(void) { return g_err; }
 
 const char* orbx_kernel_name(int id) {
-    static const char* names[K_COUNT] = {"k_copy_level0", "k_resize", "k_blur", "k_fast",
-                                         "k_octree", "k_orient_desc", "k_stereo"};
+    static const char* names[K_COUNT] = {"k_level", "k_fast", "k_octree", "k_orient_desc",
+                                         "k_stereo"};
     return (id >= 0 && id < K_COUNT) ? names[id] : "";
 }
 
@@ -548,7 +614,7 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     hipStream_t st = h->stream;
     if (!HIPOK(hipMemcpy2DAsync(h->d_in.p, width, img, stride, width, height, hipMemcpyHostToDevice, st)))
         return ORBX_ERR_DEVICE;
-    s = run_extract(h, h->d_in.as<uint8_t>(), 1, width, (size_t)width * height, st);
+    s = run_extract(h, h->d_in.as<uint8_t>(), nullptr, 1, 1, width, (size_t)width * height, st);
     if (s != ORBX_OK) return s;
     int n = 0;
     if (!HIPOK(hipMemcpyAsync(&n, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
@@ -585,6 +651,15 @@ orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t*
     return ORBX_OK;
 }
 
+orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int batch,
+                                   int* kp_cap) {
+    if (!h || width <= 0 || height <= 0 || batch < 1) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, batch);
+    if (s == ORBX_OK && kp_cap) *kp_cap = h->hg.kp_cap;
+    return s;
+}
+
 orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int batch,
                                       int width, int height, size_t stride, size_t batch_stride,
                                       void* stream) {
@@ -593,7 +668,7 @@ orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, 
     std::lock_guard<std::mutex> lk(h->mu);
     orbx_status s = ensure_workspace(h, width, height, batch);
     if (s != ORBX_OK) return s;
-    return run_extract(h, d_imgs, batch, stride, batch_stride, pick_stream(h, stream));
+    return run_extract(h, d_imgs, nullptr, batch, batch, stride, batch_stride, pick_stream(h, stream));
 }
 
 orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {
@@ -649,8 +724,8 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float
     if (!HIPOK(hipEventRecord(right->done, right->stream)) ||
         !HIPOK(hipStreamWaitEvent(st, right->done, 0)))
         return ORBX_ERR_DEVICE;
-    orbx_status s = run_stereo(left, right, mbf, mb, left->d_uR.as<float>(), left->d_dep.as<float>(),
-                               left->d_nv.as<int>(), st);
+    orbx_status s = run_stereo(left, right, 1, 0, 0, mbf, mb, left->d_uR.as<float>(),
+                               left->d_dep.as<float>(), left->d_nv.as<int>(), st);
     if (s != ORBX_OK) return s;
     int n = 0, nv = 0;
     if (!HIPOK(hipMemcpyAsync(&n, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
@@ -675,8 +750,26 @@ orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor*
                                            int32_t* d_nvalid, void* stream) {
     if (!left || !right || left == right || !d_uRight || !d_depth) return ORBX_ERR_INVALID;
     (void)hipSetDevice(left->device);
-    return run_stereo(left, right, mbf, mb, d_uRight, d_depth, d_nvalid,
+    if (left->last_batch != right->last_batch) return ORBX_ERR_INVALID;
+    return run_stereo(left, right, left->last_batch, 0, 0, mbf, mb, d_uRight, d_depth, d_nvalid,
                       pick_stream(left, stream));
+}
+
+orbx_status orbx_stereo_frames_device(orbx_extractor* h, const uint8_t* d_left,
+                                      const uint8_t* d_right, int batch, int width, int height,
+                                      size_t stride, size_t batch_stride, float mbf, float mb,
+                                      float* d_uRight, float* d_depth, int32_t* d_nvalid,
+                                      void* stream) {
+    if (!h || !d_left || !d_right || batch < 1 || width <= 0 || height <= 0 ||
+        stride < (size_t)width || !d_uRight || !d_depth)
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, 2 * batch);
+    if (s != ORBX_OK) return s;
+    hipStream_t st = pick_stream(h, stream);
+    s = run_extract(h, d_left, d_right, batch, 2 * batch, stride, batch_stride, st);
+    if (s != ORBX_OK) return s;
+    return run_stereo(h, h, batch, 0, batch, mbf, mb, d_uRight, d_depth, d_nvalid, st);
 }
 
 }  // extern "C"

@@ -35,8 +35,9 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
-// Exclusive scan across a 256-thread workgroup (4 waves).  `tmp` = 4 ints of LDS.
-// Every thread must call it (contains barriers).
+// Exclusive scan across a workgroup of NW waves (default 4 = 256 threads).  `tmp` = NW ints
+// of LDS.  Every thread must call it (contains barriers).
+template <int NW = 4>
 __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int& total) {
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     int incl = wave_incl_scan(v);
@@ -44,7 +45,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int& total) {
     __syncthreads();
     int base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
         int s = tmp[w];
         base += (w < wid) ? s : 0;
         tot += s;
@@ -54,10 +55,70 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int& total) {
     return base + incl - v;
 }
 
+template <int NW = 4>
 __device__ __forceinline__ int block_sum(int v, int* tmp) {
     int total;
-    block_excl_scan(v, tmp, total);
+    block_excl_scan<NW>(v, tmp, total);
     return total;
+}
+
+}  // namespace orbx
+
+namespace orbx {
+
+// Stage a rows x ndw-dword window (row r at gsrc + r*gpitch, 4-byte aligned rows) into LDS
+// (row r at lds + r*lpitch_dw dwords).  Each thread issues up to 8 loads before its first
+// LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.
+template <int NT>
+__device__ __forceinline__ void stage_dwords(const uint8_t* __restrict__ gsrc, size_t gpitch,
+                                             int rows, int ndw, uint32_t* lds, int lpitch_dw,
+                                             int tid) {
+    const int n = rows * ndw;
+    if (n <= 0) return;
+    for (int base = 0; base < n; base += NT * 8) {
+        uint32_t v[8];
+        // unconditional loads (index clamped): a guarded load becomes a branch + vmcnt(0)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = min(base + k * NT + tid, n - 1);
+            const int r = i / ndw, c = i - r * ndw;
+            v[k] = *(const uint32_t*)(gsrc + (size_t)r * gpitch + 4 * c);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = base + k * NT + tid;
+            if (i < n) {
+                const int r = i / ndw, c = i - r * ndw;
+                lds[r * lpitch_dw + c] = v[k];
+            }
+        }
+    }
+}
+
+// Same for an arbitrary byte window (no alignment), 16 loads in flight per thread.
+template <int NT>
+__device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, size_t gpitch,
+                                            int rows, int cols, uint8_t* lds, int lpitch,
+                                            int tid) {
+    const int n = rows * cols;
+    if (n <= 0) return;
+    for (int base = 0; base < n; base += NT * 16) {
+        uint8_t v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int i = min(base + k * NT + tid, n - 1);
+            const int r = i / cols, c = i - r * cols;
+            v[k] = gsrc[(size_t)r * gpitch + c];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int i = base + k * NT + tid;
+            if (i < n) {
+                const int r = i / cols, c = i - r * cols;
+                lds[r * lpitch + c] = v[k];
+            }
+        }
+    }
 }
 
 }  // namespace orbx

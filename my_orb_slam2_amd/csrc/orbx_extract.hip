@@ -1,9 +1,7 @@
 // orbx_extract.hip — the ORB extractor as gfx950 kernels, batched over B images.
 //
 // Replaces ORB_SLAM2::ORBextractor::operator() (src/ORBextractor.cc:1065-1127).  Stages:
-//   k_copy_level0  input -> pyramid level 0                     (ComputePyramid :1148-1150)
-//   k_resize       level l-1 -> level l, INTER_LINEAR 8U         (ComputePyramid :1140-1146)
-//   k_blur         7x7 Gaussian sigma 2 of every level           (operator() :1106-1108)
+//   k_level        level l from l-1 + its 7x7 Gaussian (orbx_pyramid.hip; :1129-1154, :1108)
 //   k_fast         FAST-9 + cell-local NMS per 30px cell         (ComputeKeyPointsOctTree :801-850)
 //   k_octree       quadtree distribution, one workgroup/level    (DistributeOctTree :539-765)
 //   k_orient_desc  IC angle + rBRIEF + level-major assembly      (:872-874, :77-147, :1097-1126)
@@ -23,170 +21,6 @@ namespace orbx {
 __constant__ int8_t c_pattern[1024] = {
 #include "orbx_pattern.inc"
 };
-
-__device__ __forceinline__ int reflect101(int p, int len) {
-    if ((unsigned)p < (unsigned)len) return p;
-    if (len == 1) return 0;
-    do {
-        if (p < 0) p = -p;
-        else p = 2 * len - 2 - p;
-    } while ((unsigned)p >= (unsigned)len);
-    return p;
-}
-
-__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
-
-// ----------------------------------------------------------------------------------------
-// Pyramid
-// ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_copy_level0(const Geometry* __restrict__ g,
-                                                     const uint8_t* __restrict__ src,
-                                                     size_t stride, size_t batch_stride,
-                                                     uint8_t* __restrict__ pyr) {
-    const int b = blockIdx.z, y = blockIdx.y;
-    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    const LevelGeom& L = g->lv[0];
-    if (x0 >= L.w) return;
-    const uint8_t* s = src + b * batch_stride + (size_t)y * stride + x0;
-    uint8_t* d = pyr + b * g->pyr_bytes + L.off + (size_t)y * L.pitch + x0;
-    if (x0 + 3 < L.w) {
-        uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) |
-                     ((uint32_t)s[3] << 24);
-        *(uint32_t*)d = v;
-    } else {
-        for (int j = 0; x0 + j < L.w; ++j) d[j] = s[j];
-    }
-}
-
-// cv::resize INTER_LINEAR 8U restated over precomputed OpenCV coefficient tables
-// (xofs/alpha/yofs/beta, built on the host exactly as imgwarp.cpp builds them).
-__global__ __launch_bounds__(256) void k_resize(const Geometry* __restrict__ g,
-                                                const int16_t* __restrict__ rtab,
-                                                uint8_t* __restrict__ pyr, int level) {
-    const int b = blockIdx.z, y = blockIdx.y;
-    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    const LevelGeom& L = g->lv[level];
-    const LevelGeom& S = g->lv[level - 1];
-    if (x0 >= L.w) return;
-    const uint8_t* src = pyr + b * g->pyr_bytes + S.off;
-    uint8_t* dst = pyr + b * g->pyr_bytes + L.off + (size_t)y * L.pitch;
-    uint32_t out = 0;
-    const int nx = min(4, L.w - x0);
-    if (L.copy) {
-        for (int j = 0; j < nx; ++j) out |= (uint32_t)src[(size_t)y * S.pitch + x0 + j] << (8 * j);
-    } else if (L.area2) {
-        const uint8_t* s0 = src + (size_t)(2 * y) * S.pitch;
-        const uint8_t* s1 = s0 + S.pitch;
-        for (int j = 0; j < nx; ++j) {
-            int x = 2 * (x0 + j);
-            out |= (uint32_t)((s0[x] + s0[x + 1] + s1[x] + s1[x + 1] + 2) >> 2) << (8 * j);
-        }
-    } else {
-        const int16_t* xofs = rtab + L.rtab_off;
-        const int16_t* alpha = xofs + L.w;
-        const int16_t* yofs = alpha + 2 * L.w;
-        const int16_t* beta = yofs + L.h;
-        const int sy0 = yofs[y];
-        const int r0 = min(max(sy0, 0), S.h - 1), r1 = min(max(sy0 + 1, 0), S.h - 1);
-        const uint8_t* s0 = src + (size_t)r0 * S.pitch;
-        const uint8_t* s1 = src + (size_t)r1 * S.pitch;
-        const int b0 = beta[2 * y], b1 = beta[2 * y + 1];
-        for (int j = 0; j < nx; ++j) {
-            const int x = x0 + j;
-            const int sx = xofs[x];
-            int h0, h1;
-            if (x < L.xmax) {
-                const int a0 = alpha[2 * x], a1 = alpha[2 * x + 1];
-                h0 = s0[sx] * a0 + s0[sx + 1] * a1;
-                h1 = s1[sx] * a0 + s1[sx + 1] * a1;
-            } else {
-                h0 = s0[sx] * 2048;
-                h1 = s1[sx] * 2048;
-            }
-            int v;
-            if (x < L.rsimd_end) {
-                // VResizeLinearVec_32s8u: packs(>>4), mulhi, adds, (+2)>>2, packus
-                int t0 = min(max(h0 >> 4, -32768), 32767);
-                int t1 = min(max(h1 >> 4, -32768), 32767);
-                int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
-                m = min(max(m, -32768), 32767);
-                m = min(max(m + 2, -32768), 32767);
-                v = sat_u8(m >> 2);
-            } else {
-                v = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);   // FixedPtCast<int,uchar,22>
-            }
-            out |= (uint32_t)v << (8 * j);
-        }
-    }
-    if (nx == 4) {
-        *(uint32_t*)(dst + x0) = out;
-    } else {
-        for (int j = 0; j < nx; ++j) dst[x0 + j] = (uint8_t)(out >> (8 * j));
-    }
-}
-
-// ----------------------------------------------------------------------------------------
-// 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of every level: 64x16 output tile per
-// workgroup, source tile + row pass staged in LDS.
-// ----------------------------------------------------------------------------------------
-#define BT_W 64
-#define BT_H 16
-__global__ __launch_bounds__(256) void k_blur(const Geometry* __restrict__ g,
-                                              const uint8_t* __restrict__ pyr,
-                                              uint8_t* __restrict__ blur) {
-    __shared__ uint8_t tin[BT_H + 6][BT_W + 8];
-    __shared__ int trow[BT_H + 6][BT_W + 1];
-    const int b = blockIdx.y;
-    const int t = blockIdx.x;
-    int level = 0;
-    while (level + 1 < g->nlevels && t >= g->blur_tile_begin[level + 1]) ++level;
-    const LevelGeom& L = g->lv[level];
-    const int tl = t - g->blur_tile_begin[level];
-    const int ntx = (L.w + BT_W - 1) / BT_W;
-    const int X0 = (tl % ntx) * BT_W, Y0 = (tl / ntx) * BT_H;
-    const uint8_t* src = pyr + b * g->pyr_bytes + L.off;
-    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
-        const int r = i / (BT_W + 6), c = i % (BT_W + 6);
-        const int yy = reflect101(Y0 + r - 3, L.h), xx = reflect101(X0 + c - 3, L.w);
-        tin[r][c] = src[(size_t)yy * L.pitch + xx];
-    }
-    __syncthreads();
-    const int k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3];
-    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
-        const int r = i / BT_W, c = i % BT_W;
-        const uint8_t* p = &tin[r][c];
-        trow[r][c] = k0 * p[0] + k1 * p[1] + k2 * p[2] + k3 * p[3] + g->taps[4] * p[4] +
-                     g->taps[5] * p[5] + g->taps[6] * p[6];
-    }
-    __syncthreads();
-    const float f0 = (float)k3 * (1.f / 65536.f), f1 = (float)g->taps[4] * (1.f / 65536.f),
-                f2 = (float)g->taps[5] * (1.f / 65536.f), f3 = (float)g->taps[6] * (1.f / 65536.f);
-    uint8_t* dst = blur + b * g->pyr_bytes + L.off;
-    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
-        const int r = i / BT_W, c = i % BT_W;
-        const int x = X0 + c, y = Y0 + r;
-        if (x >= L.w || y >= L.h) continue;
-        const int c0 = trow[r + 3][c];
-        const int p1 = trow[r + 4][c] + trow[r + 2][c];
-        const int p2 = trow[r + 5][c] + trow[r + 1][c];
-        const int p3 = trow[r + 6][c] + trow[r][c];
-        int v;
-        if (x < L.bsimd_end) {
-            // SymmColumnVec_32s8u: float accumulate, cvtps2dq (half-even), packs, packus
-            float s = (float)c0 * f0;
-            s = s + 0.0f;
-            s = s + (float)p1 * f1;
-            s = s + (float)p2 * f2;
-            s = s + (float)p3 * f3;
-            v = (int)rintf(s);
-            v = min(max(v, -32768), 32767);
-        } else {
-            const int s0 = k3 * c0 + g->taps[4] * p1 + g->taps[5] * p2 + g->taps[6] * p3;
-            v = (s0 + (1 << 15)) >> 16;   // FixedPtCastEx<int,uchar>(16)
-        }
-        dst[(size_t)y * L.pitch + x] = sat_u8(v);
-    }
-}
 
 // ----------------------------------------------------------------------------------------
 // FAST-9 per cell: one wave per 30px cell.  The reference calls cv::FAST on every cell ROI
@@ -248,6 +82,7 @@ __device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, i
     const int m = p[0];
     if (m <= t) return false;
     const int s = m - 1;
+    if (s <= 0) return false;   // every neighbour score is >= 0
     score = s;
 #define ORBX_NB(o) { const int q = p[o]; if (q > t && q - 1 >= s) return false; }
     ORBX_NB(-mw - 1) ORBX_NB(-mw) ORBX_NB(-mw + 1) ORBX_NB(-1) ORBX_NB(1)
@@ -255,6 +90,9 @@ __device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, i
 #undef ORBX_NB
     return true;
 }
+
+#define FAST_LIST 512
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
                                               const CellDesc* __restrict__ cells,
@@ -265,43 +103,66 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int ci = blockIdx.x * 4 + wid;
-    const bool active = ci < g->n_cells;
+    if (ci >= g->n_cells) return;   // no block-level barriers below: waves are independent
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
-    uint8_t* roi = smem + wid * (roi_cap + mb_cap);
+    uint8_t* roi = smem + wid * (roi_cap + mb_cap + FAST_LIST * 2);
     uint8_t* mb = roi + roi_cap;
-    CellDesc c;
-    int rows = 0, cols = 0, dh = 0, dw = 0;
-    if (active) {
-        c = cells[ci];
-        rows = c.rows; cols = c.cols;
-        dh = rows - 6; dw = cols - 6;
-        const LevelGeom& L = g->lv[c.level];
-        const uint8_t* src = pyr + b * g->pyr_bytes + L.off + (size_t)c.ini_y * L.pitch + c.ini_x;
-        for (int i = lane; i < rows * cols; i += 64) {
-            const int r = i / cols, cc = i - r * cols;
-            roi[i] = src[(size_t)r * L.pitch + cc];
-        }
-        if (dh > 0 && dw > 0)
-            for (int i = lane; i < (dh + 2) * (dw + 2); i += 64) mb[i] = 0;
-    }
-    __syncthreads();
-    const int mw = dw + 2;
-    const int npx = (dh > 0 && dw > 0) ? dh * dw : 0;
-    for (int p = lane; p < npx; p += 64) {
-        const int rr = p / dw, cc = p - rr * dw;
-        const int m = fast_arc_score(roi, cols, rr + 3, cc + 3);
-        mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
-    }
-    __syncthreads();
-    if (!active) return;
+    int16_t* list = (int16_t*)(mb + mb_cap);
+    const CellDesc c = cells[ci];
+    const int rows = c.rows, cols = c.cols, dh = rows - 6, dw = cols - 6;
     int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
-    if (npx == 0) {
+    if (dh <= 0 || dw <= 0) {
         if (lane == 0) *cnt_out = 0;
         return;
     }
-    // pass 1: any corner at iniThFAST in this cell?
+    const LevelGeom& L = g->lv[c.level];
+    // ROI rows staged as aligned dwords, all loads of a lane in flight before the LDS stores
+    const int ax0 = c.ini_x & ~3, xo = c.ini_x - ax0;
+    const int ndw = (xo + cols + 3) >> 2;
+    const int rp = ndw * 4;   // LDS row pitch of the ROI
+    stage_dwords<64>(pyr + (size_t)b * g->pyr_bytes + L.off + (size_t)c.ini_y * L.pitch + ax0,
+                     L.pitch, rows, ndw, (uint32_t*)roi, ndw, lane);
+    roi += xo;
+    const int mw = dw + 2;
+    for (int i = lane; i < (dh + 2) * mw; i += 64) mb[i] = 0;
+    wave_sync();
+    const int npx = dh * dw;
+    // 1. compass pre-test at the lower threshold: a 9-pixel arc over threshold t contains two
+    //    neighbouring compass pixels (circle indices i, i+4) both beyond t on the same side.
+    const int tq = min(g->ini_th, g->min_th);
+    for (int p0 = 0; p0 < npx; p0 += FAST_LIST) {
+        int nlist = 0;
+        for (int k = 0; k < FAST_LIST && p0 + k < npx; k += 64) {
+            const int p = p0 + k + lane;
+            bool pass = false;
+            if (p < npx) {
+                const int rr = p / dw + 3, cc = p - (p / dw) * dw + 3;
+                const uint8_t* q = roi + rr * rp + cc;
+                const int v = q[0];
+                const int n0 = q[3 * rp], n4 = q[3], n8 = q[-3 * rp], n12 = q[-3];
+                const int hi = v + tq, lo = v - tq;
+                const bool b0 = n0 > hi, b4 = n4 > hi, b8 = n8 > hi, b12 = n12 > hi;
+                const bool d0 = n0 < lo, d4 = n4 < lo, d8 = n8 < lo, d12 = n12 < lo;
+                pass = (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0) || (d0 && d4) ||
+                       (d4 && d8) || (d8 && d12) || (d12 && d0);
+            }
+            const uint64_t m = __ballot(pass);
+            if (pass) list[nlist + lanes_below(m)] = (int16_t)p;
+            nlist += __popcll(m);
+        }
+        wave_sync();
+        // 2. full arc score for the survivors only (dense across lanes)
+        for (int j = lane; j < nlist; j += 64) {
+            const int p = list[j];
+            const int rr = p / dw, cc = p - rr * dw;
+            const int m = fast_arc_score(roi, rp, rr + 3, cc + 3);
+            mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
+        }
+        wave_sync();
+    }
+    // 3. any corner at iniThFAST in this cell?  (else fall back to minThFAST, :833-837)
     int t = g->ini_th;
-    int found = 0;
+    bool found = false;
     for (int p0 = 0; p0 < npx && !found; p0 += 64) {
         const int p = p0 + lane;
         int s;
@@ -313,17 +174,16 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
         found = __ballot(k) != 0;
     }
     if (!found) t = g->min_th;
-    // pass 2: ordered compaction (raster order inside the cell, as cv::FAST emits)
+    // 4. ordered compaction (raster order inside the cell, as cv::FAST emits)
     uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
-    const LevelGeom& L = g->lv[c.level];
-    (void)L;
     int base = 0;
     for (int p0 = 0; p0 < npx; p0 += 64) {
         const int p = p0 + lane;
         int s = 0, rr = 0, cc = 0;
         bool k = false;
         if (p < npx) {
-            rr = p / dw; cc = p - rr * dw;
+            rr = p / dw;
+            cc = p - rr * dw;
             k = fast_nms_kp(mb, mw, rr, cc, t, s);
         }
         const uint64_t m = __ballot(k);
@@ -336,6 +196,11 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
         base += __popcll(m);
     }
     if (lane == 0) *cnt_out = min(base, c.cap);
+}
+
+size_t fast_lds_bytes(const Geometry& G) {
+    const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
+    return (size_t)4 * (roi_cap + mb_cap + FAST_LIST * 2);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -788,31 +653,12 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const Geometry& G = *a.hg;
     KernelTimer dummy;
     KernelTimer& T = a.timer ? *a.timer : dummy;
-    hipEvent_t e;
-    {
-        dim3 grid((G.lv[0].w + 1023) / 1024, G.lv[0].h, a.batch);
-        e = T.start(st);
-        hipLaunchKernelGGL(k_copy_level0, grid, dim3(256), 0, st, a.dg, a.d_imgs, a.stride,
-                           a.batch_stride, a.pyr);
-        T.stop(K_COPY0, e, st);
-    }
-    for (int l = 1; l < G.nlevels; ++l) {
-        dim3 grid((G.lv[l].w + 1023) / 1024, G.lv[l].h, a.batch);
-        e = T.start(st);
-        hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, st, a.dg, a.rtab, a.pyr, l);
-        T.stop(K_RESIZE, e, st);
-    }
-    e = T.start(st);
-    hipLaunchKernelGGL(k_blur, dim3(G.blur_tiles, a.batch), dim3(256), 0, st, a.dg, a.pyr, a.blur);
-    T.stop(K_BLUR, e, st);
-    {
-        const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
-        const size_t lds = (size_t)4 * (roi_cap + mb_cap);
-        e = T.start(st);
-        hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 3) / 4, a.batch), dim3(256), lds, st, a.dg,
-                           a.cells, a.pyr, a.ccnt, a.cand);
-        T.stop(K_FAST, e, st);
-    }
+    hipError_t err = launch_levels(a, st);
+    if (err != hipSuccess) return err;
+    hipEvent_t e = T.start(st);
+    hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 3) / 4, a.batch), dim3(256), fast_lds_bytes(G), st,
+                       a.dg, a.cells, a.pyr, a.ccnt, a.cand);
+    T.stop(K_FAST, e, st);
     e = T.start(st);
     hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
                        a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
@@ -840,10 +686,16 @@ size_t octree_lds_bytes(int ncap, int kcap) {
 
 namespace orbx {
 hipError_t prepare_stereo(size_t lds);
+hipError_t prepare_level(size_t lds);
 // Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).
-hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds) {
+hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
+                           size_t fast_lds) {
     hipError_t e = hipFuncSetAttribute((const void*)k_octree,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)fast_lds);
+    if (e == hipSuccess) e = prepare_level(level_lds);
     if (e != hipSuccess) return e;
     return prepare_stereo(stereo_lds);
 }

@@ -40,6 +40,7 @@ struct LevelGeom {
     int area2;              // resize at exactly 1/2: INTER_AREA 2x2 fast path
     int copy;               // resize to the same size: plain copy
     int patch_size;         // (int)(31*scale)
+    int ntx, nty;           // k_level tiles of this level
 };
 
 struct CellDesc {
@@ -67,6 +68,8 @@ struct Geometry {
     int umax[16];           // src/ORBextractor.cc:454-469
     int ini_th, min_th;     // FAST thresholds, clamped to [0, 255]
     int stereo_win;         // row-bucket search half-window: ceil(2*max scale) + 2
+    int ltw, lth;           // k_level output tile
+    int win_cap;            // k_level: largest staged source window (bytes)
     LevelGeom lv[ORBX_MAX_LEVELS];
 };
 

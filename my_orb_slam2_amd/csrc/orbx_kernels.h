@@ -10,7 +10,7 @@
 
 namespace orbx {
 
-enum KernelId { K_COPY0 = 0, K_RESIZE, K_BLUR, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_COUNT };
+enum KernelId { K_LEVEL = 0, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_COUNT };
 
 // Optional per-kernel HIP-event timing (orbx_profile_*): events bracket each launch on the
 // stream it is launched on; durations are read back by collect().
@@ -66,9 +66,12 @@ struct ExtractLaunch {
     const Geometry* dg;        // device copy
     const CellDesc* cells;     // device
     const int16_t* rtab;       // device
-    const uint8_t* d_imgs;
+    const uint8_t* d_imgs;      // images [0, split)
+    const uint8_t* d_imgs2;     // images [split, batch) (stereo: right views)
+    int split;
     size_t stride, batch_stride;
     int batch;
+    size_t level_lds;
     uint8_t* pyr;
     uint8_t* blur;
     int* ccnt;
@@ -105,6 +108,9 @@ struct StereoLaunch {
 };
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
+hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st);
+size_t level_lds_bytes(int ltw, int lth, int win_cap);
+size_t fast_lds_bytes(const Geometry& g);
 size_t octree_lds_bytes(int ncap, int kcap);
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st);
 size_t stereo_lds_bytes(int kp_cap, int height);

@@ -1,0 +1,374 @@
+// orbx_pyramid.hip — one fused kernel per pyramid level: level l from level l-1
+// (ComputePyramid, src/ORBextractor.cc:1129-1154) and its 7x7 Gaussian (operator(),
+// :1106-1108) in the same pass.
+//
+// A 256-thread workgroup owns a 128 x 32 output tile of level l.  It stages the source
+// window of the tile + the 3-pixel blur halo (coordinates reflected as BORDER_REFLECT_101)
+// in LDS with aligned dword loads (all loads of a thread in flight before its first LDS
+// store), computes level l on tile + halo in groups of 4 adjacent pixels (the window bytes
+// of a group come from 3 dword LDS reads per source row; OpenCV INTER_LINEAR fixed-point
+// coefficients from per-group packed tables), writes the tile, then runs the separable
+// blur on 4-pixel groups (3 dword reads per row pass, 7 b64 reads per column pass) and
+// writes the blurred tile.  Level l is read from HBM once (by level l+1's launch).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_kernels.h"
+
+namespace orbx {
+
+#define LT_W 128              // output tile width  (32 groups of 4)
+#define LT_H 32               // output tile height
+#define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
+#define LT_HR (LT_H + 6)      // halo rows: y = Y0-3 .. Y0+LT_H+2
+#define LT_GW (LT_W / 4)      // output groups per row
+
+__device__ __forceinline__ int reflect101_i(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+__device__ __forceinline__ int sat8(int v) { return min(max(v, 0), 255); }
+
+// min / max of reflect101(p) over p in [lo, hi].
+__device__ __forceinline__ void reflected_range(int lo, int hi, int len, int& mn, int& mx) {
+    mn = 1 << 30;
+    mx = -1;
+    const int a = max(lo, 0), b = min(hi, len - 1);
+    if (a <= b) { mn = a; mx = b; }
+    for (int p = lo; p < min(0, hi + 1); ++p) {
+        const int r = reflect101_i(p, len);
+        mn = min(mn, r); mx = max(mx, r);
+    }
+    for (int p = max(len, lo); p <= hi; ++p) {
+        const int r = reflect101_i(p, len);
+        mn = min(mn, r); mx = max(mx, r);
+    }
+}
+
+// byte k (runtime, 0..11) of the 12-byte little-endian sequence d0 d1 d2
+__device__ __forceinline__ int byte12(uint32_t d0, uint32_t d1, uint32_t d2, int k) {
+    const uint32_t v = k < 4 ? d0 : (k < 8 ? d1 : d2);
+    return (int)((v >> ((k & 3) * 8)) & 255u);
+}
+
+// OpenCV INTER_LINEAR 8U value from the two horizontal sums (VResizeLinear + cast).
+__device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1, bool simd) {
+    if (simd) {   // VResizeLinearVec_32s8u: packs(>>4), mulhi, adds, (+2)>>2, packus
+        const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
+        int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
+        m = min(max(m, -32768), 32767);
+        m = min(m + 2, 32767);
+        return sat8(m >> 2);
+    }
+    return sat8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);   // FixedPtCast<int, uchar, 22>
+}
+
+__global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
+                                               const int16_t* __restrict__ rtab,
+                                               const uint8_t* __restrict__ in0,
+                                               const uint8_t* __restrict__ in1, int split,
+                                               size_t stride, size_t bstride,
+                                               uint8_t* __restrict__ pyr,
+                                               uint8_t* __restrict__ blur, int level) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom& L = g->lv[level];
+    const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
+    const int X0 = tx * LT_W, Y0 = ty * LT_H;
+    const int vw = min(LT_W, L.w - X0), vh = min(LT_H, L.h - Y0);
+
+    uint8_t* p = smem;
+    auto take = [&](size_t n) { uint8_t* r = p; p += (n + 15) & ~(size_t)15; return r; };
+    uint32_t* lvl = (uint32_t*)take((size_t)LT_HR * LT_G * 4);      // [38][34] dwords
+    uint16_t* rows = (uint16_t*)take((size_t)LT_HR * LT_W * 2);     // [38][128] row sums
+    uint2* cgrp = (uint2*)take((size_t)LT_G * 8);                    // per group: 4 x sx (u16)
+    uint32_t* cinf = (uint32_t*)take((size_t)LT_G * 4);              // per group: flags
+    uint4* calp = (uint4*)take((size_t)LT_G * 16);                   // per group: 4 x (a0, a1)
+    uint2* rinf = (uint2*)take((size_t)LT_HR * 8);                   // per row: ry0, ry1, b0, b1
+    int* sc = (int*)take(16 * 4);
+    uint8_t* win = p;                                                // source window
+
+    const int mode = level == 0 ? 0 : (L.copy ? 1 : (L.area2 ? 2 : 3));
+    const LevelGeom& S = g->lv[level > 0 ? level - 1 : 0];
+    const int16_t* xofs = rtab + L.rtab_off;
+    const int16_t* alpha = xofs + L.w;
+    const int16_t* yofs = alpha + 2 * L.w;
+    const int16_t* beta = yofs + L.h;
+    // needed halo ranges (level coordinates, before reflection)
+    const int nx0 = X0 - 3, nx1 = X0 + vw + 2, ny0 = Y0 - 3, ny1 = Y0 + vh + 2;
+
+    // ---- 1. source window ----
+    if (tid == 0) {
+        int x0, x1, y0, y1;
+        if (mode == 3) {
+            int mnx, mxx, mny, mxy;
+            reflected_range(nx0, nx1, L.w, mnx, mxx);
+            reflected_range(ny0, ny1, L.h, mny, mxy);
+            x0 = xofs[mnx] & ~3;
+            x1 = min((int)xofs[mxx] + 1, S.w - 1);
+            y0 = min(max((int)yofs[mny], 0), S.h - 1);
+            y1 = min(max((int)yofs[mxy] + 1, 0), S.h - 1);
+        } else {   // copy of the input (mode 0) or of level l-1 (mode 1); mode 2 reads direct
+            x0 = max(X0 - 4, 0);
+            x1 = min(X0 + LT_W + 3, L.w - 1);
+            y0 = max(Y0 - 3, 0);
+            y1 = min(Y0 + LT_H + 2, L.h - 1);
+        }
+        sc[0] = x0; sc[1] = x1 - x0 + 1; sc[2] = y0; sc[3] = y1 - y0 + 1;
+    }
+    __syncthreads();
+    const int wx0 = sc[0], WWb = sc[1], wy0 = sc[2], WH = sc[3];
+    // window row pitch; modes 0/1 place x at column x - (X0 - 4) so that groups are dword-aligned
+    const int WP = (mode == 3) ? ((WWb + 3) & ~3) : LT_G * 4;
+    const int wcol0 = (mode == 3) ? 0 : wx0 - (X0 - 4);
+    if (mode == 0) {
+        const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
+        stage_bytes<256>(src + (size_t)wy0 * stride + wx0, stride, WH, WWb, win + wcol0, WP, tid);
+    } else if (mode == 1) {
+        const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;   // wx0 is a multiple of 4
+        stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, (WWb + 3) >> 2,
+                          (uint32_t*)(win + wcol0), WP / 4, tid);
+    } else if (mode == 3) {
+        const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;
+        stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4, (uint32_t*)win,
+                          WP / 4, tid);
+    }
+    // per-group column tables and per-row tables of the halo
+    if (tid < LT_G) {
+        const int q = tid;
+        int sx[4];
+        uint32_t fl = 0;
+        uint32_t al[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 4; ++j) {
+            const int xr = reflect101_i(X0 - 4 + 4 * q + j, L.w);
+            if (mode == 3) {
+                sx[j] = xofs[xr] - wx0;
+                al[j] = (uint32_t)(uint16_t)alpha[2 * xr] | ((uint32_t)(uint16_t)alpha[2 * xr + 1] << 16);
+                fl |= (uint32_t)((xr < L.xmax ? 1 : 0) | (xr < L.rsimd_end ? 2 : 0)) << (2 * j);
+            } else {
+                sx[j] = (mode == 2) ? xr : xr - (X0 - 4);   // window column (modes 0/1)
+            }
+            // Pixels of a group outside the needed halo may reflect anywhere; keep their
+            // (unused) reads inside the window.  Needed pixels are always inside already.
+            if (mode == 3) sx[j] = min(max(sx[j], 0), max(WWb - 1, 0));
+            else if (mode != 2) sx[j] = min(max(sx[j], 0), LT_G * 4 - 1);
+        }
+        // contig: x..x+3 unreflected and dword-aligned in the window (modes 0/1)
+        const bool contig = sx[1] == sx[0] + 1 && sx[2] == sx[0] + 2 && sx[3] == sx[0] + 3 &&
+                            (sx[0] & 3) == 0;
+        // simple: the group's taps lie in the 12 bytes from (sx0 & ~3) (mode 3)
+        const int o0 = sx[0] & 3;
+        const bool simple = sx[1] >= sx[0] && sx[2] >= sx[1] && sx[3] >= sx[2] &&
+                            o0 + (sx[3] - sx[0]) + 1 <= 11;
+        cgrp[q] = make_uint2((uint32_t)sx[0] | ((uint32_t)sx[1] << 16),
+                             (uint32_t)sx[2] | ((uint32_t)sx[3] << 16));
+        cinf[q] = fl | (contig ? 0x100u : 0u) | (simple ? 0x200u : 0u);
+        calp[q] = make_uint4(al[0], al[1], al[2], al[3]);
+    } else if (tid >= 64 && tid < 64 + LT_HR) {
+        const int r = tid - 64;
+        const int yr = reflect101_i(Y0 - 3 + r, L.h);
+        if (mode == 3) {
+            const int sy = yofs[yr];
+            const uint32_t y0r = (uint32_t)(min(max(sy, 0), S.h - 1) - wy0);
+            const uint32_t y1r = (uint32_t)(min(max(sy + 1, 0), S.h - 1) - wy0);
+            rinf[r] = make_uint2(y0r | (y1r << 16),
+                                 (uint32_t)(uint16_t)beta[2 * yr] | ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16));
+        } else {
+            rinf[r] = make_uint2((uint32_t)(mode == 2 ? yr : yr - wy0), 0u);
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. level l on tile + halo, 4 pixels per item ----
+    const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
+    for (int i = tid; i < LT_HR * LT_G; i += 256) {
+        const int hr = i / LT_G, q = i - hr * LT_G;
+        const int y = Y0 - 3 + hr, xg = X0 - 4 + 4 * q;
+        uint32_t out = 0;
+        if (y >= ny0 && y <= ny1 && xg + 3 >= nx0 && xg <= nx1) {
+            const uint2 cg = cgrp[q];
+            const uint32_t ci = cinf[q];
+            const uint2 ri = rinf[hr];
+            const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
+                               (int)(cg.y >> 16)};
+            if (mode == 3) {
+                const uint4 al = calp[q];
+                const uint32_t als[4] = {al.x, al.y, al.z, al.w};
+                const int r0 = (int)(ri.x & 0xFFFF), r1 = (int)(ri.x >> 16);
+                const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
+                const uint8_t* w0 = win + r0 * WP;
+                const uint8_t* w1 = win + r1 * WP;
+                if (ci & 0x200u) {
+                    const int base = xs[0] & ~3;
+                    const uint32_t* d0p = (const uint32_t*)(w0 + base);
+                    const uint32_t* d1p = (const uint32_t*)(w1 + base);
+                    const uint32_t a0 = d0p[0], a1 = d0p[1], a2 = d0p[2];
+                    const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int k = xs[j] - base;
+                        const int f = (int)(ci >> (2 * j)) & 3;
+                        int h0, h1;
+                        if (f & 1) {
+                            const int aa = (int)(int16_t)(als[j] & 0xFFFF), ab = (int)(int16_t)(als[j] >> 16);
+                            h0 = byte12(a0, a1, a2, k) * aa + byte12(a0, a1, a2, k + 1) * ab;
+                            h1 = byte12(c0, c1, c2, k) * aa + byte12(c0, c1, c2, k + 1) * ab;
+                        } else {
+                            h0 = byte12(a0, a1, a2, k) * 2048;
+                            h1 = byte12(c0, c1, c2, k) * 2048;
+                        }
+                        out |= (uint32_t)vresize(h0, h1, b0, b1, (f & 2) != 0) << (8 * j);
+                    }
+                } else {   // reflected border group: bytes one by one
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int sxj = xs[j];
+                        const int f = (int)(ci >> (2 * j)) & 3;
+                        int h0, h1;
+                        if (f & 1) {
+                            const int aa = (int)(int16_t)(als[j] & 0xFFFF), ab = (int)(int16_t)(als[j] >> 16);
+                            h0 = w0[sxj] * aa + w0[sxj + 1] * ab;
+                            h1 = w1[sxj] * aa + w1[sxj + 1] * ab;
+                        } else {
+                            h0 = w0[sxj] * 2048;
+                            h1 = w1[sxj] * 2048;
+                        }
+                        out |= (uint32_t)vresize(h0, h1, b0, b1, (f & 2) != 0) << (8 * j);
+                    }
+                }
+            } else if (mode == 2) {
+                const int yr = (int)ri.x;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint8_t* s0 = src2 + (size_t)(2 * yr) * S.pitch + 2 * xs[j];
+                    out |= (uint32_t)((s0[0] + s0[1] + s0[S.pitch] + s0[S.pitch + 1] + 2) >> 2) << (8 * j);
+                }
+            } else {
+                const uint8_t* wr = win + (int)(ri.x & 0xFFFF) * WP;
+                if (ci & 0x100u) {
+                    out = *(const uint32_t*)(wr + xs[0]);
+                } else {
+                    out = (uint32_t)wr[xs[0]] | ((uint32_t)wr[xs[1]] << 8) |
+                          ((uint32_t)wr[xs[2]] << 16) | ((uint32_t)wr[xs[3]] << 24);
+                }
+            }
+        }
+        lvl[hr * LT_G + q] = out;
+    }
+    __syncthreads();
+
+    uint8_t* dlev = pyr + (size_t)b * g->pyr_bytes + L.off;
+    uint8_t* dblur = blur + (size_t)b * g->pyr_bytes + L.off;
+    const int ng = (vw + 3) >> 2;
+    // ---- 3. level tile out (output x = X0 + 4g  <->  halo group g + 1) ----
+    for (int i = tid; i < vh * LT_GW; i += 256) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (gq >= ng) continue;
+        const uint32_t v = lvl[(r + 3) * LT_G + gq + 1];
+        uint8_t* d = dlev + (size_t)(Y0 + r) * L.pitch + X0 + 4 * gq;
+        if (4 * gq + 4 <= vw) *(uint32_t*)d = v;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
+    }
+    // ---- 4. blur row pass (RowFilter<uchar,int>: exact; sums <= 257*255 fit u16) ----
+    const int k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3];
+    const int k4 = g->taps[4], k5 = g->taps[5], k6 = g->taps[6];
+    for (int i = tid; i < (vh + 6) * LT_GW; i += 256) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (gq >= ng) continue;
+        const uint32_t* s = lvl + r * LT_G + gq;   // bytes of x = X0 + 4gq - 4 .. + 7
+        const uint32_t d0 = s[0], d1 = s[1], d2 = s[2];
+        int px[12];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            px[k] = (int)((d0 >> (8 * k)) & 255u);
+            px[4 + k] = (int)((d1 >> (8 * k)) & 255u);
+            px[8 + k] = (int)((d2 >> (8 * k)) & 255u);
+        }
+        uint32_t lo, hi;
+        int sum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)   // x = X0+4gq+j needs halo bytes 1+j .. 7+j
+            sum[j] = k0 * px[1 + j] + k1 * px[2 + j] + k2 * px[3 + j] + k3 * px[4 + j] +
+                     k4 * px[5 + j] + k5 * px[6 + j] + k6 * px[7 + j];
+        lo = (uint32_t)sum[0] | ((uint32_t)sum[1] << 16);
+        hi = (uint32_t)sum[2] | ((uint32_t)sum[3] << 16);
+        *(uint2*)(rows + r * LT_W + 4 * gq) = make_uint2(lo, hi);
+    }
+    __syncthreads();
+    // ---- 5. blur column pass (SymmColumnFilter / SymmColumnVec_32s8u) ----
+    const float f0 = (float)k3 * (1.f / 65536.f), f1 = (float)k4 * (1.f / 65536.f),
+                f2 = (float)k5 * (1.f / 65536.f), f3 = (float)k6 * (1.f / 65536.f);
+    for (int i = tid; i < vh * LT_GW; i += 256) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (gq >= ng) continue;
+        uint2 v[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v[k] = *(const uint2*)(rows + (r + k) * LT_W + 4 * gq);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto at = [&](int k) {
+                const uint32_t w = (j < 2) ? v[k].x : v[k].y;
+                return (int)((w >> (16 * (j & 1))) & 0xFFFFu);
+            };
+            const int c0 = at(3);
+            const int p1 = at(4) + at(2), p2 = at(5) + at(1), p3 = at(6) + at(0);
+            int val;
+            if (X0 + 4 * gq + j < L.bsimd_end) {
+                float s = (float)c0 * f0;
+                s = s + 0.0f;
+                s = s + (float)p1 * f1;
+                s = s + (float)p2 * f2;
+                s = s + (float)p3 * f3;
+                val = min(max((int)rintf(s), -32768), 32767);
+            } else {
+                val = (k3 * c0 + k4 * p1 + k5 * p2 + k6 * p3 + (1 << 15)) >> 16;
+            }
+            packed |= (uint32_t)sat8(val) << (8 * j);
+        }
+        uint8_t* d = dblur + (size_t)(Y0 + r) * L.pitch + X0 + 4 * gq;
+        if (4 * gq + 4 <= vw) *(uint32_t*)d = packed;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+    }
+}
+
+size_t level_lds_bytes(int ltw, int lth, int win_cap) {
+    (void)ltw;
+    (void)lth;
+    auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    size_t s = r((size_t)LT_HR * LT_G * 4) + r((size_t)LT_HR * LT_W * 2) + r(LT_G * 8) +
+               r(LT_G * 4) + r(LT_G * 16) + r(LT_HR * 8) + r(64);
+    return s + r((size_t)win_cap + 16);
+}
+
+hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
+    const Geometry& G = *a.hg;
+    KernelTimer dummy;
+    KernelTimer& T = a.timer ? *a.timer : dummy;
+    for (int l = 0; l < G.nlevels; ++l) {
+        const LevelGeom& L = G.lv[l];
+        hipEvent_t e = T.start(st);
+        hipLaunchKernelGGL(k_level, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
+                           a.rtab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
+                           a.blur, l);
+        T.stop(K_LEVEL, e, st);
+    }
+    return hipGetLastError();
+}
+
+hipError_t prepare_level(size_t lds) {
+    return hipFuncSetAttribute((const void*)k_level, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds);
+}
+
+}  // namespace orbx

@@ -115,6 +115,13 @@ class ORBextractor:
         return out
 
     # ---- batched device path ----
+    def prepare(self, width: int, height: int, batch: int) -> int:
+        """Allocate the workspace for `batch` images of width x height; returns kp_cap."""
+        kc = ctypes.c_int(0)
+        check("orbx_extractor_prepare", self._L.orbx_extractor_prepare(
+            self._h, width, height, batch, ctypes.byref(kc)))
+        return kc.value
+
     def extract_batch_device(self, images, stream=None):
         """Extract a [B, H, W] uint8 CUDA/HIP tensor already resident in HBM."""
         B, H, W = images.shape
@@ -170,41 +177,50 @@ def compute_stereo_matches(left: ORBextractor, right: ORBextractor, mbf: float, 
 class StereoBatch:
     """Batched stereo front-end: B rectified pairs per call, all on one HIP stream.
 
-    Runs ORBextractor on the B left and the B right images (two handles, as the reference's
-    Frame holds two extractors, src/Frame.cc:89-92) and ComputeStereoMatches per pair.
-    Outputs stay in HBM (torch tensors / the handles' workspaces).
+    The reference's stereo Frame runs two ORBextractor objects with the same parameters on
+    the left and right images (src/Frame.cc:89-92, Tracking.cc:136-139) and then
+    ComputeStereoMatches (:102).  Here one handle extracts the 2B views as one batch
+    (images [0,B) left, [B,2B) right) and matches image i with image B+i.  Outputs stay in
+    HBM; ``fetch`` copies them to host.
     """
 
     def __init__(self, batch: int, nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20,
                  minThFAST=7, cv_simd=1, device=0):
         import torch
         self.batch = batch
-        self.left = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
-                                 cv_simd=cv_simd, max_batch=batch, device=device)
-        self.right = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
-                                  cv_simd=cv_simd, max_batch=batch, device=device)
+        self.ext = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                cv_simd=cv_simd, max_batch=2 * batch, device=device)
         self.device = torch.device("cuda", device)
         self.uR = self.depth = self.nvalid = None
 
     def __call__(self, left_imgs, right_imgs, mbf: float, mb: float, stream=None):
         import torch
+        B, H, W = left_imgs.shape
+        assert right_imgs.shape == left_imgs.shape
+        assert left_imgs.stride() == right_imgs.stride(), "left/right tensors need equal strides"
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        self.left.extract_batch_device(left_imgs, st)
-        self.right.extract_batch_device(right_imgs, st)
-        kc = self.left.batch_view().kp_cap
-        B = left_imgs.shape[0]
-        if self.uR is None or self.uR.shape != (B, kc):
+        if self.uR is None or self.uR.shape[0] != B:
+            kc = self._kp_cap(W, H)
             self.uR = torch.empty((B, kc), dtype=torch.float32, device=self.device)
             self.depth = torch.empty((B, kc), dtype=torch.float32, device=self.device)
             self.nvalid = torch.empty((B,), dtype=torch.int32, device=self.device)
-        check("orbx_stereo_match_batch_device", self.left._L.orbx_stereo_match_batch_device(
-            self.left._h, self.right._h, mbf, mb, ptr(self.uR), ptr(self.depth),
-            ptr(self.nvalid), ctypes.c_void_p(st)))
+        stride = left_imgs.stride(1) * left_imgs.element_size()
+        bstride = left_imgs.stride(0) * left_imgs.element_size()
+        check("orbx_stereo_frames_device", self.ext._L.orbx_stereo_frames_device(
+            self.ext._h, ptr(left_imgs), ptr(right_imgs), B, W, H, stride, bstride, mbf, mb,
+            ptr(self.uR), ptr(self.depth), ptr(self.nvalid), ctypes.c_void_p(st)))
         return self.uR, self.depth, self.nvalid
 
-    def outputs(self, side: str = "left"):
-        """(keypoints [B,kp_cap] structured-view tensor bytes, desc, nkp) device tensors."""
-        import torch
-        ext = self.left if side == "left" else self.right
-        v = ext.batch_view()
-        return v
+    def _kp_cap(self, W, H):
+        return self.ext.prepare(W, H, 2 * self.batch)
+
+    def fetch(self, side: str = "left"):
+        """Host copies (nkp, keypoints, descriptors) of the left or right views."""
+        first = 0 if side == "left" else self.batch
+        return self.ext.batch_fetch(first, self.batch)
+
+    def profile(self, on: bool = True):
+        self.ext.profile(on)
+
+    def collect_profile(self):
+        return self.ext.collect_profile()

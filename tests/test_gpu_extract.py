@@ -99,13 +99,16 @@ def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
     mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
     uR, dep, nv = sb(Ls, Rs, KITTI_MBF, mb)
     torch.cuda.synchronize()
-    nkp, kps, desc = sb.left.batch_fetch()
+    nkp, kps, desc = sb.fetch("left")
+    nkpr, kpsr, descr = sb.fetch("right")
     uRh, deph, nvh = uR.cpu().numpy(), dep.cpu().numpy(), nv.cpu().numpy()
     for i in range(B):
         ol = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
         orr = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
         k_o, d_o = ol(pairs[i][0])
-        orr(pairs[i][1])
+        kr_o, dr_o = orr(pairs[i][1])
+        assert_kps_equal(kpsr[i, :nkpr[i]], kr_o, f"batch item {i} right")
+        assert_bytes_equal(descr[i, :nkpr[i]], dr_o, f"batch item {i} right desc")
         n = nkp[i]
         assert_kps_equal(kps[i, :n], k_o, f"batch item {i}")
         assert_bytes_equal(desc[i, :n], d_o, f"batch item {i} desc")
