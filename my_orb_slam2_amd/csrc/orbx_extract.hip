@@ -105,9 +105,11 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
     const int ci = blockIdx.x * 4 + wid;
     if (ci >= g->n_cells) return;   // no block-level barriers below: waves are independent
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
-    uint8_t* roi = smem + wid * (roi_cap + mb_cap + FAST_LIST * 2);
+    const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
+    uint8_t* roi = smem + wid * (roi_cap + mb_cap + FAST_LIST * 2 + cl_cap);
     uint8_t* mb = roi + roi_cap;
     int16_t* list = (int16_t*)(mb + mb_cap);
+    int16_t* corners = list + FAST_LIST;   // pixels with M > min threshold, raster order
     const CellDesc c = cells[ci];
     const int rows = c.rows, cols = c.cols, dh = rows - 6, dw = cols - 6;
     int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
@@ -124,20 +126,24 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
                      L.pitch, rows, ndw, (uint32_t*)roi, ndw, lane);
     roi += xo;
     const int mw = dw + 2;
-    for (int i = lane; i < (dh + 2) * mw; i += 64) mb[i] = 0;
+    for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
     wave_sync();
-    const int npx = dh * dw;
+    // Lane mapping without divisions: a wave covers 64 / 2^rsh detection rows per pass,
+    // 2^rsh lanes per row (cells are at most 60 wide), so ballot order is raster order.
+    const int rsh = dw <= 32 ? 5 : 6;
+    const int rpp = 64 >> rsh;
+    const int sub = lane >> rsh, cl = lane & ((1 << rsh) - 1);
     // 1. compass pre-test at the lower threshold: a 9-pixel arc over threshold t contains two
     //    neighbouring compass pixels (circle indices i, i+4) both beyond t on the same side.
     const int tq = min(g->ini_th, g->min_th);
-    for (int p0 = 0; p0 < npx; p0 += FAST_LIST) {
+    int ncorner = 0;
+    for (int rb = 0; rb < dh; rb += FAST_LIST / 64 * rpp) {
         int nlist = 0;
-        for (int k = 0; k < FAST_LIST && p0 + k < npx; k += 64) {
-            const int p = p0 + k + lane;
+        for (int r0 = rb; r0 < min(dh, rb + FAST_LIST / 64 * rpp); r0 += rpp) {
+            const int rr = r0 + sub;
             bool pass = false;
-            if (p < npx) {
-                const int rr = p / dw + 3, cc = p - (p / dw) * dw + 3;
-                const uint8_t* q = roi + rr * rp + cc;
+            if (rr < dh && cl < dw) {
+                const uint8_t* q = roi + (rr + 3) * rp + cl + 3;
                 const int v = q[0];
                 const int n0 = q[3 * rp], n4 = q[3], n8 = q[-3 * rp], n12 = q[-3];
                 const int hi = v + tq, lo = v - tq;
@@ -147,29 +153,38 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
                        (d4 && d8) || (d8 && d12) || (d12 && d0);
             }
             const uint64_t m = __ballot(pass);
-            if (pass) list[nlist + lanes_below(m)] = (int16_t)p;
+            if (pass) list[nlist + lanes_below(m)] = (int16_t)((rr << 6) | cl);
             nlist += __popcll(m);
         }
         wave_sync();
-        // 2. full arc score for the survivors only (dense across lanes)
-        for (int j = lane; j < nlist; j += 64) {
-            const int p = list[j];
-            const int rr = p / dw, cc = p - rr * dw;
-            const int m = fast_arc_score(roi, rp, rr + 3, cc + 3);
-            mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
+        // 2. full arc score for the survivors only (dense across lanes); those above the lower
+        //    threshold are appended to the corner list, keeping raster order
+        for (int j0 = 0; j0 < nlist; j0 += 64) {
+            const int j = j0 + lane;
+            int pe = 0, m = 0;
+            if (j < nlist) {
+                pe = list[j];
+                const int rr = pe >> 6, cc = pe & 63;
+                m = fast_arc_score(roi, rp, rr + 3, cc + 3);
+                mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
+            }
+            const bool corner = j < nlist && m > tq;
+            const uint64_t cm = __ballot(corner);
+            if (corner) corners[ncorner + lanes_below(cm)] = (int16_t)pe;
+            ncorner += __popcll(cm);
         }
         wave_sync();
     }
     // 3. any corner at iniThFAST in this cell?  (else fall back to minThFAST, :833-837)
     int t = g->ini_th;
     bool found = false;
-    for (int p0 = 0; p0 < npx && !found; p0 += 64) {
-        const int p = p0 + lane;
+    for (int j0 = 0; j0 < ncorner && !found; j0 += 64) {
+        const int j = j0 + lane;
         int s;
         bool k = false;
-        if (p < npx) {
-            const int rr = p / dw, cc = p - rr * dw;
-            k = fast_nms_kp(mb, mw, rr, cc, t, s);
+        if (j < ncorner) {
+            const int pe = corners[j];
+            k = fast_nms_kp(mb, mw, pe >> 6, pe & 63, t, s);
         }
         found = __ballot(k) != 0;
     }
@@ -177,13 +192,14 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
     // 4. ordered compaction (raster order inside the cell, as cv::FAST emits)
     uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
     int base = 0;
-    for (int p0 = 0; p0 < npx; p0 += 64) {
-        const int p = p0 + lane;
+    for (int j0 = 0; j0 < ncorner; j0 += 64) {
+        const int j = j0 + lane;
         int s = 0, rr = 0, cc = 0;
         bool k = false;
-        if (p < npx) {
-            rr = p / dw;
-            cc = p - rr * dw;
+        if (j < ncorner) {
+            const int pe = corners[j];
+            rr = pe >> 6;
+            cc = pe & 63;
             k = fast_nms_kp(mb, mw, rr, cc, t, s);
         }
         const uint64_t m = __ballot(k);
@@ -200,7 +216,8 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
 
 size_t fast_lds_bytes(const Geometry& G) {
     const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
-    return (size_t)4 * (roi_cap + mb_cap + FAST_LIST * 2);
+    const int cl_cap = (G.max_cell_px * 2 + 15) & ~15;
+    return (size_t)4 * (roi_cap + mb_cap + FAST_LIST * 2 + cl_cap);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -560,6 +577,8 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
 // ----------------------------------------------------------------------------------------
 // Orientation + rBRIEF + assembly: one wave per keypoint.
 // ----------------------------------------------------------------------------------------
+#define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
+#define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
 __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict__ g,
                                                      const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
@@ -568,6 +587,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
                                                      float* __restrict__ kps,
                                                      uint8_t* __restrict__ desc,
                                                      int* __restrict__ nkp) {
+    __shared__ uint32_t patch[4][31 * OD_RAW_DW + 37 * OD_BLR_DW];
     const int b = blockIdx.y, blk = blockIdx.x;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int level = 0;
@@ -588,8 +608,37 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
     const int pitch = L.pitch;
 
+    // stage the 31x31 raw patch (IC_Angle) and the 37x37 blurred patch (rBRIEF offsets are
+    // within +-18) as aligned dwords: every load of a lane is issued before its LDS stores
+    const int ax_r = (x - 15) & ~3, ax_b = (x - 18) & ~3;
+    const uint8_t* pr = pyr + b * g->pyr_bytes + L.off + (size_t)(y - 15) * pitch + ax_r;
+    const uint8_t* pb = blur + b * g->pyr_bytes + L.off + (size_t)(y - 18) * pitch + ax_b;
+    uint32_t* P = patch[wid];
+    {
+        constexpr int n1 = 31 * OD_RAW_DW, n2 = 37 * OD_BLR_DW;
+        uint32_t v[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {   // branch-free address select: one load per k
+            const int t = min(lane + 64 * k, n1 + n2 - 1);
+            const bool isr = t < n1;
+            const int tt = isr ? t : t - n1;
+            const int row = isr ? tt / OD_RAW_DW : tt / OD_BLR_DW;
+            const int col = tt - row * (isr ? OD_RAW_DW : OD_BLR_DW);
+            const uint8_t* base = isr ? pr : pb;
+            v[k] = *(const uint32_t*)(base + (size_t)row * pitch + 4 * col);
+        }
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const int t = lane + 64 * k;
+            if (t < n1 + n2) P[t] = v[k];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint8_t* raw = (const uint8_t*)P;                       // [31][36], x at col x-ax_r
+    const uint8_t* blr = (const uint8_t*)(P + 31 * OD_RAW_DW);    // [37][40]
+
     // IC_Angle (src/ORBextractor.cc:77-104) on the unblurred level; exact integer moments.
-    const uint8_t* center = pyr + b * g->pyr_bytes + L.off + (size_t)y * pitch + x;
+    const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ax_r);
     int m10 = 0, m01 = 0;
     {
         const int half = lane >> 5, l31 = lane & 31;
@@ -600,7 +649,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
             const int vb = half ? 8 : 1, ve = half ? 16 : 8;
             for (int v = vb; v < ve; ++v) {
                 if (au <= g->umax[v]) {
-                    const int vp = center[u + v * pitch], vm = center[u - v * pitch];
+                    const int vp = center[u + v * (OD_RAW_DW * 4)], vm = center[u - v * (OD_RAW_DW * 4)];
                     m10 += u * (vp + vm);
                     m01 += v * (vp - vm);
                 }
@@ -615,7 +664,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
-    const uint8_t* bc = blur + b * g->pyr_bytes + L.off + (size_t)y * pitch + x;
+    const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ax_b);
     uint64_t words[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -624,8 +673,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
         const float x2 = (float)c_pattern[4 * k + 2], y2 = (float)c_pattern[4 * k + 3];
         const float r1a = x1 * sb, r1b = y1 * ca, c1a = x1 * ca, c1b = y1 * sb;
         const float r2a = x2 * sb, r2b = y2 * ca, c2a = x2 * ca, c2b = y2 * sb;
-        const int t0 = bc[cv_round(r1a + r1b) * pitch + cv_round(c1a - c1b)];
-        const int t1 = bc[cv_round(r2a + r2b) * pitch + cv_round(c2a - c2b)];
+        const int t0 = bc[cv_round(r1a + r1b) * (OD_BLR_DW * 4) + cv_round(c1a - c1b)];
+        const int t1 = bc[cv_round(r2a + r2b) * (OD_BLR_DW * 4) + cv_round(c2a - c2b)];
         words[w] = __ballot(t0 < t1);
     }
     const size_t o = (size_t)b * g->kp_cap + off + i;

@@ -59,7 +59,8 @@ struct Geometry {
     int max_ncand_level;    // max cand_cap over levels
     int max_out_cap;
     int max_roi_bytes;      // largest FAST cell ROI (rows*cols)
-    int max_mbuf_bytes;     // largest FAST score buffer ((dh+2)*(dw+2))
+    int max_mbuf_bytes;     // largest FAST score buffer ((dh+2)*(dw+2)), dword padded
+    int max_cell_px;        // largest FAST detection region (dh*dw)
     int blur_tiles;         // Σ_l ceil(w/64)*ceil(h/16)
     int orient_blocks;      // Σ_l ceil(out_cap/4)
     int blur_tile_begin[ORBX_MAX_LEVELS + 1];
