@@ -18,6 +18,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
 KERNELS = ["k_level", "k_fast", "k_octree", "k_orient_desc", "k_stereo"]
+MATCH_KERNELS = ["k_bow", "k_triangulate", "k_proj_search", "k_proj_resolve"]
 
 STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
           -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_STATE"}
@@ -67,6 +68,24 @@ SIGNATURES = {
     "orbx_profile_enable": (_i, [_vp, _i]),
     "orbx_profile_collect": (_i, [_vp, _vp, _vp]),
     "orbx_kernel_name": (ctypes.c_char_p, [_i]),
+    # include/orbx_match.h
+    "orbx_matcher_create": (_i, [_vp, ctypes.POINTER(_vp)]),
+    "orbx_matcher_destroy": (_i, [_vp]),
+    "orbx_compute_three_maxima": (None, [_vp, _i, _vp, _vp, _vp]),
+    "orbx_search_by_bow_kf_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbx_search_by_bow_kf_kf": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbx_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _i,
+                                           _i, _vp, _i, _vp]),
+    "orbx_search_by_projection": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _i, _i, _vp, _vp]),
+    "orbx_search_by_sim3": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp]),
+    "orbx_search_for_initialization": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
+    "orbx_search_by_bow_kf_frame_batch_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbx_search_for_triangulation_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp, _vp,
+                                                        _vp, _i, _i, _vp, _vp, _vp, _vp]),
+    "orbx_matcher_sync": (_i, [_vp, _vp]),
+    "orbx_matcher_profile_enable": (_i, [_vp, _i]),
+    "orbx_matcher_profile_collect": (_i, [_vp, _vp, _vp]),
+    "orbx_match_kernel_name": (ctypes.c_char_p, [_i]),
 }
 
 _lib = None

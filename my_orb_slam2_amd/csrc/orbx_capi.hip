@@ -27,34 +27,16 @@ hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_ld
 
 using namespace orbx;
 
-static thread_local char g_err[256] = "";
-// Records the first failing HIP call for orbx_last_error().
-static bool hip_ok(hipError_t e, const char* what) {
+#include "orbx_host.h"
+
+namespace orbx {
+thread_local char g_err[256] = "";
+bool hip_ok(hipError_t e, const char* what) {
     if (e == hipSuccess) return true;
     snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
     return false;
 }
-#define HIPOK(call) hip_ok((call), #call)
-
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t n = 0;
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-    }
-    bool ensure(size_t bytes) {
-        if (bytes <= n && p) return true;
-        release();
-        if (bytes == 0) bytes = 16;
-        if (!HIPOK(hipMalloc(&p, bytes))) { p = nullptr; return false; }
-        n = bytes;
-        return true;
-    }
-    template <class T> T* as() const { return (T*)p; }
-};
+}  // namespace orbx
 
 struct orbx_extractor {
     orbx_extractor_params prm;

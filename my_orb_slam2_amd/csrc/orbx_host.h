@@ -1,0 +1,35 @@
+// orbx_host.h — host-side helpers shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace orbx {
+
+// Text of the first failing HIP call on this thread (orbx_last_error()).
+extern thread_local char g_err[256];
+// Records a failing HIP call into g_err; returns e == hipSuccess.
+bool hip_ok(hipError_t e, const char* what);
+#define HIPOK(call) ::orbx::hip_ok((call), #call)
+
+// A growable device allocation (contents are not preserved across growth).
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    bool ensure(size_t bytes) {
+        if (bytes <= n && p) return true;
+        release();
+        if (bytes == 0) bytes = 16;
+        if (!HIPOK(hipMalloc(&p, bytes))) { p = nullptr; return false; }
+        n = bytes;
+        return true;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+}  // namespace orbx

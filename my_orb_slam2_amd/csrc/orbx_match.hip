@@ -1,0 +1,722 @@
+// orbx_match.hip — gfx950 kernels of the descriptor matchers (src/ORBmatcher.cc).
+//
+// The matchers are integer/bit work (XOR + v_bcnt over 256-bit descriptors) with a greedy,
+// order-dependent claim step.  The kernels keep the reference's exact selection semantics
+// while moving the distance work off the sequential chain:
+//   k_bow<NPL>       one wave per (keyframe, frame) job, walking the shared FeatureVector
+//                    nodes; the node's candidate descriptors live in VGPRs (NPL per lane),
+//                    each greedy step is 8 XOR + 8 BCNT per candidate and two DPP wave-min
+//                    reductions over (distance, position) keys (first-min semantics).
+//   k_triangulate    one workgroup per keyframe pair, one wave per KF1 node; every idx1 is
+//                    independent (vbMatched2 is never set, :722), so each is a wave-min over
+//                    (distance, reversed position) keys = the reference's last-wins ties.
+//   k_proj_search    one wave per projected MapPoint: the grid window is a set of contiguous
+//                    CSR spans (one per grid column), scanned 64 candidates at a time; yields
+//                    the static top-2 (or the final answer for the claim-free modes).
+//   k_proj_resolve   one wave replays the greedy claims in MapPoint order; a query whose
+//                    static best/second are still unclaimed is decided from them (exact:
+//                    the dynamic candidate set is a subset), otherwise the wave re-scans
+//                    its window against the claim state in LDS.
+//   k_proj_finish    rotation-consistency filter (ComputeThreeMaxima) and count.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+
+#include "orbx_device.h"
+#include "orbx_kernels.h"
+#include "orbx_match_kernels.h"
+
+namespace orbx {
+namespace {
+
+constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO = 30;
+constexpr uint32_t INF = 0xFFFFFFFFu;
+
+struct Desc {
+    uint32_t w[8];
+};
+
+__device__ __forceinline__ Desc load_desc(const uint8_t* base, long long i) {
+    const uint4* p = (const uint4*)(base + 32 * i);
+    const uint4 a = p[0], b = p[1];
+    return Desc{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+
+// ORBmatcher::DescriptorDistance (:1715-1731): popcount of the XOR, 8 words.
+__device__ __forceinline__ int hamming(const Desc& a, const Desc& b) {
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d += __popc(a.w[k] ^ b.w[k]);
+    return d;
+}
+
+// Wave-wide unsigned min, uniform result: DPP within rows of 16, then 4 readlanes.
+// Must be called with all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, true));
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+
+// Rotation bin of the matchers (e.g. :269-275): float difference, +360 when negative,
+// round(rot * (1.0f/30)) half away from zero, 30 -> 0.
+__device__ __forceinline__ int rot_bin(float a1, float a2) {
+    const float factor = 1.0f / HISTO;
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO) bin = 0;
+    return bin;
+}
+
+// ComputeThreeMaxima (:1669-1710) on 30 counts.  Returns the kept bins.
+struct Top3 {
+    int i1, i2, i3;
+    __device__ bool keeps(int b) const { return b == i1 || b == i2 || b == i3; }
+};
+
+__device__ __forceinline__ Top3 three_maxima(const int* h) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < HISTO; i++) {
+        const int s = h[i];
+        const bool g1 = s > max1, g2 = !g1 && s > max2, g3 = !g1 && !g2 && s > max3;
+        // branch-free form of the reference's if / else-if chain
+        max3 = g1 || g2 ? max2 : (g3 ? s : max3);
+        ind3 = g1 || g2 ? ind2 : (g3 ? i : ind3);
+        max2 = g1 ? max1 : (g2 ? s : max2);
+        ind2 = g1 ? ind1 : (g2 ? i : ind2);
+        max1 = g1 ? s : max1;
+        ind1 = g1 ? i : ind1;
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1; ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+    return {ind1, ind2, ind3};
+}
+
+// float -> int as the x86-64 reference converts (int)floor(v): cvttss2si yields INT_MIN for
+// NaN and out-of-range values (the GPU's v_cvt_i32_f32 saturates instead).
+__device__ __forceinline__ int x86_int(float f) {
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : INT_MIN;
+}
+
+// ---------------------------------------------------------------------------------------
+// SearchByBoW (:182-319 and :563-696)
+// ---------------------------------------------------------------------------------------
+
+template <int NPL>
+__global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
+    extern __shared__ int lds[];
+    const int job = blockIdx.x, lane = threadIdx.x;
+    const int ka = g.a_fixed ? 0 : job, kb = g.b_fixed ? 0 : job;
+    const int fa0 = g.A.feat_off[ka], nA = g.A.feat_off[ka + 1] - fa0;
+    const int fb0 = g.B.feat_off[kb], nBt = g.B.feat_off[kb + 1] - fb0;
+    const int nOut = g.kf_kf ? nA : nBt;
+    int32_t* out = g.out + (size_t)job * g.out_stride;
+    if (nA < 0 || nBt < 0 || nA > g.A.max_feat || nBt > g.B.max_feat || nOut > g.out_stride) {
+        for (int i = lane; i < g.out_stride; i += 64) out[i] = -1;
+        if (lane == 0) {
+            g.nmatches[job] = 0;
+            atomicOr(g.err, 1);
+        }
+        return;
+    }
+    const int smax = g.kf_kf ? g.A.max_feat : g.B.max_feat;
+    int* state = lds;                                    // match | bin << 24, or -1
+    uint32_t* claimed = (uint32_t*)(lds + smax);         // B features claimed (bitmap)
+    int* hist = (int*)(claimed + (g.B.max_feat + 31) / 32);
+    for (int i = lane; i < nOut; i += 64) state[i] = -1;
+    for (int i = lane; i < (nBt + 31) / 32; i += 64) claimed[i] = 0u;
+    if (lane < 32) hist[lane] = 0;
+    __syncthreads();
+
+    const bool kfkf = g.kf_kf != 0;
+    const int na0 = g.A.node_off[ka], na1 = g.A.node_off[ka + 1];
+    int bn = g.B.node_off[kb];
+    const int bn1 = g.B.node_off[kb + 1];
+    for (int ga = na0; ga < na1; ++ga) {
+        // Lock-step FeatureVector walk (:205-295): both maps ascending, so the shared nodes
+        // are found by advancing the B cursor to the first id >= the A id.
+        const uint32_t id = g.A.node_id[ga];
+        while (bn < bn1 && g.B.node_id[bn] < id) ++bn;
+        if (bn >= bn1) break;
+        if (g.B.node_id[bn] != id) continue;
+        const int a0 = g.A.node_feat_off[ga], a1 = g.A.node_feat_off[ga + 1];
+        const int b0 = g.B.node_feat_off[bn], nB = g.B.node_feat_off[bn + 1] - b0;
+        ++bn;
+        if (nB <= 0) continue;
+        if (nB <= 64 * NPL) {
+            // Candidates resident in VGPRs for the whole node.
+            Desc bd[NPL];
+            int bf[NPL];
+            bool ok[NPL];
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) {
+                ok[c] = false;
+                bf[c] = 0;
+                if (c * 64 < nB) {
+                    const int pos = c * 64 + lane;
+                    const int f = g.B.node_feat[b0 + min(pos, nB - 1)];
+                    const bool in = pos < nB && (unsigned)f < (unsigned)nBt;
+                    const int fc = in ? f : 0;
+                    bd[c] = load_desc(g.B.desc, (long long)fb0 + fc);
+                    bf[c] = fc;
+                    ok[c] = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
+                            (!kfkf || g.B.flag[fb0 + fc]);
+                }
+            }
+            for (int ia = a0; ia < a1; ++ia) {
+                const int fa = g.A.node_feat[ia];
+                if ((unsigned)fa >= (unsigned)nA) continue;
+                if (!g.A.flag[fa0 + fa]) continue;   // :224-228 / :599-603
+                const Desc ad = load_desc(g.A.desc, (long long)fa0 + fa);
+                uint32_t k1 = INF, k2 = INF;
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    if (c * 64 < nB) {
+                        const int d = hamming(ad, bd[c]);
+                        const uint32_t key =
+                            (ok[c] && d < 256) ? ((uint32_t)d << 20 | (uint32_t)(c * 64 + lane)) : INF;
+                        if (key < k1) { k2 = k1; k1 = key; }
+                        else if (key < k2) { k2 = key; }
+                    }
+                }
+                const uint32_t m1 = wave_min_u32(k1);
+                const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
+                const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
+                const int d2 = m2 == INF ? 256 : (int)(m2 >> 20);
+                const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
+                                 (float)d1 < g.ratio * (float)d2;
+                if (acc) {
+                    const int pos = (int)(m1 & 0xFFFFFu);
+#pragma unroll
+                    for (int c = 0; c < NPL; ++c)
+                        if (pos == c * 64 + lane) {
+                            ok[c] = false;
+                            const int fbm = bf[c];
+                            claimed[fbm >> 5] |= 1u << (fbm & 31);
+                            int bin = 0;
+                            if (g.check_ori) {
+                                bin = rot_bin(g.A.keys[fa0 + fa].angle, g.B.keys[fb0 + fbm].angle);
+                                atomicAdd(&hist[bin], 1);
+                            }
+                            if (kfkf) state[fa] = fbm | (bin << 24);
+                            else state[fbm] = fa | (bin << 24);
+                        }
+                }
+            }
+        } else {
+            // Large node: candidates re-read every step, claims from the LDS bitmap.
+            for (int ia = a0; ia < a1; ++ia) {
+                const int fa = g.A.node_feat[ia];
+                if ((unsigned)fa >= (unsigned)nA) continue;
+                if (!g.A.flag[fa0 + fa]) continue;
+                const Desc ad = load_desc(g.A.desc, (long long)fa0 + fa);
+                uint32_t k1 = INF, k2 = INF;
+                for (int base = 0; base < nB; base += 64) {
+                    const int pos = base + lane;
+                    const int f = g.B.node_feat[b0 + min(pos, nB - 1)];
+                    const bool in = pos < nB && (unsigned)f < (unsigned)nBt;
+                    const int fc = in ? f : 0;
+                    const Desc bdd = load_desc(g.B.desc, (long long)fb0 + fc);
+                    const bool okc = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
+                                     (!kfkf || g.B.flag[fb0 + fc]);
+                    const int d = hamming(ad, bdd);
+                    const uint32_t key = (okc && d < 256) ? ((uint32_t)d << 20 | (uint32_t)pos) : INF;
+                    if (key < k1) { k2 = k1; k1 = key; }
+                    else if (key < k2) { k2 = key; }
+                }
+                const uint32_t m1 = wave_min_u32(k1);
+                const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
+                const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
+                const int d2 = m2 == INF ? 256 : (int)(m2 >> 20);
+                const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
+                                 (float)d1 < g.ratio * (float)d2;
+                if (acc) {
+                    const int pos = (int)(m1 & 0xFFFFFu);
+                    const int fbm = g.B.node_feat[b0 + pos];
+                    if (lane == 0) {
+                        claimed[fbm >> 5] |= 1u << (fbm & 31);
+                        int bin = 0;
+                        if (g.check_ori) {
+                            bin = rot_bin(g.A.keys[fa0 + fa].angle, g.B.keys[fb0 + fbm].angle);
+                            hist[bin] += 1;
+                        }
+                        if (kfkf) state[fa] = fbm | (bin << 24);
+                        else state[fbm] = fa | (bin << 24);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // Rotation consistency (:298-316 / :675-693) and the count.
+    const Top3 top = g.check_ori ? three_maxima(hist) : Top3{-1, -1, -1};
+    int cnt = 0;
+    for (int i = lane; i < nOut; i += 64) {
+        const int s = state[i];
+        int r = -1;
+        if (s >= 0) {
+            const int bin = s >> 24;
+            if (!g.check_ori || top.keeps(bin)) {
+                r = s & 0xFFFFFF;
+                ++cnt;
+            }
+        }
+        out[i] = r;
+    }
+    for (int i = nOut + lane; i < g.out_stride; i += 64) out[i] = -1;
+    cnt = wave_sum(cnt);
+    if (lane == 0) g.nmatches[job] = cnt;
+}
+
+// ---------------------------------------------------------------------------------------
+// SearchForTriangulation (:702-872) + CheckDistEpipolarLine (:147-167)
+// ---------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
+    extern __shared__ int lds[];
+    int* state = lds;
+    int* hist = lds + g.db.max_feat;
+    __shared__ int red[4];
+    const int job = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int k1 = g.kf1[job], k2 = g.kf2[job];
+    const orbx_kf_db& db = g.db;
+    const int f10 = db.feat_off[k1], n1 = db.feat_off[k1 + 1] - f10;
+    const int f20 = db.feat_off[k2], n2 = db.feat_off[k2 + 1] - f20;
+    int32_t* out = g.out + g.job_off[job];
+    if (n1 < 0 || n2 < 0 || n1 > db.max_feat || n2 > db.max_feat ||
+        g.job_off[job + 1] - g.job_off[job] < n1) {
+        if (tid == 0) {
+            g.nmatches[job] = 0;
+            atomicOr(g.err, 1);
+        }
+        return;
+    }
+    for (int i = tid; i < n1; i += 256) state[i] = -1;
+    if (tid < 32) hist[tid] = 0;
+    __syncthreads();
+
+    float F[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) F[k] = g.F12[9 * job + k];
+    const float ex = g.epi[2 * job], ey = g.epi[2 * job + 1];
+    const int na0 = db.node_off[k1], na1 = db.node_off[k1 + 1];
+    const int nb0 = db.node_off[k2], nb1 = db.node_off[k2 + 1];
+    for (int ga = na0 + w; ga < na1; ga += 4) {
+        const uint32_t id = db.node_id[ga];
+        int lo = nb0, hi = nb1;   // lower_bound
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (db.node_id[mid] < id) lo = mid + 1; else hi = mid;
+        }
+        if (lo >= nb1 || db.node_id[lo] != id) continue;
+        const int a0 = db.node_feat_off[ga], a1 = db.node_feat_off[ga + 1];
+        const int b0 = db.node_feat_off[lo], nB = db.node_feat_off[lo + 1] - b0;
+        for (int ia = a0; ia < a1; ++ia) {
+            const int idx1 = db.node_feat[ia];
+            if ((unsigned)idx1 >= (unsigned)n1) continue;
+            if (db.flag[f10 + idx1]) continue;   // :749
+            const bool bStereo1 = (db.u_right ? db.u_right[f10 + idx1] : -1.0f) >= 0;
+            if (g.only_stereo && !bStereo1) continue;
+            const orbx_keypoint kp1 = db.keys[f10 + idx1];
+            // CheckDistEpipolarLine's line coefficients depend on kp1 only.
+            const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
+            const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
+            const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+            const float den = a * a + b * b;
+            const Desc d1 = load_desc(db.desc, (long long)f10 + idx1);
+            uint32_t key = INF;
+            for (int base = 0; base < nB; base += 64) {
+                const int pos = base + lane;
+                const int idx2 = db.node_feat[b0 + min(pos, nB - 1)];
+                if (pos >= nB || (unsigned)idx2 >= (unsigned)n2) continue;
+                if (db.flag[f20 + idx2]) continue;   // :773
+                const bool bStereo2 = (db.u_right ? db.u_right[f20 + idx2] : -1.0f) >= 0;
+                if (g.only_stereo && !bStereo2) continue;
+                const int dist = hamming(d1, load_desc(db.desc, (long long)f20 + idx2));
+                if (dist > TH_LOW) continue;   // :786 (the dist > bestDist half is the min)
+                const orbx_keypoint kp2 = db.keys[f20 + idx2];
+                const int o2 = min(max(kp2.octave, 0), MATCH_MAX_LEVELS - 1);
+                if (!bStereo1 && !bStereo2) {   // :791-798
+                    const float distex = ex - kp2.x;
+                    const float distey = ey - kp2.y;
+                    if (distex * distex + distey * distey < 100 * g.scale[o2]) continue;
+                }
+                if (den == 0) continue;
+                const float num = a * kp2.x + b * kp2.y + c;
+                const float dsqr = num * num / den;
+                if (!((double)dsqr < 3.84 * (double)g.sigma2[o2])) continue;
+                // ties: the LAST accepted candidate wins (:786 skips only dist > bestDist)
+                key = min(key, (uint32_t)dist << 20 | (uint32_t)(0xFFFFF - pos));
+            }
+            const uint32_t m = wave_min_u32(key);
+            if (m != INF) {
+                const int pos = 0xFFFFF - (int)(m & 0xFFFFFu);
+                const int idx2 = db.node_feat[b0 + pos];
+                if (lane == 0) {
+                    int bin = 0;
+                    if (g.check_ori) {
+                        bin = rot_bin(kp1.angle, db.keys[f20 + idx2].angle);
+                        atomicAdd(&hist[bin], 1);
+                    }
+                    state[idx1] = idx2 | (bin << 24);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const Top3 top = g.check_ori ? three_maxima(hist) : Top3{-1, -1, -1};
+    int cnt = 0;
+    for (int i = tid; i < n1; i += 256) {
+        const int s = state[i];
+        int r = -1;
+        if (s >= 0) {
+            const int bin = s >> 24;
+            if (!g.check_ori || top.keeps(bin)) {
+                r = s & 0xFFFFFF;
+                ++cnt;
+            }
+        }
+        out[i] = r;
+    }
+    const int tot = block_sum<4>(cnt, red);
+    if (tid == 0) g.nmatches[job] = tot;
+}
+
+// ---------------------------------------------------------------------------------------
+// Projection searches (:46-132, :321-434, :879-1156, :1158-1382, :1392-1667, :446-561)
+// ---------------------------------------------------------------------------------------
+
+struct ModeInfo {
+    bool frame_grid;   // Frame::GetFeaturesInArea with level arguments
+    bool init256;      // best (and second) initialised to 256: a distance of 256 never counts
+    bool stereo;       // |ur - uRight| > radius rejects (uRight > 0)
+    bool kf_level;     // octave in [pred-1, pred] (matcher-side)
+    bool fuse;         // reprojection chi2 test (:968-992)
+    bool rot;          // rotation-consistency filter
+    bool greedy;       // sequential claims
+    int th;            // acceptance threshold on the best distance
+};
+
+__device__ __forceinline__ ModeInfo mode_info(int mode, int orb_dist) {
+    switch (mode) {
+        case ORBX_PROJ_FRAME_MAPPOINTS: return {true, true, true, false, false, false, true, TH_HIGH};
+        case ORBX_PROJ_KF_SCW:          return {false, true, false, true, false, false, true, TH_LOW};
+        case ORBX_PROJ_LAST_FRAME:      return {true, true, true, false, false, true, true, TH_HIGH};
+        case ORBX_PROJ_KEYFRAME:        return {true, true, false, false, false, true, true, orb_dist};
+        case ORBX_PROJ_FUSE:            return {false, true, false, true, true, false, false, TH_LOW};
+        case ORBX_PROJ_FUSE_SCW:        return {false, false, false, true, false, false, false, TH_LOW};
+        case ORBX_PROJ_SIM3:            return {false, false, false, true, false, false, false, TH_HIGH};
+        default:                        return {true, false, false, false, false, true, true, TH_LOW};
+    }
+}
+
+struct NoDyn {
+    __device__ bool operator()(int, int) const { return true; }
+};
+struct ClaimDyn {   // claimed features are skipped
+    const uint8_t* claimed;
+    __device__ bool operator()(int i, int) const { return claimed[i] == 0; }
+};
+struct InitDyn {    // :485 vMatchedDistance[i2] <= dist skips
+    const int* mdist;
+    __device__ bool operator()(int i, int d) const { return mdist[i] > d; }
+};
+
+constexpr uint32_t POS_MASK = (1u << 23) - 1;
+
+// GetFeaturesInArea + the mode's candidate filters + DescriptorDistance, reduced to the
+// first two keys (distance << 23 | grid CSR position) in the reference's visiting order
+// (cell column ix, then row iy, then the cell's vector: exactly increasing CSR position).
+template <class Dyn>
+__device__ void window_top2(const ProjLaunch& g, const ModeInfo& mi, const orbx_proj_query& q,
+                            const Desc& qd, Dyn dyn, uint32_t& o1, uint32_t& o2) {
+    const orbx_featureset& T = g.T;
+    const int lane = lane_id();
+    o1 = o2 = INF;
+    const float x = q.u, y = q.v, r = q.radius;
+    const int nMinCellX = max(0, x86_int(floorf((x - T.min_x - r) * T.grid_inv_w)));
+    if (nMinCellX >= T.grid_cols) return;
+    const int nMaxCellX = min(T.grid_cols - 1, x86_int(ceilf((x - T.min_x + r) * T.grid_inv_w)));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, x86_int(floorf((y - T.min_y - r) * T.grid_inv_h)));
+    if (nMinCellY >= T.grid_rows) return;
+    const int nMaxCellY = min(T.grid_rows - 1, x86_int(ceilf((y - T.min_y + r) * T.grid_inv_h)));
+    if (nMaxCellY < 0) return;
+    const bool checkLevels = mi.frame_grid && ((q.min_level > 0) || (q.max_level >= 0));
+    uint32_t k1 = INF, k2 = INF;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int p0 = T.grid_off[ix * T.grid_rows + nMinCellY];
+        const int p1 = T.grid_off[ix * T.grid_rows + nMaxCellY + 1];
+        for (int base = p0; base < p1; base += 64) {
+            const int p = base + lane;
+            if (p >= p1) continue;
+            const int i = T.grid_feat[p];
+            if ((unsigned)i >= (unsigned)T.n) continue;
+            const orbx_keypoint kp = T.keys[i];
+            if (checkLevels) {
+                if (kp.octave < q.min_level) continue;
+                if (q.max_level >= 0 && kp.octave > q.max_level) continue;
+            }
+            const float distx = kp.x - x, disty = kp.y - y;
+            if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+            if (mi.kf_level && (kp.octave < q.pred_level - 1 || kp.octave > q.pred_level)) continue;
+            const float uR = T.u_right ? T.u_right[i] : -1.0f;
+            if (mi.stereo && uR > 0) {
+                const float er = fabsf(q.ur - uR);
+                if (er > r) continue;
+            }
+            if (mi.fuse) {
+                const float is2 = g.inv_sigma2[min(max(kp.octave, 0), MATCH_MAX_LEVELS - 1)];
+                const float ex = x - kp.x, ey = y - kp.y;
+                if (uR >= 0) {
+                    const float er = q.ur - uR;
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if ((double)(e2 * is2) > 7.8) continue;
+                } else {
+                    const float e2 = ex * ex + ey * ey;
+                    if ((double)(e2 * is2) > 5.99) continue;
+                }
+            }
+            const int d = hamming(qd, load_desc(T.desc, i));
+            if (mi.init256 && d >= 256) continue;
+            if (!dyn(i, d)) continue;
+            const uint32_t key = (uint32_t)d << 23 | (uint32_t)p;
+            if (key < k1) { k2 = k1; k1 = key; }
+            else if (key < k2) { k2 = key; }
+        }
+    }
+    o1 = wave_min_u32(k1);
+    o2 = wave_min_u32(k1 == o1 ? k2 : k1);
+}
+
+struct Cand {
+    int i, d, lvl, bin;
+};
+
+__device__ __forceinline__ Cand decode_key(const ProjLaunch& g, const ModeInfo& mi, uint32_t k,
+                                           float qangle) {
+    if (k == INF) return {-1, 0, -1, 0};
+    const int i = g.T.grid_feat[k & POS_MASK];
+    const orbx_keypoint kp = g.T.keys[i];
+    return {i, (int)(k >> 23), kp.octave, mi.rot ? rot_bin(qangle, kp.angle) : 0};
+}
+
+__device__ __forceinline__ int pack_cand(const Cand& c) {
+    return c.d | (c.lvl & 0xF) << 9 | c.bin << 13;
+}
+
+__global__ __launch_bounds__(256) void k_proj_search(ProjLaunch g) {
+    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+    if (qi >= g.nq) return;
+    const ModeInfo mi = mode_info(g.mode, g.orb_dist);
+    const orbx_proj_query q = g.q[qi];
+    if (!(q.radius >= 0)) {
+        if (lane == 0) {
+            if (mi.greedy) g.top2[qi] = make_int4(-1, -1, 0, 0);
+            else g.out[qi] = -1;
+        }
+        return;
+    }
+    const Desc qd = load_desc(g.qdesc, qi);
+    uint32_t m1, m2;
+    window_top2(g, mi, q, qd, NoDyn{}, m1, m2);
+    if (lane != 0) return;
+    if (mi.greedy) {
+        const Cand c1 = decode_key(g, mi, m1, q.angle), c2 = decode_key(g, mi, m2, q.angle);
+        g.top2[qi] = make_int4(c1.i, c2.i, pack_cand(c1), pack_cand(c2));
+    } else {
+        g.out[qi] = (m1 != INF && (int)(m1 >> 23) <= mi.th) ? g.T.grid_feat[m1 & POS_MASK] : -1;
+    }
+}
+
+// Sequential greedy replay in MapPoint order (one wave).
+__global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
+    extern __shared__ int lds[];
+    const int lane = lane_id();
+    const ModeInfo mi = mode_info(g.mode, g.orb_dist);
+    const bool init = g.mode == PROJ_INIT;
+    const int nT = g.T.n, nq = g.nq;
+    int* hist = lds;                         // 32
+    uint8_t* claimed = (uint8_t*)(lds + 32); // nT (claim modes)
+    int* mdist = lds + 32;                   // nT (init): vMatchedDistance
+    int* m21 = mdist + nT;                   // nT (init): vnMatches21
+    int* m12 = m21 + nT;                     // nq (init): vnMatches12
+    if (lane < 32) hist[lane] = 0;
+    if (init) {
+        for (int i = lane; i < nT; i += 64) { mdist[i] = INT_MAX; m21[i] = -1; }
+        for (int i = lane; i < nq; i += 64) m12[i] = -1;
+    } else {
+        for (int i = lane; i < nT; i += 64) claimed[i] = g.claimed_in ? (g.claimed_in[i] != 0) : 0;
+    }
+    __syncthreads();
+    for (int qb = 0; qb < nq; qb += 64) {
+        const int cnt = min(64, nq - qb);
+        const int4 s = (lane < cnt) ? g.top2[qb + lane] : make_int4(-1, -1, 0, 0);
+        for (int t = 0; t < cnt; ++t) {
+            const int qi = qb + t;
+            Cand b = {__builtin_amdgcn_readlane(s.x, t), 0, -1, 0};
+            Cand c = {__builtin_amdgcn_readlane(s.y, t), 0, -1, 0};
+            const int w1 = __builtin_amdgcn_readlane(s.z, t), w2 = __builtin_amdgcn_readlane(s.w, t);
+            b.d = w1 & 0x1FF; b.lvl = (w1 >> 9) & 0xF; b.bin = (w1 >> 13) & 0x1F;
+            c.d = w2 & 0x1FF; c.lvl = (w2 >> 9) & 0xF; c.bin = (w2 >> 13) & 0x1F;
+            if (b.i < 0) {
+                if (lane == 0 && !init) g.out[qi] = -1;
+                continue;   // no static candidate: none under any claim state either
+            }
+            auto pass = [&](const Cand& x) {
+                return init ? (mdist[x.i] > x.d) : (claimed[x.i] == 0);
+            };
+            const bool fast = pass(b) && (c.i < 0 || pass(c));
+            if (!fast) {
+                // The static best or second is gone: re-scan the window against the state.
+                const orbx_proj_query q = g.q[qi];
+                const Desc qd = load_desc(g.qdesc, qi);
+                uint32_t m1, m2;
+                if (init) window_top2(g, mi, q, qd, InitDyn{mdist}, m1, m2);
+                else window_top2(g, mi, q, qd, ClaimDyn{claimed}, m1, m2);
+                b = decode_key(g, mi, m1, q.angle);
+                c = decode_key(g, mi, m2, q.angle);
+            }
+            bool acc;
+            if (g.mode == ORBX_PROJ_FRAME_MAPPOINTS) {   // :121-124
+                const int bestDist = b.i >= 0 ? b.d : 256, bestLevel = b.i >= 0 ? b.lvl : -1;
+                const int bestDist2 = c.i >= 0 ? c.d : 256, bestLevel2 = c.i >= 0 ? c.lvl : -1;
+                acc = bestDist <= TH_HIGH &&
+                      !(bestLevel == bestLevel2 && (float)bestDist > g.ratio * (float)bestDist2);
+            } else if (init) {                           // :500-502
+                const int bestDist = b.i >= 0 ? b.d : INT_MAX;
+                const int bestDist2 = c.i >= 0 ? c.d : INT_MAX;
+                acc = bestDist <= TH_LOW && (float)bestDist < (float)bestDist2 * g.ratio;
+            } else {
+                acc = b.i >= 0 && b.d <= mi.th;
+            }
+            if (lane == 0) {
+                if (init) {
+                    if (acc) {   // :504-512 (re-assignment)
+                        const int prev = m21[b.i];
+                        if (prev >= 0) m12[prev] = -1;
+                        m12[qi] = b.i;
+                        m21[b.i] = qi;
+                        mdist[b.i] = b.d;
+                        g.out_bin[qi] = (int8_t)b.bin;
+                        if (g.check_ori) hist[b.bin] += 1;
+                    }
+                } else {
+                    g.out[qi] = acc ? b.i : -1;
+                    if (acc) {
+                        claimed[b.i] = 1;
+                        g.out_bin[qi] = (int8_t)b.bin;
+                        if (mi.rot && g.check_ori) hist[b.bin] += 1;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (init)
+        for (int i = lane; i < nq; i += 64) g.out[i] = m12[i];
+    if (lane < 32) g.hist[lane] = hist[lane];
+}
+
+__global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
+    __shared__ int red[4];
+    __shared__ int h[32];
+    const int tid = threadIdx.x;
+    const ModeInfo mi = mode_info(g.mode, g.orb_dist);
+    const bool filt = mi.rot && g.check_ori;
+    if (tid < 32) h[tid] = filt ? g.hist[tid] : 0;
+    __syncthreads();
+    const Top3 top = filt ? three_maxima(h) : Top3{-1, -1, -1};
+    int cnt = 0;
+    for (int i = tid; i < g.nq; i += 256) {
+        int r = g.out[i];
+        if (r >= 0 && filt) {
+            const int bin = g.out_bin[i];
+            if (!top.keeps(bin)) {
+                r = -1;
+                g.out[i] = -1;
+            }
+        }
+        cnt += r >= 0;
+    }
+    const int tot = block_sum<4>(cnt, red);
+    if (tid == 0) g.nmatches[0] = tot;
+}
+
+}  // namespace
+
+bool proj_mode_greedy(int mode) {
+    return mode == ORBX_PROJ_FRAME_MAPPOINTS || mode == ORBX_PROJ_KF_SCW ||
+           mode == ORBX_PROJ_LAST_FRAME || mode == ORBX_PROJ_KEYFRAME || mode == PROJ_INIT;
+}
+
+static int bow_npl(int max_feat) { return max_feat <= 256 ? 4 : 16; }
+
+size_t bow_lds_bytes(const BowLaunch& a) {
+    const int smax = a.kf_kf ? a.A.max_feat : a.B.max_feat;
+    return 4 * ((size_t)smax + (a.B.max_feat + 31) / 32 + 32);
+}
+
+hipError_t launch_bow(const BowLaunch& a, hipStream_t st) {
+    if (a.njobs <= 0) return hipSuccess;
+    const size_t lds = bow_lds_bytes(a);
+    if (bow_npl(a.B.max_feat) == 4)
+        hipLaunchKernelGGL(k_bow<4>, dim3(a.njobs), dim3(64), lds, st, a);
+    else
+        hipLaunchKernelGGL(k_bow<16>, dim3(a.njobs), dim3(64), lds, st, a);
+    return hipGetLastError();
+}
+
+size_t tri_lds_bytes(int max_feat) { return 4 * ((size_t)max_feat + 32); }
+
+hipError_t launch_triangulate(const TriLaunch& a, hipStream_t st) {
+    if (a.njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_triangulate, dim3(a.njobs), dim3(256), tri_lds_bytes(a.db.max_feat), st, a);
+    return hipGetLastError();
+}
+
+size_t proj_resolve_lds_bytes(int mode, int n_target, int nq) {
+    if (mode == PROJ_INIT) return 4 * (32 + 2 * (size_t)n_target + (size_t)nq);
+    return 4 * 32 + (size_t)n_target + 16;
+}
+
+hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer) {
+    if (a.nq <= 0) return hipSuccess;
+    hipEvent_t e = timer ? timer->start(st) : nullptr;
+    hipLaunchKernelGGL(k_proj_search, dim3((a.nq + 3) / 4), dim3(256), 0, st, a);
+    if (timer) timer->stop(ORBX_MK_PROJ_SEARCH, e, st);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    if (proj_mode_greedy(a.mode)) {
+        e = timer ? timer->start(st) : nullptr;
+        hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64),
+                           proj_resolve_lds_bytes(a.mode, a.T.n, a.nq), st, a);
+        if (timer) timer->stop(ORBX_MK_PROJ_RESOLVE, e, st);
+        err = hipGetLastError();
+        if (err != hipSuccess) return err;
+    }
+    hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t prepare_match_kernels() {
+    const int lds = (int)MATCH_MAX_LDS;
+    hipError_t e;
+    if ((e = hipFuncSetAttribute((const void*)k_bow<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_bow<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_triangulate, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_proj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+}  // namespace orbx

@@ -1,0 +1,78 @@
+// orbx_match_kernels.h — launch descriptors of the matcher kernels (orbx_match.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbx_match.h"
+
+namespace orbx {
+
+// Internal projection mode after the public ones: SearchForInitialization (:446-561).
+constexpr int PROJ_INIT = ORBX_PROJ_MODE_COUNT;
+constexpr int MATCH_MAX_LEVELS = 16;
+
+// SearchByBoW over jobs: job j pairs keyframe (a_fixed ? 0 : j) of A with keyframe
+// (b_fixed ? 0 : j) of B.  kf_kf = 0: SearchByBoW(KeyFrame*, Frame&) (A = keyframe, B = frame,
+// outputs indexed by B feature); kf_kf = 1: SearchByBoW(KeyFrame*, KeyFrame*) (outputs indexed
+// by A feature).
+struct BowLaunch {
+    orbx_kf_db A, B;
+    int a_fixed, b_fixed, kf_kf, njobs;
+    float ratio;
+    int check_ori;
+    int32_t* out;
+    int out_stride;
+    int32_t* nmatches;
+    int* err;
+};
+
+struct TriLaunch {
+    orbx_kf_db db;
+    int njobs;
+    const int32_t* kf1;
+    const int32_t* kf2;
+    const float* F12;
+    const float* epi;
+    float sigma2[MATCH_MAX_LEVELS];
+    float scale[MATCH_MAX_LEVELS];
+    int only_stereo, check_ori;
+    const int32_t* job_off;
+    int32_t* out;
+    int32_t* nmatches;
+    int* err;
+};
+
+// One projection search (modes of orbx_proj_mode plus PROJ_INIT).
+struct ProjLaunch {
+    int mode;
+    orbx_featureset T;           // device pointers
+    const uint8_t* qdesc;
+    const orbx_proj_query* q;
+    int nq;
+    float inv_sigma2[MATCH_MAX_LEVELS];
+    int orb_dist;
+    float ratio;
+    int check_ori;
+    const uint8_t* claimed_in;   // may be null
+    int32_t* out;                // nq
+    int4* top2;                  // nq (greedy modes)
+    int8_t* out_bin;             // nq
+    int32_t* hist;               // 32
+    int32_t* nmatches;           // 1
+    int* err;
+};
+
+bool proj_mode_greedy(int mode);
+hipError_t launch_bow(const BowLaunch& a, hipStream_t st);
+size_t bow_lds_bytes(const BowLaunch& a);
+hipError_t launch_triangulate(const TriLaunch& a, hipStream_t st);
+size_t tri_lds_bytes(int max_feat);
+// Phase A (window search, static top-2), B (sequential greedy claims), C (rotation filter
+// and count).  launch_proj runs the phases the mode needs; `timer` ids ORBX_MK_*.
+struct KernelTimer;
+hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer);
+size_t proj_resolve_lds_bytes(int mode, int n_target, int nq);
+hipError_t prepare_match_kernels();
+constexpr size_t MATCH_MAX_LDS = 160 * 1024;
+
+}  // namespace orbx

@@ -1,0 +1,158 @@
+"""Per-frame feature arrays the matchers read (the POD view of Frame / KeyFrame).
+
+``FeatureSet`` holds what ORBmatcher touches on a Frame or KeyFrame (src/Frame.h,
+src/KeyFrame.h): mvKeysUn, mDescriptors, mvuRight, mFeatVec and mGrid.  The grid and the
+FeatureVector are built here with the reference's host rules:
+
+* ``assign_features_to_grid`` — Frame::AssignFeaturesToGrid + PosInGrid
+  (src/Frame.cc:243-258, 407-417) with the cell size of Frame.cc:114-115 / 168-169 / 225-226
+  (mfGridElementWidthInv = float(FRAME_GRID_COLS) / float(mnMaxX - mnMinX)).
+* ``feature_vector`` — DBoW2::FeatureVector (Thirdparty/DBoW2/DBoW2/FeatureVector.cpp:31-45):
+  std::map<NodeId, vector<feature index>>, features appended in extraction order.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import KEYPOINT_DTYPE
+
+FRAME_GRID_COLS = 64   # include/Frame.h:38
+FRAME_GRID_ROWS = 48   # include/Frame.h:37
+
+
+def round_half_away(v) -> np.ndarray:
+    """std::round on float values (half away from zero), exactly, via float64."""
+    v = np.asarray(v, np.float64)
+    return (np.sign(v) * np.floor(np.abs(v) + 0.5)).astype(np.int64)
+
+
+@dataclass
+class Grid:
+    cols: int
+    rows: int
+    off: np.ndarray        # int32 [cols*rows + 1], cell c = ix*rows + iy
+    feat: np.ndarray       # int32
+    min_x: float
+    min_y: float
+    max_x: float
+    max_y: float
+    inv_w: float
+    inv_h: float
+
+
+def assign_features_to_grid(keys: np.ndarray, min_x: float, max_x: float, min_y: float,
+                            max_y: float, cols: int = FRAME_GRID_COLS,
+                            rows: int = FRAME_GRID_ROWS) -> Grid:
+    """Frame::AssignFeaturesToGrid (src/Frame.cc:243-258) as a CSR grid."""
+    f32 = np.float32
+    inv_w = f32(cols) / f32(f32(max_x) - f32(min_x))
+    inv_h = f32(rows) / f32(f32(max_y) - f32(min_y))
+    x = np.asarray(keys["x"], f32)
+    y = np.asarray(keys["y"], f32)
+    px = round_half_away((x - f32(min_x)) * inv_w)     # PosInGrid, Frame.cc:409-410
+    py = round_half_away((y - f32(min_y)) * inv_h)
+    ok = (px >= 0) & (px < cols) & (py >= 0) & (py < rows)
+    idx = np.nonzero(ok)[0]
+    cell = px[idx] * rows + py[idx]
+    order = np.argsort(cell, kind="stable")            # within a cell: index order
+    feat = idx[order].astype(np.int32)
+    counts = np.bincount(cell, minlength=cols * rows)
+    off = np.zeros(cols * rows + 1, np.int32)
+    np.cumsum(counts, out=off[1:])
+    return Grid(cols, rows, off, feat, float(f32(min_x)), float(f32(min_y)), float(f32(max_x)),
+                float(f32(max_y)), float(inv_w), float(inv_h))
+
+
+@dataclass
+class FeatureVector:
+    node_id: np.ndarray    # uint32, ascending
+    off: np.ndarray        # int32 [n_nodes + 1]
+    feat: np.ndarray       # int32
+
+
+def feature_vector(node_of_feature: np.ndarray) -> FeatureVector:
+    """FeatureVector from the node each feature was assigned to (-1 = none)."""
+    nodes = np.asarray(node_of_feature, np.int64)
+    idx = np.nonzero(nodes >= 0)[0]
+    order = np.argsort(nodes[idx], kind="stable")
+    feat = idx[order].astype(np.int32)
+    ids, counts = np.unique(nodes[idx][order], return_counts=True)
+    off = np.zeros(len(ids) + 1, np.int32)
+    np.cumsum(counts, out=off[1:])
+    return FeatureVector(ids.astype(np.uint32), off, feat)
+
+
+@dataclass
+class FeatureSet:
+    """mvKeysUn / mDescriptors / mvuRight / mFeatVec / mGrid of one Frame or KeyFrame."""
+    keys: np.ndarray                      # KEYPOINT_DTYPE [n]
+    desc: np.ndarray                      # uint8 [n, 32]
+    u_right: np.ndarray | None = None     # float32 [n] (None = monocular)
+    fvec: FeatureVector | None = None
+    grid: Grid | None = None
+    _keep: list = field(default_factory=list, repr=False)
+
+    def __post_init__(self):
+        self.keys = np.ascontiguousarray(self.keys, KEYPOINT_DTYPE)
+        self.desc = np.ascontiguousarray(self.desc, np.uint8).reshape(-1, 32)
+        if self.u_right is not None:
+            self.u_right = np.ascontiguousarray(self.u_right, np.float32)
+        if len(self.keys) != len(self.desc):
+            raise ValueError("keys and descriptors differ in length")
+
+    @property
+    def n(self) -> int:
+        return len(self.keys)
+
+
+class FeatureSetC(ctypes.Structure):
+    """orbx_featureset (include/orbx_match.h)."""
+    _fields_ = [("n", ctypes.c_int32), ("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("u_right", ctypes.c_void_p), ("n_nodes", ctypes.c_int32),
+                ("node_id", ctypes.c_void_p), ("node_off", ctypes.c_void_p),
+                ("node_feat", ctypes.c_void_p), ("grid_cols", ctypes.c_int32),
+                ("grid_rows", ctypes.c_int32), ("grid_off", ctypes.c_void_p),
+                ("grid_feat", ctypes.c_void_p), ("min_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_x", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("grid_inv_w", ctypes.c_float), ("grid_inv_h", ctypes.c_float)]
+
+
+def _addr(a):
+    return None if a is None else a.ctypes.data
+
+
+def featureset_c(fs: FeatureSet) -> FeatureSetC:
+    """The C view of a FeatureSet (host pointers; `fs` must outlive the struct)."""
+    s = FeatureSetC()
+    s.n = fs.n
+    s.keys = _addr(fs.keys)
+    s.desc = _addr(fs.desc)
+    s.u_right = _addr(fs.u_right)
+    if fs.fvec is not None:
+        s.n_nodes = len(fs.fvec.node_id)
+        s.node_id, s.node_off, s.node_feat = (_addr(fs.fvec.node_id), _addr(fs.fvec.off),
+                                              _addr(fs.fvec.feat))
+    if fs.grid is not None:
+        g = fs.grid
+        s.grid_cols, s.grid_rows = g.cols, g.rows
+        s.grid_off, s.grid_feat = _addr(g.off), _addr(g.feat)
+        s.min_x, s.min_y, s.max_x, s.max_y = g.min_x, g.min_y, g.max_x, g.max_y
+        s.grid_inv_w, s.grid_inv_h = g.inv_w, g.inv_h
+    return s
+
+
+PROJ_QUERY_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("radius", "<f4"),
+                             ("min_level", "<i4"), ("max_level", "<i4"),
+                             ("pred_level", "<i4"), ("angle", "<f4")])
+
+# orbx_proj_mode (include/orbx_match.h)
+PROJ_FRAME_MAPPOINTS = 0
+PROJ_KF_SCW = 1
+PROJ_LAST_FRAME = 2
+PROJ_KEYFRAME = 3
+PROJ_FUSE = 4
+PROJ_FUSE_SCW = 5
+PROJ_SIM3 = 6

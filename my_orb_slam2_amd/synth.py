@@ -93,3 +93,191 @@ def edge_cases(width: int = 640, height: int = 480):
         "checker8": (((xx // 8 + yy // 8) % 2) * 255).astype(np.uint8),
         "tiny64": frame(7, 64, 64),
     }
+
+
+# ---- matcher workloads ----------------------------------------------------------------------
+
+def scale_tables(nlevels: int = 8, scale_factor: float = 1.2):
+    """mvScaleFactors / mvLevelSigma2 / mvInvLevelSigma2 as ORBextractor builds them
+    (src/ORBextractor.cc:415-433: float products of the double scale factor)."""
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(scale_factor))))
+    s = np.array(s, np.float32)
+    s2 = (s * s).astype(np.float32)
+    return s, s2, (np.float32(1.0) / s2).astype(np.float32)
+
+
+def _octaves(rng, n, nlevels=8, scale_factor=1.2):
+    w = np.float64(scale_factor) ** -np.arange(nlevels)
+    return rng.choice(nlevels, size=n, p=w / w.sum()).astype(np.int32)
+
+
+def _flip(rng, desc, nflip):
+    d = desc.copy()
+    for i, k in enumerate(nflip):
+        if k:
+            bits = rng.choice(256, size=int(k), replace=False)
+            np.bitwise_xor.at(d[i], bits // 8, (1 << (bits % 8)).astype(np.uint8))
+    return d
+
+
+def _node_of(desc, nodes):
+    # a stand-in vocabulary: the node a descriptor falls into depends on a few of its bits,
+    # so near-identical descriptors usually (not always) share it; ids are sparse
+    key = (desc[:, 0].astype(np.int64) * 131 + desc[:, 5].astype(np.int64) * 7) % nodes
+    return 1000 + 3 * key
+
+
+def feature_pair(seed: int, n1: int = 1000, n2: int = 1000, width: int = 752,
+                 height: int = 480, match_frac: float = 0.6, nodes: int = 40,
+                 stereo_frac: float = 0.5, rotation: float = 25.0, dup_frac: float = 0.05,
+                 single_node: bool = False, max_flip: int = 40, nlevels: int = 8):
+    """Two correlated feature sets (Frame/KeyFrame arrays) for the matcher tests.
+
+    A fraction of set-2 features are noisy copies of set-1 features (position +-2 px, angle
+    rotated by `rotation` with 10% outliers, 0..max_flip flipped descriptor bits); a few
+    set-2 descriptors are duplicated onto neighbours so distance ties occur.  Returns
+    (f1, f2, truth) with truth[i] = the set-2 copy of set-1 feature i or -1.
+    """
+    from .features import FeatureSet, assign_features_to_grid, feature_vector
+    from ._lib import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    k1 = np.zeros(n1, KEYPOINT_DTYPE)
+    k1["x"] = rng.uniform(0, width, n1)
+    k1["y"] = rng.uniform(0, height, n1)
+    k1["octave"] = _octaves(rng, n1, nlevels)
+    k1["angle"] = rng.uniform(0, 360, n1)
+    k1["size"] = 31
+    k1["class_id"] = -1
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+
+    nm = min(int(match_frac * min(n1, n2)), n1, n2)
+    src = rng.choice(n1, size=nm, replace=False)
+    dst = rng.choice(n2, size=nm, replace=False)
+    k2 = np.zeros(n2, KEYPOINT_DTYPE)
+    k2["x"] = rng.uniform(0, width, n2)
+    k2["y"] = rng.uniform(0, height, n2)
+    k2["octave"] = _octaves(rng, n2, nlevels)
+    k2["angle"] = rng.uniform(0, 360, n2)
+    k2["size"] = 31
+    k2["class_id"] = -1
+    d2 = rng.integers(0, 256, (n2, 32), dtype=np.uint8)
+    k2["x"][dst] = np.clip(k1["x"][src] + rng.normal(0, 2, nm), 0, width - 1e-3)
+    k2["y"][dst] = np.clip(k1["y"][src] + rng.normal(0, 2, nm), 0, height - 1e-3)
+    k2["octave"][dst] = np.clip(k1["octave"][src] + rng.integers(-1, 2, nm), 0, nlevels - 1)
+    ang = (k1["angle"][src] - rotation + rng.normal(0, 4, nm)) % 360
+    out = rng.random(nm) < 0.1
+    ang[out] = rng.uniform(0, 360, out.sum())
+    k2["angle"][dst] = ang.astype(np.float32)
+    d2[dst] = _flip(rng, d1[src], rng.integers(0, max_flip + 1, nm))
+    # duplicated descriptors next to each other: exact distance ties
+    nd = int(dup_frac * n2)
+    if nd:
+        a = rng.choice(n2, size=nd, replace=False)
+        b = rng.choice(n2, size=nd, replace=False)
+        d2[b] = d2[a]
+        k2["x"][b] = np.clip(k2["x"][a] + rng.uniform(-3, 3, nd), 0, width - 1e-3)
+        k2["y"][b] = np.clip(k2["y"][a] + rng.uniform(-3, 3, nd), 0, height - 1e-3)
+        k2["octave"][b] = k2["octave"][a]
+    truth = np.full(n1, -1, np.int64)
+    truth[src] = dst
+
+    def stereo(keys):
+        ur = np.full(len(keys), -1.0, np.float32)
+        s = rng.random(len(keys)) < stereo_frac
+        ur[s] = (keys["x"][s] - rng.uniform(2, 64, s.sum())).astype(np.float32)
+        return ur
+
+    def fset(keys, desc):
+        nodes_of = np.zeros(len(keys), np.int64) if single_node else _node_of(desc, nodes)
+        fs = FeatureSet(keys, desc, stereo(keys), feature_vector(nodes_of),
+                        assign_features_to_grid(keys, 0.0, width, 0.0, height))
+        return fs
+
+    return fset(k1, d1), fset(k2, d2), truth
+
+
+def projection_queries(seed: int, f1, f2, truth, th: float = 3.0, nlevels: int = 8,
+                       mode_levels: str = "frame", inactive_frac: float = 0.05,
+                       max_flip: int = 20):
+    """MapPoint projections into f2 built from f1's features (for the projection searches):
+    matched features project near their f2 copy, the rest anywhere.  Returns
+    (queries PROJ_QUERY_DTYPE, descriptors)."""
+    from .features import PROJ_QUERY_DTYPE
+    rng = np.random.default_rng(seed)
+    scale, _, _ = scale_tables(nlevels)
+    n = f1.n
+    q = np.zeros(n, PROJ_QUERY_DTYPE)
+    has = truth >= 0
+    tx = np.where(has, f2.keys["x"][np.maximum(truth, 0)], rng.uniform(0, 752, n))
+    ty = np.where(has, f2.keys["y"][np.maximum(truth, 0)], rng.uniform(0, 480, n))
+    q["u"] = (tx + rng.normal(0, 1.5, n)).astype(np.float32)
+    q["v"] = (ty + rng.normal(0, 1.5, n)).astype(np.float32)
+    pred = np.where(has, f2.keys["octave"][np.maximum(truth, 0)], f1.keys["octave"])
+    pred = np.clip(pred + rng.integers(-1, 2, n), 0, nlevels - 1).astype(np.int32)
+    q["pred_level"] = pred
+    q["radius"] = (np.float32(th) * scale[pred]).astype(np.float32)
+    if mode_levels == "frame":
+        q["min_level"] = pred - 1
+        q["max_level"] = pred
+    else:
+        q["min_level"] = -1
+        q["max_level"] = -1
+    ur = f2.u_right[np.maximum(truth, 0)] if f2.u_right is not None else np.full(n, -1, np.float32)
+    q["ur"] = np.where(has & (ur > 0), ur + rng.normal(0, 1.0, n), q["u"] - 30).astype(np.float32)
+    q["angle"] = f1.keys["angle"]
+    q["radius"][rng.random(n) < inactive_frac] = -1.0
+    desc = _flip(rng, f1.desc, rng.integers(0, max_flip + 1, n))
+    return q, desc
+
+
+def _rot(rng, max_deg):
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    a = np.deg2rad(rng.uniform(-max_deg, max_deg))
+    Kx = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + np.sin(a) * Kx + (1 - np.cos(a)) * Kx @ Kx
+
+
+def keyframe_pair(seed: int, n1: int = 1000, n2: int = 1000, width: int = 752,
+                  height: int = 480, fx: float = 458.654, fy: float = 457.296,
+                  cx: float = 367.215, cy: float = 248.375, baseline: float = 0.5,
+                  match_frac: float = 0.6, nodes: int = 40, single_node: bool = False,
+                  stereo_frac: float = 0.3):
+    """Two keyframes observing one random 3D scene (LocalMapping's SearchForTriangulation
+    workload): set-2 copies of set-1 features sit at the true projection (+-0.5 px), so the
+    epipolar test passes for them.  Returns (kf1, kf2, F12 float32 3x3, (ex, ey), truth).
+    F12 = K^-T [t12]x R12 K^-1 as LocalMapping::ComputeF12 (LocalMapping.cc:612-629); the
+    epipole with the float expressions of ORBmatcher.cc:712-715."""
+    f1, f2, truth = feature_pair(seed, n1, n2, width, height, match_frac, nodes, stereo_frac,
+                                 rotation=5.0, single_node=single_node)
+    from .features import assign_features_to_grid
+    rng = np.random.default_rng(seed + 7919)
+    K = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1.0]])
+    R1w, t1w = np.eye(3), np.zeros(3)
+    R2w = _rot(rng, 5.0)
+    # baseline direction: sideways and/or forward, so the epipole is sometimes in view
+    C2w = baseline * np.array([rng.uniform(-1, 1), rng.uniform(-0.2, 0.2), rng.uniform(-1.2, 1.2)])
+    t2w = -R2w @ C2w
+    src = np.nonzero(truth >= 0)[0]
+    dst = truth[src]
+    z = rng.uniform(2.0, 25.0, len(src))
+    P = np.stack([(f1.keys["x"][src] - cx) / fx * z, (f1.keys["y"][src] - cy) / fy * z, z], 1)
+    Pc2 = P @ R2w.T + t2w
+    u2 = fx * Pc2[:, 0] / Pc2[:, 2] + cx + rng.normal(0, 0.5, len(src))
+    v2 = fy * Pc2[:, 1] / Pc2[:, 2] + cy + rng.normal(0, 0.5, len(src))
+    f2.keys["x"][dst] = np.clip(u2, 0, width - 1e-3)
+    f2.keys["y"][dst] = np.clip(v2, 0, height - 1e-3)
+    f2.grid = assign_features_to_grid(f2.keys, 0.0, width, 0.0, height)
+    R12 = R1w @ R2w.T
+    t12 = -R1w @ R2w.T @ t2w + t1w
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    Kinv = np.linalg.inv(K)
+    F12 = (Kinv.T @ tx @ R12 @ Kinv).astype(np.float32)
+    Cw = (-R1w.T @ t1w).astype(np.float32)
+    C2 = (R2w.astype(np.float32) @ Cw + t2w.astype(np.float32)).astype(np.float32)
+    invz = np.float32(1.0) / C2[2]
+    ex = np.float32(np.float32(np.float32(fx) * C2[0]) * invz) + np.float32(cx)
+    ey = np.float32(np.float32(np.float32(fy) * C2[1]) * invz) + np.float32(cy)
+    return f1, f2, F12, (float(ex), float(ey)), truth

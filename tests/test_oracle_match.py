@@ -1,0 +1,326 @@
+"""CPU checks of the ORBmatcher restatement (oracle/orb_matcher_oracle.cpp).
+
+The reference ships no matcher fixtures and cannot be built here, so the C++ restatement is
+cross-checked against a second, independent reading of src/ORBmatcher.cc written below in
+plain Python (small sizes), plus known answers for ComputeThreeMaxima and the grid.  Also
+checks the product's host-side grid / FeatureVector builders against the oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from my_orb_slam2_amd import synth
+from my_orb_slam2_amd.features import (PROJ_FRAME_MAPPOINTS, PROJ_FUSE, PROJ_KEYFRAME,
+                                       PROJ_KF_SCW, PROJ_LAST_FRAME, assign_features_to_grid,
+                                       feature_vector)
+from oracle import matcher as om
+
+f32 = np.float32
+
+
+def hd(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def rot_bin(a1, a2):
+    rot = f32(f32(a1) - f32(a2))
+    if rot < 0.0:
+        rot = f32(rot + f32(360.0))
+    v = float(f32(rot * f32(f32(1.0) / f32(30))))
+    b = int(np.floor(v + 0.5))   # round half away (v >= 0)
+    return 0 if b == 30 else b
+
+
+def three_maxima_py(counts):
+    max1 = max2 = max3 = 0
+    i1 = i2 = i3 = -1
+    for i, s in enumerate(counts):
+        if s > max1:
+            max3, max2, max1 = max2, max1, s
+            i3, i2, i1 = i2, i1, i
+        elif s > max2:
+            max3, max2 = max2, s
+            i3, i2 = i2, i
+        elif s > max3:
+            max3, i3 = s, i
+    if max2 < f32(0.1) * f32(max1):
+        i2 = i3 = -1
+    elif max3 < f32(0.1) * f32(max1):
+        i3 = -1
+    return i1, i2, i3
+
+
+@pytest.mark.parametrize("counts,expect", [
+    ([0] * 30, (-1, -1, -1)),
+    ([5] + [0] * 29, (0, -1, -1)),
+    ([1, 2, 3] + [0] * 27, (2, 1, 0)),
+    ([100, 9, 10] + [0] * 27, (0, 2, -1)),     # 9 < 0.1*100 drops the third
+    ([100, 5, 3] + [0] * 27, (0, -1, -1)),     # second below 10%: both dropped
+    ([4, 4, 4, 4] + [0] * 26, (0, 1, 2)),      # ties keep the first bins (strict >)
+])
+def test_three_maxima_kat(counts, expect):
+    assert om.three_maxima(counts) == expect
+    assert three_maxima_py(counts) == expect
+
+
+def test_three_maxima_random():
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        c = rng.integers(0, 20, 30) * (rng.random(30) < 0.3)
+        assert om.three_maxima(c) == three_maxima_py(list(c))
+
+
+def test_grid_matches_oracle():
+    for seed in range(4):
+        f1, _, _ = synth.feature_pair(seed, n1=600, n2=10)
+        g = f1.grid
+        off, feat = om.assign_grid(f1.keys, g.min_x, g.min_y, g.inv_w, g.inv_h)
+        np.testing.assert_array_equal(off, g.off)
+        np.testing.assert_array_equal(feat, g.feat)
+
+
+def test_grid_rounding_edges():
+    # PosInGrid uses std::round (half away from zero): x exactly on a half cell
+    from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
+    k = np.zeros(6, KEYPOINT_DTYPE)
+    k["x"] = [0.0, 5.875, 5.874, 751.99, -0.1, -5.875]
+    k["y"] = [0.0, 5.0, 5.0, 479.9, 3.0, 3.0]
+    g = assign_features_to_grid(k, 0.0, 752.0, 0.0, 480.0)
+    off, feat = om.assign_grid(k, g.min_x, g.min_y, g.inv_w, g.inv_h)
+    np.testing.assert_array_equal(off, g.off)
+    np.testing.assert_array_equal(feat, g.feat)
+
+
+def test_feature_vector_layout():
+    fv = feature_vector(np.array([7, 3, 7, -1, 3, 11]))
+    np.testing.assert_array_equal(fv.node_id, [3, 7, 11])
+    np.testing.assert_array_equal(fv.off, [0, 2, 4, 5])
+    np.testing.assert_array_equal(fv.feat, [1, 4, 0, 2, 5])
+
+
+# ---- independent restatements (plain Python) ----------------------------------------------
+
+def nodes(fs):
+    return {int(fs.fvec.node_id[j]): [int(i) for i in fs.fvec.feat[fs.fvec.off[j]:fs.fvec.off[j + 1]]]
+            for j in range(len(fs.fvec.node_id))}
+
+
+def bow_kf_frame_py(kf, valid, f, ratio, check_ori):
+    match = [-1] * f.n
+    hist = [[] for _ in range(30)]
+    n = 0
+    fn = nodes(f)
+    for nid, kfi in sorted(nodes(kf).items()):
+        if nid not in fn:
+            continue
+        for ik in kfi:
+            if not valid[ik]:
+                continue
+            b1, b2, bi = 256, 256, -1
+            for jf in fn[nid]:
+                if match[jf] >= 0:
+                    continue
+                d = hd(kf.desc[ik], f.desc[jf])
+                if d < b1:
+                    b2, b1, bi = b1, d, jf
+                elif d < b2:
+                    b2 = d
+            if b1 <= 50 and f32(b1) < f32(ratio) * f32(b2):
+                match[bi] = ik
+                if check_ori:
+                    hist[rot_bin(kf.keys["angle"][ik], f.keys["angle"][bi])].append(bi)
+                n += 1
+    if check_ori:
+        t = three_maxima_py([len(h) for h in hist])
+        for b in range(30):
+            if b not in t:
+                for j in hist[b]:
+                    match[j] = -1
+                    n -= 1
+    return n, np.array(match, np.int32)
+
+
+def epi_ok(kp1, kp2, F, sigma2):
+    a = f32(f32(f32(kp1["x"]) * F[0]) + f32(f32(kp1["y"]) * F[3])) + F[6]
+    b = f32(f32(f32(kp1["x"]) * F[1]) + f32(f32(kp1["y"]) * F[4])) + F[7]
+    c = f32(f32(f32(kp1["x"]) * F[2]) + f32(f32(kp1["y"]) * F[5])) + F[8]
+    a, b, c = f32(a), f32(b), f32(c)
+    num = f32(f32(f32(a * f32(kp2["x"])) + f32(b * f32(kp2["y"]))) + c)
+    den = f32(f32(a * a) + f32(b * b))
+    if den == 0:
+        return False
+    dsqr = f32(f32(num * num) / den)
+    return float(dsqr) < 3.84 * float(sigma2[kp2["octave"]])
+
+
+def triangulation_py(k1, h1, k2, h2, F, ex, ey, sigma2, scale, only_stereo):
+    F = np.asarray(F, f32).reshape(9)
+    out = {}
+    n2 = nodes(k2)
+    for nid, l1 in sorted(nodes(k1).items()):
+        if nid not in n2:
+            continue
+        for i1 in l1:
+            if h1[i1]:
+                continue
+            s1 = k1.u_right[i1] >= 0
+            if only_stereo and not s1:
+                continue
+            best, bi = 50, -1
+            for i2 in n2[nid]:
+                if h2[i2]:
+                    continue
+                s2 = k2.u_right[i2] >= 0
+                if only_stereo and not s2:
+                    continue
+                d = hd(k1.desc[i1], k2.desc[i2])
+                if d > 50 or d > best:
+                    continue
+                kp2 = k2.keys[i2]
+                if not s1 and not s2:
+                    dx, dy = f32(f32(ex) - kp2["x"]), f32(f32(ey) - kp2["y"])
+                    if f32(f32(dx * dx) + f32(dy * dy)) < f32(f32(100) * scale[kp2["octave"]]):
+                        continue
+                if epi_ok(k1.keys[i1], kp2, F, sigma2):
+                    best, bi = d, i2
+            if bi >= 0:
+                out[i1] = bi
+    pairs = np.array(sorted(out.items()), np.int32).reshape(-1, 2)
+    return len(pairs), pairs
+
+
+def area_py(fs, x, y, r, minl, maxl):
+    g = fs.grid
+    x, y, r = f32(x), f32(y), f32(r)
+    fl = lambda v: int(np.floor(v)) if np.isfinite(v) else -2**31
+    cx0 = max(0, fl(f32(f32(f32(x - f32(g.min_x)) - r) * f32(g.inv_w))))
+    if cx0 >= g.cols:
+        return []
+    cx1 = min(g.cols - 1, int(np.ceil(f32(f32(f32(x - f32(g.min_x)) + r) * f32(g.inv_w)))))
+    if cx1 < 0:
+        return []
+    cy0 = max(0, fl(f32(f32(f32(y - f32(g.min_y)) - r) * f32(g.inv_h))))
+    if cy0 >= g.rows:
+        return []
+    cy1 = min(g.rows - 1, int(np.ceil(f32(f32(f32(y - f32(g.min_y)) + r) * f32(g.inv_h)))))
+    if cy1 < 0:
+        return []
+    check = minl > 0 or maxl >= 0
+    out = []
+    for ix in range(cx0, cx1 + 1):
+        for iy in range(cy0, cy1 + 1):
+            c = ix * g.rows + iy
+            for i in g.feat[g.off[c]:g.off[c + 1]]:
+                kp = fs.keys[i]
+                if check:
+                    if kp["octave"] < minl:
+                        continue
+                    if maxl >= 0 and kp["octave"] > maxl:
+                        continue
+                if abs(f32(kp["x"] - x)) < r and abs(f32(kp["y"] - y)) < r:
+                    out.append(int(i))
+    return out
+
+
+def projection_py(mode, T, q, qdesc, claimed, ratio, check_ori, orb_dist=100, inv_sigma2=None):
+    cl = [bool(c) for c in claimed] if claimed is not None else [False] * T.n
+    out = [-1] * len(q)
+    owner = {}
+    hist = [[] for _ in range(30)]
+    n = 0
+    for iq, qq in enumerate(q):
+        if not qq["radius"] >= 0:
+            continue
+        if mode in (PROJ_FRAME_MAPPOINTS, PROJ_LAST_FRAME, PROJ_KEYFRAME):
+            cand = area_py(T, qq["u"], qq["v"], qq["radius"], qq["min_level"], qq["max_level"])
+        else:
+            cand = area_py(T, qq["u"], qq["v"], qq["radius"], -1, -1)
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for i in cand:
+            if mode in (PROJ_FRAME_MAPPOINTS, PROJ_KF_SCW, PROJ_LAST_FRAME, PROJ_KEYFRAME) and cl[i]:
+                continue
+            kp = T.keys[i]
+            if mode in (PROJ_KF_SCW, PROJ_FUSE):
+                if kp["octave"] < qq["pred_level"] - 1 or kp["octave"] > qq["pred_level"]:
+                    continue
+            if mode in (PROJ_FRAME_MAPPOINTS, PROJ_LAST_FRAME) and T.u_right[i] > 0:
+                if abs(f32(qq["ur"] - T.u_right[i])) > qq["radius"]:
+                    continue
+            if mode == PROJ_FUSE:
+                ex, ey = f32(qq["u"] - kp["x"]), f32(qq["v"] - kp["y"])
+                if T.u_right[i] >= 0:
+                    er = f32(qq["ur"] - T.u_right[i])
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * inv_sigma2[kp["octave"]])) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * inv_sigma2[kp["octave"]])) > 5.99:
+                        continue
+            d = hd(qdesc[iq], T.desc[i])
+            if d < bd:
+                bd2, bl2, bd, bl, bi = bd, bl, d, int(kp["octave"]), i
+            elif d < bd2:
+                bd2, bl2 = d, int(kp["octave"])
+        th = {PROJ_FRAME_MAPPOINTS: 100, PROJ_KF_SCW: 50, PROJ_LAST_FRAME: 100,
+              PROJ_KEYFRAME: orb_dist, PROJ_FUSE: 50}[mode]
+        if bd <= th:
+            if mode == PROJ_FRAME_MAPPOINTS and bl == bl2 and f32(bd) > f32(ratio) * f32(bd2):
+                continue
+            if mode != PROJ_FUSE:
+                cl[bi] = True
+            out[iq] = bi
+            owner[bi] = iq
+            n += 1
+            if check_ori and mode in (PROJ_LAST_FRAME, PROJ_KEYFRAME):
+                hist[rot_bin(qq["angle"], T.keys["angle"][bi])].append(bi)
+    if check_ori and mode in (PROJ_LAST_FRAME, PROJ_KEYFRAME):
+        t = three_maxima_py([len(h) for h in hist])
+        for b in range(30):
+            if b not in t:
+                for j in hist[b]:
+                    out[owner[j]] = -1
+                    n -= 1
+    return n, np.array(out, np.int32)
+
+
+# ---- cross-checks ----------------------------------------------------------------------
+
+@pytest.mark.parametrize("seed,check_ori,ratio,single", [(0, True, 0.75, False),
+                                                         (1, False, 0.6, False),
+                                                         (2, True, 0.7, True)])
+def test_bow_kf_frame_crosscheck(seed, check_ori, ratio, single):
+    f1, f2, _ = synth.feature_pair(seed, n1=160, n2=150, nodes=6, single_node=single)
+    valid = np.random.default_rng(seed).random(f1.n) < 0.8
+    n_o, m_o = om.search_by_bow_kf_frame(f1, valid, f2, ratio, check_ori)
+    n_p, m_p = bow_kf_frame_py(f1, valid, f2, ratio, check_ori)
+    assert n_o == n_p and n_o > 0
+    np.testing.assert_array_equal(m_o, m_p)
+
+
+@pytest.mark.parametrize("seed,only_stereo", [(0, False), (1, True), (2, False)])
+def test_triangulation_crosscheck(seed, only_stereo):
+    k1, k2, F, epi, _ = synth.keyframe_pair(seed, n1=220, n2=220, nodes=5, stereo_frac=0.4)
+    rng = np.random.default_rng(seed + 10)
+    h1, h2 = rng.random(k1.n) < 0.3, rng.random(k2.n) < 0.3
+    s, s2, _ = synth.scale_tables()
+    n_o, p_o = om.search_for_triangulation(k1, h1, k2, h2, F, epi, s2, s, only_stereo,
+                                           check_ori=False)
+    n_p, p_p = triangulation_py(k1, h1, k2, h2, F, epi[0], epi[1], s2, s, only_stereo)
+    assert n_o == n_p and n_o > 0
+    np.testing.assert_array_equal(p_o, p_p)
+
+
+@pytest.mark.parametrize("mode", [PROJ_FRAME_MAPPOINTS, PROJ_KF_SCW, PROJ_LAST_FRAME,
+                                  PROJ_KEYFRAME, PROJ_FUSE])
+def test_projection_crosscheck(mode):
+    f1, f2, t = synth.feature_pair(11 + mode, n1=150, n2=160, dup_frac=0.15)
+    q, d = synth.projection_queries(5 + mode, f1, f2, t, th=6.0,
+                                    mode_levels="frame" if mode in (0, 2, 3) else "kf")
+    claimed = np.random.default_rng(mode).random(f2.n) < 0.1
+    _, _, isg = synth.scale_tables()
+    n_o, m_o = om.search_by_projection(mode, f2, q, d, claimed, isg, orb_dist=64, nnratio=0.8)
+    n_p, m_p = projection_py(mode, f2, q, d, claimed, 0.8, True, orb_dist=64, inv_sigma2=isg)
+    assert n_o == n_p and n_o > 0
+    np.testing.assert_array_equal(m_o, m_p)
