@@ -34,6 +34,11 @@ MBF, FX = 386.1448, 718.856            # Examples/Stereo/KITTI00-02.yaml:8,25
 HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
+                       ("r01_pmc_fetch_b256.csv", "r01_pmc_write_b256.csv"))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,8 +49,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--traffic-csv", default=None,
-                    help="rocprofv3 --pmc counter_collection.csv for the roofline traffic field")
+    ap.add_argument("--traffic-csv", default=DEFAULT_PMC,
+                    help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
+                         " and WRITE_SIZE for the roofline traffic field (default: the"
+                         " committed profiles/ summaries of this workload)")
     return ap.parse_args()
 
 
@@ -176,26 +183,32 @@ def kernel_bytes(sb, B):
     }
 
 
-def traffic_from_csv(path, kernel):
-    if not path or not os.path.exists(path):
-        return None
+def traffic_from_csv(paths, kernel):
+    """HBM bytes per launch of `kernel` from rocprofv3 --pmc counter CSVs (FETCH_SIZE and
+    WRITE_SIZE come from separate passes, MI355X_MICROARCH.md §HBM): each counter is
+    averaged over the kernel's dispatches in the file that holds it; both are KiB; FETCH_SIZE
+    is doubled (gfx950 tallies a wide streaming read at half its bytes)."""
     import csv
-    fetch = write = 0.0
-    n = set()
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel not in row.get("Kernel_Name", ""):
-                continue
-            n.add(row.get("Dispatch_Id"))
-            if row.get("Counter_Name") == "FETCH_SIZE":
-                fetch += float(row["Counter_Value"])
-            elif row.get("Counter_Name") == "WRITE_SIZE":
-                write += float(row["Counter_Value"])
-    if not n:
+    import glob
+    files = []
+    for p in (paths or "").split(","):
+        files += sorted(glob.glob(p.strip())) if p.strip() else []
+    per = {}
+    for path in files:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel not in row.get("Kernel_Name", ""):
+                    continue
+                name = row.get("Counter_Name")
+                if name in ("FETCH_SIZE", "WRITE_SIZE"):
+                    tot, ids = per.setdefault(name, [0.0, set()])
+                    per[name][0] = tot + float(row["Counter_Value"])
+                    ids.add((path, row.get("Dispatch_Id")))
+    if "FETCH_SIZE" not in per or "WRITE_SIZE" not in per:
         return None
-    # gfx950: FETCH_SIZE reads 1/2 of a wide streaming read (MI355X_MICROARCH.md §HBM);
-    # both counters are in KiB.
-    return (2.0 * fetch + write) * 1024.0 / len(n)
+    fetch = per["FETCH_SIZE"][0] / len(per["FETCH_SIZE"][1])
+    write = per["WRITE_SIZE"][0] / len(per["WRITE_SIZE"][1])
+    return (2.0 * fetch + write) * 1024.0
 
 
 def cpu_baseline(pairs, mb, budget_s):

@@ -1,0 +1,16 @@
+#!/bin/bash
+# One GPU session: GPU tests, kernel trace + PMC passes, then the bench line with the CPU
+# baseline and the measured traffic.  usage: tools/gpu_session.sh TAG [bench args...]
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1 || { echo "GPU TESTS FAILED"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+bash tools/prof_counters.sh $OUT/prof "$@" || { echo "PROFILING FAILED"; exit 1; }
+F=$(ls $OUT/prof/pmc3/*counter_collection.csv 2>/dev/null | head -1)
+W=$(ls $OUT/prof/pmc4/*counter_collection.csv 2>/dev/null | head -1)
+echo "pmc: $F $W"
+timeout -k 10 600 python bench.py --traffic-csv "$F,$W" "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
