@@ -49,6 +49,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--workload", default="stereo", choices=["stereo", "reloc", "triangulation"],
+                    help="stereo = the BASELINE metric (configs[1]); reloc = configs[3] "
+                         "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
+                         "(512 SearchForTriangulation jobs, sharded)")
+    ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
+    ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
     ap.add_argument("--traffic-csv", default=DEFAULT_PMC,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"
@@ -63,6 +69,8 @@ def algorithmic_bytes_fast(level_sizes, cells_area_read, ncand):
 
 def main():
     args = parse()
+    if args.workload != "stereo":
+        return main_match(args)
     import torch
     import torch.distributed as dist
 
@@ -246,6 +254,260 @@ def cpu_baseline(pairs, mb, budget_s):
             "sample": f"{done} KITTI-size synthetic stereo pairs, L/R extraction on 2 threads + "
                       f"ComputeStereoMatches (Frame.cc:89-102), {el:.1f} s",
             "cpu_model": model, "host_cpus": os.cpu_count()}
+
+
+# ---- matcher workloads (configs[3], configs[4]) ----------------------------------------------
+
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 128 lane-ops/clk x 2.4 GHz (guide)
+
+
+def _hash_bytes(torch, idx, salt):
+    """Deterministic pseudo-random bytes of global indices (same on every rank)."""
+    x = idx * 6364136223846793005 + (1442695040888963407 + salt)
+    x = x ^ (x >> 29)
+    x = x * -49064778989728563
+    x = x ^ (x >> 32)
+    return x
+
+
+def _reloc_db(torch, dev, k0, k1, F):
+    """Keyframes [k0, k1) of the synthetic relocalisation database: F features each, one
+    FeatureVector node per keyframe (the brute-force anchor of SURVEY §8c), 90 % of the
+    features with a valid MapPoint."""
+    from my_orb_slam2_amd.matcher import KfDbC
+    K = k1 - k0
+    g = torch.arange(k0 * F, k1 * F, device=dev, dtype=torch.int64)
+    words = _hash_bytes(torch, g[:, None] * 8 + torch.arange(8, device=dev), 0)
+    desc = (words & 0xFFFFFFFF).to(torch.int32).contiguous().view(torch.uint8).reshape(-1, 32)
+    keys = torch.zeros(K * F, 7, dtype=torch.float32, device=dev)
+    keys[:, 3] = (_hash_bytes(torch, g, 77) & 0xFFFF).to(torch.float32) * (360.0 / 65536.0)
+    flag = ((_hash_bytes(torch, g, 99) & 1023) < 922).to(torch.uint8)
+    feat_off = (torch.arange(K + 1, device=dev, dtype=torch.int32) * F).contiguous()
+    node_off = torch.arange(K + 1, device=dev, dtype=torch.int32)
+    node_id = torch.zeros(max(K, 1), dtype=torch.int32, device=dev)
+    node_feat = torch.arange(F, device=dev, dtype=torch.int32).repeat(K).contiguous()
+    keep = [desc, keys, flag, feat_off, node_off, node_id, node_feat]
+    c = KfDbC(K, F, feat_off.data_ptr(), keys.data_ptr(), desc.data_ptr(), 0, flag.data_ptr(),
+              node_off.data_ptr(), node_id.data_ptr(), feat_off.data_ptr(), node_feat.data_ptr())
+    return c, keep, int(flag.sum().item())
+
+
+def _reloc_query(torch, dev, n_kfs, F, seed=5):
+    """The query frame: 30 % of its descriptors are noisy copies of 30 features from each of
+    10 database keyframes (so those keyframes pass the >= 15 match test), the rest random."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    true_kfs = torch.randperm(n_kfs, generator=g)[:10]
+    src = (true_kfs[:, None] * F + torch.randint(0, F, (10, 30), generator=g)).reshape(-1)
+    n_copy = src.numel()
+    rnd = torch.randint(0, 2**31, (F - n_copy, 8), generator=g, dtype=torch.int64)
+    words = torch.cat([_hash_bytes(torch, src[:, None] * 8 + torch.arange(8), 0), rnd])
+    desc = (words & 0xFFFFFFFF).to(torch.int32).contiguous().view(torch.uint8).reshape(-1, 32)
+    flips = torch.randint(0, 256, (n_copy, 20), generator=g)
+    keepflip = torch.rand(n_copy, 20, generator=g) < torch.rand(n_copy, 1, generator=g)
+    for i in range(n_copy):
+        for b in flips[i][keepflip[i]].tolist():
+            desc[i, b // 8] ^= (1 << (b % 8))
+    keys = torch.zeros(F, 7, dtype=torch.float32)
+    ang = (_hash_bytes(torch, src, 77) & 0xFFFF).to(torch.float32) * (360.0 / 65536.0)
+    keys[:n_copy, 3] = torch.remainder(ang - 20.0 + torch.randn(n_copy, generator=g), 360.0)
+    keys[n_copy:, 3] = torch.rand(F - n_copy, generator=g) * 360.0
+    return desc.to(dev), keys.to(dev), true_kfs
+
+
+def main_match(args):
+    import torch
+    import torch.distributed as dist
+    from my_orb_slam2_amd import ORBmatcher
+    from my_orb_slam2_amd.distributed import all_gather_counts, broadcast_query, shard_range
+    from my_orb_slam2_amd.features import FeatureSetC
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    if args.workload == "reloc":
+        F = 1000
+        k0, k1 = shard_range(args.kfs, rank, world)
+        db, keep, nvalid = _reloc_db(torch, dev, k0, k1, F)
+        qdesc, qkeys, true_kfs = _reloc_query(torch, dev, args.kfs, F)
+        qn_off = torch.tensor([0, F], dtype=torch.int32, device=dev)
+        q_node = torch.zeros(1, dtype=torch.int32, device=dev)
+        q_feat = torch.arange(F, dtype=torch.int32, device=dev)
+        fc = FeatureSetC()
+        fc.n, fc.keys, fc.desc = F, qkeys.data_ptr(), qdesc.data_ptr()
+        fc.n_nodes, fc.node_id, fc.node_off, fc.node_feat = (1, q_node.data_ptr(),
+                                                            qn_off.data_ptr(), q_feat.data_ptr())
+        m = ORBmatcher(0.75, True, device=local)      # Tracking.cc:1461
+        out = torch.empty((k1 - k0, F), dtype=torch.int32, device=dev)
+        cnt = torch.empty(max(k1 - k0, 1), dtype=torch.int32, device=dev)
+
+        def step():
+            if world > 1:
+                broadcast_query([qdesc, qkeys])
+            m.search_by_bow_kf_frame_batch_device(db, fc, out, cnt, st)
+            if world > 1:
+                return all_gather_counts(cnt[:k1 - k0], args.kfs, world)
+            return cnt[:k1 - k0]
+        units, unit_name = 1, "query frames/sec"
+        work_ops = 16.0 * nvalid * F                   # 8 XOR + 8 BCNT per distance
+        kern = "k_bow"
+        cfg = {"workload": "relocalisation_bf_vs_keyframes", "keyframes": args.kfs,
+               "features_per_keyframe": F, "query_features": F, "nnratio": 0.75,
+               "check_orientation": True, "featurevector": "single node (brute force)",
+               "parallelism": f"keyframe shards x{world}, RCCL broadcast + all-gather"}
+        metric = "relocalisation query frames/sec, 1000-descriptor frame vs 10k keyframes"
+    else:
+        from my_orb_slam2_amd import synth
+        from my_orb_slam2_amd.matcher import DeviceKfDb
+        j0, j1 = shard_range(args.jobs, rank, world)
+        kfs, flags, F12, epi = [], [], [], []
+        for j in range(j0, j1):
+            k1f, k2f, F, e, _ = synth.keyframe_pair(10000 + j, n1=2000, n2=2000, nodes=100)
+            rng = np.random.default_rng(j)
+            kfs += [k1f, k2f]
+            flags += [rng.random(k1f.n) < 0.3, rng.random(k2f.n) < 0.3]
+            F12.append(F.reshape(9))
+            epi.append(e)
+        db = DeviceKfDb(kfs, flags, dev)
+        nj = j1 - j0
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        kf1 = T(np.arange(nj, dtype=np.int32) * 2)
+        kf2 = T(np.arange(nj, dtype=np.int32) * 2 + 1)
+        n1 = np.array([kfs[2 * i].n for i in range(nj)], np.int32)
+        job_off = T(np.concatenate([[0], np.cumsum(n1)]).astype(np.int32))
+        dF, dE = T(np.array(F12, np.float32)), T(np.array(epi, np.float32))
+        s, s2, _ = synth.scale_tables()
+        m = ORBmatcher(0.6, False, device=local)      # LocalMapping.cc:276
+        out = torch.empty(int(n1.sum()), dtype=torch.int32, device=dev)
+        cnt = torch.empty(max(nj, 1), dtype=torch.int32, device=dev)
+
+        def step():
+            m.search_for_triangulation_batch_device(db.c, kf1, kf2, dF, dE, s2, s, job_off, out,
+                                                    cnt, stream=st)
+            if world > 1:
+                return all_gather_counts(cnt[:nj], args.jobs, world)
+            return cnt[:nj]
+        units, unit_name = args.jobs, "keyframe-pair jobs/sec"
+        work_ops = None
+        kern = "k_triangulate"
+        cfg = {"workload": "batched_search_for_triangulation", "jobs": args.jobs,
+               "features_per_keyframe": 2000, "vocabulary_nodes": 100, "only_stereo": False,
+               "check_orientation": False, "parallelism": f"job shards x{world}, RCCL all-gather"}
+        metric = "SearchForTriangulation keyframe-pair jobs/sec (512 jobs, 2000 features/KF)"
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize(dev)
+    m.sync(st)
+    m.profile(not args.no_kernel_timing)
+    m.collect_profile()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    m.sync(st)
+    prof = m.collect_profile() if not args.no_kernel_timing else {}
+    counts = res.cpu().numpy()
+    roof = None
+    if prof and prof.get(kern, (0, 0))[1]:
+        tot_ms, launches = prof[kern]
+        avg_s = tot_ms / 1000.0 / launches
+        if work_ops is not None:
+            ach = work_ops / avg_s / 1e12
+            roof = {"kernel": kern, "bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
+                    "unit": "Tops/s (int32 lane-ops)", "frac": ach / VALU_PEAK_TOPS,
+                    "traffic": None, "algorithmic_ops_per_launch": work_ops,
+                    "avg_launch_ms": avg_s * 1000.0}
+        else:
+            nbytes = float(sum(fs.n for fs in kfs) * (32 + 28 + 4 + 1))
+            ach = nbytes / avg_s / 1e9
+            roof = {"kernel": kern, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                    "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": avg_s * 1000.0}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = match_cpu_baseline(args, torch, keep if args.workload == "reloc" else None,
+                                 (qdesc, qkeys) if args.workload == "reloc" else None,
+                                 None if args.workload == "reloc" else (kfs, flags, F12, epi))
+    if rank == 0:
+        extra = {}
+        if args.workload == "reloc":
+            from my_orb_slam2_amd.distributed import relocalisation_candidates
+            cand = relocalisation_candidates(counts)
+            extra = {"candidates_ge_15": int(len(cand)),
+                     "true_keyframes_found": int(np.isin(true_kfs.numpy(), cand).sum())
+                     if world > 1 or args.kfs == k1 - k0 else None}
+        else:
+            extra = {"mean_pairs_per_job": float(counts.mean())}
+        out_line = {"metric": metric, "value": units * args.steps / elapsed, "unit": unit_name,
+                    "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                    "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+                    "scaling": "strong", "vs_baseline": None, "dtype": "u8 (256-bit Hamming)",
+                    "data": "synthetic", "config": cfg, **extra, "roofline": roof,
+                    "cpu_baseline": cpu}
+        print(json.dumps(out_line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def match_cpu_baseline(args, torch, db_keep, query, tri):
+    """The matcher restatement (oracle/) timed on one host core over a bounded sample of the
+    same workload, scaled to the workload's unit."""
+    try:
+        from oracle import matcher as om
+    except Exception:
+        return None
+    from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
+    from my_orb_slam2_amd.features import FeatureSet, feature_vector
+    budget = min(args.cpu_seconds, 20.0)
+    done, t0 = 0, time.perf_counter()
+    if db_keep is not None:
+        desc, keys, flag = (t.cpu().numpy() for t in db_keep[:3])
+        F = 1000
+        qd, qk = (t.cpu().numpy() for t in query)
+
+        def fs(d, k):
+            kp = np.zeros(len(d), KEYPOINT_DTYPE)
+            kp["angle"] = k[:, 3]
+            return FeatureSet(kp, d, None, feature_vector(np.zeros(len(d))), None)
+        frame = fs(qd, qk)
+        nkf = len(desc) // F
+        while time.perf_counter() - t0 < budget and done < nkf:
+            sl = slice(done * F, (done + 1) * F)
+            om.search_by_bow_kf_frame(fs(desc[sl], keys[sl]), flag[sl], frame, 0.75, True)
+            done += 1
+        el = time.perf_counter() - t0
+        return {"value": done / el / args.kfs, "unit": "query frames/sec", "cores": 1,
+                "kind": "port", "sample": f"SearchByBoW(KF, F) restatement on {done} of the "
+                f"{args.kfs} keyframes in {el:.1f} s, scaled to the whole database"}
+    kfs, flags, F12, epi = tri
+    from my_orb_slam2_amd import synth
+    s, s2, _ = synth.scale_tables()
+    nj = len(F12)
+    while time.perf_counter() - t0 < budget and done < nj:
+        om.search_for_triangulation(kfs[2 * done], flags[2 * done], kfs[2 * done + 1],
+                                    flags[2 * done + 1], F12[done].reshape(3, 3), epi[done], s2,
+                                    s, False, False)
+        done += 1
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "keyframe-pair jobs/sec", "cores": 1, "kind": "port",
+            "sample": f"SearchForTriangulation restatement on {done} of the {nj} jobs, "
+                      f"{el:.1f} s"}
 
 
 if __name__ == "__main__":

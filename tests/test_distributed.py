@@ -1,0 +1,59 @@
+"""CPU (gloo, world_size 2) tests of the multi-GPU plumbing: shard ranges, query broadcast and
+the count all-gather used by the sharded relocalisation / triangulation workloads."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from my_orb_slam2_amd.distributed import (all_gather_counts, broadcast_query,
+                                          relocalisation_candidates, shard_range)
+
+
+@pytest.mark.parametrize("n,world", [(10000, 8), (7, 3), (3, 4), (0, 2), (512, 8)])
+def test_shard_range_partitions(n, world):
+    spans = [shard_range(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (b0, e0), (b1, e1) in zip(spans, spans[1:]):
+        assert e0 == b1
+    sizes = [e - b for b, e in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        desc = torch.zeros(5, 32, dtype=torch.uint8)
+        if rank == 0:
+            desc[:] = torch.arange(160, dtype=torch.uint8).reshape(5, 32)
+        broadcast_query([desc])
+        b, e = shard_range(n_total, rank, world)
+        # each rank "matches" its shard: count = global keyframe id % 20
+        local = torch.arange(b, e, dtype=torch.int32) % 20
+        allc = all_gather_counts(local, n_total, world)
+        q.put((rank, desc.sum().item(), allc.numpy().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_broadcast_and_gather():
+    world, n_total = 2, 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    expect = (np.arange(n_total) % 20).tolist()
+    for rank, s, allc in res:
+        assert s == int(np.arange(160).sum())
+        assert allc == expect
+    cand = relocalisation_candidates(np.array(expect))
+    np.testing.assert_array_equal(cand, [i for i in range(n_total) if i % 20 >= 15])
