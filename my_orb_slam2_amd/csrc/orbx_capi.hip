@@ -162,6 +162,9 @@ int vresize_simd_end(int width) {
 orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     Geometry& G = h->hg;
     memset(&G, 0, sizeof(G));
+    // k_level's row pass folds the symmetric Gaussian taps (getGaussianKernel is symmetric)
+    for (int i = 0; i < 3; ++i)
+        if (h->taps[i] != h->taps[6 - i]) return ORBX_ERR_UNSUPPORTED;
     h->cells.clear();
     h->rtab.clear();
     const int L = h->prm.nlevels;

@@ -68,30 +68,34 @@ namespace orbx {
 
 // Stage a rows x ndw-dword window (row r at gsrc + r*gpitch, 4-byte aligned rows) into LDS
 // (row r at lds + r*lpitch_dw dwords).  Each thread issues up to 8 loads before its first
-// LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.
+// LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.  Element
+// (row, col) indices advance by NT per step incrementally: one division per thread, none
+// per element.
 template <int NT>
 __device__ __forceinline__ void stage_dwords(const uint8_t* __restrict__ gsrc, size_t gpitch,
                                              int rows, int ndw, uint32_t* lds, int lpitch_dw,
                                              int tid) {
     const int n = rows * ndw;
     if (n <= 0) return;
+    const int dr = NT / ndw, dc = NT - dr * ndw;
+    int r = tid / ndw, c = tid - (tid / ndw) * ndw;
     for (int base = 0; base < n; base += NT * 8) {
         uint32_t v[8];
-        // unconditional loads (index clamped): a guarded load becomes a branch + vmcnt(0)
+        int at[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const int i = min(base + k * NT + tid, n - 1);
-            const int r = i / ndw, c = i - r * ndw;
-            v[k] = *(const uint32_t*)(gsrc + (size_t)r * gpitch + 4 * c);
+            // unconditional loads (index clamped): a guarded load becomes a branch + vmcnt(0)
+            const bool in = base + k * NT + tid < n;
+            const int ra = in ? r : rows - 1, ca = in ? c : ndw - 1;
+            v[k] = *(const uint32_t*)(gsrc + (size_t)ra * gpitch + 4 * ca);
+            at[k] = in ? ra * lpitch_dw + ca : -1;
+            c += dc;
+            r += dr;
+            if (c >= ndw) { c -= ndw; ++r; }
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = base + k * NT + tid;
-            if (i < n) {
-                const int r = i / ndw, c = i - r * ndw;
-                lds[r * lpitch_dw + c] = v[k];
-            }
-        }
+        for (int k = 0; k < 8; ++k)
+            if (at[k] >= 0) lds[at[k]] = v[k];
     }
 }
 
@@ -102,22 +106,24 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, si
                                             int tid) {
     const int n = rows * cols;
     if (n <= 0) return;
+    const int dr = NT / cols, dc = NT - dr * cols;
+    int r = tid / cols, c = tid - (tid / cols) * cols;
     for (int base = 0; base < n; base += NT * 16) {
         uint8_t v[16];
+        int at[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int i = min(base + k * NT + tid, n - 1);
-            const int r = i / cols, c = i - r * cols;
-            v[k] = gsrc[(size_t)r * gpitch + c];
+            const bool in = base + k * NT + tid < n;
+            const int ra = in ? r : rows - 1, ca = in ? c : cols - 1;
+            v[k] = gsrc[(size_t)ra * gpitch + ca];
+            at[k] = in ? ra * lpitch + ca : -1;
+            c += dc;
+            r += dr;
+            if (c >= cols) { c -= cols; ++r; }
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int i = base + k * NT + tid;
-            if (i < n) {
-                const int r = i / cols, c = i - r * cols;
-                lds[r * lpitch + c] = v[k];
-            }
-        }
+        for (int k = 0; k < 16; ++k)
+            if (at[k] >= 0) lds[at[k]] = v[k];
     }
 }
 
