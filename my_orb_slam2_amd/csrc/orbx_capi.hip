@@ -53,10 +53,11 @@ struct orbx_extractor {
     Geometry hg;
     std::vector<CellDesc> cells;
     std::vector<int16_t> rtab;
+    std::vector<uint8_t> ltab;   // k_level per-tile tables (LevelColTab / LevelRowTab)
     int ncap = 0, kcap = 0;
     size_t octree_lds = 0, stereo_lds = 0, level_lds = 0;
     int cap_batch = 0;
-    DevBuf d_geom, d_cells, d_rtab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
+    DevBuf d_geom, d_cells, d_rtab, d_ltab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
     long long kscratch_per_image = 0;
     KernelTimer timer;
@@ -316,10 +317,12 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
             }
         }
     }
-    // k_level tiles (128 x 32) and the largest source window it stages (as the kernel does)
-    G.ltw = 128;
-    G.lth = 32;
+    // k_level tiles (128 x 32): per tile column / row the staged source window and the
+    // group / row tables the kernel reads (LevelColTab / LevelRowTab), and the largest window
+    G.ltw = LT_W;
+    G.lth = LT_H;
     G.win_cap = 16;
+    h->ltab.clear();
     for (int l = 0; l < L; ++l) {
         LevelGeom& lv = G.lv[l];
         lv.ntx = (lv.w + G.ltw - 1) / G.ltw;
@@ -327,28 +330,113 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         const int mode = l == 0 ? 0 : (lv.copy ? 1 : (lv.area2 ? 2 : 3));
         const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
         const int16_t* xofs = h->rtab.data() + lv.rtab_off;
-        const int16_t* yofs = xofs + 3 * lv.w;
-        for (int ty = 0; ty < lv.nty; ++ty) {
-            const int Y0 = ty * G.lth, vh = std::min(G.lth, lv.h - Y0);
-            int mny, mxy;
-            reflected_range_h(Y0 - 3, Y0 + vh + 2, lv.h, mny, mxy);
-            for (int tx = 0; tx < lv.ntx; ++tx) {
-                const int X0 = tx * G.ltw, vw = std::min(G.ltw, lv.w - X0);
-                int bytes = 0;
-                if (mode == 0 || mode == 1) {
-                    const int y0 = std::max(Y0 - 3, 0), y1 = std::min(Y0 + G.lth + 2, lv.h - 1);
-                    bytes = (G.ltw + 8) * (y1 - y0 + 1);
-                } else if (mode == 3) {
-                    int mnx, mxx;
-                    reflected_range_h(X0 - 3, X0 + vw + 2, lv.w, mnx, mxx);
-                    const int x0 = xofs[mnx] & ~3, x1 = std::min((int)xofs[mxx] + 1, S.w - 1);
-                    const int y0 = std::min(std::max((int)yofs[mny], 0), S.h - 1);
-                    const int y1 = std::min(std::max((int)yofs[mxy] + 1, 0), S.h - 1);
-                    bytes = (((x1 - x0 + 1) + 3) & ~3) * (y1 - y0 + 1);
+        const int16_t* alpha = xofs + lv.w;
+        const int16_t* yofs = alpha + 2 * lv.w;
+        const int16_t* beta = yofs + lv.h;
+        std::vector<LevelColTab> ct(lv.ntx);
+        std::vector<LevelRowTab> rt(lv.nty);
+        for (int tx = 0; tx < lv.ntx; ++tx) {
+            const int X0 = tx * G.ltw, vw = std::min(G.ltw, lv.w - X0);
+            int x0, x1;
+            if (mode == 3) {
+                int mnx, mxx;
+                reflected_range_h(X0 - 3, X0 + vw + 2, lv.w, mnx, mxx);
+                x0 = xofs[mnx] & ~3;
+                x1 = std::min((int)xofs[mxx] + 1, S.w - 1);
+            } else {
+                x0 = std::max(X0 - 4, 0);
+                x1 = std::min(X0 + G.ltw + 3, lv.w - 1);
+            }
+            LevelColTab& c = ct[tx];
+            memset(&c, 0, sizeof(c));
+            c.x0 = x0;
+            c.ww = x1 - x0 + 1;
+            for (int q = 0; q < LT_G; ++q) {
+                int sx[4];
+                uint32_t fl = 0, al[4] = {0, 0, 0, 0};
+                for (int j = 0; j < 4; ++j) {
+                    const int xr = reflect101_h(X0 - 4 + 4 * q + j, lv.w);
+                    if (mode == 3) {
+                        sx[j] = xofs[xr] - x0;
+                        al[j] = (uint32_t)(uint16_t)alpha[2 * xr] |
+                                ((uint32_t)(uint16_t)alpha[2 * xr + 1] << 16);
+                        fl |= (uint32_t)((xr < lv.xmax ? 1 : 0) | (xr < lv.rsimd_end ? 2 : 0))
+                              << (2 * j);
+                    } else {
+                        sx[j] = (mode == 2) ? xr : xr - (X0 - 4);   // window column (modes 0/1)
+                    }
+                    // pixels of a group outside the needed halo may reflect anywhere: keep
+                    // their (unused) reads inside the window
+                    if (mode == 3) sx[j] = std::min(std::max(sx[j], 0), std::max(c.ww - 1, 0));
+                    else if (mode != 2) sx[j] = std::min(std::max(sx[j], 0), LT_G * 4 - 1);
                 }
-                G.win_cap = std::max(G.win_cap, bytes);
+                const bool contig = sx[1] == sx[0] + 1 && sx[2] == sx[0] + 2 &&
+                                    sx[3] == sx[0] + 3 && (sx[0] & 3) == 0;
+                const int o0 = sx[0] & 3;
+                const bool simple = sx[1] >= sx[0] && sx[2] >= sx[1] && sx[3] >= sx[2] &&
+                                    o0 + (sx[3] - sx[0]) + 1 <= 11;
+                c.cgrp[2 * q] = (uint32_t)sx[0] | ((uint32_t)sx[1] << 16);
+                c.cgrp[2 * q + 1] = (uint32_t)sx[2] | ((uint32_t)sx[3] << 16);
+                uint32_t hi = 0;
+                for (int j = 0; j < 4; ++j) {
+                    // simple groups: pixel j's taps are bytes k, k+1 of the 12 bytes from
+                    // (sx0 & ~3); v_perm picks them from dwords 0-1 (k <= 6) or 1-2 as u16s
+                    const int k = sx[j] - (sx[0] & ~3);
+                    const int kk = (k > 6) ? k - 4 : k;
+                    if (k > 6) hi |= 0x1000u << j;
+                    c.csel[4 * q + j] = (uint32_t)(kk & 7) | (0x0Cu << 8) |
+                                        ((uint32_t)((kk + 1) & 7) << 16) | (0x0Cu << 24);
+                    // right of xmax HResizeLinear uses S[sx] * 2048: the same dot product
+                    // with alphas (2048, 0)
+                    if (mode == 3 && !((fl >> (2 * j)) & 1u)) al[j] = 2048u;
+                }
+                c.cinf[q] = fl | (contig ? 0x100u : 0u) | (simple ? 0x200u : 0u) | hi;
+                for (int j = 0; j < 4; ++j) c.calp[4 * q + j] = al[j];
             }
         }
+        for (int ty = 0; ty < lv.nty; ++ty) {
+            const int Y0 = ty * G.lth, vh = std::min(G.lth, lv.h - Y0);
+            int y0, y1;
+            if (mode == 3) {
+                int mny, mxy;
+                reflected_range_h(Y0 - 3, Y0 + vh + 2, lv.h, mny, mxy);
+                y0 = std::min(std::max((int)yofs[mny], 0), S.h - 1);
+                y1 = std::min(std::max((int)yofs[mxy] + 1, 0), S.h - 1);
+            } else {
+                y0 = std::max(Y0 - 3, 0);
+                y1 = std::min(Y0 + G.lth + 2, lv.h - 1);
+            }
+            LevelRowTab& r = rt[ty];
+            memset(&r, 0, sizeof(r));
+            r.y0 = y0;
+            r.wh = y1 - y0 + 1;
+            for (int k = 0; k < LT_HR; ++k) {
+                const int yr = reflect101_h(Y0 - 3 + k, lv.h);
+                if (mode == 3) {
+                    const int sy = yofs[yr];
+                    const uint32_t y0r = (uint32_t)(std::min(std::max(sy, 0), S.h - 1) - y0);
+                    const uint32_t y1r = (uint32_t)(std::min(std::max(sy + 1, 0), S.h - 1) - y0);
+                    r.rinf[2 * k] = y0r | (y1r << 16);
+                    r.rinf[2 * k + 1] = (uint32_t)(uint16_t)beta[2 * yr] |
+                                        ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16);
+                } else {
+                    r.rinf[2 * k] = (uint32_t)(mode == 2 ? yr : yr - y0);
+                }
+            }
+        }
+        for (int ty = 0; ty < lv.nty; ++ty)
+            for (int tx = 0; tx < lv.ntx; ++tx) {
+                int bytes = 0;
+                if (mode == 0 || mode == 1) bytes = (G.ltw + 8) * rt[ty].wh;
+                else if (mode == 3) bytes = ((ct[tx].ww + 3) & ~3) * rt[ty].wh;
+                G.win_cap = std::max(G.win_cap, bytes);
+            }
+        lv.ctab = (int)h->ltab.size();
+        h->ltab.insert(h->ltab.end(), (const uint8_t*)ct.data(),
+                       (const uint8_t*)(ct.data() + ct.size()));
+        lv.rowtab = (int)h->ltab.size();
+        h->ltab.insert(h->ltab.end(), (const uint8_t*)rt.data(),
+                       (const uint8_t*)(rt.data() + rt.size()));
     }
     h->level_lds = level_lds_bytes(G.ltw, G.lth, G.win_cap);
     if (h->level_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
@@ -389,6 +477,9 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         if (!h->d_geom.ensure(sizeof(Geometry))) return ORBX_ERR_DEVICE;
         if (!h->d_cells.ensure(std::max<size_t>(h->cells.size(), 1) * sizeof(CellDesc))) return ORBX_ERR_DEVICE;
         if (!h->d_rtab.ensure(std::max<size_t>(h->rtab.size(), 1) * 2)) return ORBX_ERR_DEVICE;
+        if (!h->d_ltab.ensure(std::max<size_t>(h->ltab.size(), 16))) return ORBX_ERR_DEVICE;
+        if (!HIPOK(hipMemcpy(h->d_ltab.p, h->ltab.data(), h->ltab.size(), hipMemcpyHostToDevice)))
+            return ORBX_ERR_DEVICE;
         if (!HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
             return ORBX_ERR_DEVICE;
         if (!h->cells.empty() &&
@@ -427,6 +518,7 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.dg = h->d_geom.as<Geometry>();
     a.cells = h->d_cells.as<CellDesc>();
     a.rtab = h->d_rtab.as<int16_t>();
+    a.ltab = h->d_ltab.as<uint8_t>();
     a.d_imgs = d_imgs;
     a.d_imgs2 = d_imgs2 ? d_imgs2 : d_imgs;
     a.split = d_imgs2 ? split : batch;
@@ -563,7 +655,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (!h) return ORBX_ERR_INVALID;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_in, &h->d_pyr, &h->d_blur,
+    DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_in, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv};
     for (DevBuf* b : bufs) b->release();

@@ -41,6 +41,30 @@ struct LevelGeom {
     int copy;               // resize to the same size: plain copy
     int patch_size;         // (int)(31*scale)
     int ntx, nty;           // k_level tiles of this level
+    int ctab, rowtab;       // k_level: byte offsets of the level's column / row tables
+};
+
+// k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
+#define LT_W 128              // output tile width  (32 groups of 4)
+#define LT_H 32               // output tile height
+#define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
+#define LT_HR (LT_H + 6)      // halo rows: y = Y0-3 .. Y0+LT_H+2
+
+// Per-tile-column tables of k_level (host-built, build_geometry): the staged source window's
+// x range and, per halo group of 4 pixels, the source columns, flags and resize alphas.
+struct LevelColTab {
+    int32_t x0, ww, pad0, pad1;
+    uint32_t cgrp[2 * LT_G];  // 4 x u16 source column (window relative)
+    uint32_t cinf[LT_G];      // 2 bits/pixel (xmax, rsimd) | 0x100 contig | 0x200 simple
+                              // | 0x1000 << j: pixel j's taps sit in dwords 1-2
+    uint32_t pad2[2];
+    uint32_t calp[4 * LT_G];  // 4 x (alpha0 | alpha1 << 16); (2048, 0) right of xmax
+    uint32_t csel[4 * LT_G];  // 4 x v_perm selector of the pixel's 2 taps (see k_level)
+};
+// Per-tile-row tables: the window's y range and, per halo row, source rows and betas.
+struct LevelRowTab {
+    int32_t y0, wh, pad0, pad1;
+    uint32_t rinf[2 * LT_HR]; // (ry0 | ry1 << 16, beta0 | beta1 << 16)
 };
 
 struct CellDesc {

@@ -66,6 +66,7 @@ struct ExtractLaunch {
     const Geometry* dg;        // device copy
     const CellDesc* cells;     // device
     const int16_t* rtab;       // device
+    const uint8_t* ltab;       // device: k_level per-tile tables
     const uint8_t* d_imgs;      // images [0, split)
     const uint8_t* d_imgs2;     // images [split, batch) (stereo: right views)
     int split;

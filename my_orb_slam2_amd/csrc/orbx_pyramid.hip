@@ -19,10 +19,21 @@
 
 namespace orbx {
 
-#define LT_W 128              // output tile width  (32 groups of 4)
-#define LT_H 32               // output tile height
-#define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
-#define LT_HR (LT_H + 6)      // halo rows: y = Y0-3 .. Y0+LT_H+2
+#ifdef ORBX_STAMPS
+// Diagnostic build only (tools/level_stamps.py): per-workgroup phase clocks of k_level.
+__device__ unsigned long long g_level_stamps[8][4096][6];
+#define STAMP(k)                                                                         \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        if (tid == 0 && blockIdx.y == 0 && blockIdx.x < 4096) g_level_stamps[level][blockIdx.x][k] = t_; \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 #define LT_GW (LT_W / 4)      // output groups per row
 
 __device__ __forceinline__ int reflect101_i(int p, int len) {
@@ -36,6 +47,8 @@ __device__ __forceinline__ int reflect101_i(int p, int len) {
 }
 
 __device__ __forceinline__ int sat8(int v) { return min(max(v, 0), 255); }
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // min / max of reflect101(p) over p in [lo, hi].
 __device__ __forceinline__ void reflected_range(int lo, int hi, int len, int& mn, int& mx) {
@@ -72,7 +85,7 @@ __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1, bool simd
 }
 
 __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
-                                               const int16_t* __restrict__ rtab,
+                                               const uint8_t* __restrict__ ltab,
                                                const uint8_t* __restrict__ in0,
                                                const uint8_t* __restrict__ in1, int split,
                                                size_t stride, size_t bstride,
@@ -80,6 +93,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                                                uint8_t* __restrict__ blur, int level) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int b = blockIdx.y, tid = threadIdx.x;
+    STAMP(0);
     const LevelGeom& L = g->lv[level];
     const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
     const int X0 = tx * LT_W, Y0 = ty * LT_H;
@@ -92,40 +106,28 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     uint2* cgrp = (uint2*)take((size_t)LT_G * 8);                    // per group: 4 x sx (u16)
     uint32_t* cinf = (uint32_t*)take((size_t)LT_G * 4);              // per group: flags
     uint4* calp = (uint4*)take((size_t)LT_G * 16);                   // per group: 4 x (a0, a1)
+    uint4* csel = (uint4*)take((size_t)LT_G * 16);                   // per group: 4 x selector
     uint2* rinf = (uint2*)take((size_t)LT_HR * 8);                   // per row: ry0, ry1, b0, b1
-    int* sc = (int*)take(16 * 4);
     uint8_t* win = p;                                                // source window
 
     const int mode = level == 0 ? 0 : (L.copy ? 1 : (L.area2 ? 2 : 3));
     const LevelGeom& S = g->lv[level > 0 ? level - 1 : 0];
-    const int16_t* xofs = rtab + L.rtab_off;
-    const int16_t* alpha = xofs + L.w;
-    const int16_t* yofs = alpha + 2 * L.w;
-    const int16_t* beta = yofs + L.h;
     // needed halo ranges (level coordinates, before reflection)
     const int nx0 = X0 - 3, nx1 = X0 + vw + 2, ny0 = Y0 - 3, ny1 = Y0 + vh + 2;
 
-    // ---- 1. source window ----
-    if (tid == 0) {
-        int x0, x1, y0, y1;
-        if (mode == 3) {
-            int mnx, mxx, mny, mxy;
-            reflected_range(nx0, nx1, L.w, mnx, mxx);
-            reflected_range(ny0, ny1, L.h, mny, mxy);
-            x0 = xofs[mnx] & ~3;
-            x1 = min((int)xofs[mxx] + 1, S.w - 1);
-            y0 = min(max((int)yofs[mny], 0), S.h - 1);
-            y1 = min(max((int)yofs[mxy] + 1, 0), S.h - 1);
-        } else {   // copy of the input (mode 0) or of level l-1 (mode 1); mode 2 reads direct
-            x0 = max(X0 - 4, 0);
-            x1 = min(X0 + LT_W + 3, L.w - 1);
-            y0 = max(Y0 - 3, 0);
-            y1 = min(Y0 + LT_H + 2, L.h - 1);
-        }
-        sc[0] = x0; sc[1] = x1 - x0 + 1; sc[2] = y0; sc[3] = y1 - y0 + 1;
+    // ---- 1. source window + tables (host-built per tile column / row, build_geometry) ----
+    const LevelColTab* CT = (const LevelColTab*)(ltab + L.ctab) + tx;
+    const LevelRowTab* RT = (const LevelRowTab*)(ltab + L.rowtab) + ty;
+    const int wx0 = CT->x0, WWb = CT->ww, wy0 = RT->y0, WH = RT->wh;
+    // table loads issued before the window loads, so both land in one round trip
+    uint4 tc = make_uint4(0, 0, 0, 0), ta = make_uint4(0, 0, 0, 0), ts = ta;
+    if (tid < LT_G) {
+        tc = make_uint4(CT->cgrp[2 * tid], CT->cgrp[2 * tid + 1], CT->cinf[tid], 0);
+        ta = *(const uint4*)&CT->calp[4 * tid];
+        ts = *(const uint4*)&CT->csel[4 * tid];
+    } else if (tid >= 64 && tid < 64 + LT_HR) {
+        tc = make_uint4(RT->rinf[2 * (tid - 64)], RT->rinf[2 * (tid - 64) + 1], 0, 0);
     }
-    __syncthreads();
-    const int wx0 = sc[0], WWb = sc[1], wy0 = sc[2], WH = sc[3];
     // window row pitch; modes 0/1 place x at column x - (X0 - 4) so that groups are dword-aligned
     const int WP = (mode == 3) ? ((WWb + 3) & ~3) : LT_G * 4;
     const int wcol0 = (mode == 3) ? 0 : wx0 - (X0 - 4);
@@ -141,49 +143,13 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4, (uint32_t*)win,
                           WP / 4, tid);
     }
-    // per-group column tables and per-row tables of the halo
     if (tid < LT_G) {
-        const int q = tid;
-        int sx[4];
-        uint32_t fl = 0;
-        uint32_t al[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 4; ++j) {
-            const int xr = reflect101_i(X0 - 4 + 4 * q + j, L.w);
-            if (mode == 3) {
-                sx[j] = xofs[xr] - wx0;
-                al[j] = (uint32_t)(uint16_t)alpha[2 * xr] | ((uint32_t)(uint16_t)alpha[2 * xr + 1] << 16);
-                fl |= (uint32_t)((xr < L.xmax ? 1 : 0) | (xr < L.rsimd_end ? 2 : 0)) << (2 * j);
-            } else {
-                sx[j] = (mode == 2) ? xr : xr - (X0 - 4);   // window column (modes 0/1)
-            }
-            // Pixels of a group outside the needed halo may reflect anywhere; keep their
-            // (unused) reads inside the window.  Needed pixels are always inside already.
-            if (mode == 3) sx[j] = min(max(sx[j], 0), max(WWb - 1, 0));
-            else if (mode != 2) sx[j] = min(max(sx[j], 0), LT_G * 4 - 1);
-        }
-        // contig: x..x+3 unreflected and dword-aligned in the window (modes 0/1)
-        const bool contig = sx[1] == sx[0] + 1 && sx[2] == sx[0] + 2 && sx[3] == sx[0] + 3 &&
-                            (sx[0] & 3) == 0;
-        // simple: the group's taps lie in the 12 bytes from (sx0 & ~3) (mode 3)
-        const int o0 = sx[0] & 3;
-        const bool simple = sx[1] >= sx[0] && sx[2] >= sx[1] && sx[3] >= sx[2] &&
-                            o0 + (sx[3] - sx[0]) + 1 <= 11;
-        cgrp[q] = make_uint2((uint32_t)sx[0] | ((uint32_t)sx[1] << 16),
-                             (uint32_t)sx[2] | ((uint32_t)sx[3] << 16));
-        cinf[q] = fl | (contig ? 0x100u : 0u) | (simple ? 0x200u : 0u);
-        calp[q] = make_uint4(al[0], al[1], al[2], al[3]);
+        cgrp[tid] = make_uint2(tc.x, tc.y);
+        cinf[tid] = tc.z;
+        calp[tid] = ta;
+        csel[tid] = ts;
     } else if (tid >= 64 && tid < 64 + LT_HR) {
-        const int r = tid - 64;
-        const int yr = reflect101_i(Y0 - 3 + r, L.h);
-        if (mode == 3) {
-            const int sy = yofs[yr];
-            const uint32_t y0r = (uint32_t)(min(max(sy, 0), S.h - 1) - wy0);
-            const uint32_t y1r = (uint32_t)(min(max(sy + 1, 0), S.h - 1) - wy0);
-            rinf[r] = make_uint2(y0r | (y1r << 16),
-                                 (uint32_t)(uint16_t)beta[2 * yr] | ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16));
-        } else {
-            rinf[r] = make_uint2((uint32_t)(mode == 2 ? yr : yr - wy0), 0u);
-        }
+        rinf[tid - 64] = make_uint2(tc.x, tc.y);
     }
     __syncthreads();
 
@@ -207,6 +173,10 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                 const uint8_t* w0 = win + r0 * WP;
                 const uint8_t* w1 = win + r1 * WP;
                 if (ci & 0x200u) {
+                    // branch-free: v_perm gathers each pixel's two taps as u16s, v_dot2 applies
+                    // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
+                    const uint4 sl = csel[q];
+                    const uint32_t sels[4] = {sl.x, sl.y, sl.z, sl.w};
                     const int base = xs[0] & ~3;
                     const uint32_t* d0p = (const uint32_t*)(w0 + base);
                     const uint32_t* d1p = (const uint32_t*)(w1 + base);
@@ -214,18 +184,16 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                     const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int k = xs[j] - base;
-                        const int f = (int)(ci >> (2 * j)) & 3;
-                        int h0, h1;
-                        if (f & 1) {
-                            const int aa = (int)(int16_t)(als[j] & 0xFFFF), ab = (int)(int16_t)(als[j] >> 16);
-                            h0 = byte12(a0, a1, a2, k) * aa + byte12(a0, a1, a2, k + 1) * ab;
-                            h1 = byte12(c0, c1, c2, k) * aa + byte12(c0, c1, c2, k + 1) * ab;
-                        } else {
-                            h0 = byte12(a0, a1, a2, k) * 2048;
-                            h1 = byte12(c0, c1, c2, k) * 2048;
-                        }
-                        out |= (uint32_t)vresize(h0, h1, b0, b1, (f & 2) != 0) << (8 * j);
+                        const bool hi = (ci >> (12 + j)) & 1u;
+                        const uint32_t p0 = __builtin_amdgcn_perm(hi ? a2 : a1, hi ? a1 : a0, sels[j]);
+                        const uint32_t p1 = __builtin_amdgcn_perm(hi ? c2 : c1, hi ? c1 : c0, sels[j]);
+                        const us2 al = __builtin_bit_cast(us2, als[j]);
+                        const int h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
+                        const int h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
+                        // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind
+                        const int vs = min((((h0 >> 4) * b0 >> 16) + ((h1 >> 4) * b1 >> 16) + 2) >> 2, 255);
+                        const int vc = min((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 255);
+                        out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
                     }
                 } else {   // reflected border group: bytes one by one
 #pragma unroll
@@ -264,6 +232,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         lvl[hr * LT_G + q] = out;
     }
     __syncthreads();
+    STAMP(3);
 
     uint8_t* dlev = pyr + (size_t)b * g->pyr_bytes + L.off;
     uint8_t* dblur = blur + (size_t)b * g->pyr_bytes + L.off;
@@ -307,6 +276,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         *(uint2*)(rows + r * LT_W + 4 * gq) = make_uint2(lo, hi);
     }
     __syncthreads();
+    STAMP(4);
     // ---- 5. blur column pass (SymmColumnFilter / SymmColumnVec_32s8u) ----
     const float f0 = (float)k3 * (1.f / 65536.f), f1 = (float)k4 * (1.f / 65536.f),
                 f2 = (float)k5 * (1.f / 65536.f), f3 = (float)k6 * (1.f / 65536.f);
@@ -342,6 +312,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
     }
+    STAMP(5);
 }
 
 size_t level_lds_bytes(int ltw, int lth, int win_cap) {
@@ -349,7 +320,7 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     (void)lth;
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t s = r((size_t)LT_HR * LT_G * 4) + r((size_t)LT_HR * LT_W * 2) + r(LT_G * 8) +
-               r(LT_G * 4) + r(LT_G * 16) + r(LT_HR * 8) + r(64);
+               r(LT_G * 4) + r(LT_G * 16) + r(LT_G * 16) + r(LT_HR * 8) + r(64);
     return s + r((size_t)win_cap + 16);
 }
 
@@ -361,12 +332,18 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
         const LevelGeom& L = G.lv[l];
         hipEvent_t e = T.start(st);
         hipLaunchKernelGGL(k_level, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
-                           a.rtab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
+                           a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
                            a.blur, l);
         T.stop(K_LEVEL, e, st);
     }
     return hipGetLastError();
 }
+
+#ifdef ORBX_STAMPS
+extern "C" int orbx_diag_level_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_level_stamps), sizeof(g_level_stamps));
+}
+#endif
 
 hipError_t prepare_level(size_t lds) {
     return hipFuncSetAttribute((const void*)k_level, hipFuncAttributeMaxDynamicSharedMemorySize,
