@@ -82,6 +82,11 @@ orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int
 orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out,
                                int* width, int* height);
 
+/* The 7x7 Gaussian of level `level` that the descriptors sample (the `workingMat` clone
+ * blurred at src/ORBextractor.cc:1107-1108), copied to host like orbx_pyramid_level. */
+orbx_status orbx_blur_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
+                            int* height);
+
 /* ---- batched, device-resident API (throughput path) -------------------------------------
  * d_imgs: `batch` images in device memory, image i at d_imgs + i*batch_stride, rows
  * `stride` bytes apart.  Results stay in the handle's workspace; orbx_batch_view exposes

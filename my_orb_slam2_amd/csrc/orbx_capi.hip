@@ -713,8 +713,8 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     return n > kp_cap ? ORBX_ERR_CAPACITY : ORBX_OK;
 }
 
-orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
-                               int* height) {
+static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,
+                              uint8_t* out, int* width, int* height) {
     if (!h || !h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
         index >= h->last_batch)
         return ORBX_ERR_INVALID;
@@ -724,11 +724,23 @@ orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t*
     if (!out) return ORBX_OK;
     std::lock_guard<std::mutex> lk(h->mu);
     (void)hipSetDevice(h->device);
-    const uint8_t* src = h->d_pyr.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
+    const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
     if (!HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
         !HIPOK(hipStreamSynchronize(h->stream)))
         return ORBX_ERR_DEVICE;
     return ORBX_OK;
+}
+
+orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
+                               int* height) {
+    if (!h) return ORBX_ERR_INVALID;
+    return copy_level(h, h->d_pyr, index, level, out, width, height);
+}
+
+orbx_status orbx_blur_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
+                            int* height) {
+    if (!h) return ORBX_ERR_INVALID;
+    return copy_level(h, h->d_blur, index, level, out, width, height);
 }
 
 orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int batch,

@@ -248,38 +248,36 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
     }
     // ---- 4. blur row pass (RowFilter<uchar,int>: exact; sums <= 257*255 fit u16) ----
+    // pixel x = X0+4gq+j needs halo bytes 1+j .. 7+j: two v_dot4_u32_u8 over the byte runs
+    // 1+j..4+j (taps k0..k3) and 5+j..8+j (taps k4..k6, 0)
     const int k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3];
     const int k4 = g->taps[4], k5 = g->taps[5], k6 = g->taps[6];
+    const uint32_t tapA = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24;
+    const uint32_t tapB = (uint32_t)k4 | (uint32_t)k5 << 8 | (uint32_t)k6 << 16;
     for (int i = tid; i < (vh + 6) * LT_GW; i += 256) {
         const int r = i / LT_GW, gq = i - r * LT_GW;
         if (gq >= ng) continue;
         const uint32_t* s = lvl + r * LT_G + gq;   // bytes of x = X0 + 4gq - 4 .. + 7
         const uint32_t d0 = s[0], d1 = s[1], d2 = s[2];
-        int px[12];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            px[k] = (int)((d0 >> (8 * k)) & 255u);
-            px[4 + k] = (int)((d1 >> (8 * k)) & 255u);
-            px[8 + k] = (int)((d2 >> (8 * k)) & 255u);
-        }
-        uint32_t lo, hi;
-        int sum[4];
-        // x = X0+4gq+j needs halo bytes 1+j .. 7+j; the taps are symmetric (k0=k6, k1=k5,
-        // k2=k4, checked on the host) and integer sums are exact in any order
-        (void)k4; (void)k5; (void)k6;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            sum[j] = k0 * (px[1 + j] + px[7 + j]) + k1 * (px[2 + j] + px[6 + j]) +
-                     k2 * (px[3 + j] + px[5 + j]) + k3 * px[4 + j];
-        lo = (uint32_t)sum[0] | ((uint32_t)sum[1] << 16);
-        hi = (uint32_t)sum[2] | ((uint32_t)sum[3] << 16);
+        uint32_t sum[4];
+        sum[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), tapB, 0u, false), false);
+        sum[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), tapB, 0u, false), false);
+        sum[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tapB, 0u, false), false);
+        sum[3] = __builtin_amdgcn_udot4(d1, tapA, __builtin_amdgcn_udot4(d2, tapB, 0u, false), false);
+        const uint32_t lo = sum[0] | (sum[1] << 16), hi = sum[2] | (sum[3] << 16);
         *(uint2*)(rows + r * LT_W + 4 * gq) = make_uint2(lo, hi);
     }
     __syncthreads();
     STAMP(4);
     // ---- 5. blur column pass (SymmColumnFilter / SymmColumnVec_32s8u) ----
-    const float f0 = (float)k3 * (1.f / 65536.f), f1 = (float)k4 * (1.f / 65536.f),
-                f2 = (float)k5 * (1.f / 65536.f), f3 = (float)k6 * (1.f / 65536.f);
+    // The SSE2 float form s = c0*f0 + p1*f1 + p2*f2 + p3*f3 (f = k/65536) is exact here:
+    // every product k*v is an integer < 2^24 scaled by a power of two, and every partial
+    // sum S = k3*c0 + k4*p1 + ... stays exact while S < 2^24 (partials only grow); at
+    // S >= 2^24 both forms give >= 256 and saturate to 255.  So rintf(S/65536) is
+    // round-half-even of the integer S, and the scalar tail is (S + 32768) >> 16.
     for (int i = tid; i < vh * LT_GW; i += 256) {
         const int r = i / LT_GW, gq = i - r * LT_GW;
         if (gq >= ng) continue;
@@ -295,17 +293,10 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
             };
             const int c0 = at(3);
             const int p1 = at(4) + at(2), p2 = at(5) + at(1), p3 = at(6) + at(0);
-            int val;
-            if (X0 + 4 * gq + j < L.bsimd_end) {
-                float s = (float)c0 * f0;   // + delta 0.0f: exact no-op, c0*f0 >= +0
-                s = s + (float)p1 * f1;
-                s = s + (float)p2 * f2;
-                s = s + (float)p3 * f3;
-                val = min(max((int)rintf(s), -32768), 32767);
-            } else {
-                val = (k3 * c0 + k4 * p1 + k5 * p2 + k6 * p3 + (1 << 15)) >> 16;
-            }
-            packed |= (uint32_t)sat8(val) << (8 * j);
+            const int S = k3 * c0 + k4 * p1 + k5 * p2 + k6 * p3;
+            const bool simd = X0 + 4 * gq + j < L.bsimd_end;
+            const int val = (S + (simd ? 32767 + ((S >> 16) & 1) : 32768)) >> 16;
+            packed |= (uint32_t)min(val, 255) << (8 * j);
         }
         uint8_t* d = dblur + (size_t)(Y0 + r) * L.pitch + X0 + 4 * gq;
         if (4 * gq + 4 <= vw) *(uint32_t*)d = packed;

@@ -114,6 +114,16 @@ class ORBextractor:
             self._h, index, level, ptr(out), ctypes.byref(w), ctypes.byref(h)))
         return out
 
+    def blur_level(self, level: int, index: int = 0) -> np.ndarray:
+        """The 7x7 Gaussian of a level that the descriptors sample (ORBextractor.cc:1107-1108)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check("orbx_blur_level", self._L.orbx_blur_level(
+            self._h, index, level, None, ctypes.byref(w), ctypes.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        check("orbx_blur_level", self._L.orbx_blur_level(
+            self._h, index, level, ptr(out), ctypes.byref(w), ctypes.byref(h)))
+        return out
+
     # ---- batched device path ----
     def prepare(self, width: int, height: int, batch: int) -> int:
         """Allocate the workspace for `batch` images of width x height; returns kp_cap."""

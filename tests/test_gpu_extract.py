@@ -116,3 +116,20 @@ def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
         assert_f32_bits_equal(uRh[i, :n], u_o, f"batch item {i} uRight")
         assert_f32_bits_equal(deph[i, :n], d_oo, f"batch item {i} depth")
         assert nvh[i] == n_o
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_blurred_levels_bitwise(oracle_mod, orbx_lib, gpu, simd):
+    """Every blurred level vs GaussianBlur(7x7, sigma 2) restated on the same level, including
+    saturated images (row sums of 255s drive the column sums past 2^24)."""
+    import my_orb_slam2_amd as m
+    rng = np.random.default_rng(9)
+    sat = np.where(rng.random((376, 1241)) < 0.7, 255, rng.integers(0, 256, (376, 1241))).astype(np.uint8)
+    cases = {"kitti": synth.frame(3), "saturated": sat, **synth.edge_cases()}
+    g = m.ORBextractor(2000, 1.2, 8, 20, 7, cv_simd=simd)
+    for name, img in cases.items():
+        g(img)
+        for l in range(8):
+            lvl = g.pyramid_level(l)
+            want = oracle_mod.gaussian7(lvl, simd)
+            assert_bytes_equal(g.blur_level(l), want, f"{name} simd={simd} blur L{l}")
