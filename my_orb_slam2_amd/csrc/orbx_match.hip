@@ -155,13 +155,16 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
         ++bn;
         if (nB <= 0) continue;
         if (nB <= 64 * NPL) {
-            // Candidates resident in VGPRs for the whole node.
+            // Candidates resident in VGPRs for the whole node.  pm[c] is the candidate's
+            // position (the key's low bits) or INF once unavailable, so a key is one
+            // v_lshl_or: (dist << 20) | pm.  A distance of 256 needs no test: its key sorts
+            // below INF but d1 = 256 is rejected and d2 = 256 equals the reference's init.
             Desc bd[NPL];
             int bf[NPL];
-            bool ok[NPL];
+            uint32_t pm[NPL];
 #pragma unroll
             for (int c = 0; c < NPL; ++c) {
-                ok[c] = false;
+                pm[c] = INF;
                 bf[c] = 0;
                 if (c * 64 < nB) {
                     const int pos = c * 64 + lane;
@@ -170,48 +173,53 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
                     const int fc = in ? f : 0;
                     bd[c] = load_desc(g.B.desc, (long long)fb0 + fc);
                     bf[c] = fc;
-                    ok[c] = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
-                            (!kfkf || g.B.flag[fb0 + fc]);
+                    const bool ok = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
+                                    (!kfkf || g.B.flag[fb0 + fc]);
+                    pm[c] = ok ? (uint32_t)pos : INF;
                 }
             }
-            for (int ia = a0; ia < a1; ++ia) {
-                const int fa = g.A.node_feat[ia];
-                if ((unsigned)fa >= (unsigned)nA) continue;
-                if (!g.A.flag[fa0 + fa]) continue;   // :224-228 / :599-603
-                const Desc ad = load_desc(g.A.desc, (long long)fa0 + fa);
-                uint32_t k1 = INF, k2 = INF;
+            // A features of the node, 64 at a time: lane l loads step l's descriptor, the
+            // steps read it back with v_readlane (no load on the sequential chain)
+            for (int ib = a0; ib < a1; ib += 64) {
+                const int ial = ib + lane;
+                const int fal = ial < a1 ? g.A.node_feat[ial] : -1;
+                const bool vl = (unsigned)fal < (unsigned)nA && g.A.flag[fa0 + max(fal, 0)];
+                const Desc adl = load_desc(g.A.desc, (long long)fa0 + (vl ? fal : 0));
+                uint64_t todo = __ballot(vl);   // :224-228 / :599-603
+                while (todo) {
+                    const int t = __builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    Desc ad;
 #pragma unroll
-                for (int c = 0; c < NPL; ++c) {
-                    if (c * 64 < nB) {
-                        const int d = hamming(ad, bd[c]);
-                        const uint32_t key =
-                            (ok[c] && d < 256) ? ((uint32_t)d << 20 | (uint32_t)(c * 64 + lane)) : INF;
-                        if (key < k1) { k2 = k1; k1 = key; }
-                        else if (key < k2) { k2 = key; }
-                    }
-                }
-                const uint32_t m1 = wave_min_u32(k1);
-                const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
-                const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
-                const int d2 = m2 == INF ? 256 : (int)(m2 >> 20);
-                const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
-                                 (float)d1 < g.ratio * (float)d2;
-                if (acc) {
-                    const int pos = (int)(m1 & 0xFFFFFu);
+                    for (int k = 0; k < 8; ++k) ad.w[k] = (uint32_t)__builtin_amdgcn_readlane((int)adl.w[k], t);
+                    const int fa = __builtin_amdgcn_readlane(fal, t);
+                    uint32_t k1 = INF, k2 = INF;
 #pragma unroll
-                    for (int c = 0; c < NPL; ++c)
-                        if (pos == c * 64 + lane) {
-                            ok[c] = false;
-                            const int fbm = bf[c];
-                            claimed[fbm >> 5] |= 1u << (fbm & 31);
-                            int bin = 0;
-                            if (g.check_ori) {
-                                bin = rot_bin(g.A.keys[fa0 + fa].angle, g.B.keys[fb0 + fbm].angle);
-                                atomicAdd(&hist[bin], 1);
-                            }
-                            if (kfkf) state[fa] = fbm | (bin << 24);
-                            else state[fbm] = fa | (bin << 24);
+                    for (int c = 0; c < NPL; ++c) {
+                        if (c * 64 < nB) {
+                            const uint32_t key = ((uint32_t)hamming(ad, bd[c]) << 20) | pm[c];
+                            k2 = min(k2, max(k1, key));
+                            k1 = min(k1, key);
                         }
+                    }
+                    const uint32_t m1 = wave_min_u32(k1);
+                    const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
+                    const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
+                    const int d2 = m2 == INF ? 256 : min((int)(m2 >> 20), 256);
+                    const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
+                                     (float)d1 < g.ratio * (float)d2;
+                    if (acc) {
+                        const int pos = (int)(m1 & 0xFFFFFu);
+#pragma unroll
+                        for (int c = 0; c < NPL; ++c)
+                            if (pos == c * 64 + lane) {
+                                pm[c] = INF;
+                                const int fbm = bf[c];
+                                claimed[fbm >> 5] |= 1u << (fbm & 31);
+                                if (kfkf) state[fa] = fbm;
+                                else state[fbm] = fa;
+                            }
+                    }
                 }
             }
         } else {
@@ -246,20 +254,29 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
                     const int fbm = g.B.node_feat[b0 + pos];
                     if (lane == 0) {
                         claimed[fbm >> 5] |= 1u << (fbm & 31);
-                        int bin = 0;
-                        if (g.check_ori) {
-                            bin = rot_bin(g.A.keys[fa0 + fa].angle, g.B.keys[fb0 + fbm].angle);
-                            hist[bin] += 1;
-                        }
-                        if (kfkf) state[fa] = fbm | (bin << 24);
-                        else state[fbm] = fa | (bin << 24);
+                        if (kfkf) state[fa] = fbm;
+                        else state[fbm] = fa;
                     }
                 }
             }
         }
     }
     __syncthreads();
-    // Rotation consistency (:298-316 / :675-693) and the count.
+    // Rotation consistency (:298-316 / :675-693) and the count.  The histogram only needs
+    // the bin of every match, so it is built here from the final state (loads in parallel)
+    // instead of on the sequential chain.
+    if (g.check_ori) {
+        for (int i = lane; i < nOut; i += 64) {
+            const int s = state[i];
+            if (s >= 0) {
+                const int ia = kfkf ? i : s, ib = kfkf ? s : i;
+                const int bin = rot_bin(g.A.keys[fa0 + ia].angle, g.B.keys[fb0 + ib].angle);
+                state[i] = s | (bin << 24);
+                atomicAdd(&hist[bin], 1);
+            }
+        }
+        __syncthreads();
+    }
     const Top3 top = g.check_ori ? three_maxima(hist) : Top3{-1, -1, -1};
     int cnt = 0;
     for (int i = lane; i < nOut; i += 64) {
