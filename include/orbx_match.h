@@ -220,10 +220,26 @@ orbx_status orbx_search_for_triangulation_batch_device(
  * keyframe above max_feat since the last sync (the flag is then cleared). */
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream);
 
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:252-313) for npoints map points:
+ * point p's observed descriptors are rows [off[p], off[p+1]) of desc (n x 32, in the order
+ * the reference walks mObservations, skipping bad keyframes).  best[p] = the row (relative
+ * to off[p]) with the least median distance to the others (first on ties), or -1 when the
+ * point has no descriptor (the reference then keeps mDescriptor).  At most
+ * ORBX_MAX_OBSERVATIONS rows per point (ORBX_ERR_UNSUPPORTED above). */
+enum { ORBX_MAX_OBSERVATIONS = 256 };
+orbx_status orbx_compute_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc,
+                                                 const int32_t* off, int32_t npoints,
+                                                 int32_t* best);
+/* Same on device arrays, on the caller's stream (points above the limit get -1 and are
+ * flagged for orbx_matcher_sync). */
+orbx_status orbx_compute_distinctive_descriptors_device(orbx_matcher* m, const uint8_t* d_desc,
+                                                        const int32_t* d_off, int32_t npoints,
+                                                        int32_t* d_best, void* stream);
+
 /* ---- per-kernel timing for the matcher handle ------------------------------------------ */
 typedef enum {
     ORBX_MK_BOW = 0, ORBX_MK_TRIANGULATE, ORBX_MK_PROJ_SEARCH, ORBX_MK_PROJ_RESOLVE,
-    ORBX_MK_COUNT
+    ORBX_MK_DISTINCTIVE, ORBX_MK_COUNT
 } orbx_match_kernel_id;
 orbx_status orbx_matcher_profile_enable(orbx_matcher* m, int on);
 orbx_status orbx_matcher_profile_collect(orbx_matcher* m, double* total_ms, int64_t* launches);

@@ -678,7 +678,74 @@ __global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
     if (tid == 0) g.nmatches[0] = tot;
 }
 
+// ---------------------------------------------------------------------------------------
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:252-313)
+// ---------------------------------------------------------------------------------------
+// One wave per map point: its N descriptors are staged in LDS, lane i computes row i of the
+// distance matrix into LDS (u16), finds the row's median vDists[(N-1)/2] by a binary search
+// over distance values (9 counting passes), and a wave-min over (median << 16 | i) keeps the
+// first row with the least median.
+__global__ __launch_bounds__(64) void k_distinctive(const uint8_t* __restrict__ desc,
+                                                    const int32_t* __restrict__ off, int np,
+                                                    int32_t* __restrict__ best, int* err) {
+    extern __shared__ uint32_t dl[];   // [MAXOBS][8] descriptors, then [64][MAXOBS+1] u16 rows
+    constexpr int MAXN = ORBX_MAX_OBSERVATIONS;
+    uint16_t* rows = (uint16_t*)(dl + MAXN * 8);
+    const int p = blockIdx.x, lane = threadIdx.x;
+    if (p >= np) return;
+    const int o0 = off[p], N = off[p + 1] - o0;
+    if (N <= 0 || N > MAXN) {
+        if (lane == 0) {
+            best[p] = -1;
+            if (N > MAXN) atomicOr(err, 1);
+        }
+        return;
+    }
+    for (int t = lane; t < N * 8; t += 64)
+        dl[t] = ((const uint32_t*)(desc + 32 * (size_t)o0))[t];
+    __syncthreads();
+    const int k = (N - 1) >> 1;   // vDists[0.5*(N-1)]
+    uint32_t bestkey = INF;
+    uint16_t* row = rows + lane * (MAXN + 1);
+    for (int i0 = 0; i0 < N; i0 += 64) {
+        const int i = i0 + lane;
+        const bool has = i < N;
+        const int ic = has ? i : N - 1;
+        Desc di;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) di.w[w] = dl[ic * 8 + w];
+        for (int j = 0; j < N; ++j) {
+            Desc dj;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) dj.w[w] = dl[j * 8 + w];
+            row[j] = (uint16_t)hamming(di, dj);
+        }
+        int lo = 0, hi = 256;   // smallest v with #(row <= v) >= k + 1
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (int j = 0; j < N; ++j) cnt += row[j] <= mid;
+            if (cnt >= k + 1) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t key = has ? ((uint32_t)lo << 16 | (uint32_t)i) : INF;
+        bestkey = min(bestkey, wave_min_u32(key));
+    }
+    if (lane == 0) best[p] = (int)(bestkey & 0xFFFFu);
+}
+
 }  // namespace
+
+hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, int32_t* best,
+                              int* err, hipStream_t st) {
+    if (np <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_distinctive, dim3(np), dim3(64), distinctive_lds_bytes(), st, desc, off,
+                       np, best, err);
+    return hipGetLastError();
+}
+
+size_t distinctive_lds_bytes() {
+    return (size_t)ORBX_MAX_OBSERVATIONS * 32 + 64 * (ORBX_MAX_OBSERVATIONS + 1) * 2;
+}
 
 bool proj_mode_greedy(int mode) {
     return mode == ORBX_PROJ_FRAME_MAPPOINTS || mode == ORBX_PROJ_KF_SCW ||
@@ -740,6 +807,7 @@ hipError_t prepare_match_kernels() {
     if ((e = hipFuncSetAttribute((const void*)k_bow<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_bow<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_triangulate, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_distinctive, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)k_proj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 

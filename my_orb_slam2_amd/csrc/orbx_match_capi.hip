@@ -621,6 +621,52 @@ orbx_status orbx_search_for_triangulation_batch_device(
     return ORBX_OK;
 }
 
+orbx_status orbx_compute_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc,
+                                                 const int32_t* off, int32_t npoints,
+                                                 int32_t* best) {
+    if (!m || !off || !best || npoints < 0) return ORBX_ERR_INVALID;
+    if (npoints == 0) return ORBX_OK;
+    if (off[0] < 0) return ORBX_ERR_INVALID;
+    for (int p = 0; p < npoints; ++p) {
+        if (off[p + 1] < off[p]) return ORBX_ERR_INVALID;
+        if (off[p + 1] - off[p] > ORBX_MAX_OBSERVATIONS) return ORBX_ERR_UNSUPPORTED;
+    }
+    const int n = off[npoints] - off[0];
+    if (n > 0 && !desc) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    Packer P(m->staging);
+    const size_t od = P.add(n > 0 ? desc + 32 * (size_t)off[0] : nullptr, 32 * (size_t)n);
+    std::vector<int32_t> rel((size_t)npoints + 1);
+    for (int p = 0; p <= npoints; ++p) rel[p] = off[p] - off[0];
+    const size_t oo = P.add(rel.data(), 4 * rel.size());
+    orbx_status s = upload(m);
+    if (s != ORBX_OK) return s;
+    if (!m->d_out.ensure(4 * (size_t)npoints)) return ORBX_ERR_DEVICE;
+    uint8_t* base = m->d_in.as<uint8_t>();
+    hipEvent_t e = m->timer.start(m->stream);
+    if (!HIPOK(launch_distinctive(base + od, (const int32_t*)(base + oo),
+                                  npoints, m->d_out.as<int32_t>(), m->d_err, m->stream)))
+        return ORBX_ERR_DEVICE;
+    m->timer.stop(ORBX_MK_DISTINCTIVE, e, m->stream);
+    return finish(m, best, m->d_out.p, 4 * (size_t)npoints);
+}
+
+orbx_status orbx_compute_distinctive_descriptors_device(orbx_matcher* m, const uint8_t* d_desc,
+                                                        const int32_t* d_off, int32_t npoints,
+                                                        int32_t* d_best, void* stream) {
+    if (!m || !d_off || !d_best || !d_desc || npoints < 0) return ORBX_ERR_INVALID;
+    if (npoints == 0) return ORBX_OK;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e = m->timer.start(st);
+    if (!HIPOK(launch_distinctive(d_desc, d_off, npoints, d_best, m->d_err, st)))
+        return ORBX_ERR_DEVICE;
+    m->timer.stop(ORBX_MK_DISTINCTIVE, e, st);
+    return ORBX_OK;
+}
+
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream) {
     if (!m) return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(m->mu);
@@ -655,7 +701,7 @@ orbx_status orbx_matcher_profile_collect(orbx_matcher* m, double* total_ms, int6
 
 const char* orbx_match_kernel_name(int id) {
     static const char* names[ORBX_MK_COUNT] = {"k_bow", "k_triangulate", "k_proj_search",
-                                               "k_proj_resolve"};
+                                               "k_proj_resolve", "k_distinctive"};
     return (id >= 0 && id < ORBX_MK_COUNT) ? names[id] : "";
 }
 

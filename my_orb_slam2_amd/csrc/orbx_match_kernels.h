@@ -73,6 +73,9 @@ struct KernelTimer;
 hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer);
 size_t proj_resolve_lds_bytes(int mode, int n_target, int nq);
 hipError_t prepare_match_kernels();
+hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, int32_t* best,
+                              int* err, hipStream_t st);
+size_t distinctive_lds_bytes();
 // 160 KB of LDS per workgroup on gfx950, minus room for the kernels' static arrays
 constexpr size_t MATCH_MAX_LDS = 160 * 1024 - 256;
 

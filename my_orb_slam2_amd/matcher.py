@@ -202,6 +202,19 @@ class ORBmatcher:
             ptr(out), ctypes.byref(n)))
         return n.value, out[:f1.n]
 
+    # ---- MapPoint::ComputeDistinctiveDescriptors ------------------------------------------
+    def compute_distinctive_descriptors(self, desc, off):
+        """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:252-313) for many map points:
+        point p's observed descriptors are rows off[p]..off[p+1] of desc; returns the chosen
+        row per point (relative to off[p]), -1 for points without descriptors."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        o = np.ascontiguousarray(off, np.int32)
+        best = np.full(max(len(o) - 1, 1), -1, np.int32)
+        check("orbx_compute_distinctive_descriptors",
+              self._lib.orbx_compute_distinctive_descriptors(self._h, ptr(d), ptr(o), len(o) - 1,
+                                                              ptr(best)))
+        return best[:len(o) - 1]
+
     # ---- batched device path ---------------------------------------------------------------
     def search_by_bow_kf_frame_batch_device(self, db: KfDbC, frame_c, d_match, d_nmatches,
                                             stream=0):

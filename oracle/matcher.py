@@ -152,3 +152,14 @@ def search_for_initialization(f1, f2, prev_matched, window, nnratio=0.9, check_o
     n = lib().oracle_search_for_initialization(ctypes.byref(a), ctypes.byref(b), _a(prev_matched),
                                                int(window), nnratio, int(check_ori), _a(out))
     return n, out[:len(f1.keys)]
+
+
+def distinctive_descriptors(desc, off):
+    """MapPoint::ComputeDistinctiveDescriptors restated, many points at once."""
+    d = np.ascontiguousarray(desc, np.uint8)
+    o = np.ascontiguousarray(off, np.int32)
+    out = np.zeros(max(len(o) - 1, 1), np.int32)
+    L = lib()
+    L.oracle_distinctive_descriptors.argtypes = [_vp, _vp, _i, _vp]
+    L.oracle_distinctive_descriptors(_a(d), _a(o), len(o) - 1, _a(out))
+    return out[:len(o) - 1]

@@ -536,3 +536,36 @@ int oracle_search_for_initialization(const orbx_featureset* F1, const orbx_featu
 }
 
 }  // extern "C"
+
+extern "C" {
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:252-313): the row with the least
+// median distance (vDists[0.5*(N-1)] of the sorted row), first on ties; -1 when N == 0.
+void oracle_distinctive_descriptors(const uint8_t* desc, const int32_t* off, int np,
+                                    int32_t* best) {
+    for (int p = 0; p < np; ++p) {
+        const int o0 = off[p];
+        const size_t N = (size_t)(off[p + 1] - o0);
+        if (N == 0) { best[p] = -1; continue; }
+        std::vector<std::vector<float>> Distances(N, std::vector<float>(N));
+        for (size_t i = 0; i < N; i++) {
+            Distances[i][i] = 0;
+            for (size_t j = i + 1; j < N; j++) {
+                const int distij = dd(desc + 32 * (size_t)(o0 + i), desc + 32 * (size_t)(o0 + j));
+                Distances[i][j] = distij;
+                Distances[j][i] = distij;
+            }
+        }
+        int BestMedian = INT_MAX, BestIdx = 0;
+        for (size_t i = 0; i < N; i++) {
+            std::vector<int> vDists(Distances[i].begin(), Distances[i].end());
+            std::sort(vDists.begin(), vDists.end());
+            const int median = vDists[0.5 * (N - 1)];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = (int)i;
+            }
+        }
+        best[p] = BestIdx;
+    }
+}
+}  // extern "C"

@@ -209,3 +209,13 @@ def test_batch_triangulation(oracle_mod, orbx_lib, gpu):
         idx1 = np.nonzero(seg >= 0)[0]
         assert cnt[j] == n_o
         np.testing.assert_array_equal(np.stack([idx1, seg[idx1]], 1), p_o)
+
+
+def test_distinctive_descriptors(oracle_mod, orbx_lib, gpu):
+    from oracle import matcher as om
+    from test_oracle_match import _distinctive_case
+    for seed, npts, maxn in [(0, 500, 40), (1, 40, 256)]:
+        desc, off = _distinctive_case(seed, npts, maxn)
+        m = _matcher(0.6, True)
+        np.testing.assert_array_equal(m.compute_distinctive_descriptors(desc, off),
+                                      om.distinctive_descriptors(desc, off))

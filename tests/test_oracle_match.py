@@ -324,3 +324,40 @@ def test_projection_crosscheck(mode):
     n_p, m_p = projection_py(mode, f2, q, d, claimed, 0.8, True, orb_dist=64, inv_sigma2=isg)
     assert n_o == n_p and n_o > 0
     np.testing.assert_array_equal(m_o, m_p)
+
+
+def _distinctive_case(seed, npts=60, maxn=40):
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(0, maxn + 1, npts)
+    sizes[:3] = [0, 1, 2]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    base = rng.integers(0, 256, (npts, 32), dtype=np.uint8)
+    desc = np.repeat(base, sizes, axis=0)
+    flips = rng.random(desc.shape) < 0.05   # observations of one point are similar
+    desc = desc ^ (flips * rng.integers(1, 256, desc.shape)).astype(np.uint8)
+    dup = rng.random(len(desc)) < 0.1       # repeated observations: median ties
+    desc[1:][dup[1:]] = desc[:-1][dup[1:]]
+    return desc, off
+
+
+def distinctive_py(desc, off):
+    out = []
+    for p in range(len(off) - 1):
+        rows = desc[off[p]:off[p + 1]]
+        n = len(rows)
+        if n == 0:
+            out.append(-1)
+            continue
+        D = [[hd(rows[i], rows[j]) for j in range(n)] for i in range(n)]
+        best, bi = None, 0
+        for i in range(n):
+            med = sorted(D[i])[int(0.5 * (n - 1))]
+            if best is None or med < best:
+                best, bi = med, i
+        out.append(bi)
+    return np.array(out, np.int32)
+
+
+def test_distinctive_descriptors_crosscheck():
+    desc, off = _distinctive_case(1, npts=40, maxn=12)
+    np.testing.assert_array_equal(om.distinctive_descriptors(desc, off), distinctive_py(desc, off))
