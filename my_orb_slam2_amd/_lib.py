@@ -89,6 +89,14 @@ SIGNATURES = {
     "orbx_matcher_profile_enable": (_i, [_vp, _i]),
     "orbx_matcher_profile_collect": (_i, [_vp, _vp, _vp]),
     "orbx_match_kernel_name": (ctypes.c_char_p, [_i]),
+    # include/orbx_vocab.h
+    "orbx_vocabulary_load_text": (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_vp)]),
+    "orbx_vocabulary_destroy": (_i, [_vp]),
+    "orbx_vocabulary_info": (_i, [_vp] + [_vp] * 6),
+    "orbx_vocabulary_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp]),
+    "orbx_vocabulary_transform_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "orbx_bow_score_l1": (ctypes.c_double, [_vp, _vp, _i, _vp, _vp, _i]),
 }
 
 _lib = None

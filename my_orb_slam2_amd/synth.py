@@ -281,3 +281,32 @@ def keyframe_pair(seed: int, n1: int = 1000, n2: int = 1000, width: int = 752,
     ex = np.float32(np.float32(np.float32(fx) * C2[0]) * invz) + np.float32(cx)
     ey = np.float32(np.float32(np.float32(fy) * C2[1]) * invz) + np.float32(cy)
     return f1, f2, F12, (float(ex), float(ey)), truth
+
+
+def write_vocabulary(path, k: int = 10, L: int = 3, seed: int = 0, scoring: int = 0,
+                     weighting: int = 0, flip: float = 0.25, stop_frac: float = 0.02):
+    """A synthetic DBoW2 text vocabulary (ORBvoc.txt format: "k L scoring weighting", then
+    "parent isLeaf d0..d31 weight" per node, breadth-first).  Children descriptors are noisy
+    copies of their parent's, so descriptors descend meaningfully; leaf weights are
+    idf-like positives with a few stop words (weight 0).  Returns the node count."""
+    rng = np.random.default_rng(seed)
+    lines = [f"{k} {L} {scoring} {weighting}"]
+    desc = {0: rng.integers(0, 256, 32, dtype=np.uint8)}
+    frontier, nid = [0], 1
+    for level in range(1, L + 1):
+        nxt = []
+        for p in frontier:
+            for _ in range(k):
+                bits = rng.random(256) < flip
+                d = desc[p] ^ np.packbits(bits, bitorder="little")
+                desc[nid] = d
+                leaf = level == L
+                w = 0.0 if leaf and rng.random() < stop_frac else (
+                    float(np.round(rng.uniform(0.5, 8.0), 6)) if leaf else 0.0)
+                lines.append(f"{p} {int(leaf)} " + " ".join(str(int(b)) for b in d) + f" {w}")
+                nxt.append(nid)
+                nid += 1
+        frontier = nxt
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return nid

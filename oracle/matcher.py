@@ -163,3 +163,46 @@ def distinctive_descriptors(desc, off):
     L.oracle_distinctive_descriptors.argtypes = [_vp, _vp, _i, _vp]
     L.oracle_distinctive_descriptors(_a(d), _a(o), len(o) - 1, _a(out))
     return out[:len(o) - 1]
+
+
+class OracleVocabulary:
+    """The DBoW2 restatement (oracle/orb_vocab_oracle.cpp)."""
+
+    def __init__(self, path):
+        L = lib()
+        L.oracle_vocab_load.restype = _vp
+        L.oracle_vocab_load.argtypes = [ctypes.c_char_p]
+        L.oracle_vocab_free.argtypes = [_vp]
+        L.oracle_vocab_transform.argtypes = [_vp, _vp, _i, _i] + [_vp] * 9
+        L.oracle_bow_score_l1.restype = ctypes.c_double
+        L.oracle_bow_score_l1.argtypes = [_vp, _vp, _i, _vp, _vp, _i]
+        self._h = L.oracle_vocab_load(str(path).encode())
+        if not self._h:
+            raise ValueError(f"cannot load {path}")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_vocab_free(self._h)
+            self._h = None
+
+    def transform(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8)
+        n = len(d)
+        cap = max(n, 1)
+        word, node = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+        bw, bv = np.zeros(cap, np.uint32), np.zeros(cap, np.float64)
+        fn, fo, ff = np.zeros(cap, np.uint32), np.zeros(cap + 1, np.int32), np.zeros(cap, np.int32)
+        nb, nf = ctypes.c_int32(), ctypes.c_int32()
+        lib().oracle_vocab_transform(self._h, _a(d), n, levelsup, _a(word), _a(node),
+                                     ctypes.byref(nb), _a(bw), _a(bv), ctypes.byref(nf), _a(fn),
+                                     _a(fo), _a(ff))
+        return (word[:n], node[:n], (bw[:nb.value], bv[:nb.value]),
+                (fn[:nf.value], fo[:nf.value + 1], ff[:fo[nf.value]]))
+
+
+def bow_score_l1(b1, b2):
+    w1, v1 = np.ascontiguousarray(b1[0], np.uint32), np.ascontiguousarray(b1[1], np.float64)
+    w2, v2 = np.ascontiguousarray(b2[0], np.uint32), np.ascontiguousarray(b2[1], np.float64)
+    lib().oracle_bow_score_l1.restype = ctypes.c_double
+    lib().oracle_bow_score_l1.argtypes = [_vp, _vp, _i, _vp, _vp, _i]
+    return lib().oracle_bow_score_l1(_a(w1), _a(v1), len(w1), _a(w2), _a(v2), len(w2))
