@@ -97,6 +97,11 @@ SIGNATURES = {
                                        _vp]),
     "orbx_vocabulary_transform_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
     "orbx_bow_score_l1": (ctypes.c_double, [_vp, _vp, _i, _vp, _vp, _i]),
+    # include/orbx_frame.h
+    "orbx_undistort_keypoints": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i]),
+    "orbx_undistort_keypoints_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp]),
+    "orbx_image_bounds": (_i, [_vp, _vp, _i, _i, _i, _vp]),
+    "orbx_assign_grid_device": (_i, [_vp, _i, _i, _i, _f, _f, _f, _f, _vp, _vp, _vp]),
 }
 
 _lib = None

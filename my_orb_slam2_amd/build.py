@@ -16,10 +16,10 @@ PKG = pathlib.Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "liborbx.so"
 SOURCES = ["orbx_pyramid.hip", "orbx_extract.hip", "orbx_stereo.hip", "orbx_match.hip",
-           "orbx_capi.hip", "orbx_match_capi.hip", "orbx_vocab.hip"]
+           "orbx_capi.hip", "orbx_match_capi.hip", "orbx_vocab.hip", "orbx_frame.hip"]
 HEADERS = ["orbx_internal.h", "orbx_device.h", "orbx_math.h", "orbx_kernels.h", "orbx_host.h",
            "orbx_match_kernels.h", "orbx_pattern.inc", "../../include/orbx.h",
-           "../../include/orbx_match.h", "../../include/orbx_vocab.h"]
+           "../../include/orbx_match.h", "../../include/orbx_vocab.h", "../../include/orbx_frame.h"]
 
 # -ffp-contract=off: every float a*b+c in the path is two roundings, as in the x86 reference
 # (hipcc defaults to fast contraction).  No -ffast-math: IEEE division/rounding throughout.

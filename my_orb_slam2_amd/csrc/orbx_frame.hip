@@ -1,0 +1,200 @@
+// orbx_frame.hip — per-frame geometry around the matchers (include/orbx_frame.h).
+//
+//   k_undistort    one lane per keypoint: cvUndistortPoints (OpenCV 3.2) in double, the
+//                  same __host__ __device__ routine the host uses for ComputeImageBounds
+//   k_grid_count / k_grid_fill   Frame::AssignFeaturesToGrid as a counting sort: cell of
+//                  every keypoint (PosInGrid, std::round half away from zero in float),
+//                  per-cell counts, an exclusive scan over the 3072 cells, then a stable
+//                  fill (each cell keeps ascending feature indices, as push_back does)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "../../include/orbx_frame.h"
+#include "orbx_device.h"
+#include "orbx_host.h"
+
+using namespace orbx;
+
+namespace {
+
+struct UndistParams {
+    double k[8];
+    double fx, fy, cx, cy, ifx, ify;
+    int iters;
+};
+
+__host__ __device__ inline void undistort_pt(const UndistParams& P, float xs, float ys,
+                                             float& xo, float& yo) {
+    const double* k = P.k;
+    double x = xs, y = ys;
+    const double x0 = x = (x - P.cx) * P.ifx;
+    const double y0 = y = (y - P.cy) * P.ify;
+    for (int j = 0; j < P.iters; j++) {   // compensate distortion iteratively
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) /
+                              (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    // RR = P * I = K: xx = RR00*x + RR01*y + RR02, ..., ww = 1/(0*x + 0*y + 1)
+    const double xx = P.fx * x + 0.0 * y + P.cx;
+    const double yy = 0.0 * x + P.fy * y + P.cy;
+    const double ww = 1. / (0.0 * x + 0.0 * y + 1.0);
+    xo = (float)(xx * ww);
+    yo = (float)(yy * ww);
+}
+
+bool make_params(const float* K4, const float* dist, int ndist, UndistParams& P) {
+    if (!K4 || !dist || (ndist != 4 && ndist != 5 && ndist != 8)) return false;
+    for (int i = 0; i < 8; ++i) P.k[i] = i < ndist ? (double)dist[i] : 0.0;
+    P.fx = K4[0];
+    P.fy = K4[1];
+    P.cx = K4[2];
+    P.cy = K4[3];
+    P.ifx = 1. / P.fx;
+    P.ify = 1. / P.fy;
+    P.iters = 5;   // distortion coefficients given (cvUndistortPoints)
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_undistort(UndistParams P, const orbx_keypoint* in,
+                                                   int n, orbx_keypoint* out, int copy) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    orbx_keypoint kp = in[i];
+    if (!copy) undistort_pt(P, kp.x, kp.y, kp.x, kp.y);
+    out[i] = kp;
+}
+
+// PosInGrid (Frame.cc:407-417): round((x - mnMinX) * inv) in float, half away from zero.
+__device__ inline int grid_cell(const orbx_keypoint& kp, int cols, int rows, float min_x,
+                                float min_y, float inv_w, float inv_h) {
+    const int px = (int)roundf((kp.x - min_x) * inv_w);
+    const int py = (int)roundf((kp.y - min_y) * inv_h);
+    if (px < 0 || px >= cols || py < 0 || py >= rows) return -1;
+    return px * rows + py;
+}
+
+__global__ __launch_bounds__(1024) void k_grid(const orbx_keypoint* __restrict__ kps, int n,
+                                               int cols, int rows, float min_x, float min_y,
+                                               float inv_w, float inv_h,
+                                               int32_t* __restrict__ off,
+                                               int32_t* __restrict__ feat) {
+    // one workgroup: counts in LDS, scan, then a stable fill in index order
+    extern __shared__ int cnt[];   // cells + 32
+    const int ncell = cols * rows, tid = threadIdx.x;
+    for (int c = tid; c < ncell; c += 1024) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int c = grid_cell(kps[i], cols, rows, min_x, min_y, inv_w, inv_h);
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {   // exclusive scan over <= 3072 cells (once per frame)
+        int s = 0;
+        for (int c = 0; c < ncell; ++c) {
+            const int v = cnt[c];
+            cnt[c] = s;
+            off[c] = s;
+            s += v;
+        }
+        off[ncell] = s;
+    }
+    __syncthreads();
+    // stable fill: features in index order, 1024 at a time; within a chunk, the rank of a
+    // feature among earlier features of the same cell comes from a ballot-free LDS pass
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + tid;
+        const int c = i < n ? grid_cell(kps[i], cols, rows, min_x, min_y, inv_w, inv_h) : -1;
+        // serialise by cell order inside the chunk with one thread per cell run: simple and
+        // deterministic — each thread counts earlier chunk members of its cell
+        __shared__ int cell_of[1024];
+        cell_of[tid] = c;
+        __syncthreads();
+        if (c >= 0) {
+            int r = 0;
+            for (int j = 0; j < tid; ++j) r += cell_of[j] == c;
+            feat[cnt[c] + r] = i;
+        }
+        __syncthreads();
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbx_undistort_keypoints_device(const float* K4, const float* dist, int32_t ndist,
+                                            const orbx_keypoint* d_kps, int32_t n,
+                                            orbx_keypoint* d_kps_un, void* stream) {
+    UndistParams P;
+    if (!make_params(K4, dist, ndist, P) || n < 0 || (n > 0 && (!d_kps || !d_kps_un)))
+        return ORBX_ERR_INVALID;
+    if (n == 0) return ORBX_OK;
+    const int copy = dist[0] == 0.0f;   // Frame.cc:431: mvKeysUn = mvKeys
+    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, P,
+                       d_kps, n, d_kps_un, copy);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_undistort_keypoints(const float* K4, const float* dist, int32_t ndist,
+                                     const orbx_keypoint* kps, int32_t n,
+                                     orbx_keypoint* kps_un, int device) {
+    UndistParams P;
+    if (!make_params(K4, dist, ndist, P) || n < 0 || (n > 0 && (!kps || !kps_un)))
+        return ORBX_ERR_INVALID;
+    if (n == 0) return ORBX_OK;
+    if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
+    orbx_keypoint* d = nullptr;
+    const size_t bytes = sizeof(orbx_keypoint) * (size_t)n;
+    if (!HIPOK(hipMalloc((void**)&d, bytes))) return ORBX_ERR_DEVICE;
+    orbx_status s = ORBX_OK;
+    if (!HIPOK(hipMemcpy(d, kps, bytes, hipMemcpyHostToDevice))) s = ORBX_ERR_DEVICE;
+    if (s == ORBX_OK) s = orbx_undistort_keypoints_device(K4, dist, ndist, d, n, d, nullptr);
+    if (s == ORBX_OK && !HIPOK(hipMemcpy(kps_un, d, bytes, hipMemcpyDeviceToHost))) s = ORBX_ERR_DEVICE;
+    (void)hipFree(d);
+    return s;
+}
+
+orbx_status orbx_image_bounds(const float* K4, const float* dist, int32_t ndist, int32_t width,
+                              int32_t height, float* bounds) {
+    UndistParams P;
+    if (!make_params(K4, dist, ndist, P) || !bounds || width <= 0 || height <= 0)
+        return ORBX_ERR_INVALID;
+    if (dist[0] != 0.0f) {   // Frame.cc:463-480
+        const float cx[4] = {0.0f, (float)width, 0.0f, (float)width};
+        const float cy[4] = {0.0f, 0.0f, (float)height, (float)height};
+        float ux[4], uy[4];
+        for (int i = 0; i < 4; ++i) undistort_pt(P, cx[i], cy[i], ux[i], uy[i]);
+        bounds[0] = std::min(ux[0], ux[2]);
+        bounds[1] = std::max(ux[1], ux[3]);
+        bounds[2] = std::min(uy[0], uy[1]);
+        bounds[3] = std::max(uy[2], uy[3]);
+    } else {   // :482-487
+        bounds[0] = 0.0f;
+        bounds[1] = (float)width;
+        bounds[2] = 0.0f;
+        bounds[3] = (float)height;
+    }
+    return ORBX_OK;
+}
+
+orbx_status orbx_assign_grid_device(const orbx_keypoint* d_kps, int32_t n, int32_t cols,
+                                    int32_t rows, float min_x, float min_y, float inv_w,
+                                    float inv_h, int32_t* d_grid_off, int32_t* d_grid_feat,
+                                    void* stream) {
+    if (n < 0 || cols <= 0 || rows <= 0 || (long long)cols * rows > 16384 - 32 || !d_grid_off ||
+        (n > 0 && (!d_kps || !d_grid_feat)))
+        return ORBX_ERR_INVALID;
+    const size_t lds = 4 * ((size_t)cols * rows + 32);   // <= 64 KB: no attribute needed
+    hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), lds, (hipStream_t)stream, d_kps, n, cols,
+                       rows, min_x, min_y, inv_w, inv_h, d_grid_off, d_grid_feat);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+}  // extern "C"

@@ -156,3 +156,48 @@ PROJ_KEYFRAME = 3
 PROJ_FUSE = 4
 PROJ_FUSE_SCW = 5
 PROJ_SIM3 = 6
+
+
+# ---- Frame geometry (include/orbx_frame.h) ------------------------------------------------
+
+def _cam(K4, dist):
+    k = np.ascontiguousarray(K4, np.float32).reshape(4)
+    d = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    if len(d) not in (4, 5, 8):
+        raise ValueError("distortion needs 4, 5 or 8 coefficients")
+    return k, d
+
+
+def undistort_keypoints(keys: np.ndarray, K4, dist, device: int = 0) -> np.ndarray:
+    """Frame::UndistortKeyPoints (src/Frame.cc:429-459) on the GPU: mvKeysUn from mvKeys."""
+    from ._lib import check, load, ptr
+    k, d = _cam(K4, dist)
+    src = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    out = src.copy()
+    check("orbx_undistort_keypoints", load().orbx_undistort_keypoints(
+        ptr(k), ptr(d), len(d), ptr(src), len(src), ptr(out), device))
+    return out
+
+
+def image_bounds(K4, dist, width: int, height: int):
+    """Frame::ComputeImageBounds (src/Frame.cc:461-489) -> (minX, maxX, minY, maxY)."""
+    from ._lib import check, load, ptr
+    k, d = _cam(K4, dist)
+    b = np.zeros(4, np.float32)
+    check("orbx_image_bounds", load().orbx_image_bounds(ptr(k), ptr(d), len(d), width, height,
+                                                         ptr(b)))
+    return tuple(float(v) for v in b)
+
+
+def assign_grid_device(d_keys, n: int, min_x: float, max_x: float, min_y: float, max_y: float,
+                       d_off, d_feat, cols: int = FRAME_GRID_COLS, rows: int = FRAME_GRID_ROWS,
+                       stream: int = 0):
+    """Frame::AssignFeaturesToGrid on device keypoints (torch tensors) -> fills d_off
+    (cols*rows + 1) and d_feat (n)."""
+    from ._lib import check, load, ptr
+    f32 = np.float32
+    inv_w = f32(cols) / f32(f32(max_x) - f32(min_x))
+    inv_h = f32(rows) / f32(f32(max_y) - f32(min_y))
+    check("orbx_assign_grid_device", load().orbx_assign_grid_device(
+        ptr(d_keys), n, cols, rows, float(f32(min_x)), float(f32(min_y)), float(inv_w),
+        float(inv_h), ptr(d_off), ptr(d_feat), ctypes.c_void_p(stream)))

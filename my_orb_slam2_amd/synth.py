@@ -14,6 +14,11 @@ import numpy as np
 KITTI = dict(width=1241, height=376, nfeatures=2000, fx=718.856, mbf=386.1448)  # KITTI00-02.yaml
 TUM = dict(width=640, height=480, nfeatures=1000)                             # TUM1.yaml
 EUROC = dict(width=752, height=480, nfeatures=1000)                           # EuRoC.yaml
+# camera intrinsics (fx, fy, cx, cy) and distortion (k1, k2, p1, p2[, k3]) of the examples
+EUROC_CAM = ((458.654, 457.296, 367.215, 248.375),
+             (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05))   # Monocular/EuRoC.yaml:8-16
+TUM1_CAM = ((517.306408, 516.469215, 318.643040, 255.313989),
+            (0.262383, -0.953104, -0.005358, 0.002628, 1.163314))     # Monocular/TUM1.yaml:8-17
 
 
 def _scene(rng, width, height, n_rect, n_disk):

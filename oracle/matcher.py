@@ -206,3 +206,25 @@ def bow_score_l1(b1, b2):
     lib().oracle_bow_score_l1.restype = ctypes.c_double
     lib().oracle_bow_score_l1.argtypes = [_vp, _vp, _i, _vp, _vp, _i]
     return lib().oracle_bow_score_l1(_a(w1), _a(v1), len(w1), _a(w2), _a(v2), len(w2))
+
+
+def undistort_keypoints(keys, K4, dist):
+    """Frame::UndistortKeyPoints restated: returns the undistorted (x, y) float32 [n, 2]."""
+    k = np.ascontiguousarray(K4, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    xy = np.ascontiguousarray(np.stack([keys["x"], keys["y"]], 1), np.float32)
+    out = np.zeros_like(xy)
+    L = lib()
+    L.oracle_undistort_keypoints.argtypes = [_vp, _vp, _i, _vp, _i, _vp]
+    L.oracle_undistort_keypoints(_a(k), _a(d), len(d), _a(xy), len(xy), _a(out))
+    return out
+
+
+def image_bounds(K4, dist, cols, rows):
+    k = np.ascontiguousarray(K4, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    out = np.zeros(4, np.float32)
+    L = lib()
+    L.oracle_image_bounds.argtypes = [_vp, _vp, _i, _i, _i, _vp]
+    L.oracle_image_bounds(_a(k), _a(d), len(d), cols, rows, _a(out))
+    return tuple(float(v) for v in out)

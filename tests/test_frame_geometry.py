@@ -1,0 +1,103 @@
+"""Frame geometry around the matchers: undistortion (cvUndistortPoints, OpenCV 3.2 restated),
+image bounds and the feature grid.  CPU: the restatement against a numpy float64 reading and
+the host bounds; GPU: device undistortion and grid against the restatement."""
+import numpy as np
+import pytest
+
+from my_orb_slam2_amd import synth
+from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
+from my_orb_slam2_amd.features import assign_features_to_grid, image_bounds
+
+CAMS = {"euroc": synth.EUROC_CAM, "tum1": synth.TUM1_CAM,
+        "rational": ((500.0, 501.0, 320.5, 240.25), (0.1, -0.05, 0.001, -0.002, 0.01, 0.02, -0.01, 0.005))}
+
+
+def undistort_np(xy, K4, dist):
+    """cvUndistortPoints (OpenCV 3.2) in numpy float64, same operation order."""
+    k = np.zeros(8)
+    d = np.asarray(dist, np.float32).astype(np.float64)
+    k[:len(d)] = d
+    fx, fy, cx, cy = (float(np.float32(v)) for v in K4)
+    ifx, ify = 1.0 / fx, 1.0 / fy
+    x = (xy[:, 0].astype(np.float64) - cx) * ifx
+    y = (xy[:, 1].astype(np.float64) - cy) * ify
+    x0, y0 = x.copy(), y.copy()
+    for _ in range(5):
+        r2 = x * x + y * y
+        icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2)
+        dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x)
+        dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y
+        x = (x0 - dx) * icdist
+        y = (y0 - dy) * icdist
+    xx = fx * x + 0.0 * y + cx
+    yy = 0.0 * x + fy * y + cy
+    ww = 1.0 / (0.0 * x + 0.0 * y + 1.0)
+    return np.stack([(xx * ww).astype(np.float32), (yy * ww).astype(np.float32)], 1)
+
+
+def _keys(n, w=752, h=480, seed=0):
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(0, w, n)
+    k["y"] = rng.uniform(0, h, n)
+    k["octave"] = rng.integers(0, 8, n)
+    k["angle"] = rng.uniform(0, 360, n)
+    return k
+
+
+@pytest.mark.parametrize("cam", list(CAMS))
+def test_undistort_oracle_vs_numpy(cam):
+    from oracle import matcher as om
+    K4, dist = CAMS[cam]
+    k = _keys(3000)
+    got = om.undistort_keypoints(k, K4, dist)
+    want = undistort_np(np.stack([k["x"], k["y"]], 1).astype(np.float32), K4, dist)
+    np.testing.assert_array_equal(got.view(np.int32), want.view(np.int32))
+
+
+def test_undistort_zero_k1_copies():
+    from oracle import matcher as om
+    k = _keys(50)
+    got = om.undistort_keypoints(k, synth.EUROC_CAM[0], (0.0, 0.1, 0.01, 0.01))
+    np.testing.assert_array_equal(got[:, 0], k["x"])
+
+
+@pytest.mark.parametrize("cam", list(CAMS))
+def test_image_bounds_host(orbx_lib, cam):
+    from oracle import matcher as om
+    K4, dist = CAMS[cam]
+    assert image_bounds(K4, dist, 752, 480) == om.image_bounds(K4, dist, 752, 480)
+    assert image_bounds(K4, (0, 0, 0, 0), 640, 480) == (0.0, 640.0, 0.0, 480.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cam", list(CAMS))
+def test_undistort_gpu(oracle_mod, orbx_lib, gpu, cam):
+    from oracle import matcher as om
+    from my_orb_slam2_amd.features import undistort_keypoints
+    K4, dist = CAMS[cam]
+    k = _keys(5000, seed=3)
+    un = undistort_keypoints(k, K4, dist)
+    want = om.undistort_keypoints(k, K4, dist)
+    np.testing.assert_array_equal(un["x"].view(np.int32), want[:, 0].view(np.int32))
+    np.testing.assert_array_equal(un["y"].view(np.int32), want[:, 1].view(np.int32))
+    np.testing.assert_array_equal(un["octave"], k["octave"])
+
+
+@pytest.mark.gpu
+def test_grid_gpu(orbx_lib, gpu):
+    import torch
+    from my_orb_slam2_amd.features import assign_grid_device
+    for seed, n in [(0, 2000), (1, 1), (2, 0), (3, 4500)]:
+        k = _keys(n, seed=seed)
+        if n >= 5:
+            k["x"][:5] = [0.0, 751.99, -3.0, 5.875, 760.0]   # borders and outside
+        bmin_x, bmax_x, bmin_y, bmax_y = image_bounds(*synth.EUROC_CAM, 752, 480)
+        g = assign_features_to_grid(k, bmin_x, bmax_x, bmin_y, bmax_y)
+        dk = torch.from_numpy(k.view(np.uint8).copy()).to(gpu) if n else torch.zeros(28, dtype=torch.uint8, device=gpu)
+        off = torch.zeros(64 * 48 + 1, dtype=torch.int32, device=gpu)
+        feat = torch.full((max(n, 1),), -1, dtype=torch.int32, device=gpu)
+        assign_grid_device(dk, n, bmin_x, bmax_x, bmin_y, bmax_y, off, feat)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(off.cpu().numpy(), g.off)
+        np.testing.assert_array_equal(feat.cpu().numpy()[:len(g.feat)], g.feat)
