@@ -49,6 +49,22 @@ orbx_status orbx_vocabulary_transform_device(orbx_vocabulary* v, const uint8_t* 
 double orbx_bow_score_l1(const uint32_t* w1, const double* v1, int32_t n1, const uint32_t* w2,
                          const double* v2, int32_t n2);
 
+/* The scoring pass of KeyFrameDatabase::DetectRelocalizationCandidates / DetectLoopCandidates
+ * (src/KeyFrameDatabase.cc:220-278, 44-163) for nkf keyframes at once: common[i] = the
+ * number of the query's words keyframe i's BowVector holds (mnRelocWords / mnLoopWords, the
+ * inverted-file count), score[i] = (float)L1Scoring::score(query, keyframe i) (mRelocScore).
+ * Keyframe i's BowVector is words/values [kf_off[i], kf_off[i+1]) (ascending words).  The
+ * candidate selection that follows (minCommonWords, covisibility accumulation) reads the
+ * Map's covisibility graph and stays with the caller.  Host-pointer version: */
+orbx_status orbx_bow_db_score(const uint32_t* qword, const double* qval, int32_t nq, int32_t nkf,
+                              const int32_t* kf_off, const uint32_t* word, const double* val,
+                              int32_t* common, float* score, int device);
+/* Device version (all arrays device memory), on the caller's stream. */
+orbx_status orbx_bow_db_score_device(const uint32_t* d_qword, const double* d_qval, int32_t nq,
+                                     int32_t nkf, const int32_t* d_kf_off,
+                                     const uint32_t* d_word, const double* d_val,
+                                     int32_t* d_common, float* d_score, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

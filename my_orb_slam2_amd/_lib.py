@@ -97,6 +97,8 @@ SIGNATURES = {
                                        _vp]),
     "orbx_vocabulary_transform_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
     "orbx_bow_score_l1": (ctypes.c_double, [_vp, _vp, _i, _vp, _vp, _i]),
+    "orbx_bow_db_score": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _i]),
+    "orbx_bow_db_score_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     # include/orbx_frame.h
     "orbx_undistort_keypoints": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i]),
     "orbx_undistort_keypoints_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp]),

@@ -68,6 +68,69 @@ __global__ __launch_bounds__(256) void k_transform(const uint8_t* __restrict__ d
     onode[i] = nid < 0 ? id : nid;   // a leaf above level L-levelsup: the reference leaves nid unset
 }
 
+// BoW database scoring: one wave per keyframe.  Lanes binary-search the keyframe's words in
+// the query (LDS), the matched terms fabs(v-w) - fabs(v) - fabs(w) land in LDS in word order
+// and lane 0 adds them in that order (L1Scoring::score's sequential double sum; unmatched
+// positions are skipped, which adds nothing to the sum).
+__global__ __launch_bounds__(256) void k_bow_score(const uint32_t* __restrict__ qword,
+                                                   const double* __restrict__ qval, int nq,
+                                                   int nkf, const int32_t* __restrict__ kf_off,
+                                                   const uint32_t* __restrict__ word,
+                                                   const double* __restrict__ val,
+                                                   int32_t* __restrict__ common,
+                                                   float* __restrict__ score) {
+    extern __shared__ uint8_t sm[];
+    uint32_t* qw = (uint32_t*)sm;                          // nq
+    double* qv = (double*)(sm + ((4 * (size_t)nq + 7) & ~(size_t)7));
+    double* term = qv + nq + 64 * (threadIdx.x >> 6);      // 64 per wave
+    for (int i = threadIdx.x; i < nq; i += 256) {
+        qw[i] = qword[i];
+        qv[i] = qval[i];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int kf = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kf >= nkf) return;
+    const int o0 = kf_off[kf], o1 = kf_off[kf + 1];
+    int cnt = 0;
+    double s = 0;
+    for (int base = o0; base < o1; base += 64) {
+        const int p = base + lane;
+        double t = 0;
+        bool hit = false;
+        if (p < o1) {
+            const uint32_t w = word[p];
+            int lo = 0, hi = nq;   // lower_bound in the query's words
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (qw[mid] < w) lo = mid + 1; else hi = mid;
+            }
+            if (lo < nq && qw[lo] == w) {
+                const double vi = qv[lo], wi = val[p];
+                t = fabs(vi - wi) - fabs(vi) - fabs(wi);
+                hit = true;
+            }
+        }
+        term[lane] = t;
+        const uint64_t m = __ballot(hit);
+        cnt += __popcll(m);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) {
+            uint64_t mm = m;
+            while (mm) {
+                const int j = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                s += term[j];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (lane == 0) {
+        common[kf] = cnt;
+        score[kf] = (float)(-s / 2.0);
+    }
+}
+
 }  // namespace
 
 struct orbx_vocabulary {
@@ -274,6 +337,65 @@ orbx_status orbx_vocabulary_transform(orbx_vocabulary* v, const uint8_t* desc, i
     }
     *fv_n = j;
     return ORBX_OK;
+}
+
+orbx_status orbx_bow_db_score_device(const uint32_t* d_qword, const double* d_qval, int32_t nq,
+                                     int32_t nkf, const int32_t* d_kf_off,
+                                     const uint32_t* d_word, const double* d_val,
+                                     int32_t* d_common, float* d_score, void* stream) {
+    if (nq < 0 || nkf < 0 || (nkf > 0 && (!d_kf_off || !d_common || !d_score)) ||
+        (nq > 0 && (!d_qword || !d_qval)))
+        return ORBX_ERR_INVALID;
+    const size_t lds = ((4 * (size_t)nq + 7) & ~(size_t)7) + 8 * ((size_t)nq + 256);
+    if (lds > 64 * 1024) return ORBX_ERR_UNSUPPORTED;   // query BowVector up to ~5400 words
+    if (nkf == 0) return ORBX_OK;
+    hipLaunchKernelGGL(k_bow_score, dim3((nkf + 3) / 4), dim3(256), lds, (hipStream_t)stream,
+                       d_qword, d_qval, nq, nkf, d_kf_off, d_word, d_val, d_common, d_score);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_bow_db_score(const uint32_t* qword, const double* qval, int32_t nq, int32_t nkf,
+                              const int32_t* kf_off, const uint32_t* word, const double* val,
+                              int32_t* common, float* score, int device) {
+    if (nq < 0 || nkf < 0 || (nkf > 0 && (!kf_off || !common || !score))) return ORBX_ERR_INVALID;
+    if (nkf == 0) return ORBX_OK;
+    const int nw = kf_off[nkf] - kf_off[0];
+    if (nw < 0 || (nw > 0 && (!word || !val)) || (nq > 0 && (!qword || !qval)))
+        return ORBX_ERR_INVALID;
+    if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
+    std::vector<int32_t> rel(nkf + 1);
+    for (int i = 0; i <= nkf; ++i) rel[i] = kf_off[i] - kf_off[0];
+    const size_t bytes = 4 * (size_t)nq + 8 * (size_t)nq + 4 * rel.size() + 4 * (size_t)nw +
+                         8 * (size_t)nw + 8 * (size_t)nkf + 64 * 6;
+    DevBuf buf;
+    if (!buf.ensure(bytes)) return ORBX_ERR_DEVICE;
+    uint8_t* b = buf.as<uint8_t>();
+    size_t o = 0;
+    auto put = [&](const void* src, size_t n) {
+        uint8_t* d = b + o;
+        o = (o + n + 63) & ~(size_t)63;
+        if (n && src && !HIPOK(hipMemcpy(d, src, n, hipMemcpyHostToDevice))) return (uint8_t*)nullptr;
+        return d;
+    };
+    uint8_t* dqv = put(qval, 8 * (size_t)nq);
+    uint8_t* dqw = put(qword, 4 * (size_t)nq);
+    uint8_t* dv = put(nw ? val + kf_off[0] : nullptr, 8 * (size_t)nw);
+    uint8_t* dw = put(nw ? word + kf_off[0] : nullptr, 4 * (size_t)nw);
+    uint8_t* doff = put(rel.data(), 4 * rel.size());
+    uint8_t* dsc = put(nullptr, 4 * (size_t)nkf);
+    uint8_t* dcm = put(nullptr, 4 * (size_t)nkf);
+    orbx_status s = ORBX_ERR_DEVICE;
+    if (dqv && dqw && dv && dw && doff) {
+        s = orbx_bow_db_score_device((uint32_t*)dqw, (double*)dqv, nq, nkf, (int32_t*)doff,
+                                     (uint32_t*)dw, (double*)dv, (int32_t*)dcm, (float*)dsc,
+                                     nullptr);
+        if (s == ORBX_OK &&
+            (!HIPOK(hipMemcpy(common, dcm, 4 * (size_t)nkf, hipMemcpyDeviceToHost)) ||
+             !HIPOK(hipMemcpy(score, dsc, 4 * (size_t)nkf, hipMemcpyDeviceToHost))))
+            s = ORBX_ERR_DEVICE;
+    }
+    buf.release();
+    return s;
 }
 
 double orbx_bow_score_l1(const uint32_t* w1, const double* v1, int32_t n1, const uint32_t* w2,

@@ -63,3 +63,23 @@ def bow_score_l1(bow1, bow2) -> float:
     w1, v1 = (np.ascontiguousarray(bow1[0], np.uint32), np.ascontiguousarray(bow1[1], np.float64))
     w2, v2 = (np.ascontiguousarray(bow2[0], np.uint32), np.ascontiguousarray(bow2[1], np.float64))
     return float(load().orbx_bow_score_l1(ptr(w1), ptr(v1), len(w1), ptr(w2), ptr(v2), len(w2)))
+
+
+def bow_db_score(query_bow, kf_bows, device: int = 0):
+    """Scoring pass of KeyFrameDatabase::DetectRelocalizationCandidates
+    (src/KeyFrameDatabase.cc:220-278) on the GPU: for every keyframe BowVector, the number of
+    words it shares with the query and (float)L1Scoring::score(query, keyframe)."""
+    qw = np.ascontiguousarray(query_bow[0], np.uint32)
+    qv = np.ascontiguousarray(query_bow[1], np.float64)
+    nkf = len(kf_bows)
+    sizes = np.array([len(b[0]) for b in kf_bows], np.int64)
+    off = np.zeros(nkf + 1, np.int32)
+    np.cumsum(sizes, out=off[1:])
+    words = np.concatenate([np.asarray(b[0], np.uint32) for b in kf_bows]) if nkf else np.zeros(0, np.uint32)
+    vals = np.concatenate([np.asarray(b[1], np.float64) for b in kf_bows]) if nkf else np.zeros(0)
+    common = np.zeros(max(nkf, 1), np.int32)
+    score = np.zeros(max(nkf, 1), np.float32)
+    check("orbx_bow_db_score", load().orbx_bow_db_score(
+        ptr(qw), ptr(qv), len(qw), nkf, ptr(off), ptr(np.ascontiguousarray(words)),
+        ptr(np.ascontiguousarray(vals)), ptr(common), ptr(score), device))
+    return common[:nkf], score[:nkf]

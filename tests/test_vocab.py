@@ -131,3 +131,27 @@ def test_vocab_gpu(tmp_path, oracle_mod, orbx_lib, gpu, k, L, sc, wt, levelsup):
         np.testing.assert_array_equal(fv.feat, off)
         bows.append((bw, bv))
     assert bow_score_l1(bows[0], bows[1]) == o_score(bows[0], bows[1])
+
+
+@pytest.mark.gpu
+def test_bow_db_score_gpu(tmp_path, oracle_mod, orbx_lib, gpu):
+    """KeyFrameDatabase scoring pass: shared-word counts and (float) L1 scores of 300
+    keyframe BowVectors against one query, vs the restated L1Scoring::score."""
+    from oracle.matcher import OracleVocabulary, bow_score_l1 as o_score
+    from my_orb_slam2_amd.vocabulary import bow_db_score
+    path = tmp_path / "voc.txt"
+    synth.write_vocabulary(path, k=10, L=3, seed=5)
+    ov = OracleVocabulary(path)
+    rng = np.random.default_rng(0)
+    base = rng.integers(0, 256, (800, 32), dtype=np.uint8)
+    q = ov.transform(base, 2)[2]
+    kfs = []
+    for i in range(300):
+        d = base.copy() if i % 3 == 0 else rng.integers(0, 256, (rng.integers(0, 900), 32), dtype=np.uint8)
+        if i % 3 == 0:
+            d[rng.random(len(d)) < 0.5] = rng.integers(0, 256, 32, dtype=np.uint8)
+        kfs.append(ov.transform(d, 2)[2])
+    common, score = bow_db_score(q, kfs)
+    for i, b in enumerate(kfs):
+        assert common[i] == len(np.intersect1d(q[0], b[0]))
+        assert score[i] == np.float32(o_score(q, b)), i
