@@ -40,6 +40,17 @@ orbx_status orbx_assign_grid_device(const orbx_keypoint* d_kps, int32_t n, int32
                                     float inv_h, int32_t* d_grid_off, int32_t* d_grid_feat,
                                     void* stream);
 
+/* Tracking's colour input (src/Tracking.cc:189-214): cv::cvtColor(*2GRAY) for 3- or 4-channel
+ * 8-bit images, OpenCV 3.2's integer path RGB2Gray<uchar> (Y = (R*4899 + G*9617 + B*1868 +
+ * 8192) >> 14).  rgb = 1 for RGB/RGBA order (mbRGB), 0 for BGR/BGRA.  OpenCV builds with IPP
+ * may route BGR2GRAY through ippiColorToGray instead: PARITY UNPINNED against the library. */
+orbx_status orbx_cvt_color_device(const uint8_t* d_src, int32_t width, int32_t height,
+                                  size_t src_stride, int32_t channels, int32_t rgb,
+                                  uint8_t* d_dst, size_t dst_stride, void* stream);
+orbx_status orbx_cvt_color(const uint8_t* src, int32_t width, int32_t height, size_t src_stride,
+                           int32_t channels, int32_t rgb, uint8_t* dst, size_t dst_stride,
+                           int device);
+
 #ifdef __cplusplus
 }
 #endif

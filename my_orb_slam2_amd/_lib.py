@@ -104,6 +104,8 @@ SIGNATURES = {
     "orbx_undistort_keypoints_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp]),
     "orbx_image_bounds": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "orbx_assign_grid_device": (_i, [_vp, _i, _i, _i, _f, _f, _f, _f, _vp, _vp, _vp]),
+    "orbx_cvt_color": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _i]),
+    "orbx_cvt_color_device": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _vp]),
 }
 
 _lib = None

@@ -125,9 +125,71 @@ __global__ __launch_bounds__(1024) void k_grid(const orbx_keypoint* __restrict__
     }
 }
 
+// cvtColor(*2GRAY), OpenCV 3.2 RGB2Gray<uchar>: the three table terms summed with the
+// 1 << 13 rounding constant, >> 14.  One thread per 4 output pixels.
+__global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ src, int w, int h,
+                                              size_t sstride, int scn, int rgb,
+                                              uint8_t* __restrict__ dst, size_t dstride) {
+    const int y = blockIdx.y;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (x0 >= w) return;
+    const uint8_t* s = src + (size_t)y * sstride + (size_t)x0 * scn;
+    const int c0 = rgb ? 4899 : 1868, c2 = rgb ? 1868 : 4899;   // coeff of src[0], src[2]
+    uint32_t out = 0;
+    const int nx = min(4, w - x0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < nx) {
+            const int v = (c0 * s[j * scn] + 9617 * s[j * scn + 1] + c2 * s[j * scn + 2] + (1 << 13)) >> 14;
+            out |= (uint32_t)v << (8 * j);
+        }
+    }
+    uint8_t* d = dst + (size_t)y * dstride + x0;
+    for (int j = 0; j < nx; ++j) d[j] = (uint8_t)(out >> (8 * j));
+}
+
 }  // namespace
 
 extern "C" {
+
+orbx_status orbx_cvt_color_device(const uint8_t* d_src, int32_t width, int32_t height,
+                                  size_t src_stride, int32_t channels, int32_t rgb,
+                                  uint8_t* d_dst, size_t dst_stride, void* stream) {
+    if (width < 0 || height < 0 || (channels != 3 && channels != 4)) return ORBX_ERR_INVALID;
+    if (width == 0 || height == 0) return ORBX_OK;
+    if (!d_src || !d_dst || src_stride < (size_t)width * channels || dst_stride < (size_t)width)
+        return ORBX_ERR_INVALID;
+    hipLaunchKernelGGL(k_gray, dim3((width + 1023) / 1024, height), dim3(256), 0,
+                       (hipStream_t)stream, d_src, width, height, src_stride, channels, rgb,
+                       d_dst, dst_stride);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_cvt_color(const uint8_t* src, int32_t width, int32_t height, size_t src_stride,
+                           int32_t channels, int32_t rgb, uint8_t* dst, size_t dst_stride,
+                           int device) {
+    if (width < 0 || height < 0 || (channels != 3 && channels != 4)) return ORBX_ERR_INVALID;
+    if (width == 0 || height == 0) return ORBX_OK;
+    if (!src || !dst || src_stride < (size_t)width * channels || dst_stride < (size_t)width)
+        return ORBX_ERR_INVALID;
+    if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
+    const size_t sb = (size_t)width * channels * height, db = (size_t)width * height;
+    DevBuf buf;
+    if (!buf.ensure(sb + db)) return ORBX_ERR_DEVICE;
+    uint8_t* ds = buf.as<uint8_t>();
+    orbx_status s = ORBX_OK;
+    if (!HIPOK(hipMemcpy2D(ds, (size_t)width * channels, src, src_stride, (size_t)width * channels,
+                           height, hipMemcpyHostToDevice)))
+        s = ORBX_ERR_DEVICE;
+    if (s == ORBX_OK)
+        s = orbx_cvt_color_device(ds, width, height, (size_t)width * channels, channels, rgb,
+                                  ds + sb, width, nullptr);
+    if (s == ORBX_OK && !HIPOK(hipMemcpy2D(dst, dst_stride, ds + sb, width, width, height,
+                                           hipMemcpyDeviceToHost)))
+        s = ORBX_ERR_DEVICE;
+    buf.release();
+    return s;
+}
 
 orbx_status orbx_undistort_keypoints_device(const float* K4, const float* dist, int32_t ndist,
                                             const orbx_keypoint* d_kps, int32_t n,

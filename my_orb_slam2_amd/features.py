@@ -201,3 +201,17 @@ def assign_grid_device(d_keys, n: int, min_x: float, max_x: float, min_y: float,
     check("orbx_assign_grid_device", load().orbx_assign_grid_device(
         ptr(d_keys), n, cols, rows, float(f32(min_x)), float(f32(min_y)), float(inv_w),
         float(inv_h), ptr(d_off), ptr(d_feat), ctypes.c_void_p(stream)))
+
+
+def cvt_color_gray(img: np.ndarray, rgb: bool = False, device: int = 0) -> np.ndarray:
+    """Tracking's colour conversion (src/Tracking.cc:189-214): cvtColor(*2GRAY) of an 8-bit
+    3- or 4-channel image on the GPU (rgb=True for RGB/RGBA order, mbRGB)."""
+    from ._lib import check, load, ptr
+    src = np.ascontiguousarray(img, np.uint8)
+    if src.ndim != 3 or src.shape[2] not in (3, 4):
+        raise ValueError("expected an H x W x 3 or H x W x 4 uint8 image")
+    h, w, c = src.shape
+    out = np.zeros((h, w), np.uint8)
+    check("orbx_cvt_color", load().orbx_cvt_color(ptr(src), w, h, w * c, c, int(rgb), ptr(out),
+                                                   w, device))
+    return out

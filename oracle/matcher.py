@@ -228,3 +228,13 @@ def image_bounds(K4, dist, cols, rows):
     L.oracle_image_bounds.argtypes = [_vp, _vp, _i, _i, _i, _vp]
     L.oracle_image_bounds(_a(k), _a(d), len(d), cols, rows, _a(out))
     return tuple(float(v) for v in out)
+
+
+def cvt_gray(img, rgb):
+    s = np.ascontiguousarray(img, np.uint8)
+    h, w, c = s.shape
+    out = np.zeros((h, w), np.uint8)
+    L = lib()
+    L.oracle_cvt_gray.argtypes = [_vp, _i, _i, _i, _i, _vp]
+    L.oracle_cvt_gray(_a(s), w, h, c, int(rgb), _a(out))
+    return out

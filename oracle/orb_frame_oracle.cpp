@@ -72,3 +72,25 @@ void oracle_image_bounds(const float* K4, const float* dist, int ndist, int cols
 }
 
 }  // extern "C"
+
+extern "C" {
+// cvtColor(*2GRAY), OpenCV 3.2 RGB2Gray<uchar> (imgproc/src/color.cpp): tab-based integer
+// path, yuv_shift = 14, R2Y = 4899, G2Y = 9617, B2Y = 1868, rounding 1 << 13 in the third
+// table.  blueIdx = 0 for BGR, 2 for RGB.
+void oracle_cvt_gray(const uint8_t* src, int w, int h, int scn, int rgb, uint8_t* dst) {
+    const int coeffs[3] = {4899, 9617, 1868};   // R2Y, G2Y, B2Y
+    const int blueIdx = rgb ? 2 : 0;
+    int tab[256 * 3];
+    int b = 0, g = 0, r = (1 << 13);
+    const int db = coeffs[blueIdx ^ 2], dg = coeffs[1], dr = coeffs[blueIdx];
+    for (int i = 0; i < 256; i++, b += db, g += dg, r += dr) {
+        tab[i] = b;
+        tab[i + 256] = g;
+        tab[i + 512] = r;
+    }
+    for (int i = 0; i < w * h; i++) {
+        const uint8_t* s = src + (size_t)i * scn;
+        dst[i] = (uint8_t)((tab[s[0]] + tab[s[1] + 256] + tab[s[2] + 512]) >> 14);
+    }
+}
+}

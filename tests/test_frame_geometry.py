@@ -101,3 +101,22 @@ def test_grid_gpu(orbx_lib, gpu):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(off.cpu().numpy(), g.off)
         np.testing.assert_array_equal(feat.cpu().numpy()[:len(g.feat)], g.feat)
+
+
+@pytest.mark.parametrize("rgb,c", [(0, 3), (1, 3), (0, 4), (1, 4)])
+def test_cvt_gray_oracle_vs_numpy(rgb, c):
+    from oracle import matcher as om
+    img = np.random.default_rng(c + rgb).integers(0, 256, (37, 53, c), dtype=np.uint8)
+    r, g, b = (img[..., 0], img[..., 1], img[..., 2]) if rgb else (img[..., 2], img[..., 1], img[..., 0])
+    r, g, b = (v.astype(np.int64) for v in (r, g, b))
+    want = ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+    np.testing.assert_array_equal(om.cvt_gray(img, rgb), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rgb,c", [(0, 3), (1, 3), (0, 4), (1, 4)])
+def test_cvt_gray_gpu(orbx_lib, gpu, rgb, c):
+    from oracle import matcher as om
+    from my_orb_slam2_amd.features import cvt_color_gray
+    img = np.random.default_rng(7).integers(0, 256, (376, 1241, c), dtype=np.uint8)
+    np.testing.assert_array_equal(cvt_color_gray(img, bool(rgb)), om.cvt_gray(img, rgb))

@@ -14,3 +14,7 @@ W=$(ls $OUT/prof/pmc4/*counter_collection.csv 2>/dev/null | head -1)
 echo "pmc: $F $W"
 timeout -k 10 600 python bench.py --traffic-csv "$F,$W" "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
+timeout -k 10 600 python bench.py --workload reloc --steps 10 --warmup 2 > $OUT/reloc.json 2> $OUT/reloc.err || { echo "RELOC BENCH FAILED"; tail -20 $OUT/reloc.err; exit 1; }
+cat $OUT/reloc.json
+timeout -k 10 600 python bench.py --workload triangulation --steps 20 --warmup 3 > $OUT/tri.json 2> $OUT/tri.err || { echo "TRI BENCH FAILED"; tail -20 $OUT/tri.err; exit 1; }
+cat $OUT/tri.json
