@@ -39,6 +39,10 @@ DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
                        ("r01_pmc_fetch_b256.csv", "r01_pmc_write_b256.csv"))
 
 
+DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
+                             ("r01_pmc_fetch_euroc.csv", "r01_pmc_write_euroc.csv"))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -49,13 +53,17 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--workload", default="stereo", choices=["stereo", "reloc", "triangulation"],
-                    help="stereo = the BASELINE metric (configs[1]); reloc = configs[3] "
+    ap.add_argument("--workload", default="stereo",
+                    choices=["stereo", "euroc", "reloc", "triangulation"],
+                    help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
+                         "extract + SearchByProjection vs the local map); reloc = configs[3] "
                          "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
                          "(512 SearchForTriangulation jobs, sharded)")
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
-    ap.add_argument("--traffic-csv", default=DEFAULT_PMC,
+    ap.add_argument("--queries", type=int, default=2000,
+                    help="euroc: projected local-map MapPoints per frame")
+    ap.add_argument("--traffic-csv", default=None,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"
                          " committed profiles/ summaries of this workload)")
@@ -69,6 +77,10 @@ def algorithmic_bytes_fast(level_sizes, cells_area_read, ncand):
 
 def main():
     args = parse()
+    if args.traffic_csv is None:
+        args.traffic_csv = DEFAULT_PMC if args.workload == "stereo" else DEFAULT_PMC_EUROC
+    if args.workload == "euroc":
+        return main_euroc(args)
     if args.workload != "stereo":
         return main_match(args)
     import torch
@@ -138,7 +150,7 @@ def main():
         dom = max(prof, key=lambda k: prof[k][0])
         tot_ms, launches = prof[dom]
         avg_s = tot_ms / 1000.0 / max(launches, 1)
-        geo = kernel_bytes(sb, B)
+        geo = kernel_bytes(sb.ext, 2 * B, B)
         alg = geo.get(dom)
         achieved = (alg / avg_s / 1e9) if (alg and avg_s > 0) else None
         roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -169,13 +181,12 @@ def main():
         dist.destroy_process_group()
 
 
-def kernel_bytes(sb, B):
+def kernel_bytes(ext, n, B):
     """Algorithmic HBM bytes per launch of each kernel.  One launch
-    covers the 2B views (k_level: one level of them)."""
-    v = sb.ext.batch_view()
+    covers the n images (k_level: one level of them); B stereo pairs for k_stereo."""
+    v = ext.batch_view()
     L = 8
     area = [v.level_w[l] * v.level_h[l] for l in range(L)]
-    n = 2 * B
     kc = v.kp_cap
     return {
         # per level: read level l-1 (level 0: the input), write level l and its blur
@@ -254,6 +265,173 @@ def cpu_baseline(pairs, mb, budget_s):
             "sample": f"{done} KITTI-size synthetic stereo pairs, L/R extraction on 2 threads + "
                       f"ComputeStereoMatches (Frame.cc:89-102), {el:.1f} s",
             "cpu_model": model, "host_cpus": os.cpu_count()}
+
+
+# ---- EuRoC mono tracking (configs[2]) ----------------------------------------------------------
+
+EUROC_W, EUROC_H, EUROC_NFEAT = 752, 480, 1000     # Examples/Monocular/EuRoC.yaml
+
+
+def main_euroc(args):
+    """configs[2]: per frame, ORBextractor (1000 features) + UndistortKeyPoints +
+    AssignFeaturesToGrid + SearchLocalPoints' SearchByProjection(Frame, local MapPoints)
+    (Tracking.cc:1297-1347) against `--queries` projected MapPoints of a 20-keyframe local
+    map.  The projections (Frame::isInFrustum output: u, v, radius, predicted level) and the
+    motion-model claims are inputs resident in HBM; B frames per step on one stream."""
+    import torch
+    import torch.distributed as dist
+    from my_orb_slam2_amd import synth
+    from my_orb_slam2_amd.tracking import MonoTrackBatch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    K4, distc = synth.EUROC_CAM
+    B = args.batch
+    P = max(1, min(args.distinct, B))
+    frames = [synth.frame(2000 * rank + 7 + i, EUROC_W, EUROC_H) for i in range(P)]
+    idx = [i % P for i in range(B)]
+    d_imgs = torch.from_numpy(np.stack([frames[i] for i in idx])).to(dev)
+    mt = MonoTrackBatch(B, EUROC_W, EUROC_H, K4, distc, EUROC_NFEAT, device=local)
+
+    # inputs: the local map projected into each frame (built from the frame's own features)
+    mt.frames(d_imgs, st)
+    nkp, ku, desc = mt.fetch_undistorted()
+    per = {}
+    qs, ds, cls = [], [], []
+    for b in range(B):
+        p = idx[b]
+        if p not in per:
+            n = int(nkp[b])
+            q, d = synth.local_map_queries(p, ku[b, :n], desc[b, :n], args.queries,
+                                           EUROC_W, EUROC_H)
+            cl = np.random.default_rng(p).random(mt.kp_cap) < 0.2
+            per[p] = (q, d, cl.astype(np.uint8))
+        qs.append(per[p][0])
+        ds.append(per[p][1])
+        cls.append(per[p][2])
+    q_off_h = np.concatenate([[0], np.cumsum([len(q) for q in qs])]).astype(np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    d_q, d_d, d_cl = T(np.concatenate(qs)), T(np.concatenate(ds)), T(np.concatenate(cls))
+    d_qoff = torch.from_numpy(q_off_h).to(dev)
+    out = torch.empty(int(q_off_h[-1]), dtype=torch.int32, device=dev)
+    cnt = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def step():
+        mt(d_imgs, d_d, d_q, d_qoff, out, cnt, d_cl, st)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    mt.matcher.sync(st)
+    prof_on = not args.no_kernel_timing
+    mt.ext.profile(prof_on)
+    mt.matcher.profile(prof_on)
+    mt.ext.collect_profile()
+    mt.matcher.collect_profile()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    mt.matcher.sync(st)
+    prof = {}
+    if prof_on:
+        prof.update(mt.ext.collect_profile())
+        prof.update({k: v for k, v in mt.matcher.collect_profile().items() if v[1]})
+    counts = cnt.cpu().numpy()
+    roof = None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][0])
+        tot_ms, launches = prof[dom]
+        avg_s = tot_ms / 1000.0 / max(launches, 1)
+        geo = kernel_bytes(mt.ext, B, 0)
+        kc = mt.kp_cap
+        nq = int(q_off_h[-1])
+        # window search: query (16 B record + 32 B descriptor) in, the grid cells of the
+        # window and the candidates' keypoints + descriptors (L2-resident) counted once per
+        # frame, 16 B top-2 out per query
+        geo["k_proj_search"] = nq * (48 + 16) + B * (kc * (28 + 32) + 4 * 3073)
+        alg = geo.get(dom)
+        ach = alg / avg_s / 1e9 if alg else None
+        roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
+                "traffic": traffic_from_csv(args.traffic_csv, dom),
+                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg_s * 1000.0,
+                "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4)
+                                       for k, v in prof.items() if v[1]}}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = euroc_cpu_baseline(frames, [per[p] for p in range(P)], args.cpu_seconds)
+    if rank == 0:
+        out_line = {"metric": "frames/sec ORB extract + SearchByProjection vs 20-KF local map, "
+                              "EuRoC 752x480 mono",
+                    "value": B * args.steps * world / elapsed, "unit": "frames/sec",
+                    "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                    "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+                    "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+                    "config": {"workload": "euroc_mono_extract_search_local_points",
+                               "width": EUROC_W, "height": EUROC_H, "nfeatures": EUROC_NFEAT,
+                               "queries_per_frame": args.queries, "nnratio": 0.8, "th": 1.0,
+                               "frames_per_step_per_gpu": B, "distinct_frames": P,
+                               "parallelism": f"dp{world}"},
+                    "mean_keypoints": float(nkp.mean()),
+                    "mean_local_map_matches": float(counts.mean()),
+                    "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out_line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def euroc_cpu_baseline(frames, inputs, budget_s):
+    """The CPU restatement of the same per-frame work on one host core: extraction,
+    undistortion, grid and the projection search (Tracking runs them on one thread)."""
+    try:
+        import oracle
+        from oracle import matcher as om
+    except Exception:
+        return None
+    from my_orb_slam2_amd import synth
+    from my_orb_slam2_amd.features import (PROJ_FRAME_MAPPOINTS, FeatureSet,
+                                           assign_features_to_grid)
+    K4, distc = synth.EUROC_CAM
+    bounds = None
+    ox = oracle.OracleExtractor(EUROC_NFEAT, 1.2, 8, 20, 7)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        p = done % len(frames)
+        k, d = ox(frames[p])
+        un = om.undistort_keypoints(k, K4, distc)
+        if bounds is None:
+            bounds = om.image_bounds(K4, distc, EUROC_W, EUROC_H)
+        ku = k.copy()
+        ku["x"], ku["y"] = un[:, 0], un[:, 1]
+        g = assign_features_to_grid(ku, *bounds)
+        q, qd, cl = inputs[p]
+        om.search_by_projection(PROJ_FRAME_MAPPOINTS, FeatureSet(ku, d, None, None, g), q, qd,
+                                cl[:len(k)], None, nnratio=0.8)
+        done += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "frames/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} EuRoC-size synthetic frames: extraction + undistort + grid + "
+                      f"SearchByProjection restatement, one thread, {el:.1f} s",
+            "host_cpus": os.cpu_count()}
 
 
 # ---- matcher workloads (configs[3], configs[4]) ----------------------------------------------

@@ -33,12 +33,26 @@ orbx_status orbx_image_bounds(const float* K4, const float* dist, int32_t ndist,
 
 /* Frame::AssignFeaturesToGrid (Frame.cc:243-258, PosInGrid :407-417) on device keypoints:
  * grid_off (cols*rows + 1) and grid_feat (n; features outside the grid are dropped) in the
- * orbx_featureset layout (cell c = ix*rows + iy, indices ascending within a cell).
- * *n_in_grid (device, may be NULL) receives grid_off[cols*rows]. */
+ * orbx_featureset layout (cell c = ix*rows + iy, indices ascending within a cell). */
 orbx_status orbx_assign_grid_device(const orbx_keypoint* d_kps, int32_t n, int32_t cols,
                                     int32_t rows, float min_x, float min_y, float inv_w,
                                     float inv_h, int32_t* d_grid_off, int32_t* d_grid_feat,
                                     void* stream);
+
+/* Batched forms for frames laid out like orbx_batch_view (frame f's keypoints at
+ * d_kps + f*kp_stride, d_n[f] of them, device counts).  Grid: frame f's grid_off block at
+ * d_grid_off + f*(cols*rows+1), its grid_feat (frame-local indices) at
+ * d_grid_feat + f*kp_stride.  Undistort: slots past d_n[f] are left untouched. */
+orbx_status orbx_assign_grid_batch_device(const orbx_keypoint* d_kps, int32_t kp_stride,
+                                          const int32_t* d_n, int32_t batch, int32_t cols,
+                                          int32_t rows, float min_x, float min_y, float inv_w,
+                                          float inv_h, int32_t* d_grid_off,
+                                          int32_t* d_grid_feat, void* stream);
+orbx_status orbx_undistort_keypoints_batch_device(const float* K4, const float* dist,
+                                                  int32_t ndist, const orbx_keypoint* d_kps,
+                                                  int32_t kp_stride, const int32_t* d_n,
+                                                  int32_t batch, orbx_keypoint* d_kps_un,
+                                                  void* stream);
 
 /* Tracking's colour input (src/Tracking.cc:189-214): cv::cvtColor(*2GRAY) for 3- or 4-channel
  * 8-bit images, OpenCV 3.2's integer path RGB2Gray<uchar> (Y = (R*4899 + G*9617 + B*1868 +

@@ -216,6 +216,28 @@ orbx_status orbx_search_for_triangulation_batch_device(
     const float* scale, int32_t nlevels, int32_t only_stereo, const int32_t* d_job_off,
     int32_t* d_match12, int32_t* d_nmatches, void* stream);
 
+/* SearchByProjection over njobs frames at once — one Tracking::SearchLocalPoints
+ * (Tracking.cc:1297-1347, ORBmatcher.cc:41-136) per frame, or any other
+ * non-initialisation orbx_proj_mode, each job independent of the others.
+ * `frames` holds DEVICE pointers to the concatenation of the frames: keys / desc / u_right
+ * (u_right may be NULL) with frame j's features at [d_feat_off[j], d_feat_off[j+1]);
+ * grid_off = njobs blocks of grid_cols*grid_rows+1 entries (frame-local positions, frame j's
+ * block at j*(cells+1)); grid_feat with frame j's entries from d_grid_off[j] (frame-local
+ * feature indices).  Grid geometry (cols, rows, bounds, inverse cell sizes) is shared: one
+ * camera.  frames->n is ignored; max_feat (host) bounds every frame's size.
+ * Queries: d_qdesc / d_q with frame j's at [d_q_off[j], d_q_off[j+1]), nq in total.
+ * d_claimed: device, one byte per feature of the concatenation (already-matched features of
+ * the KEYFRAME / FUSE modes), or NULL.  inv_sigma2: HOST table of nlevels floats.
+ * Outputs (device): d_match[nq] frame-local feature index or -1, d_nmatches[njobs].
+ * Scratch belongs to the matcher: calls on one matcher must share `stream` or be serialised.
+ * A frame above max_feat gets no matches and is flagged for orbx_matcher_sync. */
+orbx_status orbx_search_by_projection_batch_device(
+    orbx_matcher* m, int32_t mode, const orbx_featureset* frames, int32_t njobs,
+    const int32_t* d_feat_off, const int32_t* d_grid_off, int32_t max_feat,
+    const uint8_t* d_claimed, const uint8_t* d_qdesc, const orbx_proj_query* d_q,
+    const int32_t* d_q_off, int32_t nq, const float* inv_sigma2, int32_t nlevels,
+    int32_t orb_dist, int32_t* d_match, int32_t* d_nmatches, void* stream);
+
 /* Waits for `stream` and returns ORBX_ERR_CAPACITY if a batched call on this matcher met a
  * keyframe above max_feat since the last sync (the flag is then cleared). */
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream);

@@ -83,6 +83,8 @@ SIGNATURES = {
     "orbx_search_by_bow_kf_frame_batch_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "orbx_search_for_triangulation_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp, _vp,
                                                         _vp, _i, _i, _vp, _vp, _vp, _vp]),
+    "orbx_search_by_projection_batch_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _i, _vp, _vp,
+                                                    _vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp]),
     "orbx_matcher_sync": (_i, [_vp, _vp]),
     "orbx_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp]),
     "orbx_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
@@ -104,6 +106,9 @@ SIGNATURES = {
     "orbx_undistort_keypoints_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp]),
     "orbx_image_bounds": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "orbx_assign_grid_device": (_i, [_vp, _i, _i, _i, _f, _f, _f, _f, _vp, _vp, _vp]),
+    "orbx_assign_grid_batch_device": (_i, [_vp, _i, _vp, _i, _i, _i, _f, _f, _f, _f, _vp, _vp,
+                                           _vp]),
+    "orbx_undistort_keypoints_batch_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i, _vp, _vp]),
     "orbx_cvt_color": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _i]),
     "orbx_cvt_color_device": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _vp]),
 }

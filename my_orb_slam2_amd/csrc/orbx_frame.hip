@@ -2,10 +2,10 @@
 //
 //   k_undistort    one lane per keypoint: cvUndistortPoints (OpenCV 3.2) in double, the
 //                  same __host__ __device__ routine the host uses for ComputeImageBounds
-//   k_grid_count / k_grid_fill   Frame::AssignFeaturesToGrid as a counting sort: cell of
-//                  every keypoint (PosInGrid, std::round half away from zero in float),
-//                  per-cell counts, an exclusive scan over the 3072 cells, then a stable
-//                  fill (each cell keeps ascending feature indices, as push_back does)
+//   k_grid         Frame::AssignFeaturesToGrid as a counting sort, one workgroup per frame:
+//                  cell of every keypoint (PosInGrid, std::round half away from zero in
+//                  float), per-cell LDS counts, a block scan over the 3072 cells, an atomic
+//                  fill, then each cell sorted by feature index (the push_back order)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -78,14 +78,21 @@ __device__ inline int grid_cell(const orbx_keypoint& kp, int cols, int rows, flo
     return px * rows + py;
 }
 
+// One workgroup per frame: frame f's keypoints at kps + f*kp_stride (n_f = d_n[f] when given,
+// else n), grid_off block at f*(cells+1), grid_feat at f*kp_stride.
 __global__ __launch_bounds__(1024) void k_grid(const orbx_keypoint* __restrict__ kps, int n,
+                                               const int32_t* __restrict__ d_n, int kp_stride,
                                                int cols, int rows, float min_x, float min_y,
                                                float inv_w, float inv_h,
-                                               int32_t* __restrict__ off,
-                                               int32_t* __restrict__ feat) {
-    // one workgroup: counts in LDS, scan, then a stable fill in index order
-    extern __shared__ int cnt[];   // cells + 32
-    const int ncell = cols * rows, tid = threadIdx.x;
+                                               int32_t* __restrict__ grid_off,
+                                               int32_t* __restrict__ grid_feat) {
+    extern __shared__ int cnt[];   // cells + 1024 (scan partials)
+    const int ncell = cols * rows, tid = threadIdx.x, f = blockIdx.x;
+    if (d_n) n = min(max(d_n[f], 0), kp_stride);
+    kps += (size_t)f * kp_stride;
+    int32_t* off = grid_off + (size_t)f * (ncell + 1);
+    int32_t* feat = grid_feat + (size_t)f * kp_stride;
+    int* part = cnt + ncell;
     for (int c = tid; c < ncell; c += 1024) cnt[c] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += 1024) {
@@ -93,36 +100,57 @@ __global__ __launch_bounds__(1024) void k_grid(const orbx_keypoint* __restrict__
         if (c >= 0) atomicAdd(&cnt[c], 1);
     }
     __syncthreads();
-    if (tid == 0) {   // exclusive scan over <= 3072 cells (once per frame)
-        int s = 0;
-        for (int c = 0; c < ncell; ++c) {
-            const int v = cnt[c];
-            cnt[c] = s;
-            off[c] = s;
-            s += v;
-        }
-        off[ncell] = s;
+    // exclusive scan: each thread sums a run of `per` cells, Hillis-Steele over the partials
+    const int per = (ncell + 1023) / 1024, c0 = min(tid * per, ncell), c1 = min(c0 + per, ncell);
+    int sum = 0;
+    for (int c = c0; c < c1; ++c) sum += cnt[c];
+    part[tid] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;
+    for (int c = c0; c < c1; ++c) {
+        const int v = cnt[c];
+        cnt[c] = run;   // becomes the fill cursor
+        off[c] = run;
+        run += v;
+    }
+    if (tid == 1023) off[ncell] = part[1023];
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int c = grid_cell(kps[i], cols, rows, min_x, min_y, inv_w, inv_h);
+        if (c >= 0) feat[atomicAdd(&cnt[c], 1)] = i;
     }
     __syncthreads();
-    // stable fill: features in index order, 1024 at a time; within a chunk, the rank of a
-    // feature among earlier features of the same cell comes from a ballot-free LDS pass
-    for (int base = 0; base < n; base += 1024) {
-        const int i = base + tid;
-        const int c = i < n ? grid_cell(kps[i], cols, rows, min_x, min_y, inv_w, inv_h) : -1;
-        // serialise by cell order inside the chunk with one thread per cell run: simple and
-        // deterministic — each thread counts earlier chunk members of its cell
-        __shared__ int cell_of[1024];
-        cell_of[tid] = c;
-        __syncthreads();
-        if (c >= 0) {
-            int r = 0;
-            for (int j = 0; j < tid; ++j) r += cell_of[j] == c;
-            feat[cnt[c] + r] = i;
+    // each cell ascending by feature index (the push_back order of Frame.cc:252-256)
+    for (int c = tid; c < ncell; c += 1024) {
+        const int b = off[c], e = cnt[c];
+        for (int k = b + 1; k < e; ++k) {
+            const int v = feat[k];
+            int j = k - 1;
+            while (j >= b && feat[j] > v) {
+                feat[j + 1] = feat[j];
+                --j;
+            }
+            feat[j + 1] = v;
         }
-        __syncthreads();
-        if (c >= 0) atomicAdd(&cnt[c], 1);
-        __syncthreads();
     }
+}
+
+__global__ __launch_bounds__(256) void k_undistort_batch(UndistParams P,
+                                                         const orbx_keypoint* in, int kp_stride,
+                                                         const int32_t* d_n,
+                                                         orbx_keypoint* out, int copy) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y;
+    if (i >= min(d_n[f], kp_stride)) return;
+    const size_t k = (size_t)f * kp_stride + i;
+    orbx_keypoint kp = in[k];
+    if (!copy) undistort_pt(P, kp.x, kp.y, kp.x, kp.y);
+    out[k] = kp;
 }
 
 // cvtColor(*2GRAY), OpenCV 3.2 RGB2Gray<uchar>: the three table terms summed with the
@@ -250,12 +278,45 @@ orbx_status orbx_assign_grid_device(const orbx_keypoint* d_kps, int32_t n, int32
                                     int32_t rows, float min_x, float min_y, float inv_w,
                                     float inv_h, int32_t* d_grid_off, int32_t* d_grid_feat,
                                     void* stream) {
-    if (n < 0 || cols <= 0 || rows <= 0 || (long long)cols * rows > 16384 - 32 || !d_grid_off ||
-        (n > 0 && (!d_kps || !d_grid_feat)))
+    if (n < 0 || cols <= 0 || rows <= 0 || (long long)cols * rows > 16384 - 1024 ||
+        !d_grid_off || (n > 0 && (!d_kps || !d_grid_feat)))
         return ORBX_ERR_INVALID;
-    const size_t lds = 4 * ((size_t)cols * rows + 32);   // <= 64 KB: no attribute needed
-    hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), lds, (hipStream_t)stream, d_kps, n, cols,
-                       rows, min_x, min_y, inv_w, inv_h, d_grid_off, d_grid_feat);
+    const size_t lds = 4 * ((size_t)cols * rows + 1024);   // <= 64 KB: no attribute needed
+    hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), lds, (hipStream_t)stream, d_kps, n,
+                       (const int32_t*)nullptr, n, cols, rows, min_x, min_y, inv_w, inv_h,
+                       d_grid_off, d_grid_feat);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_assign_grid_batch_device(const orbx_keypoint* d_kps, int32_t kp_stride,
+                                          const int32_t* d_n, int32_t batch, int32_t cols,
+                                          int32_t rows, float min_x, float min_y, float inv_w,
+                                          float inv_h, int32_t* d_grid_off,
+                                          int32_t* d_grid_feat, void* stream) {
+    if (batch < 0 || kp_stride < 0 || cols <= 0 || rows <= 0 ||
+        (long long)cols * rows > 16384 - 1024)
+        return ORBX_ERR_INVALID;
+    if (batch == 0) return ORBX_OK;
+    if (!d_kps || !d_n || !d_grid_off || !d_grid_feat) return ORBX_ERR_INVALID;
+    const size_t lds = 4 * ((size_t)cols * rows + 1024);
+    hipLaunchKernelGGL(k_grid, dim3(batch), dim3(1024), lds, (hipStream_t)stream, d_kps, 0, d_n,
+                       kp_stride, cols, rows, min_x, min_y, inv_w, inv_h, d_grid_off,
+                       d_grid_feat);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_undistort_keypoints_batch_device(const float* K4, const float* dist,
+                                                  int32_t ndist, const orbx_keypoint* d_kps,
+                                                  int32_t kp_stride, const int32_t* d_n,
+                                                  int32_t batch, orbx_keypoint* d_kps_un,
+                                                  void* stream) {
+    UndistParams P;
+    if (!make_params(K4, dist, ndist, P) || batch < 0 || kp_stride < 0) return ORBX_ERR_INVALID;
+    if (batch == 0 || kp_stride == 0) return ORBX_OK;
+    if (!d_kps || !d_n || !d_kps_un || batch > 65535) return ORBX_ERR_INVALID;
+    const int copy = dist[0] == 0.0f;
+    hipLaunchKernelGGL(k_undistort_batch, dim3((kp_stride + 255) / 256, batch), dim3(256), 0,
+                       (hipStream_t)stream, P, d_kps, kp_stride, d_n, d_kps_un, copy);
     return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
 }
 

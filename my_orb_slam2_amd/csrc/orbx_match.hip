@@ -459,13 +459,45 @@ struct InitDyn {    // :485 vMatchedDistance[i2] <= dist skips
 
 constexpr uint32_t POS_MASK = (1u << 23) - 1;
 
+// The target featureset of job j (see ProjLaunch).
+__device__ __forceinline__ orbx_featureset job_target(const ProjLaunch& g, int j) {
+    orbx_featureset T = g.T;
+    if (g.t_off) {
+        const int f0 = g.t_off[j];
+        T.n = g.t_off[j + 1] - f0;
+        T.keys += f0;
+        T.desc += 32 * (size_t)f0;
+        if (T.u_right) T.u_right += f0;
+        T.grid_off += (size_t)j * (T.grid_cols * T.grid_rows + 1);
+        T.grid_feat += g.g_off[j];
+    }
+    return T;
+}
+
+__device__ __forceinline__ int job_first_query(const ProjLaunch& g, int j) {
+    return g.q_off ? g.q_off[j] : 0;
+}
+__device__ __forceinline__ int job_end_query(const ProjLaunch& g, int j) {
+    return g.q_off ? g.q_off[j + 1] : g.nq;
+}
+// job of query qi: upper_bound(q_off, qi) - 1
+__device__ __forceinline__ int job_of_query(const ProjLaunch& g, int qi) {
+    if (!g.q_off) return 0;
+    int lo = 0, hi = g.njobs;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (g.q_off[mid] <= qi) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 // GetFeaturesInArea + the mode's candidate filters + DescriptorDistance, reduced to the
 // first two keys (distance << 23 | grid CSR position) in the reference's visiting order
 // (cell column ix, then row iy, then the cell's vector: exactly increasing CSR position).
 template <class Dyn>
-__device__ void window_top2(const ProjLaunch& g, const ModeInfo& mi, const orbx_proj_query& q,
-                            const Desc& qd, Dyn dyn, uint32_t& o1, uint32_t& o2) {
-    const orbx_featureset& T = g.T;
+__device__ void window_top2(const ProjLaunch& g, const orbx_featureset& T, const ModeInfo& mi,
+                            const orbx_proj_query& q, const Desc& qd, Dyn dyn, uint32_t& o1,
+                            uint32_t& o2) {
     const int lane = lane_id();
     o1 = o2 = INF;
     const float x = q.u, y = q.v, r = q.radius;
@@ -528,11 +560,11 @@ struct Cand {
     int i, d, lvl, bin;
 };
 
-__device__ __forceinline__ Cand decode_key(const ProjLaunch& g, const ModeInfo& mi, uint32_t k,
-                                           float qangle) {
+__device__ __forceinline__ Cand decode_key(const orbx_featureset& T, const ModeInfo& mi,
+                                           uint32_t k, float qangle) {
     if (k == INF) return {-1, 0, -1, 0};
-    const int i = g.T.grid_feat[k & POS_MASK];
-    const orbx_keypoint kp = g.T.keys[i];
+    const int i = T.grid_feat[k & POS_MASK];
+    const orbx_keypoint kp = T.keys[i];
     return {i, (int)(k >> 23), kp.octave, mi.rot ? rot_bin(qangle, kp.angle) : 0};
 }
 
@@ -553,24 +585,34 @@ __global__ __launch_bounds__(256) void k_proj_search(ProjLaunch g) {
         return;
     }
     const Desc qd = load_desc(g.qdesc, qi);
+    const orbx_featureset T = job_target(g, job_of_query(g, qi));
     uint32_t m1, m2;
-    window_top2(g, mi, q, qd, NoDyn{}, m1, m2);
+    window_top2(g, T, mi, q, qd, NoDyn{}, m1, m2);
     if (lane != 0) return;
     if (mi.greedy) {
-        const Cand c1 = decode_key(g, mi, m1, q.angle), c2 = decode_key(g, mi, m2, q.angle);
+        const Cand c1 = decode_key(T, mi, m1, q.angle), c2 = decode_key(T, mi, m2, q.angle);
         g.top2[qi] = make_int4(c1.i, c2.i, pack_cand(c1), pack_cand(c2));
     } else {
-        g.out[qi] = (m1 != INF && (int)(m1 >> 23) <= mi.th) ? g.T.grid_feat[m1 & POS_MASK] : -1;
+        g.out[qi] = (m1 != INF && (int)(m1 >> 23) <= mi.th) ? T.grid_feat[m1 & POS_MASK] : -1;
     }
 }
 
-// Sequential greedy replay in MapPoint order (one wave).
+// Sequential greedy replay in MapPoint order (one wave per job).
 __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
     extern __shared__ int lds[];
-    const int lane = lane_id();
+    const int lane = lane_id(), job = blockIdx.x;
     const ModeInfo mi = mode_info(g.mode, g.orb_dist);
     const bool init = g.mode == PROJ_INIT;
-    const int nT = g.T.n, nq = g.nq;
+    const orbx_featureset T = job_target(g, job);
+    const int q0 = job_first_query(g, job), q1 = job_end_query(g, job);
+    const int nT = T.n, nq = q1 - q0;
+    const uint8_t* claimed_in = g.claimed_in ? g.claimed_in + (g.t_off ? g.t_off[job] : 0) : nullptr;
+    if (nT > g.max_t) {   // the LDS was sized for max_t: flag the job, no matches
+        if (lane == 0) atomicOr(g.err, 1);
+        for (int i = q0 + lane; i < q1; i += 64) g.out[i] = -1;
+        if (lane < 32) g.hist[32 * job + lane] = 0;
+        return;
+    }
     int* hist = lds;                         // 32
     uint8_t* claimed = (uint8_t*)(lds + 32); // nT (claim modes)
     int* mdist = lds + 32;                   // nT (init): vMatchedDistance
@@ -581,14 +623,14 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
         for (int i = lane; i < nT; i += 64) { mdist[i] = INT_MAX; m21[i] = -1; }
         for (int i = lane; i < nq; i += 64) m12[i] = -1;
     } else {
-        for (int i = lane; i < nT; i += 64) claimed[i] = g.claimed_in ? (g.claimed_in[i] != 0) : 0;
+        for (int i = lane; i < nT; i += 64) claimed[i] = claimed_in ? (claimed_in[i] != 0) : 0;
     }
     __syncthreads();
     for (int qb = 0; qb < nq; qb += 64) {
         const int cnt = min(64, nq - qb);
-        const int4 s = (lane < cnt) ? g.top2[qb + lane] : make_int4(-1, -1, 0, 0);
+        const int4 s = (lane < cnt) ? g.top2[q0 + qb + lane] : make_int4(-1, -1, 0, 0);
         for (int t = 0; t < cnt; ++t) {
-            const int qi = qb + t;
+            const int qj = qb + t, qi = q0 + qj;   // job-local / global query index
             Cand b = {__builtin_amdgcn_readlane(s.x, t), 0, -1, 0};
             Cand c = {__builtin_amdgcn_readlane(s.y, t), 0, -1, 0};
             const int w1 = __builtin_amdgcn_readlane(s.z, t), w2 = __builtin_amdgcn_readlane(s.w, t);
@@ -607,10 +649,10 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
                 const orbx_proj_query q = g.q[qi];
                 const Desc qd = load_desc(g.qdesc, qi);
                 uint32_t m1, m2;
-                if (init) window_top2(g, mi, q, qd, InitDyn{mdist}, m1, m2);
-                else window_top2(g, mi, q, qd, ClaimDyn{claimed}, m1, m2);
-                b = decode_key(g, mi, m1, q.angle);
-                c = decode_key(g, mi, m2, q.angle);
+                if (init) window_top2(g, T, mi, q, qd, InitDyn{mdist}, m1, m2);
+                else window_top2(g, T, mi, q, qd, ClaimDyn{claimed}, m1, m2);
+                b = decode_key(T, mi, m1, q.angle);
+                c = decode_key(T, mi, m2, q.angle);
             }
             bool acc;
             if (g.mode == ORBX_PROJ_FRAME_MAPPOINTS) {   // :121-124
@@ -630,8 +672,8 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
                     if (acc) {   // :504-512 (re-assignment)
                         const int prev = m21[b.i];
                         if (prev >= 0) m12[prev] = -1;
-                        m12[qi] = b.i;
-                        m21[b.i] = qi;
+                        m12[qj] = b.i;
+                        m21[b.i] = qj;
                         mdist[b.i] = b.d;
                         g.out_bin[qi] = (int8_t)b.bin;
                         if (g.check_ori) hist[b.bin] += 1;
@@ -649,8 +691,8 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
     }
     __syncthreads();
     if (init)
-        for (int i = lane; i < nq; i += 64) g.out[i] = m12[i];
-    if (lane < 32) g.hist[lane] = hist[lane];
+        for (int i = lane; i < nq; i += 64) g.out[q0 + i] = m12[i];
+    if (lane < 32) g.hist[32 * job + lane] = hist[lane];
 }
 
 __global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
@@ -659,11 +701,13 @@ __global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
     const int tid = threadIdx.x;
     const ModeInfo mi = mode_info(g.mode, g.orb_dist);
     const bool filt = mi.rot && g.check_ori;
-    if (tid < 32) h[tid] = filt ? g.hist[tid] : 0;
+    const int job = blockIdx.x;
+    const int q0 = job_first_query(g, job), q1 = job_end_query(g, job);
+    if (tid < 32) h[tid] = filt ? g.hist[32 * job + tid] : 0;
     __syncthreads();
     const Top3 top = filt ? three_maxima(h) : Top3{-1, -1, -1};
     int cnt = 0;
-    for (int i = tid; i < g.nq; i += 256) {
+    for (int i = q0 + tid; i < q1; i += 256) {
         int r = g.out[i];
         if (r >= 0 && filt) {
             const int bin = g.out_bin[i];
@@ -675,7 +719,7 @@ __global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
         cnt += r >= 0;
     }
     const int tot = block_sum<4>(cnt, red);
-    if (tid == 0) g.nmatches[0] = tot;
+    if (tid == 0) g.nmatches[job] = tot;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -791,13 +835,14 @@ hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer) 
     if (err != hipSuccess) return err;
     if (proj_mode_greedy(a.mode)) {
         e = timer ? timer->start(st) : nullptr;
-        hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64),
-                           proj_resolve_lds_bytes(a.mode, a.T.n, a.nq), st, a);
+        // LDS per job: the largest target, and (init) the largest query list = nq bound
+        hipLaunchKernelGGL(k_proj_resolve, dim3(a.njobs), dim3(64),
+                           proj_resolve_lds_bytes(a.mode, a.max_t, a.nq), st, a);
         if (timer) timer->stop(ORBX_MK_PROJ_RESOLVE, e, st);
         err = hipGetLastError();
         if (err != hipSuccess) return err;
     }
-    hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_proj_finish, dim3(a.njobs), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

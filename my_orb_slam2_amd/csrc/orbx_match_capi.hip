@@ -23,7 +23,7 @@ using namespace orbx;
 struct orbx_matcher {
     orbx_matcher_params prm;
     hipStream_t stream = nullptr;
-    DevBuf d_in, d_out, d_aux;
+    DevBuf d_in, d_out, d_aux, d_proj;
     int* d_err = nullptr;
     std::vector<uint8_t> staging;
     KernelTimer timer;
@@ -287,6 +287,8 @@ orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
     ProjLaunch L{};
     L.mode = mode;
     L.T = dev_feat(T, ot, base);
+    L.njobs = 1;
+    L.max_t = T->n;
     L.qdesc = base + od;
     L.q = (const orbx_proj_query*)(base + oq);
     L.nq = nq;
@@ -347,6 +349,7 @@ orbx_status orbx_matcher_destroy(orbx_matcher* m) {
     m->d_in.release();
     m->d_out.release();
     m->d_aux.release();
+    m->d_proj.release();
     if (m->d_err) (void)hipFree(m->d_err);
     m->timer.destroy();
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -618,6 +621,71 @@ orbx_status orbx_search_for_triangulation_batch_device(
     hipEvent_t e = m->timer.start(st);
     if (!HIPOK(launch_triangulate(L, st))) return ORBX_ERR_DEVICE;
     m->timer.stop(ORBX_MK_TRIANGULATE, e, st);
+    return ORBX_OK;
+}
+
+orbx_status orbx_search_by_projection_batch_device(
+    orbx_matcher* m, int32_t mode, const orbx_featureset* frames, int32_t njobs,
+    const int32_t* d_feat_off, const int32_t* d_grid_off, int32_t max_feat,
+    const uint8_t* d_claimed, const uint8_t* d_qdesc, const orbx_proj_query* d_q,
+    const int32_t* d_q_off, int32_t nq, const float* inv_sigma2, int32_t nlevels,
+    int32_t orb_dist, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    if (!m || !frames || njobs < 0 || nq < 0 || nq > (1 << 24)) return ORBX_ERR_INVALID;
+    if (mode < 0 || mode >= ORBX_PROJ_MODE_COUNT) return ORBX_ERR_INVALID;
+    if (max_feat < 0 || max_feat > MAX_FEAT) return ORBX_ERR_INVALID;
+    if (mode == ORBX_PROJ_FUSE && (!inv_sigma2 || nlevels <= 0)) return ORBX_ERR_INVALID;
+    if (nlevels > MATCH_MAX_LEVELS) return ORBX_ERR_UNSUPPORTED;
+    if (frames->grid_cols <= 0 || frames->grid_rows <= 0 ||
+        (long long)frames->grid_cols * frames->grid_rows > (1 << 20))
+        return ORBX_ERR_INVALID;
+    if (njobs == 0) return ORBX_OK;
+    if (!d_feat_off || !d_grid_off || !d_q_off || !d_match || !d_nmatches || !frames->keys ||
+        !frames->desc || !frames->grid_off || !frames->grid_feat || (nq > 0 && (!d_qdesc || !d_q)))
+        return ORBX_ERR_INVALID;
+    if (((uintptr_t)frames->desc & 15) || ((uintptr_t)d_qdesc & 15)) return ORBX_ERR_INVALID;
+    if (proj_mode_greedy(mode) && proj_resolve_lds_bytes(mode, max_feat, 0) > MATCH_MAX_LDS)
+        return ORBX_ERR_UNSUPPORTED;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    hipStream_t st = (hipStream_t)stream;
+    // scratch: hist[32 * njobs] | top2[nq] | bins[nq]
+    const size_t o_top = align256(128 * (size_t)njobs), o_bin = align256(o_top + 16 * (size_t)nq),
+                 o_end = align256(o_bin + (size_t)nq);
+    if (!m->d_proj.ensure(o_end)) return ORBX_ERR_DEVICE;
+    uint8_t* sb = m->d_proj.as<uint8_t>();
+    ProjLaunch L{};
+    L.mode = mode;
+    L.T = *frames;
+    L.T.n = max_feat;
+    L.T.n_nodes = 0;
+    L.T.node_id = nullptr;
+    L.T.node_off = nullptr;
+    L.T.node_feat = nullptr;
+    L.njobs = njobs;
+    L.t_off = d_feat_off;
+    L.g_off = d_grid_off;
+    L.q_off = d_q_off;
+    L.max_t = max_feat;
+    L.qdesc = d_qdesc;
+    L.q = d_q;
+    L.nq = nq;
+    for (int l = 0; l < MATCH_MAX_LEVELS; ++l)
+        L.inv_sigma2[l] = (inv_sigma2 && l < nlevels) ? inv_sigma2[l] : 0.f;
+    L.orb_dist = orb_dist;
+    L.ratio = m->prm.nnratio;
+    L.check_ori = m->prm.check_orientation;
+    L.claimed_in = d_claimed;
+    L.out = d_match;
+    L.top2 = (int4*)(sb + o_top);
+    L.out_bin = (int8_t*)(sb + o_bin);
+    L.hist = (int32_t*)sb;
+    L.nmatches = d_nmatches;
+    L.err = m->d_err;
+    if (nq == 0) {   // every job: no queries, no matches
+        if (!HIPOK(hipMemsetAsync(d_nmatches, 0, 4 * (size_t)njobs, st))) return ORBX_ERR_DEVICE;
+        return ORBX_OK;
+    }
+    if (!HIPOK(launch_proj(L, st, &m->timer))) return ORBX_ERR_DEVICE;
     return ORBX_OK;
 }
 

@@ -42,10 +42,19 @@ struct TriLaunch {
     int* err;
 };
 
-// One projection search (modes of orbx_proj_mode plus PROJ_INIT).
+// Projection searches (modes of orbx_proj_mode plus PROJ_INIT) over njobs independent jobs
+// (frames).  With t_off == nullptr there is one job: target T, queries [0, nq).  Otherwise
+// job j's target is T's arrays offset by t_off[j] features (keys/desc/u_right/claimed) and
+// g_off[j] grid entries (grid_feat, job-local indices), with its own grid_off block of
+// cols*rows+1 entries; its queries are [q_off[j], q_off[j+1]).
 struct ProjLaunch {
     int mode;
     orbx_featureset T;           // device pointers
+    int njobs;
+    const int32_t* t_off;
+    const int32_t* g_off;
+    const int32_t* q_off;
+    int max_t;                   // largest target (LDS sizing of the resolve phase)
     const uint8_t* qdesc;
     const orbx_proj_query* q;
     int nq;
@@ -57,8 +66,8 @@ struct ProjLaunch {
     int32_t* out;                // nq
     int4* top2;                  // nq (greedy modes)
     int8_t* out_bin;             // nq
-    int32_t* hist;               // 32
-    int32_t* nmatches;           // 1
+    int32_t* hist;               // 32 per job
+    int32_t* nmatches;           // per job
     int* err;
 };
 

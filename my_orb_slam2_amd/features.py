@@ -203,6 +203,35 @@ def assign_grid_device(d_keys, n: int, min_x: float, max_x: float, min_y: float,
         float(inv_h), ptr(d_off), ptr(d_feat), ctypes.c_void_p(stream)))
 
 
+def assign_grid_batch_device(d_keys, kp_stride: int, d_n, batch: int, bounds, d_off, d_feat,
+                             cols: int = FRAME_GRID_COLS, rows: int = FRAME_GRID_ROWS,
+                             stream: int = 0):
+    """AssignFeaturesToGrid for `batch` frames laid out like orbx_batch_view (device
+    tensors): d_off [batch][cols*rows + 1], d_feat [batch][kp_stride].  bounds =
+    (min_x, max_x, min_y, max_y)."""
+    from ._lib import check, load, ptr
+    f32 = np.float32
+    min_x, max_x, min_y, max_y = (f32(b) for b in bounds)
+    inv_w = f32(cols) / f32(max_x - min_x)
+    inv_h = f32(rows) / f32(max_y - min_y)
+    check("orbx_assign_grid_batch_device", load().orbx_assign_grid_batch_device(
+        ptr(d_keys), int(kp_stride), ptr(d_n), int(batch), cols, rows, float(min_x),
+        float(min_y), float(inv_w), float(inv_h), ptr(d_off), ptr(d_feat),
+        ctypes.c_void_p(stream)))
+    return float(inv_w), float(inv_h)
+
+
+def undistort_keypoints_batch_device(K4, dist, d_keys, kp_stride: int, d_n, batch: int,
+                                     d_out, stream: int = 0):
+    """Frame::UndistortKeyPoints for `batch` frames laid out like orbx_batch_view."""
+    from ._lib import check, load, ptr
+    k = np.ascontiguousarray(K4, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    check("orbx_undistort_keypoints_batch_device", load().orbx_undistort_keypoints_batch_device(
+        ptr(k), ptr(d), len(d), ptr(d_keys), int(kp_stride), ptr(d_n), int(batch), ptr(d_out),
+        ctypes.c_void_p(stream)))
+
+
 def cvt_color_gray(img: np.ndarray, rgb: bool = False, device: int = 0) -> np.ndarray:
     """Tracking's colour conversion (src/Tracking.cc:189-214): cvtColor(*2GRAY) of an 8-bit
     3- or 4-channel image on the GPU (rgb=True for RGB/RGBA order, mbRGB)."""

@@ -236,6 +236,20 @@ class ORBmatcher:
                   ptr(epi), ptr(s2), ptr(sc), len(s2), int(only_stereo), ptr(job_off),
                   ptr(d_match), ptr(d_nmatches), ctypes.c_void_p(stream)))
 
+    def search_by_projection_batch_device(self, mode: int, frames: "DeviceFrameBatch", d_qdesc,
+                                          d_q, d_q_off, d_match, d_nmatches, d_claimed=None,
+                                          inv_sigma2=None, orb_dist: int = 0, stream=0):
+        """orbx_search_by_projection_batch_device: one projection search per frame of
+        `frames`, queries of frame j at [d_q_off[j], d_q_off[j+1]) (device tensors)."""
+        isg = None if inv_sigma2 is None else np.ascontiguousarray(inv_sigma2, np.float32)
+        nq = int(d_q.numel() * d_q.element_size() // PROJ_QUERY_DTYPE.itemsize)
+        check("orbx_search_by_projection_batch_device",
+              self._lib.orbx_search_by_projection_batch_device(
+                  self._h, int(mode), ctypes.byref(frames.c), frames.njobs, ptr(frames.feat_off),
+                  ptr(frames.grid_pos_off), frames.max_feat, ptr(d_claimed), ptr(d_qdesc),
+                  ptr(d_q), ptr(d_q_off), nq, ptr(isg), 0 if isg is None else len(isg),
+                  int(orb_dist), ptr(d_match), ptr(d_nmatches), ctypes.c_void_p(stream)))
+
     def sync(self, stream=0):
         check("orbx_matcher_sync", self._lib.orbx_matcher_sync(self._h, ctypes.c_void_p(stream)))
 
@@ -279,6 +293,55 @@ class DeviceFeatureSet:
             c.n_nodes = len(fv.node_id)
             c.node_id, c.node_off = self.node_id.data_ptr(), self.node_off.data_ptr()
             c.node_feat = self.node_feat.data_ptr()
+        self.c = c
+
+
+class DeviceFrameBatch:
+    """Frames (FeatureSets with grids of one camera) concatenated in device memory for
+    orbx_search_by_projection_batch_device."""
+
+    def __init__(self, featuresets, device):
+        import torch
+        from .features import FeatureSetC
+        fss = list(featuresets)
+        g0 = fss[0].grid
+        for fs in fss:
+            g = fs.grid
+            if (g.cols, g.rows, g.min_x, g.min_y, g.inv_w, g.inv_h) != (
+                    g0.cols, g0.rows, g0.min_x, g0.min_y, g0.inv_w, g0.inv_h):
+                raise ValueError("frames of one batch share the grid geometry")
+        self.njobs = len(fss)
+        n = np.array([fs.n for fs in fss], np.int64)
+        feat_off = np.zeros(len(fss) + 1, np.int32)
+        np.cumsum(n, out=feat_off[1:])
+        gn = np.array([len(fs.grid.feat) for fs in fss], np.int64)
+        gpos = np.zeros(len(fss) + 1, np.int32)
+        np.cumsum(gn, out=gpos[1:])
+        self.max_feat = int(n.max())
+
+        def t(a, dtype=None):
+            a = np.ascontiguousarray(a if dtype is None else a.astype(dtype))
+            b = a.view(np.uint8).reshape(-1) if a.size else np.zeros(16, np.uint8)
+            return torch.from_numpy(b.copy()).to(device)
+
+        self.keys = t(np.concatenate([fs.keys for fs in fss]))
+        self.desc = t(np.concatenate([fs.desc for fs in fss]))
+        self.u_right = t(np.concatenate([fs.u_right if fs.u_right is not None else
+                                         np.full(fs.n, -1.0, np.float32) for fs in fss]),
+                         np.float32)
+        self.grid_off = t(np.concatenate([fs.grid.off for fs in fss]), np.int32)
+        self.grid_feat = t(np.concatenate([fs.grid.feat for fs in fss]), np.int32)
+        self.feat_off = torch.from_numpy(feat_off).to(device)
+        self.grid_pos_off = torch.from_numpy(gpos).to(device)
+        self.h_feat_off = feat_off
+        c = FeatureSetC()
+        c.n = int(feat_off[-1])
+        c.keys, c.desc = self.keys.data_ptr(), self.desc.data_ptr()
+        c.u_right = self.u_right.data_ptr()
+        c.grid_cols, c.grid_rows = g0.cols, g0.rows
+        c.grid_off, c.grid_feat = self.grid_off.data_ptr(), self.grid_feat.data_ptr()
+        c.min_x, c.min_y, c.max_x, c.max_y = g0.min_x, g0.min_y, g0.max_x, g0.max_y
+        c.grid_inv_w, c.grid_inv_h = g0.inv_w, g0.inv_h
         self.c = c
 
 

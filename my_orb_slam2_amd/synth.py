@@ -237,6 +237,41 @@ def projection_queries(seed: int, f1, f2, truth, th: float = 3.0, nlevels: int =
     return q, desc
 
 
+def local_map_queries(seed: int, keys_un, desc, n_queries: int, width: int = 752,
+                      height: int = 480, th: float = 1.0, inlier_frac: float = 0.6,
+                      nlevels: int = 8, max_flip: int = 24):
+    """Projected local-map MapPoints for one frame (Tracking::SearchLocalPoints inputs,
+    Tracking.cc:1297-1347): `inlier_frac` of the queries are MapPoints observed as one of the
+    frame's features (projection within ~1 px of its undistorted position, descriptor with
+    0..max_flip flipped bits, predicted level = octave +-1), the rest land anywhere with
+    random descriptors.  radius = th * RadiusByViewingCos (2.5 or 4.0, Tracking.cc:1353-1359)
+    * scale[pred] as ORBmatcher.cc:75-80 computes it.  Returns (queries, descriptors)."""
+    from .features import PROJ_QUERY_DTYPE
+    rng = np.random.default_rng(seed)
+    scale, _, _ = scale_tables(nlevels)
+    n = len(keys_un)
+    q = np.zeros(n_queries, PROJ_QUERY_DTYPE)
+    nin = min(n, int(round(inlier_frac * n_queries)))
+    src = rng.choice(n, nin, replace=False) if nin else np.zeros(0, np.int64)
+    u = rng.uniform(0, width, n_queries)
+    v = rng.uniform(0, height, n_queries)
+    u[:nin] = keys_un["x"][src] + rng.normal(0, 0.7, nin)
+    v[:nin] = keys_un["y"][src] + rng.normal(0, 0.7, nin)
+    pred = rng.integers(0, nlevels, n_queries)
+    pred[:nin] = np.clip(keys_un["octave"][src] + rng.integers(-1, 2, nin), 0, nlevels - 1)
+    r = np.where(rng.random(n_queries) < 0.7, np.float32(2.5), np.float32(4.0))
+    d = rng.integers(0, 256, (n_queries, 32), dtype=np.uint8)
+    d[:nin] = _flip(rng, desc[src], rng.integers(0, max_flip + 1, nin))
+    perm = rng.permutation(n_queries)   # MapPoint order is unrelated to feature order
+    q["u"], q["v"] = u.astype(np.float32)[perm], v.astype(np.float32)[perm]
+    q["ur"] = -1.0
+    pred = pred.astype(np.int32)[perm]
+    q["pred_level"], q["min_level"], q["max_level"] = pred, pred - 1, pred
+    q["radius"] = (np.float32(th) * r[perm] * scale[pred]).astype(np.float32)
+    q["angle"] = 0.0
+    return q, np.ascontiguousarray(d[perm])
+
+
 def _rot(rng, max_deg):
     ax = rng.normal(size=3)
     ax /= np.linalg.norm(ax)

@@ -103,6 +103,49 @@ def test_grid_gpu(orbx_lib, gpu):
         np.testing.assert_array_equal(feat.cpu().numpy()[:len(g.feat)], g.feat)
 
 
+@pytest.mark.gpu
+def test_grid_and_undistort_batch_gpu(oracle_mod, orbx_lib, gpu):
+    """Batched undistortion + grid over frames laid out like orbx_batch_view (padded slots
+    with garbage, one empty frame, one dense frame with crowded cells)."""
+    import torch
+    from oracle import matcher as om
+    from my_orb_slam2_amd.features import (assign_grid_batch_device,
+                                           undistort_keypoints_batch_device)
+    K4, dist = synth.EUROC_CAM
+    stride, ns = 1500, [1000, 0, 1500, 37, 1200]
+    frames = []
+    allk = np.zeros(len(ns) * stride, KEYPOINT_DTYPE)
+    allk["x"] = 1e30   # padding garbage
+    for f, n in enumerate(ns):
+        k = _keys(n, seed=10 + f)
+        if f == 2:   # crowd one corner so cells hold many features
+            k["x"][:400] = np.random.default_rng(0).uniform(100, 112, 400)
+            k["y"][:400] = np.random.default_rng(1).uniform(200, 211, 400)
+        allk[f * stride:f * stride + n] = k
+        frames.append(k)
+    dk = torch.from_numpy(allk.view(np.uint8).copy()).to(gpu)
+    dn = torch.tensor(ns, dtype=torch.int32, device=gpu)
+    dun = torch.zeros_like(dk)
+    undistort_keypoints_batch_device(K4, dist, dk, stride, dn, len(ns), dun)
+    bounds = image_bounds(K4, dist, 752, 480)
+    off = torch.full((len(ns), 64 * 48 + 1), -7, dtype=torch.int32, device=gpu)
+    feat = torch.full((len(ns), stride), -7, dtype=torch.int32, device=gpu)
+    assign_grid_batch_device(dun, stride, dn, len(ns), bounds, off, feat)
+    torch.cuda.synchronize()
+    un = dun.cpu().numpy().view(KEYPOINT_DTYPE)
+    off, feat = off.cpu().numpy(), feat.cpu().numpy()
+    for f, (n, k) in enumerate(zip(ns, frames)):
+        want = om.undistort_keypoints(k, K4, dist) if n else np.zeros((0, 2), np.float32)
+        got = un[f * stride:f * stride + n]
+        np.testing.assert_array_equal(got["x"].view(np.int32), want[:, 0].view(np.int32))
+        np.testing.assert_array_equal(got["y"].view(np.int32), want[:, 1].view(np.int32))
+        ku = k.copy()
+        ku["x"], ku["y"] = want[:, 0], want[:, 1]
+        g = assign_features_to_grid(ku, *bounds)
+        np.testing.assert_array_equal(off[f], g.off)
+        np.testing.assert_array_equal(feat[f, :len(g.feat)], g.feat)
+
+
 @pytest.mark.parametrize("rgb,c", [(0, 3), (1, 3), (0, 4), (1, 4)])
 def test_cvt_gray_oracle_vs_numpy(rgb, c):
     from oracle import matcher as om

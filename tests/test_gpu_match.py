@@ -211,6 +211,82 @@ def test_batch_triangulation(oracle_mod, orbx_lib, gpu):
         np.testing.assert_array_equal(np.stack([idx1, seg[idx1]], 1), p_o)
 
 
+@pytest.mark.parametrize("mode", [PROJ_FRAME_MAPPOINTS, PROJ_LAST_FRAME, PROJ_KEYFRAME,
+                                  PROJ_FUSE, PROJ_KF_SCW])
+def test_batch_projection(oracle_mod, orbx_lib, gpu, mode):
+    """One projection search per frame over 10 frames of different sizes (one of them empty
+    of queries), against the oracle frame by frame."""
+    import torch
+    from oracle import matcher as om
+    from my_orb_slam2_amd.matcher import DeviceFrameBatch
+    _, _, isg = synth.scale_tables()
+    frames, qs, ds, cls, refs = [], [], [], [], []
+    for j in range(10):
+        f1, f2, t = synth.feature_pair(300 + j, n1=600 + 97 * j, n2=500 + 131 * j,
+                                       dup_frac=0.1)
+        q, d = synth.projection_queries(j, f1, f2, t, th=12.0,
+                                        mode_levels="frame" if mode in (0, 2, 3) else "kf")
+        if j == 4:
+            q, d = q[:0], d[:0]
+        cl = np.random.default_rng(j).random(f2.n) < 0.1
+        frames.append(f2)
+        qs.append(q)
+        ds.append(d)
+        cls.append(cl)
+        refs.append(om.search_by_projection(mode, f2, q, d, cl, isg, orb_dist=64, nnratio=0.8))
+    m = _matcher(0.8, True)
+    fb = DeviceFrameBatch(frames, gpu)
+    q_off = np.concatenate([[0], np.cumsum([len(q) for q in qs])]).astype(np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(gpu)
+    d_q, d_d = T(np.concatenate(qs)), T(np.concatenate(ds))
+    out = torch.full((int(q_off[-1]),), -7, dtype=torch.int32, device=gpu)
+    cnt = torch.full((len(frames),), -7, dtype=torch.int32, device=gpu)
+    m.search_by_projection_batch_device(mode, fb, d_d, d_q, torch.from_numpy(q_off).to(gpu),
+                                        out, cnt, T(np.concatenate(cls).astype(np.uint8)),
+                                        isg, orb_dist=64)
+    m.sync()
+    out, cnt = out.cpu().numpy(), cnt.cpu().numpy()
+    for j, (n_o, m_o) in enumerate(refs):
+        assert cnt[j] == n_o, j
+        np.testing.assert_array_equal(out[q_off[j]:q_off[j + 1]], m_o)
+    assert cnt.sum() > 0
+
+
+def test_batch_projection_capacity(oracle_mod, orbx_lib, gpu):
+    """A frame above the declared max_feat is flagged (ORBX_ERR_CAPACITY at sync) and gets no
+    matches; the others are unaffected."""
+    import torch
+    from oracle import matcher as om
+    from my_orb_slam2_amd._lib import OrbxError
+    from my_orb_slam2_amd.matcher import DeviceFrameBatch
+    frames, qs, ds = [], [], []
+    for j in range(3):
+        f1, f2, t = synth.feature_pair(400 + j, n1=500, n2=400 + 300 * j)
+        q, d = synth.projection_queries(j, f1, f2, t, th=5.0)
+        frames.append(f2)
+        qs.append(q)
+        ds.append(d)
+    m = _matcher(0.8, True)
+    fb = DeviceFrameBatch(frames, gpu)
+    fb.max_feat = frames[1].n
+    q_off = np.concatenate([[0], np.cumsum([len(q) for q in qs])]).astype(np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(gpu)
+    out = torch.full((int(q_off[-1]),), -7, dtype=torch.int32, device=gpu)
+    cnt = torch.full((3,), -7, dtype=torch.int32, device=gpu)
+    m.search_by_projection_batch_device(PROJ_FRAME_MAPPOINTS, fb, T(np.concatenate(ds)),
+                                        T(np.concatenate(qs)), torch.from_numpy(q_off).to(gpu),
+                                        out, cnt, orb_dist=64)
+    with pytest.raises(OrbxError):
+        m.sync()
+    out, cnt = out.cpu().numpy(), cnt.cpu().numpy()
+    assert cnt[2] == 0 and (out[q_off[2]:] == -1).all()
+    for j in range(2):
+        n_o, m_o = om.search_by_projection(PROJ_FRAME_MAPPOINTS, frames[j], qs[j], ds[j],
+                                           None, None, orb_dist=64, nnratio=0.8)
+        assert cnt[j] == n_o
+        np.testing.assert_array_equal(out[q_off[j]:q_off[j + 1]], m_o)
+
+
 def test_distinctive_descriptors(oracle_mod, orbx_lib, gpu):
     from oracle import matcher as om
     from test_oracle_match import _distinctive_case
