@@ -494,12 +494,26 @@ __device__ __forceinline__ int job_of_query(const ProjLaunch& g, int qi) {
 // GetFeaturesInArea + the mode's candidate filters + DescriptorDistance, reduced to the
 // first two keys (distance << 23 | grid CSR position) in the reference's visiting order
 // (cell column ix, then row iy, then the cell's vector: exactly increasing CSR position).
-template <class Dyn>
-__device__ void window_top2(const ProjLaunch& g, const orbx_featureset& T, const ModeInfo& mi,
-                            const orbx_proj_query& q, const Desc& qd, Dyn dyn, uint32_t& o1,
-                            uint32_t& o2) {
-    const int lane = lane_id();
-    o1 = o2 = INF;
+// A group of G lanes (16: one DPP row, or the whole wave) scans one query's window.
+template <int G>
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t v) {
+    if constexpr (G == 64) {
+        return wave_min_u32(v);
+    } else {
+        static_assert(G == 16, "groups are DPP rows or waves");
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, true));
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, true));
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xF, 0xF, true));
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, true));
+        return v;
+    }
+}
+
+template <int G, class Dyn, class Sink>
+__device__ __forceinline__ void window_scan(const ProjLaunch& g, const orbx_featureset& T,
+                                            const ModeInfo& mi, const orbx_proj_query& q,
+                                            const Desc& qd, Dyn dyn, Sink& sink) {
+    const int lane = lane_id() & (G - 1);
     const float x = q.u, y = q.v, r = q.radius;
     const int nMinCellX = max(0, x86_int(floorf((x - T.min_x - r) * T.grid_inv_w)));
     if (nMinCellX >= T.grid_cols) return;
@@ -510,11 +524,10 @@ __device__ void window_top2(const ProjLaunch& g, const orbx_featureset& T, const
     const int nMaxCellY = min(T.grid_rows - 1, x86_int(ceilf((y - T.min_y + r) * T.grid_inv_h)));
     if (nMaxCellY < 0) return;
     const bool checkLevels = mi.frame_grid && ((q.min_level > 0) || (q.max_level >= 0));
-    uint32_t k1 = INF, k2 = INF;
     for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
         const int p0 = T.grid_off[ix * T.grid_rows + nMinCellY];
         const int p1 = T.grid_off[ix * T.grid_rows + nMaxCellY + 1];
-        for (int base = p0; base < p1; base += 64) {
+        for (int base = p0; base < p1; base += G) {
             const int p = base + lane;
             if (p >= p1) continue;
             const int i = T.grid_feat[p];
@@ -547,13 +560,72 @@ __device__ void window_top2(const ProjLaunch& g, const orbx_featureset& T, const
             const int d = hamming(qd, load_desc(T.desc, i));
             if (mi.init256 && d >= 256) continue;
             if (!dyn(i, d)) continue;
-            const uint32_t key = (uint32_t)d << 23 | (uint32_t)p;
-            if (key < k1) { k2 = k1; k1 = key; }
-            else if (key < k2) { k2 = key; }
+            sink((uint32_t)d << 23 | (uint32_t)p);
         }
     }
-    o1 = wave_min_u32(k1);
-    o2 = wave_min_u32(k1 == o1 ? k2 : k1);
+}
+
+struct Top2Sink {
+    uint32_t k1 = INF, k2 = INF;
+    __device__ void operator()(uint32_t key) {
+        if (key < k1) { k2 = k1; k1 = key; }
+        else if (key < k2) { k2 = key; }
+    }
+};
+
+// The group-wide two smallest keys of the window (INF when absent).
+template <int G = 64, class Dyn>
+__device__ void window_top2(const ProjLaunch& g, const orbx_featureset& T, const ModeInfo& mi,
+                            const orbx_proj_query& q, const Desc& qd, Dyn dyn, uint32_t& o1,
+                            uint32_t& o2) {
+    Top2Sink t;
+    window_scan<G>(g, T, mi, q, qd, dyn, t);
+    o1 = group_min_u32<G>(t.k1);
+    o2 = group_min_u32<G>(t.k1 == o1 ? t.k2 : t.k1);
+}
+
+// Lane-local sorted PROJ_K smallest keys (branch-free insertion).
+struct TopKSink {
+    uint32_t k[PROJ_K];
+    __device__ TopKSink() {
+#pragma unroll
+        for (int j = 0; j < PROJ_K; ++j) k[j] = INF;
+    }
+    __device__ void operator()(uint32_t key) {
+        uint32_t x = key;
+#pragma unroll
+        for (int j = 0; j < PROJ_K; ++j) {
+            const uint32_t lo = min(k[j], x);
+            x = max(k[j], x);
+            k[j] = lo;
+        }
+    }
+};
+
+// The group-wide PROJ_K smallest keys: group lane r < count holds the r-th; more = keys
+// beyond them.
+template <int G, class Dyn>
+__device__ void window_topk(const ProjLaunch& g, const orbx_featureset& T, const ModeInfo& mi,
+                            const orbx_proj_query& q, const Desc& qd, Dyn dyn, uint32_t& mine,
+                            int& count, bool& more) {
+    TopKSink t;
+    window_scan<G>(g, T, mi, q, qd, dyn, t);
+    const int lane = lane_id() & (G - 1);
+    mine = INF;
+    count = 0;
+    more = false;
+    for (int r = 0; r < PROJ_K; ++r) {
+        const uint32_t m = group_min_u32<G>(t.k[0]);
+        if (m == INF) return;
+        if (lane == r) mine = m;
+        ++count;
+        if (t.k[0] == m) {   // keys are unique (CSR position): one lane pops its head
+#pragma unroll
+            for (int j = 0; j < PROJ_K - 1; ++j) t.k[j] = t.k[j + 1];
+            t.k[PROJ_K - 1] = INF;
+        }
+    }
+    more = group_min_u32<G>(t.k[0]) != INF;
 }
 
 struct Cand {
@@ -573,21 +645,43 @@ __device__ __forceinline__ int pack_cand(const Cand& c) {
 }
 
 __global__ __launch_bounds__(256) void k_proj_search(ProjLaunch g) {
-    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+    // one 16-lane group (a DPP row) per query, 16 queries per block
+    constexpr int G = 16;
+    const int qi = blockIdx.x * (256 / G) + (threadIdx.x / G), lane = lane_id() & (G - 1);
     if (qi >= g.nq) return;
     const ModeInfo mi = mode_info(g.mode, g.orb_dist);
     const orbx_proj_query q = g.q[qi];
     if (!(q.radius >= 0)) {
         if (lane == 0) {
-            if (mi.greedy) g.top2[qi] = make_int4(-1, -1, 0, 0);
+            if (mi.greedy && g.mode != PROJ_INIT) g.ncand[qi] = 0;
+            else if (mi.greedy) g.top2[qi] = make_int4(-1, -1, 0, 0);
             else g.out[qi] = -1;
         }
         return;
     }
     const Desc qd = load_desc(g.qdesc, qi);
-    const orbx_featureset T = job_target(g, job_of_query(g, qi));
+    const int job = job_of_query(g, qi);
+    const orbx_featureset T = job_target(g, job);
     uint32_t m1, m2;
-    window_top2(g, T, mi, q, qd, NoDyn{}, m1, m2);
+    if (mi.greedy && g.mode != PROJ_INIT) {
+        // claim modes: the PROJ_K best candidates, sorted, for the replay.  Features claimed
+        // before the call are out for every query and are filtered here.
+        uint32_t mine;
+        int count;
+        bool more;
+        if (g.claimed_in)
+            window_topk<G>(g, T, mi, q, qd, ClaimDyn{g.claimed_in + (g.t_off ? g.t_off[job] : 0)},
+                        mine, count, more);
+        else
+            window_topk<G>(g, T, mi, q, qd, NoDyn{}, mine, count, more);
+        if (lane < PROJ_K) {
+            const Cand c = decode_key(T, mi, mine, q.angle);
+            g.cand[(size_t)qi * PROJ_K + lane] = make_int2(c.i, pack_cand(c));
+        }
+        if (lane == 0) g.ncand[qi] = more ? PROJ_K + 1 : count;
+        return;
+    }
+    window_top2<G>(g, T, mi, q, qd, NoDyn{}, m1, m2);
     if (lane != 0) return;
     if (mi.greedy) {
         const Cand c1 = decode_key(T, mi, m1, q.angle), c2 = decode_key(T, mi, m2, q.angle);
@@ -597,7 +691,12 @@ __global__ __launch_bounds__(256) void k_proj_search(ProjLaunch g) {
     }
 }
 
-// Sequential greedy replay in MapPoint order (one wave per job).
+// Claim-mode replays keep an owner word per target feature when it fits in the LDS.
+__host__ __device__ inline bool proj_resolve_parallel(int max_t) {
+    return 4 * 32 + 5 * (size_t)max_t + 16 <= MATCH_MAX_LDS;
+}
+
+// Greedy replay in MapPoint order (one wave per job).
 __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
     extern __shared__ int lds[];
     const int lane = lane_id(), job = blockIdx.x;
@@ -614,7 +713,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
         return;
     }
     int* hist = lds;                         // 32
-    uint8_t* claimed = (uint8_t*)(lds + 32); // nT (claim modes)
+    const bool par = proj_resolve_parallel(g.max_t);
+    int* owner = lds + 32;                   // nT (claim modes, par): earliest acceptor lane
+    uint8_t* claimed = (uint8_t*)(lds + 32 + (par ? g.max_t : 0));   // nT (claim modes)
     int* mdist = lds + 32;                   // nT (init): vMatchedDistance
     int* m21 = mdist + nT;                   // nT (init): vnMatches21
     int* m12 = m21 + nT;                     // nq (init): vnMatches12
@@ -624,9 +725,114 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
         for (int i = lane; i < nq; i += 64) m12[i] = -1;
     } else {
         for (int i = lane; i < nT; i += 64) claimed[i] = claimed_in ? (claimed_in[i] != 0) : 0;
+        if (par)
+            for (int i = lane; i < nT; i += 64) owner[i] = 64;
     }
     __syncthreads();
-    for (int qb = 0; qb < nq; qb += 64) {
+    for (int qb = 0; qb < nq && !init; qb += 64) {
+        // Claim modes, 64 queries at a time.  Lane t holds query t's list of its PROJ_K best
+        // candidates (sorted by key, pre-claimed features already out).  Each round every
+        // pending lane decides against the current claims; a lane whose best or second is
+        // also accepted by an earlier pending lane (owner[] holds the earliest acceptor), or
+        // that follows a lane needing a full re-scan, waits for the next round.  The lanes
+        // before the first waiting one decide exactly as the sequential loop would, and
+        // commit together.  Without the owner array (large targets) one lane per round.
+        const int cnt = min(64, nq - qb);
+        const int qi = q0 + qb + lane;
+        const bool mine = lane < cnt;
+        const int nc = mine ? g.ncand[qi] : 0;
+        const int nv = min(nc, PROJ_K);
+        int2 L[PROJ_K];
+        {
+            const int4* src = (const int4*)(g.cand + (size_t)(mine ? qi : q0) * PROJ_K);
+#pragma unroll
+            for (int k = 0; k < PROJ_K / 2; ++k) {
+                const int4 v = (2 * k < nv) ? src[k] : make_int4(-1, 0, -1, 0);
+                L[2 * k] = make_int2(v.x, v.y);
+                L[2 * k + 1] = make_int2(v.z, v.w);
+            }
+        }
+        int res = -1, rbin = 0;
+        int start = 0;
+        while (start < cnt) {
+            Cand b = {-1, 0, -1, 0}, c = {-1, 0, -1, 0};
+            int nfree = 0;
+#pragma unroll
+            for (int k = 0; k < PROJ_K; ++k) {
+                const bool fr = k < nv && claimed[max(L[k].x, 0)] == 0;
+                const Cand x = {L[k].x, L[k].y & 0x1FF, (L[k].y >> 9) & 0xF, (L[k].y >> 13) & 0x1F};
+                if (fr && nfree == 0) b = x;
+                else if (fr && nfree == 1) c = x;
+                nfree += fr;
+            }
+            const bool act = lane >= start && lane < cnt;
+            const bool rescan = act && nfree < 2 && nc > PROJ_K;
+            bool acc;
+            if (g.mode == ORBX_PROJ_FRAME_MAPPOINTS) {   // :121-124
+                const int bestDist = b.i >= 0 ? b.d : 256, bestLevel = b.i >= 0 ? b.lvl : -1;
+                const int bestDist2 = c.i >= 0 ? c.d : 256, bestLevel2 = c.i >= 0 ? c.lvl : -1;
+                acc = bestDist <= TH_HIGH &&
+                      !(bestLevel == bestLevel2 && (float)bestDist > g.ratio * (float)bestDist2);
+            } else {
+                acc = b.i >= 0 && b.d <= mi.th;
+            }
+            acc = acc && act && !rescan;
+            int f = start + 1;
+            if (par) {
+                if (acc) atomicMin(&owner[b.i], lane);
+                bool wait = rescan && lane > start;
+                if (act && lane > start) {
+                    if (b.i >= 0 && owner[b.i] < lane) wait = true;
+                    if (c.i >= 0 && owner[c.i] < lane) wait = true;
+                }
+                if (acc) owner[b.i] = 64;
+                const uint64_t w = __ballot(wait);
+                f = w ? (int)__builtin_ctzll(w) : cnt;
+            }
+            if ((__ballot(rescan) >> start) & 1) {
+                // the first pending query's list ran out: re-scan its window, alone
+                const int qs = q0 + qb + start;
+                const orbx_proj_query q = g.q[qs];
+                const Desc qd = load_desc(g.qdesc, qs);
+                uint32_t m1, m2;
+                window_top2(g, T, mi, q, qd, ClaimDyn{claimed}, m1, m2);
+                const Cand rb = decode_key(T, mi, m1, q.angle), rc = decode_key(T, mi, m2, q.angle);
+                bool racc;
+                if (g.mode == ORBX_PROJ_FRAME_MAPPOINTS) {
+                    const int bestDist = rb.i >= 0 ? rb.d : 256, bestLevel = rb.i >= 0 ? rb.lvl : -1;
+                    const int bestDist2 = rc.i >= 0 ? rc.d : 256, bestLevel2 = rc.i >= 0 ? rc.lvl : -1;
+                    racc = bestDist <= TH_HIGH &&
+                           !(bestLevel == bestLevel2 && (float)bestDist > g.ratio * (float)bestDist2);
+                } else {
+                    racc = rb.i >= 0 && rb.d <= mi.th;
+                }
+                if (lane == start) {
+                    res = racc ? rb.i : -1;
+                    if (racc) {
+                        claimed[rb.i] = 1;
+                        rbin = rb.bin;
+                        if (mi.rot && g.check_ori) atomicAdd(&hist[rb.bin], 1);
+                    }
+                }
+                ++start;
+                continue;
+            }
+            if (lane >= start && lane < f) {
+                res = acc ? b.i : -1;
+                if (acc) {
+                    claimed[b.i] = 1;
+                    rbin = b.bin;
+                    if (mi.rot && g.check_ori) atomicAdd(&hist[b.bin], 1);
+                }
+            }
+            start = f;
+        }
+        if (mine) {
+            g.out[qi] = res;
+            if (res >= 0) g.out_bin[qi] = (int8_t)rbin;
+        }
+    }
+    for (int qb = 0; qb < nq && init; qb += 64) {
         const int cnt = min(64, nq - qb);
         const int4 s = (lane < cnt) ? g.top2[q0 + qb + lane] : make_int4(-1, -1, 0, 0);
         for (int t = 0; t < cnt; ++t) {
@@ -823,13 +1029,13 @@ hipError_t launch_triangulate(const TriLaunch& a, hipStream_t st) {
 
 size_t proj_resolve_lds_bytes(int mode, int n_target, int nq) {
     if (mode == PROJ_INIT) return 4 * (32 + 2 * (size_t)n_target + (size_t)nq);
-    return 4 * 32 + (size_t)n_target + 16;
+    return 4 * 32 + (proj_resolve_parallel(n_target) ? 5 : 1) * (size_t)n_target + 16;
 }
 
 hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer) {
     if (a.nq <= 0) return hipSuccess;
     hipEvent_t e = timer ? timer->start(st) : nullptr;
-    hipLaunchKernelGGL(k_proj_search, dim3((a.nq + 3) / 4), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_proj_search, dim3((a.nq + 15) / 16), dim3(256), 0, st, a);
     if (timer) timer->stop(ORBX_MK_PROJ_SEARCH, e, st);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;

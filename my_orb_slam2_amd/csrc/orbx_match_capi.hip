@@ -277,10 +277,12 @@ orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
     if (claimed) oc = P.add(claimed, (size_t)T->n);
     orbx_status s = upload(m);
     if (s != ORBX_OK) return s;
-    // outputs: nmatches(64 ints) | out[nq] | hist[32] | top2[nq] | bins[nq]
+    // outputs: nmatches(64 ints) | out[nq] | hist[32] | top2[nq] | bins[nq] | cand | ncand
     const size_t o_out = 256, o_hist = align256(o_out + 4 * (size_t)nq),
                  o_top = align256(o_hist + 128), o_bin = align256(o_top + 16 * (size_t)nq),
-                 o_end = align256(o_bin + (size_t)nq);
+                 o_cand = align256(o_bin + (size_t)nq),
+                 o_nc = align256(o_cand + 8 * PROJ_K * (size_t)nq),
+                 o_end = align256(o_nc + 4 * (size_t)nq);
     if (!m->d_out.ensure(o_end)) return ORBX_ERR_DEVICE;
     uint8_t* base = m->d_in.as<uint8_t>();
     uint8_t* ob = m->d_out.as<uint8_t>();
@@ -300,6 +302,8 @@ orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
     L.claimed_in = claimed ? base + oc : nullptr;
     L.out = (int32_t*)(ob + o_out);
     L.top2 = (int4*)(ob + o_top);
+    L.cand = (int2*)(ob + o_cand);
+    L.ncand = (int32_t*)(ob + o_nc);
     L.out_bin = (int8_t*)(ob + o_bin);
     L.hist = (int32_t*)(ob + o_hist);
     L.nmatches = (int32_t*)ob;
@@ -648,9 +652,11 @@ orbx_status orbx_search_by_projection_batch_device(
     std::lock_guard<std::mutex> lk(m->mu);
     if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
     hipStream_t st = (hipStream_t)stream;
-    // scratch: hist[32 * njobs] | top2[nq] | bins[nq]
+    // scratch: hist[32 * njobs] | top2[nq] | bins[nq] | cand[nq * PROJ_K] | ncand[nq]
     const size_t o_top = align256(128 * (size_t)njobs), o_bin = align256(o_top + 16 * (size_t)nq),
-                 o_end = align256(o_bin + (size_t)nq);
+                 o_cand = align256(o_bin + (size_t)nq),
+                 o_nc = align256(o_cand + 8 * PROJ_K * (size_t)nq),
+                 o_end = align256(o_nc + 4 * (size_t)nq);
     if (!m->d_proj.ensure(o_end)) return ORBX_ERR_DEVICE;
     uint8_t* sb = m->d_proj.as<uint8_t>();
     ProjLaunch L{};
@@ -677,6 +683,8 @@ orbx_status orbx_search_by_projection_batch_device(
     L.claimed_in = d_claimed;
     L.out = d_match;
     L.top2 = (int4*)(sb + o_top);
+    L.cand = (int2*)(sb + o_cand);
+    L.ncand = (int32_t*)(sb + o_nc);
     L.out_bin = (int8_t*)(sb + o_bin);
     L.hist = (int32_t*)sb;
     L.nmatches = d_nmatches;

@@ -9,6 +9,7 @@ namespace orbx {
 
 // Internal projection mode after the public ones: SearchForInitialization (:446-561).
 constexpr int PROJ_INIT = ORBX_PROJ_MODE_COUNT;
+constexpr int PROJ_K = 8;             // candidate list length of the claim-mode replay
 constexpr int MATCH_MAX_LEVELS = 16;
 
 // SearchByBoW over jobs: job j pairs keyframe (a_fixed ? 0 : j) of A with keyframe
@@ -64,7 +65,9 @@ struct ProjLaunch {
     int check_ori;
     const uint8_t* claimed_in;   // may be null
     int32_t* out;                // nq
-    int4* top2;                  // nq (greedy modes)
+    int4* top2;                  // nq (PROJ_INIT: static best and second)
+    int2* cand;                  // nq x PROJ_K (claim modes: sorted candidate lists)
+    int32_t* ncand;              // nq (list length; PROJ_K + 1 = truncated)
     int8_t* out_bin;             // nq
     int32_t* hist;               // 32 per job
     int32_t* nmatches;           // per job

@@ -89,6 +89,21 @@ def test_projection(oracle_mod, orbx_lib, gpu, mode, seed, th):
     np.testing.assert_array_equal(m_g, m_o)
 
 
+@pytest.mark.parametrize("mode", [PROJ_FRAME_MAPPOINTS, PROJ_KEYFRAME])
+def test_projection_large_target(oracle_mod, orbx_lib, gpu, mode):
+    """A target of 32000 features: the claim replay runs without the per-feature owner
+    words (one query per round), and dense windows overflow the 8-candidate lists."""
+    from oracle import matcher as om
+    f1, f2, t = synth.feature_pair(77, n1=3000, n2=32000, dup_frac=0.1)
+    q, d = synth.projection_queries(5, f1, f2, t, th=6.0)
+    claimed = np.random.default_rng(5).random(f2.n) < 0.1
+    m = _matcher(0.8, True)
+    n_g, m_g = m.search_by_projection(mode, f2, q, d, claimed, orb_dist=64)
+    n_o, m_o = om.search_by_projection(mode, f2, q, d, claimed, None, orb_dist=64, nnratio=0.8)
+    assert n_g == n_o and n_o > 0
+    np.testing.assert_array_equal(m_g, m_o)
+
+
 def test_sim3(oracle_mod, orbx_lib, gpu):
     from oracle import matcher as om
     f1, f2, t = synth.feature_pair(60, n1=1000, n2=1000)
