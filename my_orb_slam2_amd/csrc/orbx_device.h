@@ -68,30 +68,37 @@ namespace orbx {
 
 // Stage a rows x ndw-dword window (row r at gsrc + r*gpitch, 4-byte aligned rows) into LDS
 // (row r at lds + r*lpitch_dw dwords).  Each thread issues up to 8 loads before its first
-// LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.  Element
-// (row, col) indices advance by NT per step incrementally: one division per thread, none
-// per element.
+// LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.  The
+// element position, its 32-bit source offset and its LDS index advance by NT elements
+// incrementally: one division per thread, no multiply per element (a 64-bit or 32-bit
+// v_mul is a quarter-rate instruction).
 template <int NT>
 __device__ __forceinline__ void stage_dwords(const uint8_t* __restrict__ gsrc, size_t gpitch,
                                              int rows, int ndw, uint32_t* lds, int lpitch_dw,
                                              int tid) {
     const int n = rows * ndw;
     if (n <= 0) return;
+    const uint32_t gp = (uint32_t)gpitch;
     const int dr = NT / ndw, dc = NT - dr * ndw;
-    int r = tid / ndw, c = tid - (tid / ndw) * ndw;
+    int r = tid / ndw, c = tid - r * ndw;
+    uint32_t go = (uint32_t)r * gp + 4u * (uint32_t)c;
+    int lo = r * lpitch_dw + c;
+    const uint32_t gstep = (uint32_t)dr * gp + 4u * (uint32_t)dc, gwrap = gp - 4u * (uint32_t)ndw;
+    const int lstep = dr * lpitch_dw + dc, lwrap = lpitch_dw - ndw;
+    const uint32_t glast = (uint32_t)(rows - 1) * gp + 4u * (uint32_t)(ndw - 1);
     for (int base = 0; base < n; base += NT * 8) {
         uint32_t v[8];
         int at[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            // unconditional loads (index clamped): a guarded load becomes a branch + vmcnt(0)
+            // unconditional loads (offset clamped): a guarded load becomes a branch + vmcnt(0)
             const bool in = base + k * NT + tid < n;
-            const int ra = in ? r : rows - 1, ca = in ? c : ndw - 1;
-            v[k] = *(const uint32_t*)(gsrc + (size_t)ra * gpitch + 4 * ca);
-            at[k] = in ? ra * lpitch_dw + ca : -1;
+            v[k] = *(const uint32_t*)(gsrc + (in ? go : glast));
+            at[k] = in ? lo : -1;
             c += dc;
-            r += dr;
-            if (c >= ndw) { c -= ndw; ++r; }
+            go += gstep;
+            lo += lstep;
+            if (c >= ndw) { c -= ndw; go += gwrap; lo += lwrap; }
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
@@ -106,20 +113,26 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, si
                                             int tid) {
     const int n = rows * cols;
     if (n <= 0) return;
+    const uint32_t gp = (uint32_t)gpitch;
     const int dr = NT / cols, dc = NT - dr * cols;
-    int r = tid / cols, c = tid - (tid / cols) * cols;
+    int r = tid / cols, c = tid - r * cols;
+    uint32_t go = (uint32_t)r * gp + (uint32_t)c;
+    int lo = r * lpitch + c;
+    const uint32_t gstep = (uint32_t)dr * gp + (uint32_t)dc, gwrap = gp - (uint32_t)cols;
+    const int lstep = dr * lpitch + dc, lwrap = lpitch - cols;
+    const uint32_t glast = (uint32_t)(rows - 1) * gp + (uint32_t)(cols - 1);
     for (int base = 0; base < n; base += NT * 16) {
         uint8_t v[16];
         int at[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const bool in = base + k * NT + tid < n;
-            const int ra = in ? r : rows - 1, ca = in ? c : cols - 1;
-            v[k] = gsrc[(size_t)ra * gpitch + ca];
-            at[k] = in ? ra * lpitch + ca : -1;
+            v[k] = gsrc[in ? go : glast];
+            at[k] = in ? lo : -1;
             c += dc;
-            r += dr;
-            if (c >= cols) { c -= cols; ++r; }
+            go += gstep;
+            lo += lstep;
+            if (c >= cols) { c -= cols; go += gwrap; lo += lwrap; }
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k)

@@ -91,8 +91,80 @@ __device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, i
     return true;
 }
 
+#ifdef ORBX_STAMPS
+// Diagnostic build only (tools/fast_stamps.py): per-wave phase cycles of k_fast (image 0).
+__device__ unsigned long long g_fast_stamps[16384][8];
+__device__ __forceinline__ unsigned long long fclock() {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define FCLK(v) const unsigned long long v = fclock()
+#define FACC(acc, a, b) acc += (b) - (a)
+#else
+#define FCLK(v) do { } while (0)
+#define FACC(acc, a, b) do { } while (0)
+#endif
+
 #define FAST_LIST 512
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Pixels s_abs and s_abs+1 of a byte run held in dwords A[0..3] as two zero-extended u16s
+// (one v_perm: selector bytes s, 0x0C (= 0x00), s+1, 0x0C over the dword pair).
+__device__ __forceinline__ u16x2 pair_u16(const uint32_t* A, int s_abs) {
+    const int k = s_abs >> 2, s = s_abs & 3;
+    const uint32_t sel = (uint32_t)s | 0x0C00u | (uint32_t)(s + 1) << 16 | 0x0C000000u;
+    return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(A[k + 1], A[k], sel));
+}
+
+// FAST compass pre-test of 4 adjacent pixels (detection columns 4gx..4gx+3 of ROI row R):
+// a 9-pixel arc beyond the threshold contains two neighbouring compass pixels (circle
+// indices i, i+4) beyond it on the same side.  Packed 16-bit saturating arithmetic, two
+// pixels per instruction: bright_i = (n_i - (v + t))+ , dark_i = ((v - t)+ - n_i)+, and a
+// pixel passes when max over the four neighbouring pairs of min(.,.) is non-zero for either
+// polarity.  XO = the ROI's byte offset in its first LDS dword (roi row = dwords, aligned).
+// Returns 4 flag bits, bit j = pixel 4gx+j.
+template <int XO>
+__device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R, int gx, u16x2 T) {
+    const uint32_t* rc = (const uint32_t*)(roi0 + R * rp) + gx;
+    const uint32_t* rd = (const uint32_t*)(roi0 + (R + 3) * rp) + gx;
+    const uint32_t* ru = (const uint32_t*)(roi0 + (R - 3) * rp) + gx;
+    constexpr int KC = (XO + 9) >> 2;               // last centre-row dword used
+    constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
+    uint32_t C[5], D[5], U[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        C[k] = k <= KC ? rc[k] : 0u;
+        D[k] = (k >= K0 && k <= K1) ? rd[k] : 0u;
+        U[k] = (k >= K0 && k <= K1) ? ru[k] : 0u;
+    }
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int o = XO + 3 + 2 * h;               // byte of pixel 2h (centre row)
+        const u16x2 V = pair_u16(C, o), N12 = pair_u16(C, o - 3), N4 = pair_u16(C, o + 3);
+        const u16x2 N0 = pair_u16(D, o), N8 = pair_u16(U, o);
+        const u16x2 HI = V + T, LO = __builtin_elementwise_sub_sat(V, T);
+        const u16x2 b0 = __builtin_elementwise_sub_sat(N0, HI), b4 = __builtin_elementwise_sub_sat(N4, HI);
+        const u16x2 b8 = __builtin_elementwise_sub_sat(N8, HI), b12 = __builtin_elementwise_sub_sat(N12, HI);
+        const u16x2 d0 = __builtin_elementwise_sub_sat(LO, N0), d4 = __builtin_elementwise_sub_sat(LO, N4);
+        const u16x2 d8 = __builtin_elementwise_sub_sat(LO, N8), d12 = __builtin_elementwise_sub_sat(LO, N12);
+#define MN(a, b) __builtin_elementwise_min(a, b)
+#define MX(a, b) __builtin_elementwise_max(a, b)
+        const u16x2 pb = MX(MX(MN(b0, b4), MN(b4, b8)), MX(MN(b8, b12), MN(b12, b0)));
+        const u16x2 pd = MX(MX(MN(d0, d4), MN(d4, d8)), MX(MN(d8, d12), MN(d12, d0)));
+        const u16x2 one = {1, 1};
+        w[h] = __builtin_bit_cast(uint32_t, MN(MX(pb, pd), one));   // 0/1 per pixel
+#undef MN
+#undef MX
+    }
+    const uint32_t f = w[0] | (w[1] << 2);          // bits 0, 16 (pixels 0, 1), 2, 18 (2, 3)
+    return (f & 5u) | ((f >> 15) & 10u);
+}
 
 __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
                                               const CellDesc* __restrict__ cells,
@@ -106,10 +178,10 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
     if (ci >= g->n_cells) return;   // no block-level barriers below: waves are independent
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
-    uint8_t* roi = smem + wid * (roi_cap + mb_cap + FAST_LIST * 2 + cl_cap);
+    uint8_t* roi = smem + wid * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
     uint8_t* mb = roi + roi_cap;
     int16_t* list = (int16_t*)(mb + mb_cap);
-    int16_t* corners = list + FAST_LIST;   // pixels with M > min threshold, raster order
+    int16_t* corners = list + FAST_LIST + 64;   // pixels with M > min threshold, raster order
     const CellDesc c = cells[ci];
     const int rows = c.rows, cols = c.cols, dh = rows - 6, dw = cols - 6;
     int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
@@ -118,45 +190,73 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
         return;
     }
     const LevelGeom& L = g->lv[c.level];
+#ifdef ORBX_STAMPS
+    unsigned long long acc_p1 = 0, acc_p2 = 0, n_list_tot = 0;
+#endif
+    FCLK(t_start);
     // ROI rows staged as aligned dwords, all loads of a lane in flight before the LDS stores
     const int ax0 = c.ini_x & ~3, xo = c.ini_x - ax0;
     const int ndw = (xo + cols + 3) >> 2;
     const int rp = ndw * 4;   // LDS row pitch of the ROI
     stage_dwords<64>(pyr + (size_t)b * g->pyr_bytes + L.off + (size_t)c.ini_y * L.pitch + ax0,
                      L.pitch, rows, ndw, (uint32_t*)roi, ndw, lane);
+    const uint8_t* roi0 = roi;
     roi += xo;
     const int mw = dw + 2;
     for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
     wave_sync();
-    // Lane mapping without divisions: a wave covers 64 / 2^rsh detection rows per pass,
-    // 2^rsh lanes per row (cells are at most 60 wide), so ballot order is raster order.
-    const int rsh = dw <= 32 ? 5 : 6;
-    const int rpp = 64 >> rsh;
-    const int sub = lane >> rsh, cl = lane & ((1 << rsh) - 1);
-    // 1. compass pre-test at the lower threshold: a 9-pixel arc over threshold t contains two
-    //    neighbouring compass pixels (circle indices i, i+4) both beyond t on the same side.
+    FCLK(t_staged);
+    // 1. compass pre-test at the lower threshold, 4 pixels per lane: 2^gsh lanes per detection
+    //    row (groups of 4 columns), 64 >> gsh rows per pass, so lane order then pixel order
+    //    within a lane is raster order.
     const int tq = min(g->ini_th, g->min_th);
+    const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
+    const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
+    const int rpp = 64 >> gsh;
+    const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
+    const uint32_t colmask = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
+    const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
     int ncorner = 0;
-    for (int rb = 0; rb < dh; rb += FAST_LIST / 64 * rpp) {
+    for (int rb = 0; rb < dh; rb += rows_blk) {
         int nlist = 0;
-        for (int r0 = rb; r0 < min(dh, rb + FAST_LIST / 64 * rpp); r0 += rpp) {
+        FCLK(t_b0);
+        for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
             const int rr = r0 + sub;
-            bool pass = false;
-            if (rr < dh && cl < dw) {
-                const uint8_t* q = roi + (rr + 3) * rp + cl + 3;
-                const int v = q[0];
-                const int n0 = q[3 * rp], n4 = q[3], n8 = q[-3 * rp], n12 = q[-3];
-                const int hi = v + tq, lo = v - tq;
-                const bool b0 = n0 > hi, b4 = n4 > hi, b8 = n8 > hi, b12 = n12 > hi;
-                const bool d0 = n0 < lo, d4 = n4 < lo, d8 = n8 < lo, d12 = n12 < lo;
-                pass = (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0) || (d0 && d4) ||
-                       (d4 && d8) || (d8 && d12) || (d12 && d0);
+            const int R = min(rr, dh - 1) + 3;
+            uint32_t f;
+            switch (xo) {
+                case 0: f = compass4<0>(roi0, rp, R, gx, T); break;
+                case 1: f = compass4<1>(roi0, rp, R, gx, T); break;
+                case 2: f = compass4<2>(roi0, rp, R, gx, T); break;
+                default: f = compass4<3>(roi0, rp, R, gx, T); break;
             }
-            const uint64_t m = __ballot(pass);
-            if (pass) list[nlist + lanes_below(m)] = (int16_t)((rr << 6) | cl);
-            nlist += __popcll(m);
+            f &= rr < dh ? colmask : 0u;
+            const uint64_t m0 = __ballot(f & 1u), m1 = __ballot(f & 2u);
+            const uint64_t m2 = __ballot(f & 4u), m3 = __ballot(f & 8u);
+            uint32_t below = __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u);
+            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), below);
+            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m1, below);
+            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), below);
+            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m2, below);
+            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), below);
+            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m3, below);
+            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), below);
+            int pos = nlist + (int)below;
+            const int e0 = (rr << 6) | (4 * gx);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // unset bits write this lane's spare slot
+                const int on = (f >> j) & 1u;
+                list[on ? pos : FAST_LIST + lane] = (int16_t)(e0 + j);
+                pos += on;
+            }
+            nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
         }
         wave_sync();
+        FCLK(t_b1);
+        FACC(acc_p1, t_b0, t_b1);
+#ifdef ORBX_STAMPS
+        n_list_tot += nlist;
+#endif
         // 2. full arc score for the survivors only (dense across lanes); those above the lower
         //    threshold are appended to the corner list, keeping raster order
         for (int j0 = 0; j0 < nlist; j0 += 64) {
@@ -174,7 +274,10 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
             ncorner += __popcll(cm);
         }
         wave_sync();
+        FCLK(t_b2);
+        FACC(acc_p2, t_b1, t_b2);
     }
+    FCLK(t_p3);
     // 3. any corner at iniThFAST in this cell?  (else fall back to minThFAST, :833-837)
     int t = g->ini_th;
     bool found = false;
@@ -212,12 +315,26 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
         base += __popcll(m);
     }
     if (lane == 0) *cnt_out = min(base, c.cap);
+#ifdef ORBX_STAMPS
+    FCLK(t_end);
+    if (lane == 0 && b == 0 && ci < 16384) {
+        unsigned long long* o = g_fast_stamps[ci];
+        o[0] = t_staged - t_start; o[1] = acc_p1; o[2] = acc_p2; o[3] = t_end - t_p3;
+        o[4] = t_end - t_start; o[5] = n_list_tot; o[6] = ncorner; o[7] = (unsigned long long)dh * dw;
+    }
+#endif
 }
+
+#ifdef ORBX_STAMPS
+extern "C" int orbx_diag_fast_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps));
+}
+#endif
 
 size_t fast_lds_bytes(const Geometry& G) {
     const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (G.max_cell_px * 2 + 15) & ~15;
-    return (size_t)4 * (roi_cap + mb_cap + FAST_LIST * 2 + cl_cap);
+    return (size_t)4 * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
 }
 
 // ----------------------------------------------------------------------------------------

@@ -338,7 +338,8 @@ orbx_status orbx_matcher_create(const orbx_matcher_params* params, orbx_matcher*
     m->prm = p;
     if (!HIPOK(hipSetDevice(p.device)) ||
         !HIPOK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking)) ||
-        !HIPOK(hipMalloc((void**)&m->d_err, 64)) || !HIPOK(prepare_match_kernels())) {
+        !HIPOK(hipMalloc((void**)&m->d_err, 64)) || !HIPOK(hipMemset(m->d_err, 0, 64)) ||
+        !HIPOK(prepare_match_kernels())) {
         orbx_matcher_destroy(m);
         return ORBX_ERR_DEVICE;
     }

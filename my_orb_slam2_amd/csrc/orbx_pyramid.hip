@@ -76,12 +76,12 @@ __device__ __forceinline__ int byte12(uint32_t d0, uint32_t d1, uint32_t d2, int
 __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1, bool simd) {
     if (simd) {   // VResizeLinearVec_32s8u: packs(>>4), mulhi, adds, (+2)>>2, packus
         const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
-        int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);
+        int m = (int)(__umul24(t0, b0) >> 16) + (int)(__umul24(t1, b1) >> 16);
         m = min(max(m, -32768), 32767);
         m = min(m + 2, 32767);
         return sat8(m >> 2);
     }
-    return sat8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);   // FixedPtCast<int, uchar, 22>
+    return sat8((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22));   // FixedPtCast<int, uchar, 22>
 }
 
 __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
@@ -155,8 +155,10 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
 
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
-    for (int i = tid; i < LT_HR * LT_G; i += 256) {
-        const int hr = i / LT_G, q = i - hr * LT_G;
+    // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
+    static_assert(256 / LT_G == 7 && 256 % LT_G == 18, "halo item stride");
+    int hr = tid / LT_G, q = tid - hr * LT_G;
+    for (int i = tid; i < LT_HR * LT_G; i += 256, hr += 7, q += 18, (q >= LT_G ? (q -= LT_G, ++hr) : 0)) {
         const int y = Y0 - 3 + hr, xg = X0 - 4 + 4 * q;
         uint32_t out = 0;
         if (y >= ny0 && y <= ny1 && xg + 3 >= nx0 && xg <= nx1) {
@@ -170,8 +172,8 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                 const uint32_t als[4] = {al.x, al.y, al.z, al.w};
                 const int r0 = (int)(ri.x & 0xFFFF), r1 = (int)(ri.x >> 16);
                 const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
-                const uint8_t* w0 = win + r0 * WP;
-                const uint8_t* w1 = win + r1 * WP;
+                const uint8_t* w0 = win + __umul24(r0, WP);
+                const uint8_t* w1 = win + __umul24(r1, WP);
                 if (ci & 0x200u) {
                     // branch-free: v_perm gathers each pixel's two taps as u16s, v_dot2 applies
                     // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
@@ -191,8 +193,10 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                         const int h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
                         const int h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
                         // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind
-                        const int vs = min((((h0 >> 4) * b0 >> 16) + ((h1 >> 4) * b1 >> 16) + 2) >> 2, 255);
-                        const int vc = min((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 255);
+                        // 24-bit multiplies (full rate): h < 2^19, b <= 2048
+                        const int vs = min(((int)(__umul24(h0 >> 4, b0) >> 16) +
+                                            (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2, 255);
+                        const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
                         out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
                     }
                 } else {   // reflected border group: bytes one by one
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                     out |= (uint32_t)((s0[0] + s0[1] + s0[S.pitch] + s0[S.pitch + 1] + 2) >> 2) << (8 * j);
                 }
             } else {
-                const uint8_t* wr = win + (int)(ri.x & 0xFFFF) * WP;
+                const uint8_t* wr = win + __umul24(ri.x & 0xFFFF, WP);
                 if (ci & 0x100u) {
                     out = *(const uint32_t*)(wr + xs[0]);
                 } else {
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         const int r = i / LT_GW, gq = i - r * LT_GW;
         if (gq >= ng) continue;
         const uint32_t v = lvl[(r + 3) * LT_G + gq + 1];
-        uint8_t* d = dlev + (size_t)(Y0 + r) * L.pitch + X0 + 4 * gq;
+        uint8_t* d = dlev + __umul24(Y0 + r, L.pitch) + X0 + 4 * gq;
         if (4 * gq + 4 <= vw) *(uint32_t*)d = v;
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
@@ -278,27 +282,35 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     // sum S = k3*c0 + k4*p1 + ... stays exact while S < 2^24 (partials only grow); at
     // S >= 2^24 both forms give >= 256 and saturate to 255.  So rintf(S/65536) is
     // round-half-even of the integer S, and the scalar tail is (S + 32768) >> 16.
+    // S_j = k3*c + k4*(r2+r4) + k5*(r1+r5) + k6*(r0+r6): per pixel three v_perm pair the
+    // symmetric rows' u16 sums and four v_dot2_u32_u16 accumulate (S < 2^24: exact).
+    const uint32_t K4 = (uint32_t)k4 * 0x10001u, K5 = (uint32_t)k5 * 0x10001u;
+    const uint32_t K6 = (uint32_t)k6 * 0x10001u, K3lo = (uint32_t)k3, K3hi = (uint32_t)k3 << 16;
     for (int i = tid; i < vh * LT_GW; i += 256) {
         const int r = i / LT_GW, gq = i - r * LT_GW;
         if (gq >= ng) continue;
         uint2 v[7];
 #pragma unroll
         for (int k = 0; k < 7; ++k) v[k] = *(const uint2*)(rows + (r + k) * LT_W + 4 * gq);
+        const int xg = X0 + 4 * gq;
         uint32_t packed = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            auto at = [&](int k) {
-                const uint32_t w = (j < 2) ? v[k].x : v[k].y;
-                return (int)((w >> (16 * (j & 1))) & 0xFFFFu);
-            };
-            const int c0 = at(3);
-            const int p1 = at(4) + at(2), p2 = at(5) + at(1), p3 = at(6) + at(0);
-            const int S = k3 * c0 + k4 * p1 + k5 * p2 + k6 * p3;
-            const bool simd = X0 + 4 * gq + j < L.bsimd_end;
-            const int val = (S + (simd ? 32767 + ((S >> 16) & 1) : 32768)) >> 16;
-            packed |= (uint32_t)min(val, 255) << (8 * j);
+            auto dw = [&](int k) { return (j < 2) ? v[k].x : v[k].y; };
+            const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;   // (a.hi, b.hi) / (a.lo, b.lo)
+            const us2 p06 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(6), dw(0), sel));
+            const us2 p15 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(5), dw(1), sel));
+            const us2 p24 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(4), dw(2), sel));
+            uint32_t S = __builtin_amdgcn_udot2(p06, __builtin_bit_cast(us2, K6), 0u, false);
+            S = __builtin_amdgcn_udot2(p15, __builtin_bit_cast(us2, K5), S, false);
+            S = __builtin_amdgcn_udot2(p24, __builtin_bit_cast(us2, K4), S, false);
+            S = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, dw(3)),
+                                       __builtin_bit_cast(us2, (j & 1) ? K3hi : K3lo), S, false);
+            const bool simd = xg + j < L.bsimd_end;
+            const uint32_t val = (S + (simd ? 32767u + ((S >> 16) & 1u) : 32768u)) >> 16;
+            packed |= min(val, 255u) << (8 * j);
         }
-        uint8_t* d = dblur + (size_t)(Y0 + r) * L.pitch + X0 + 4 * gq;
+        uint8_t* d = dblur + __umul24(Y0 + r, L.pitch) + xg;
         if (4 * gq + 4 <= vw) *(uint32_t*)d = packed;
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
