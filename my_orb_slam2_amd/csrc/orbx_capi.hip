@@ -262,7 +262,7 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         G.blur_tile_begin[l] = blur_tiles;
         blur_tiles += ((lv.w + 63) / 64) * ((lv.h + 15) / 16);
         G.orient_block_begin[l] = oblocks;
-        oblocks += (lv.out_cap + 3) / 4;
+        oblocks += (lv.out_cap + 4 * OD_NK - 1) / (4 * OD_NK);
         lv.bsimd_end = h->prm.cv_simd ? (lv.w / 4) * 4 : 0;
         // resize tables (cv::resize INTER_LINEAR 8U, imgwarp.cpp)
         lv.copy = lv.area2 = 0;

@@ -692,10 +692,23 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
 }
 
 // ----------------------------------------------------------------------------------------
-// Orientation + rBRIEF + assembly: one wave per keypoint.
+// Orientation + rBRIEF + assembly: one wave per OD_NK keypoints of one level.  The patch
+// loads of keypoint k+1 are in flight while keypoint k is computed from LDS; the per-lane
+// patch offsets are the same for every keypoint of the level and are computed once.
 // ----------------------------------------------------------------------------------------
 #define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
 #define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
+#define OD_NLOAD 11    // dword loads per lane: (31 * 9 + 37 * 10) / 64, rounded up
+
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);   // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);   // row_ror:8
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict__ g,
                                                      const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
@@ -709,106 +722,121 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int level = 0;
     while (level + 1 < g->nlevels && blk >= g->orient_block_begin[level + 1]) ++level;
-    const int i = (blk - g->orient_block_begin[level]) * 4 + wid;
+    const int i0 = ((blk - g->orient_block_begin[level]) * 4 + wid) * OD_NK;
     const int* oc = ocnt + b * g->nlevels;
-    if (level == 0 && i == 0 && lane == 0) {
+    if (level == 0 && i0 == 0 && lane == 0) {
         int tot = 0;
         for (int l = 0; l < g->nlevels; ++l) tot += oc[l];
         nkp[b] = tot;
     }
     const int n = oc[level];
-    if (i >= n) return;
+    if (i0 >= n) return;
+    const int nk = min(OD_NK, n - i0);
     int off = 0;
     for (int l = 0; l < level; ++l) off += oc[l];
     const LevelGeom& L = g->lv[level];
-    const uint32_t c = okp[(size_t)b * g->out_words + L.out_off + i];
-    const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
     const int pitch = L.pitch;
+    // every keypoint word of the wave in one load
+    const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
 
-    // stage the 31x31 raw patch (IC_Angle) and the 37x37 blurred patch (rBRIEF offsets are
-    // within +-18) as aligned dwords: every load of a lane is issued before its LDS stores
-    const int ax_r = (x - 15) & ~3, ax_b = (x - 18) & ~3;
-    const uint8_t* pr = pyr + b * g->pyr_bytes + L.off + (size_t)(y - 15) * pitch + ax_r;
-    const uint8_t* pb = blur + b * g->pyr_bytes + L.off + (size_t)(y - 18) * pitch + ax_b;
-    uint32_t* P = patch[wid];
-    {
-        constexpr int n1 = 31 * OD_RAW_DW, n2 = 37 * OD_BLR_DW;
-        uint32_t v[11];
+    // per-lane patch offsets (raw rows first, then blurred rows) relative to the patch bases
+    constexpr int n1 = 31 * OD_RAW_DW, n2 = 37 * OD_BLR_DW;
+    uint32_t so[OD_NLOAD];
+    uint32_t rawbits = 0;
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {   // branch-free address select: one load per k
-            const int t = min(lane + 64 * k, n1 + n2 - 1);
-            const bool isr = t < n1;
-            const int tt = isr ? t : t - n1;
-            const int row = isr ? tt / OD_RAW_DW : tt / OD_BLR_DW;
-            const int col = tt - row * (isr ? OD_RAW_DW : OD_BLR_DW);
-            const uint8_t* base = isr ? pr : pb;
-            v[k] = *(const uint32_t*)(base + (size_t)row * pitch + 4 * col);
-        }
-#pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const int t = lane + 64 * k;
-            if (t < n1 + n2) P[t] = v[k];
-        }
+    for (int k = 0; k < OD_NLOAD; ++k) {
+        const int t = min(lane + 64 * k, n1 + n2 - 1);
+        const bool isr = t < n1;
+        const int tt = isr ? t : t - n1;
+        const int row = isr ? tt / OD_RAW_DW : tt / OD_BLR_DW;
+        const int col = tt - row * (isr ? OD_RAW_DW : OD_BLR_DW);
+        so[k] = __umul24(row, pitch) + 4 * col;
+        rawbits |= (uint32_t)isr << k;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint8_t* raw = (const uint8_t*)P;                       // [31][36], x at col x-ax_r
-    const uint8_t* blr = (const uint8_t*)(P + 31 * OD_RAW_DW);    // [37][40]
+    const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
+    const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
+    auto issue = [&](int k, uint32_t (&v)[OD_NLOAD]) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, k);
+        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
+        const uint8_t* pr = pyr_l + __umul24(y - 15, pitch) + ((x - 15) & ~3);
+        const uint8_t* pb = blr_l + __umul24(y - 18, pitch) + ((x - 18) & ~3);
+#pragma unroll
+        for (int j = 0; j < OD_NLOAD; ++j)
+            v[j] = *(const uint32_t*)(((rawbits >> j) & 1u ? pr : pb) + so[j]);
+    };
 
-    // IC_Angle (src/ORBextractor.cc:77-104) on the unblurred level; exact integer moments.
-    const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ax_r);
-    int m10 = 0, m01 = 0;
-    {
-        const int half = lane >> 5, l31 = lane & 31;
+    // IC_Angle lane work (src/ORBextractor.cc:77-104): lane l31 < 31 is column u = l31 - 15;
+    // the lower half-wave takes rows v = 1..7 (and the m_10 centre row), the upper v = 8..15.
+    // umax decreases with v, so the rows with |u| <= umax[v] are a prefix [vb, vend).
+    const int half = lane >> 5, l31 = lane & 31;
+    const int u = l31 - 15, au = u < 0 ? -u : u;
+    const int vb = half ? 8 : 1, ve = half ? 16 : 8;
+    int vend = vb;
+    for (int v = vb; v < ve; ++v) vend += (l31 < 31 && au <= g->umax[v]) ? 1 : 0;
+
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    uint32_t* P = patch[wid];
+    const uint8_t* raw = (const uint8_t*)P;                       // [31][36]
+    const uint8_t* blr = (const uint8_t*)(P + n1);                // [37][40]
+    uint32_t v[OD_NLOAD];
+    issue(0, v);
+    for (int k = 0; k < nk; ++k) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, k);
+        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
+#pragma unroll
+        for (int j = 0; j < OD_NLOAD; ++j) {
+            const int t = lane + 64 * j;
+            if (t < n1 + n2) P[t] = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (k + 1 < nk) issue(k + 1, v);   // next patch in flight during this keypoint
+
+        const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ((x - 15) & ~3));
+        int m10 = 0, m01 = 0;
         if (l31 < 31) {
-            const int u = l31 - 15;
-            const int au = u < 0 ? -u : u;
-            if (!half) m10 += u * center[u];
-            const int vb = half ? 8 : 1, ve = half ? 16 : 8;
-            for (int v = vb; v < ve; ++v) {
-                if (au <= g->umax[v]) {
-                    const int vp = center[u + v * (OD_RAW_DW * 4)], vm = center[u - v * (OD_RAW_DW * 4)];
-                    m10 += u * (vp + vm);
-                    m01 += v * (vp - vm);
-                }
+            if (!half) m10 = __mul24(u, (int)center[u]);
+            for (int vv = vb; vv < vend; ++vv) {
+                const int vp = center[u + vv * (OD_RAW_DW * 4)], vm = center[u - vv * (OD_RAW_DW * 4)];
+                m10 += __mul24(u, vp + vm);
+                m01 += __mul24(vv, vp - vm);
             }
         }
-    }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    const float angle = cv_fast_atan2((float)m01, (float)m10);
+        m10 = wave_sum_dpp(m10);
+        m01 = wave_sum_dpp(m01);
+        const float angle = cv_fast_atan2((float)m01, (float)m10);
 
-    // computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level.
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    const float ang = angle * factorPI;
-    const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
-    const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ax_b);
-    uint64_t words[4];
+        // computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level.
+        const float ang = angle * factorPI;
+        const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
+        const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ((x - 18) & ~3));
+        uint64_t words[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int k = w * 64 + lane;
-        const float x1 = (float)c_pattern[4 * k], y1 = (float)c_pattern[4 * k + 1];
-        const float x2 = (float)c_pattern[4 * k + 2], y2 = (float)c_pattern[4 * k + 3];
-        const float r1a = x1 * sb, r1b = y1 * ca, c1a = x1 * ca, c1b = y1 * sb;
-        const float r2a = x2 * sb, r2b = y2 * ca, c2a = x2 * ca, c2b = y2 * sb;
-        const int t0 = bc[cv_round(r1a + r1b) * (OD_BLR_DW * 4) + cv_round(c1a - c1b)];
-        const int t1 = bc[cv_round(r2a + r2b) * (OD_BLR_DW * 4) + cv_round(c2a - c2b)];
-        words[w] = __ballot(t0 < t1);
-    }
-    const size_t o = (size_t)b * g->kp_cap + off + i;
-    if (lane == 0) {
-        float* kp = kps + o * 7;
-        const float sc = L.scale;
-        kp[0] = level ? (float)x * sc : (float)x;
-        kp[1] = level ? (float)y * sc : (float)y;
-        kp[2] = (float)L.patch_size;
-        kp[3] = angle;
-        kp[4] = (float)s;
-        ((int*)kp)[5] = level;
-        ((int*)kp)[6] = -1;
-    }
-    if (lane < 4) {
-        uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-        *(uint64_t*)(desc + o * 32 + lane * 8) = wv;
+        for (int w = 0; w < 4; ++w) {
+            const int q = w * 64 + lane;
+            const float x1 = (float)c_pattern[4 * q], y1 = (float)c_pattern[4 * q + 1];
+            const float x2 = (float)c_pattern[4 * q + 2], y2 = (float)c_pattern[4 * q + 3];
+            const float r1a = x1 * sb, r1b = y1 * ca, c1a = x1 * ca, c1b = y1 * sb;
+            const float r2a = x2 * sb, r2b = y2 * ca, c2a = x2 * ca, c2b = y2 * sb;
+            const int t0 = bc[cv_round(r1a + r1b) * (OD_BLR_DW * 4) + cv_round(c1a - c1b)];
+            const int t1 = bc[cv_round(r2a + r2b) * (OD_BLR_DW * 4) + cv_round(c2a - c2b)];
+            words[w] = __ballot(t0 < t1);
+        }
+        const size_t o = (size_t)b * g->kp_cap + off + i0 + k;
+        if (lane == 0) {
+            float* kp = kps + o * 7;
+            const float sc = L.scale;
+            kp[0] = level ? (float)x * sc : (float)x;
+            kp[1] = level ? (float)y * sc : (float)y;
+            kp[2] = (float)L.patch_size;
+            kp[3] = angle;
+            kp[4] = (float)s;
+            ((int*)kp)[5] = level;
+            ((int*)kp)[6] = -1;
+        }
+        if (lane < 4) {
+            uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+            *(uint64_t*)(desc + o * 32 + lane * 8) = wv;
+        }
     }
 }
 

@@ -45,6 +45,7 @@ struct LevelGeom {
 };
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
+#define OD_NK 4               // keypoints per wave in k_orient_desc
 #define LT_W 128              // output tile width  (32 groups of 4)
 #define LT_H 32               // output tile height
 #define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
@@ -86,7 +87,7 @@ struct Geometry {
     int max_mbuf_bytes;     // largest FAST score buffer ((dh+2)*(dw+2)), dword padded
     int max_cell_px;        // largest FAST detection region (dh*dw)
     int blur_tiles;         // Σ_l ceil(w/64)*ceil(h/16)
-    int orient_blocks;      // Σ_l ceil(out_cap/4)
+    int orient_blocks;      // Σ_l ceil(out_cap / (4 * OD_NK))
     int blur_tile_begin[ORBX_MAX_LEVELS + 1];
     int orient_block_begin[ORBX_MAX_LEVELS + 1];
     int taps[7];            // cvRound(getGaussianKernel(7, 2, CV_32F) * 256)
