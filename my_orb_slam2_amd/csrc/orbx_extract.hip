@@ -91,24 +91,30 @@ __device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, i
     return true;
 }
 
-#ifdef ORBX_STAMPS
-// Diagnostic build only (tools/fast_stamps.py): per-wave phase cycles of k_fast (image 0).
-__device__ unsigned long long g_fast_stamps[16384][8];
-__device__ __forceinline__ unsigned long long fclock() {
-    __builtin_amdgcn_sched_barrier(0);
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
+// Keypoint tests at both thresholds on the M map in one read of the 3x3 neighbourhood.
+__device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, int cc, int t_hi,
+                                             int t_lo, bool& k_hi, bool& k_lo, int& score) {
+    const uint8_t* p = mb + (rr + 1) * mw + (cc + 1);
+    const int m = p[0], s = m - 1;
+    score = s;
+    const int q0 = p[-mw - 1], q1 = p[-mw], q2 = p[-mw + 1], q3 = p[-1], q4 = p[1];
+    const int q5 = p[mw - 1], q6 = p[mw], q7 = p[mw + 1];
+    // a neighbour q suppresses at threshold t when q > t and q - 1 >= s, i.e. q >= m: the
+    // candidates (q >= m) are the same for both thresholds, and one suppresses at t iff the
+    // largest of them exceeds t
+    int supp = 0;
+#define ORBX_NB(q) supp = max(supp, (q) >= m ? (q) : 0);
+    ORBX_NB(q0) ORBX_NB(q1) ORBX_NB(q2) ORBX_NB(q3) ORBX_NB(q4) ORBX_NB(q5) ORBX_NB(q6) ORBX_NB(q7)
+#undef ORBX_NB
+    const bool base = s > 0;
+    k_hi = base && m > t_hi && supp <= t_hi;
+    k_lo = base && m > t_lo && supp <= t_lo;
 }
-#define FCLK(v) const unsigned long long v = fclock()
-#define FACC(acc, a, b) acc += (b) - (a)
-#else
-#define FCLK(v) do { } while (0)
-#define FACC(acc, a, b) do { } while (0)
-#endif
 
 #define FAST_LIST 512
+#define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
+#define FAST_PF 12     // prefetched ROI dwords per lane (larger ROIs are staged directly)
+__device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -174,162 +180,197 @@ __global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
-    const int ci = blockIdx.x * 4 + wid;
-    if (ci >= g->n_cells) return;   // no block-level barriers below: waves are independent
+    // one wave owns FAST_NC consecutive cells; no block-level barriers: waves are independent
+    const int c_first = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * FAST_NC);
+    if (c_first >= g->n_cells) return;
+    const int ncw = min(FAST_NC, g->n_cells - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
-    uint8_t* roi = smem + wid * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
-    uint8_t* mb = roi + roi_cap;
+    uint8_t* roi0 = smem + wid * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
+    uint8_t* mb = roi0 + roi_cap;
     int16_t* list = (int16_t*)(mb + mb_cap);
     int16_t* corners = list + FAST_LIST + 64;   // pixels with M > min threshold, raster order
-    const CellDesc c = cells[ci];
-    const int rows = c.rows, cols = c.cols, dh = rows - 6, dw = cols - 6;
-    int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
-    if (dh <= 0 || dw <= 0) {
-        if (lane == 0) *cnt_out = 0;
-        return;
-    }
-    const LevelGeom& L = g->lv[c.level];
-#ifdef ORBX_STAMPS
-    unsigned long long acc_p1 = 0, acc_p2 = 0, n_list_tot = 0;
-#endif
-    FCLK(t_start);
-    // ROI rows staged as aligned dwords, all loads of a lane in flight before the LDS stores
-    const int ax0 = c.ini_x & ~3, xo = c.ini_x - ax0;
-    const int ndw = (xo + cols + 3) >> 2;
-    const int rp = ndw * 4;   // LDS row pitch of the ROI
-    stage_dwords<64>(pyr + (size_t)b * g->pyr_bytes + L.off + (size_t)c.ini_y * L.pitch + ax0,
-                     L.pitch, rows, ndw, (uint32_t*)roi, ndw, lane);
-    const uint8_t* roi0 = roi;
-    roi += xo;
-    const int mw = dw + 2;
-    for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
-    wave_sync();
-    FCLK(t_staged);
-    // 1. compass pre-test at the lower threshold, 4 pixels per lane: 2^gsh lanes per detection
-    //    row (groups of 4 columns), 64 >> gsh rows per pass, so lane order then pixel order
-    //    within a lane is raster order.
+    const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
     const int tq = min(g->ini_th, g->min_th);
     const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
-    const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
-    const int rpp = 64 >> gsh;
-    const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
-    const uint32_t colmask = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
-    const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
-    int ncorner = 0;
-    for (int rb = 0; rb < dh; rb += rows_blk) {
-        int nlist = 0;
-        FCLK(t_b0);
-        for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
-            const int rr = r0 + sub;
-            const int R = min(rr, dh - 1) + 3;
-            uint32_t f;
-            switch (xo) {
-                case 0: f = compass4<0>(roi0, rp, R, gx, T); break;
-                case 1: f = compass4<1>(roi0, rp, R, gx, T); break;
-                case 2: f = compass4<2>(roi0, rp, R, gx, T); break;
-                default: f = compass4<3>(roi0, rp, R, gx, T); break;
-            }
-            f &= rr < dh ? colmask : 0u;
-            const uint64_t m0 = __ballot(f & 1u), m1 = __ballot(f & 2u);
-            const uint64_t m2 = __ballot(f & 4u), m3 = __ballot(f & 8u);
-            uint32_t below = __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u);
-            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), below);
-            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m1, below);
-            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), below);
-            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m2, below);
-            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), below);
-            below = __builtin_amdgcn_mbcnt_lo((uint32_t)m3, below);
-            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), below);
-            int pos = nlist + (int)below;
-            const int e0 = (rr << 6) | (4 * gx);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {   // unset bits write this lane's spare slot
-                const int on = (f >> j) & 1u;
-                list[on ? pos : FAST_LIST + lane] = (int16_t)(e0 + j);
-                pos += on;
-            }
-            nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
-        }
-        wave_sync();
-        FCLK(t_b1);
-        FACC(acc_p1, t_b0, t_b1);
-#ifdef ORBX_STAMPS
-        n_list_tot += nlist;
-#endif
-        // 2. full arc score for the survivors only (dense across lanes); those above the lower
-        //    threshold are appended to the corner list, keeping raster order
-        for (int j0 = 0; j0 < nlist; j0 += 64) {
-            const int j = j0 + lane;
-            int pe = 0, m = 0;
-            if (j < nlist) {
-                pe = list[j];
-                const int rr = pe >> 6, cc = pe & 63;
-                m = fast_arc_score(roi, rp, rr + 3, cc + 3);
-                mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
-            }
-            const bool corner = j < nlist && m > tq;
-            const uint64_t cm = __ballot(corner);
-            if (corner) corners[ncorner + lanes_below(cm)] = (int16_t)pe;
-            ncorner += __popcll(cm);
-        }
-        wave_sync();
-        FCLK(t_b2);
-        FACC(acc_p2, t_b1, t_b2);
-    }
-    FCLK(t_p3);
-    // 3. any corner at iniThFAST in this cell?  (else fall back to minThFAST, :833-837)
-    int t = g->ini_th;
-    bool found = false;
-    for (int j0 = 0; j0 < ncorner && !found; j0 += 64) {
-        const int j = j0 + lane;
-        int s;
-        bool k = false;
-        if (j < ncorner) {
-            const int pe = corners[j];
-            k = fast_nms_kp(mb, mw, pe >> 6, pe & 63, t, s);
-        }
-        found = __ballot(k) != 0;
-    }
-    if (!found) t = g->min_th;
-    // 4. ordered compaction (raster order inside the cell, as cv::FAST emits)
-    uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
-    int base = 0;
-    for (int j0 = 0; j0 < ncorner; j0 += 64) {
-        const int j = j0 + lane;
-        int s = 0, rr = 0, cc = 0;
-        bool k = false;
-        if (j < ncorner) {
-            const int pe = corners[j];
-            rr = pe >> 6;
-            cc = pe & 63;
-            k = fast_nms_kp(mb, mw, rr, cc, t, s);
-        }
-        const uint64_t m = __ballot(k);
-        if (k) {
-            const int idx = base + lanes_below(m);
-            const int x = c.ini_x + cc + 3 - ORBX_MIN_BORDER;
-            const int y = c.ini_y + rr + 3 - ORBX_MIN_BORDER;
-            if (idx < c.cap) slot[idx] = pack_cand(x, y, s);
-        }
-        base += __popcll(m);
-    }
-    if (lane == 0) *cnt_out = min(base, c.cap);
-#ifdef ORBX_STAMPS
-    FCLK(t_end);
-    if (lane == 0 && b == 0 && ci < 16384) {
-        unsigned long long* o = g_fast_stamps[ci];
-        o[0] = t_staged - t_start; o[1] = acc_p1; o[2] = acc_p2; o[3] = t_end - t_p3;
-        o[4] = t_end - t_start; o[5] = n_list_tot; o[6] = ncorner; o[7] = (unsigned long long)dh * dw;
-    }
-#endif
-}
 
-#ifdef ORBX_STAMPS
-extern "C" int orbx_diag_fast_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps));
+    // ROI of a cell as aligned dwords, dense rows of ndw dwords: LDS dword t = lane + 64j
+    uint32_t pf[FAST_PF];
+    auto prefetch = [&](const CellDesc& c) -> bool {
+        const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
+        const int n = c.rows * ndw;
+        if (n > 64 * FAST_PF || c.rows <= 6 || c.cols <= 6) return false;
+        const LevelGeom& L = g->lv[c.level];
+        const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3);
+        const uint32_t gp = (uint32_t)L.pitch;
+        const int dr = 64 / ndw, dc = 64 - dr * ndw;
+        int r = lane / ndw, col = lane - r * ndw;
+        uint32_t go = (uint32_t)r * gp + 4u * (uint32_t)col;
+        const uint32_t gstep = (uint32_t)dr * gp + 4u * (uint32_t)dc, gwrap = gp - 4u * (uint32_t)ndw;
+        const uint32_t glast = (uint32_t)(c.rows - 1) * gp + 4u * (uint32_t)(ndw - 1);
+#pragma unroll
+        for (int j = 0; j < FAST_PF; ++j) {
+            pf[j] = *(const uint32_t*)(src + (lane + 64 * j < n ? go : glast));
+            col += dc;
+            go += gstep;
+            if (col >= ndw) { col -= ndw; go += gwrap; }
+        }
+        return true;
+    };
+
+    CellDesc cn = cells[c_first];
+    bool have = prefetch(cn);
+    for (int k = 0; k < ncw; ++k) {
+        const int ci = c_first + k;
+        const CellDesc c = cn;
+        const bool pre = have;
+        const int rows = c.rows, cols = c.cols, dh = rows - 6, dw = cols - 6;
+        int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
+        const int xo = c.ini_x & 3;
+        const int ndw = (xo + cols + 3) >> 2;
+        const int rp = ndw * 4;   // LDS row pitch of the ROI
+        if (dh > 0 && dw > 0) {
+            if (pre) {
+#pragma unroll
+                for (int j = 0; j < FAST_PF; ++j)
+                    if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lane + 64 * j] = pf[j];
+            } else {
+                const LevelGeom& L = g->lv[c.level];
+                stage_dwords<64>(pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3),
+                                 L.pitch, rows, ndw, (uint32_t*)roi0, ndw, lane);
+            }
+        }
+        if (k + 1 < ncw) {   // the next cell's ROI loads stay in flight during this cell
+            cn = cells[ci + 1];
+            have = prefetch(cn);
+        }
+        if (dh <= 0 || dw <= 0) {
+            if (lane == 0) *cnt_out = 0;
+            continue;
+        }
+        const uint8_t* roi = roi0 + xo;
+        const int mw = dw + 2;
+        for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
+        lds_order();
+        // 1. compass pre-test at the lower threshold, 4 pixels per lane: 2^gsh lanes per
+        //    detection row (groups of 4 columns), 64 >> gsh rows per pass, so lane order then
+        //    pixel order within a lane is raster order.
+        const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
+        const int rpp = 64 >> gsh;
+        const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
+        const uint32_t colmask = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
+        const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
+        int ncorner = 0;
+        for (int rb = 0; rb < dh; rb += rows_blk) {
+            int nlist = 0;
+            for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
+                const int rr = r0 + sub;
+                const int R = min(rr, dh - 1) + 3;
+                uint32_t f;
+                switch (xo) {
+                    case 0: f = compass4<0>(roi0, rp, R, gx, T); break;
+                    case 1: f = compass4<1>(roi0, rp, R, gx, T); break;
+                    case 2: f = compass4<2>(roi0, rp, R, gx, T); break;
+                    default: f = compass4<3>(roi0, rp, R, gx, T); break;
+                }
+                f &= rr < dh ? colmask : 0u;
+                const uint64_t m0 = __ballot(f & 1u), m1 = __ballot(f & 2u);
+                const uint64_t m2 = __ballot(f & 4u), m3 = __ballot(f & 8u);
+                uint32_t below = __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u);
+                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), below);
+                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m1, below);
+                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), below);
+                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m2, below);
+                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), below);
+                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m3, below);
+                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), below);
+                int pos = nlist + (int)below;
+                const int e0 = (rr << 6) | (4 * gx);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {   // unset bits write this lane's spare slot
+                    const int on = (f >> j) & 1u;
+                    list[on ? pos : FAST_LIST + lane] = (int16_t)(e0 + j);
+                    pos += on;
+                }
+                nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+            }
+            lds_order();
+            // 2. full arc score for the survivors only (dense across lanes); those above the
+            //    lower threshold are appended to the corner list, keeping raster order
+            for (int j0 = 0; j0 < nlist; j0 += 64) {
+                const int j = j0 + lane;
+                int pe = 0, m = 0;
+                if (j < nlist) {
+                    pe = list[j];
+                    const int rr = pe >> 6, cc = pe & 63;
+                    m = fast_arc_score(roi, rp, rr + 3, cc + 3);
+                    mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
+                }
+                const bool corner = j < nlist && m > tq;
+                const uint64_t cm = __ballot(corner);
+                if (corner) corners[ncorner + lanes_below(cm)] = (int16_t)pe;
+                ncorner += __popcll(cm);
+            }
+            lds_order();
+        }
+        // 3. cell-local NMS at iniThFAST, or at minThFAST when the cell has no keypoint at
+        //    iniThFAST (:833-837); 4. ordered compaction (raster order, as cv::FAST emits).
+        //    Both thresholds are tested in one pass when the corners fit one wave.
+        uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
+        int base = 0;
+        const int t_ini = g->ini_th, t_min = g->min_th;
+        if (ncorner <= 64) {
+            int sc = 0, pe = 0;
+            bool k_hi = false, k_lo = false;
+            if (lane < ncorner) {
+                pe = corners[lane];
+                fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+            }
+            const uint64_t mh = __ballot(k_hi);
+            const bool kk = mh ? k_hi : k_lo;
+            const uint64_t m = mh ? mh : __ballot(k_lo);
+            if (kk) {
+                const int idx = lanes_below(m);
+                const int x = c.ini_x + (pe & 63) + 3 - ORBX_MIN_BORDER;
+                const int y = c.ini_y + (pe >> 6) + 3 - ORBX_MIN_BORDER;
+                if (idx < c.cap) slot[idx] = pack_cand(x, y, sc);
+            }
+            base = __popcll(m);
+        } else {
+            bool found = false;
+            for (int j0 = 0; j0 < ncorner && !found; j0 += 64) {
+                const int j = j0 + lane;
+                int sc = 0;
+                bool k_hi = false, k_lo = false;
+                if (j < ncorner) {
+                    const int pe = corners[j];
+                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+                }
+                found = __ballot(k_hi) != 0;
+            }
+            for (int j0 = 0; j0 < ncorner; j0 += 64) {
+                const int j = j0 + lane;
+                int sc = 0, pe = 0;
+                bool k_hi = false, k_lo = false;
+                if (j < ncorner) {
+                    pe = corners[j];
+                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+                }
+                const bool kk = found ? k_hi : k_lo;
+                const uint64_t m = __ballot(kk);
+                if (kk) {
+                    const int idx = base + lanes_below(m);
+                    const int x = c.ini_x + (pe & 63) + 3 - ORBX_MIN_BORDER;
+                    const int y = c.ini_y + (pe >> 6) + 3 - ORBX_MIN_BORDER;
+                    if (idx < c.cap) slot[idx] = pack_cand(x, y, sc);
+                }
+                base += __popcll(m);
+            }
+        }
+        if (lane == 0) *cnt_out = min(base, c.cap);
+        lds_order();
+    }
 }
-#endif
 
 size_t fast_lds_bytes(const Geometry& G) {
     const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
@@ -524,21 +565,45 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                         sm.sortb[ex] = ((uint64_t)cur.cnt[i] << 40) |
                                        ((uint64_t)(uint32_t)cur.seq[i] << 16) | (uint64_t)i;
                 });
-            int P = 1;
-            while (P < nV) P <<= 1;
-            for (int i = nV + tid; i < P; i += 256) sm.sortb[i] = 0;
             __syncthreads();
-            for (int k2 = 2; k2 <= P; k2 <<= 1) {
-                for (int j = k2 >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P; i += 256) {
-                        const int ixj = i ^ j;
-                        if (ixj > i) {
-                            const uint64_t a = sm.sortb[i], c = sm.sortb[ixj];
-                            const bool desc = (i & k2) == 0;
-                            if (desc ? (a < c) : (a > c)) { sm.sortb[i] = c; sm.sortb[ixj] = a; }
+            if (nV <= 4 * 256) {
+                // rank sort, descending: a key's position is the number of larger keys (keys
+                // are unique: they end in the node index); two barriers instead of bitonic's
+                // log^2 stages
+                uint64_t key[4];
+                int rank[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = tid + 256 * u;
+                    key[u] = i < nV ? sm.sortb[i] : 0;
+                    rank[u] = 0;
+                }
+                for (int j = 0; j < nV; ++j) {
+                    const uint64_t kj = sm.sortb[j];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) rank[u] += kj > key[u] ? 1 : 0;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (tid + 256 * u < nV) sm.sortb[rank[u]] = key[u];
+            } else {
+                int P = 1;
+                while (P < nV) P <<= 1;
+                for (int i = nV + tid; i < P; i += 256) sm.sortb[i] = 0;
+                __syncthreads();
+                for (int k2 = 2; k2 <= P; k2 <<= 1) {
+                    for (int j = k2 >> 1; j > 0; j >>= 1) {
+                        for (int i = tid; i < P; i += 256) {
+                            const int ixj = i ^ j;
+                            if (ixj > i) {
+                                const uint64_t a = sm.sortb[i], c = sm.sortb[ixj];
+                                const bool desc = (i & k2) == 0;
+                                if (desc ? (a < c) : (a > c)) { sm.sortb[i] = c; sm.sortb[ixj] = a; }
+                            }
                         }
+                        __syncthreads();
                     }
-                    __syncthreads();
                 }
             }
             // running size after processing j (descending order); stop once >= N
@@ -850,7 +915,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     hipError_t err = launch_levels(a, st);
     if (err != hipSuccess) return err;
     hipEvent_t e = T.start(st);
-    hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 3) / 4, a.batch), dim3(256), fast_lds_bytes(G), st,
+    hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch), dim3(256),
+                       fast_lds_bytes(G), st,
                        a.dg, a.cells, a.pyr, a.ccnt, a.cand);
     T.stop(K_FAST, e, st);
     e = T.start(st);
