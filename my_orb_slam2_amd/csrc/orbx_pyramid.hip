@@ -131,7 +131,34 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     // window row pitch; modes 0/1 place x at column x - (X0 - 4) so that groups are dword-aligned
     const int WP = (mode == 3) ? ((WWb + 3) & ~3) : LT_G * 4;
     const int wcol0 = (mode == 3) ? 0 : wx0 - (X0 - 4);
-    if (mode == 0) {
+    // level 0 away from the image border: the halo tile is the input itself, loaded straight
+    // into the level array (two aligned dwords + v_alignbyte per 4-pixel group)
+    const bool direct = mode == 0 && X0 >= 4 && X0 + LT_W + 8 <= L.w && Y0 >= 3 &&
+                        Y0 + LT_H + 3 <= L.h;
+    if (direct) {
+        const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
+        constexpr int NI = (LT_HR * LT_G + 255) / 256;
+        static_assert(256 / LT_G == 7 && 256 % LT_G == 18, "halo item stride");
+        uint32_t d0[NI], d1[NI], sh[NI];
+        int hr = tid / LT_G, q = tid - hr * LT_G;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int hrc = min(hr, LT_HR - 1);
+            const uintptr_t a = (uintptr_t)(src + __umul24(Y0 - 3 + hrc, (uint32_t)stride) + (X0 - 4 + 4 * q));
+            const uint32_t* ab = (const uint32_t*)(a & ~(uintptr_t)3);
+            sh[k] = (uint32_t)(a & 3);
+            d0[k] = ab[0];
+            d1[k] = ab[1];
+            hr += 7;
+            q += 18;
+            if (q >= LT_G) { q -= LT_G; ++hr; }
+        }
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int i = tid + 256 * k;
+            if (i < LT_HR * LT_G) lvl[i] = __builtin_amdgcn_alignbyte(d1[k], d0[k], sh[k]);
+        }
+    } else if (mode == 0) {
         const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
         stage_bytes<256>(src + (size_t)wy0 * stride + wx0, stride, WH, WWb, win + wcol0, WP, tid);
     } else if (mode == 1) {
@@ -156,9 +183,9 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
     // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
-    static_assert(256 / LT_G == 7 && 256 % LT_G == 18, "halo item stride");
     int hr = tid / LT_G, q = tid - hr * LT_G;
-    for (int i = tid; i < LT_HR * LT_G; i += 256, hr += 7, q += 18, (q >= LT_G ? (q -= LT_G, ++hr) : 0)) {
+    for (int i = direct ? LT_HR * LT_G : tid; i < LT_HR * LT_G;
+         i += 256, hr += 7, q += 18, (q >= LT_G ? (q -= LT_G, ++hr) : 0)) {
         const int y = Y0 - 3 + hr, xg = X0 - 4 + 4 * q;
         uint32_t out = 0;
         if (y >= ny0 && y <= ny1 && xg + 3 >= nx0 && xg <= nx1) {
