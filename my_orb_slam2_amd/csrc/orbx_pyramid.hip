@@ -211,20 +211,38 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                     const uint32_t* d1p = (const uint32_t*)(w1 + base);
                     const uint32_t a0 = d0p[0], a1 = d0p[1], a2 = d0p[2];
                     const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind; 24-bit
+                    // multiplies (full rate): h < 2^19, b <= 2048.  Groups whose 4 pixels all
+                    // take the SSE2 form (all but the right edge) skip the scalar form.
+                    const bool all_simd = ((ci >> 1) & 0x55u) == 0x55u;
+                    auto hsum = [&](int j, int& h0, int& h1) {
                         const bool hi = (ci >> (12 + j)) & 1u;
                         const uint32_t p0 = __builtin_amdgcn_perm(hi ? a2 : a1, hi ? a1 : a0, sels[j]);
                         const uint32_t p1 = __builtin_amdgcn_perm(hi ? c2 : c1, hi ? c1 : c0, sels[j]);
                         const us2 al = __builtin_bit_cast(us2, als[j]);
-                        const int h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
-                        const int h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
-                        // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind
-                        // 24-bit multiplies (full rate): h < 2^19, b <= 2048
-                        const int vs = min(((int)(__umul24(h0 >> 4, b0) >> 16) +
-                                            (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2, 255);
-                        const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
-                        out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
+                        h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
+                        h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
+                    };
+                    auto vsimd = [&](int h0, int h1) {
+                        return min(((int)(__umul24(h0 >> 4, b0) >> 16) +
+                                    (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2, 255);
+                    };
+                    if (all_simd) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            int h0, h1;
+                            hsum(j, h0, h1);
+                            out |= (uint32_t)vsimd(h0, h1) << (8 * j);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            int h0, h1;
+                            hsum(j, h0, h1);
+                            const int vs = vsimd(h0, h1);
+                            const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+                            out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
+                        }
                     }
                 } else {   // reflected border group: bytes one by one
 #pragma unroll
