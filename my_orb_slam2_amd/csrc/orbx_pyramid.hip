@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
         rinf[tid - 64] = make_uint2(tc.x, tc.y);
     }
     __syncthreads();
+    STAMP(2);
 
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only

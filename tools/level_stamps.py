@@ -13,9 +13,12 @@ from my_orb_slam2_amd import build as b  # noqa: E402
 
 DIAG = os.path.join(ROOT, "tools", "_diag", "liborbx_diag.so")
 os.makedirs(os.path.dirname(DIAG), exist_ok=True)
-if not os.path.exists(DIAG):
-    srcs = [str(b.CSRC / s) for s in b.SOURCES if (b.CSRC / s).exists()]
+srcs = [str(b.CSRC / s) for s in b.SOURCES if (b.CSRC / s).exists()]
+newest = max(os.path.getmtime(str(b.CSRC / f)) for f in os.listdir(b.CSRC))
+if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < newest:
     subprocess.run([b.hipcc()] + b.FLAGS + ["-DORBX_STAMPS"] + srcs + ["-o", DIAG], check=True)
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    sys.exit(0)
 import torch  # noqa: E402
 from my_orb_slam2_amd import _lib, synth  # noqa: E402
 _lib._lib = _lib.load(DIAG)
