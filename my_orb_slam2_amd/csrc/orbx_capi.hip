@@ -54,8 +54,8 @@ struct orbx_extractor {
     std::vector<CellDesc> cells;
     std::vector<int16_t> rtab;
     std::vector<uint8_t> ltab;   // k_level per-tile tables (LevelColTab / LevelRowTab)
-    int ncap = 0, kcap = 0;
-    size_t octree_lds = 0, stereo_lds = 0, level_lds = 0;
+    int ncap = 0, kcap = 0, ncap1 = 0, kcap1 = 0;
+    size_t octree_lds = 0, octree_lds1 = 0, stereo_lds = 0, level_lds = 0;
     int cap_batch = 0;
     DevBuf d_geom, d_cells, d_rtab, d_ltab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
@@ -455,12 +455,31 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     h->kscratch_per_image = 0;
     for (int l = 0; l < L; ++l) h->kscratch_per_image += (long long)G.lv[l].cand_cap * 8;
     h->kscratch_per_image = (long long)align_up((size_t)std::max(h->kscratch_per_image, 16LL), 256);
-    // octree LDS: node arrays for the largest list, candidate arrays up to kcap in LDS
-    h->ncap = (int)align_up((size_t)G.max_out_cap, 16);
-    int kcap = std::min(std::max(G.max_ncand_level, 64), 8192);
+    // octree LDS: node arrays for the largest list, candidate arrays up to kcap in LDS (a
+    // level with more candidates keeps them in global scratch).  Level 0 gets up to 96 KiB;
+    // levels 1.. run as a second launch sized to fit three workgroups per CU.
+    int ncand0 = 0, ncand1 = 0, oc1 = 16;
+    {
+        int c = 0;
+        for (int l = 0; l < L; ++l) {
+            int n = 0;
+            for (int k = 0; k < G.lv[l].ncells; ++k) n += h->cells[G.lv[l].cell_begin + k].cap;
+            if (l == 0) ncand0 = n; else ncand1 = std::max(ncand1, n);
+            if (l > 0) oc1 = std::max(oc1, G.lv[l].out_cap);
+            c += n;
+        }
+        (void)c;
+    }
+    h->ncap = (int)align_up((size_t)G.lv[0].out_cap, 16);
+    int kcap = std::min(std::max(ncand0, 64), 8192);
     while (kcap > 64 && octree_lds_bytes(h->ncap, kcap) > 96 * 1024) kcap -= 64;
     h->kcap = kcap;
     h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
+    h->ncap1 = (int)align_up((size_t)oc1, 16);
+    int kcap1 = std::min(std::max(ncand1, 64), 8192);
+    while (kcap1 > 64 && octree_lds_bytes(h->ncap1, kcap1) > 52 * 1024) kcap1 -= 64;
+    h->kcap1 = kcap1;
+    h->octree_lds1 = octree_lds_bytes(h->ncap1, h->kcap1);
     h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h);
     if (h->octree_lds > 160 * 1024 || h->stereo_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     if (G.kp_cap > 32767) return ORBX_ERR_UNSUPPORTED;   // 16-bit keypoint indices in stereo
@@ -537,6 +556,9 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.ncap = h->ncap;
     a.kcap = h->kcap;
     a.octree_lds = h->octree_lds;
+    a.ncap1 = h->ncap1;
+    a.kcap1 = h->kcap1;
+    a.octree_lds1 = h->octree_lds1;
     a.kps = h->d_kps.as<float>();
     a.desc = h->d_desc.as<uint8_t>();
     a.nkp = h->d_nkp.as<int>();

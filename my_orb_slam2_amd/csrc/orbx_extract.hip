@@ -694,9 +694,10 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
                                                 const uint32_t* __restrict__ cand,
                                                 int* __restrict__ ocnt, uint32_t* __restrict__ okp,
                                                 uint8_t* __restrict__ kscratch,
-                                                long long kscratch_per_image, int NCAP, int KCAP) {
+                                                long long kscratch_per_image, int NCAP, int KCAP,
+                                                int level_base) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int level = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int level = level_base + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const LevelGeom& L = g->lv[level];
     // carve LDS
     uint8_t* p = smem;
@@ -920,9 +921,13 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                        a.dg, a.cells, a.pyr, a.ccnt, a.cand);
     T.stop(K_FAST, e, st);
     e = T.start(st);
-    hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
-                       a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
-                       a.ncap, a.kcap);
+    hipLaunchKernelGGL(k_octree, dim3(1, a.batch), dim3(256), a.octree_lds, st, a.dg, a.cells,
+                       a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, a.ncap,
+                       a.kcap, 0);
+    if (G.nlevels > 1)
+        hipLaunchKernelGGL(k_octree, dim3(G.nlevels - 1, a.batch), dim3(256), a.octree_lds1, st,
+                           a.dg, a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch,
+                           a.kscratch_per_image, a.ncap1, a.kcap1, 1);
     T.stop(K_OCTREE, e, st);
     e = T.start(st);
     hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,

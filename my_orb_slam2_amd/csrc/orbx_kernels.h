@@ -81,8 +81,10 @@ struct ExtractLaunch {
     uint32_t* okp;
     uint8_t* kscratch;
     long long kscratch_per_image;
-    int ncap, kcap;
+    int ncap, kcap;          // level 0 (the largest node list)
     size_t octree_lds;
+    int ncap1, kcap1;        // levels 1.. (a second launch with a smaller LDS footprint)
+    size_t octree_lds1;
     float* kps;
     uint8_t* desc;
     int* nkp;
