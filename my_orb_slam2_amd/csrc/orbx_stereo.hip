@@ -181,11 +181,34 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         const uint8_t* PL = pyrL + (size_t)b * g->pyr_bytes + LV.off;
         const uint8_t* PR = pyrR + (size_t)b * g->pyr_bytes + LV.off;
         const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
+        // all 11 row pairs of the window are loaded before any is used (one memory latency
+        // per keypoint instead of one per row): left x-5..x+5 (4 dwords), right x-10..x+10
+        // (7 dwords), realigned with v_alignbyte
+        const uint32_t* pl0 = (const uint32_t*)(PL + (size_t)(yl - w) * pitch + ((xl - w) & ~3));
+        const uint32_t* pr0 = (const uint32_t*)(PR + (size_t)(yl - w) * pitch + ((xr - L5 - w) & ~3));
+        const int shl = (xl - w) & 3, shr = (xr - L5 - w) & 3;
+        const int pdw = pitch >> 2;   // rows are 64-byte aligned
+        uint32_t lraw[11][4], rraw[11][7];
+#pragma unroll
+        for (int r = 0; r < 11; ++r) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lraw[r][i] = pl0[r * pdw + i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) rraw[r][i] = pr0[r * pdw + i];
+        }
+        auto lrow = [&](int r, uint32_t (&o)[3]) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) o[i] = __builtin_amdgcn_alignbyte(lraw[r][i + 1], lraw[r][i], shl);
+        };
+        auto rrow = [&](int r, uint32_t (&o)[6]) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) o[i] = __builtin_amdgcn_alignbyte(rraw[r][i + 1], rraw[r][i], shr);
+        };
         int cL, cR[11];
         {
             uint32_t lc[3], rc[6];
-            load_row<3>(PL + (size_t)yl * pitch, xl - w, lc);
-            load_row<6>(PR + (size_t)yl * pitch, xr - L5 - w, rc);
+            lrow(w, lc);
+            rrow(w, rc);
             cL = byte_of(lc, 5);
 #pragma unroll
             for (int k = 0; k < 11; ++k) cR[k] = byte_of(rc, k + 5);
@@ -193,10 +216,11 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         int acc[11];
 #pragma unroll
         for (int k = 0; k < 11; ++k) acc[k] = 0;
-        for (int yy = -w; yy <= w; ++yy) {
+#pragma unroll
+        for (int r = 0; r < 11; ++r) {
             uint32_t lw[3], rw[6];
-            load_row<3>(PL + (size_t)(yl + yy) * pitch, xl - w, lw);
-            load_row<6>(PR + (size_t)(yl + yy) * pitch, xr - L5 - w, rw);
+            lrow(r, lw);
+            rrow(r, rw);
 #pragma unroll
             for (int xx = 0; xx < 11; ++xx) {
                 const int il = byte_of(lw, xx) - cL;
