@@ -20,7 +20,7 @@
 
 namespace orbx {
 
-#define ST_THREADS 512
+#define ST_THREADS 1024
 #define ST_WAVES (ST_THREADS / 64)
 
 // N bytes of a pyramid row starting at x, as ceil(N/4) dwords realigned to x (bytes of
