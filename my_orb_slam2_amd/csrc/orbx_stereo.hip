@@ -60,15 +60,11 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     uint8_t* p = smem;
     auto take = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
     int* tmp = (int*)take(32 * 4);
-    uint4* rdesc = (uint4*)take((size_t)KC * 32);
+    uint4* rdesc = (uint4*)take((size_t)KC * 32);   // in row-bucket order
     int* rowstart = (int*)take((size_t)(H + 1) * 4);
     int* cursor = (int*)take((size_t)(H + 1) * 4);
-    int16_t* bucket = (int16_t*)take((size_t)KC * 2);
-    float* rx = (float*)take((size_t)KC * 4);
-    int16_t* rmin = (int16_t*)take((size_t)KC * 2);
-    int16_t* rmax = (int16_t*)take((size_t)KC * 2);
-    int16_t* rrow = (int16_t*)take((size_t)KC * 2);
-    int8_t* roct = (int8_t*)take((size_t)KC);
+    // per right keypoint, in row-bucket order: (uR bits, rmin | rmax << 16, oct | iR << 16)
+    uint3* rrec = (uint3*)take((size_t)KC * 12);
     int* vsad = (int*)take((size_t)KC * 4);
     int16_t* vidx = (int16_t*)take((size_t)KC * 2);
     int* hist = (int*)take(256 * 4);
@@ -80,33 +76,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     float* dep = depth + (size_t)b * KC;
     for (int i = tid; i <= H; i += ST_THREADS) rowstart[i] = 0;
     if (tid == 0) tmp[16] = 0;
-    {   // right descriptors -> LDS (2 x 16 B per keypoint, loads issued before stores)
-        const uint4* src = (const uint4*)(descR + (size_t)b * KC * 32);
-        for (int base = 0; base < 2 * NR; base += ST_THREADS * 4) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = src[min(base + k * ST_THREADS + tid, 2 * NR - 1)];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int i = base + k * ST_THREADS + tid;
-                if (i < 2 * NR) rdesc[i] = v[k];
-            }
-        }
-    }
     __syncthreads();
 
-    // 1. right keypoints -> rows (src/Frame.cc:516-531)
+    // 1. right keypoints -> rows (src/Frame.cc:516-531): counts, a scan, then each keypoint's
+    //    record and descriptor written at its bucket position
     for (int iR = tid; iR < NR; iR += ST_THREADS) {
         const float ky = kR[iR * 7 + 1];
-        const int oct = ((const int*)kR)[iR * 7 + 5];
-        const float r = 2.0f * g->lv[oct].scale;
-        rmax[iR] = (int16_t)(int)ceilf(ky + r);
-        rmin[iR] = (int16_t)(int)floorf(ky - r);
-        rx[iR] = kR[iR * 7 + 0];
-        roct[iR] = (int8_t)oct;
-        const int row = min(max((int)ky, 0), H - 1);
-        rrow[iR] = (int16_t)row;
-        atomicAdd(&rowstart[row], 1);
+        atomicAdd(&rowstart[min(max((int)ky, 0), H - 1)], 1);
     }
     __syncthreads();
     {
@@ -121,9 +97,21 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
     }
     __syncthreads();
-    for (int iR = tid; iR < NR; iR += ST_THREADS) {
-        const int pos = atomicAdd(&cursor[rrow[iR]], 1);
-        bucket[pos] = (int16_t)iR;
+    {
+        const uint4* src = (const uint4*)(descR + (size_t)b * KC * 32);
+        for (int iR = tid; iR < NR; iR += ST_THREADS) {
+            const uint4 d0 = src[2 * iR], d1 = src[2 * iR + 1];
+            const float kx = kR[iR * 7 + 0], ky = kR[iR * 7 + 1];
+            const int oct = ((const int*)kR)[iR * 7 + 5];
+            const float r = 2.0f * g->lv[oct].scale;
+            const int mx = (int)ceilf(ky + r), mn = (int)floorf(ky - r);
+            const int pos = atomicAdd(&cursor[min(max((int)ky, 0), H - 1)], 1);
+            rrec[pos] = make_uint3(__float_as_uint(kx),
+                                   (uint32_t)(uint16_t)mn | ((uint32_t)(uint16_t)mx << 16),
+                                   (uint32_t)oct | ((uint32_t)iR << 16));
+            rdesc[2 * pos] = d0;
+            rdesc[2 * pos + 1] = d1;
+        }
     }
     __syncthreads();
 
@@ -147,20 +135,24 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         int best = 100, bestR = -1;   // ORBmatcher::TH_HIGH, strict '<': first minimum wins
         const int r0 = max(row - g->stereo_win, 0), r1 = min(row + g->stereo_win, H - 1);
         const int e1 = rowstart[r1 + 1];
+        int bestE = -1;
         for (int e = rowstart[r0]; e < e1; ++e) {
-            const int iR = bucket[e];
-            if (rmin[iR] > row || rmax[iR] < row) continue;
-            const int o = roct[iR];
+            const uint3 rc = rrec[e];
+            const int mn = (int)(int16_t)(rc.y & 0xFFFF), mx = (int)(int16_t)(rc.y >> 16);
+            if (mn > row || mx < row) continue;
+            const int o = (int)(rc.z & 0xFFFF);
             if (o < levelL - 1 || o > levelL + 1) continue;
-            const float u = rx[iR];
+            const float u = __uint_as_float(rc.x);
             if (u >= minU && u <= maxU) {
-                const uint4 a = rdesc[2 * iR], c = rdesc[2 * iR + 1];
+                const int iR = (int)(rc.z >> 16);
+                const uint4 a = rdesc[2 * e], c = rdesc[2 * e + 1];
                 const int dist = __popc(dl0.x ^ a.x) + __popc(dl0.y ^ a.y) + __popc(dl0.z ^ a.z) +
                                  __popc(dl0.w ^ a.w) + __popc(dl1.x ^ c.x) + __popc(dl1.y ^ c.y) +
                                  __popc(dl1.z ^ c.z) + __popc(dl1.w ^ c.w);
                 if (dist < best || (dist == best && bestR >= 0 && iR < bestR)) {
                     best = dist;
                     bestR = iR;
+                    bestE = e;
                 }
             }
         }
@@ -168,7 +160,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
 
         // ---- sliding-window SAD on the unblurred level of the left keypoint ----
         const LevelGeom& LV = g->lv[levelL];
-        const float uR0 = rx[bestR];
+        const float uR0 = __uint_as_float(rrec[bestE].x);
         const float sf = LV.inv_scale;
         const float scaleduL = roundf(uL * sf);
         const float scaledvL = roundf(vL * sf);
@@ -323,7 +315,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
 size_t stereo_lds_bytes(int kp_cap, int height) {
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t s = r(32 * 4) + r((size_t)kp_cap * 32) + 2 * r((size_t)(height + 1) * 4);
-    s += r((size_t)kp_cap * 2) + r((size_t)kp_cap * 4) + 3 * r((size_t)kp_cap * 2) + r(kp_cap);
+    s += r((size_t)kp_cap * 12);
     s += r((size_t)kp_cap * 4) + r((size_t)kp_cap * 2) + r(256 * 4);
     return s;
 }
