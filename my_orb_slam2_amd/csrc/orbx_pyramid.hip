@@ -84,6 +84,118 @@ __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1, bool simd
     return sat8((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22));   // FixedPtCast<int, uchar, 22>
 }
 
+struct BlurTaps {
+    uint32_t tapA, tapB;   // v_dot4 taps k0..k3 / k4..k6,0 (row pass)
+    uint32_t K4, K5, K6;   // (k, k) u16 pairs (column pass)
+    uint32_t k3;
+};
+
+// ---- 3. level tile out (output x = X0 + 4g  <->  halo group g + 1) ----
+// ---- 4. blur row pass (RowFilter<uchar,int>: exact; sums <= 257*255 fit u16) ----
+// pixel x = X0+4gq+j needs halo bytes 1+j .. 7+j: two v_dot4_u32_u8 over the byte runs
+// 1+j..4+j (taps k0..k3) and 5+j..8+j (taps k4..k6, 0).  FULL: a 128 x 32 tile, fixed trip
+// counts (no per-item bounds, whole-dword stores).
+template <bool FULL>
+__device__ __forceinline__ void tile_out_rows(const uint32_t* lvl, uint16_t* rows, int tid, int vw,
+                                              int vh, uint8_t* dlev, int X0, int Y0, int pitch,
+                                              const BlurTaps& tp) {
+    const int ng = FULL ? LT_GW : (vw + 3) >> 2;
+    const int n3 = FULL ? LT_H * LT_GW : vh * LT_GW;
+    auto out_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        const uint32_t v = lvl[(r + 3) * LT_G + gq + 1];
+        uint8_t* d = dlev + __umul24(Y0 + r, pitch) + X0 + 4 * gq;
+        if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = v;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
+    };
+    if constexpr (FULL) {
+        static_assert((LT_H * LT_GW) % 256 == 0, "full-tile item count");
+#pragma unroll
+        for (int k = 0; k < LT_H * LT_GW / 256; ++k) out_item(tid + 256 * k);
+    } else {
+        for (int i = tid; i < n3; i += 256) out_item(i);
+    }
+    const int n4 = FULL ? (LT_H + 6) * LT_GW : (vh + 6) * LT_GW;
+    auto row_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        const uint32_t* s = lvl + r * LT_G + gq;   // bytes of x = X0 + 4gq - 4 .. + 7
+        const uint32_t d0 = s[0], d1 = s[1], d2 = s[2];
+        uint32_t sum[4];
+        sum[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tp.tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), tp.tapB, 0u, false), false);
+        sum[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tp.tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), tp.tapB, 0u, false), false);
+        sum[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tp.tapA,
+                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tp.tapB, 0u, false), false);
+        sum[3] = __builtin_amdgcn_udot4(d1, tp.tapA, __builtin_amdgcn_udot4(d2, tp.tapB, 0u, false), false);
+        const uint32_t lo = sum[0] | (sum[1] << 16), hi = sum[2] | (sum[3] << 16);
+        *(uint2*)(rows + r * LT_W + 4 * gq) = make_uint2(lo, hi);
+    };
+    if constexpr (FULL) {
+        constexpr int K4 = ((LT_H + 6) * LT_GW) / 256, R4 = ((LT_H + 6) * LT_GW) % 256;
+#pragma unroll
+        for (int k = 0; k < K4; ++k) row_item(tid + 256 * k);
+        if (tid < R4) row_item(tid + 256 * K4);
+    } else {
+        for (int i = tid; i < n4; i += 256) row_item(i);
+    }
+}
+
+// ---- 5. blur column pass (SymmColumnFilter / SymmColumnVec_32s8u) ----
+// The SSE2 float form s = c0*f0 + p1*f1 + p2*f2 + p3*f3 (f = k/65536) is exact here:
+// every product k*v is an integer < 2^24 scaled by a power of two, and every partial
+// sum S = k3*c0 + k4*p1 + ... stays exact while S < 2^24 (partials only grow); at
+// S >= 2^24 both forms give >= 256 and saturate to 255.  So rintf(S/65536) is
+// round-half-even of the integer S, and the scalar tail is (S + 32768) >> 16.
+// S_j = k3*c + k4*(r2+r4) + k5*(r1+r5) + k6*(r0+r6): per pixel three v_perm pair the
+// symmetric rows' u16 sums and four v_dot2_u32_u16 accumulate (S < 2^24: exact).
+template <bool FULL>
+__device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int vw, int vh,
+                                             uint8_t* dblur, int X0, int Y0, int pitch,
+                                             int bsimd_end, const BlurTaps& tp) {
+    const int ng = FULL ? LT_GW : (vw + 3) >> 2;
+    const int n5 = FULL ? LT_H * LT_GW : vh * LT_GW;
+    const uint32_t K3lo = tp.k3, K3hi = tp.k3 << 16;
+    auto col_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        uint2 v[7];
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) v[kk] = *(const uint2*)(rows + (r + kk) * LT_W + 4 * gq);
+        const int xg = X0 + 4 * gq;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto dw = [&](int kk) { return (j < 2) ? v[kk].x : v[kk].y; };
+            const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;   // (a.hi, b.hi) / (a.lo, b.lo)
+            const us2 p06 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(6), dw(0), sel));
+            const us2 p15 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(5), dw(1), sel));
+            const us2 p24 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(4), dw(2), sel));
+            uint32_t S = __builtin_amdgcn_udot2(p06, __builtin_bit_cast(us2, tp.K6), 0u, false);
+            S = __builtin_amdgcn_udot2(p15, __builtin_bit_cast(us2, tp.K5), S, false);
+            S = __builtin_amdgcn_udot2(p24, __builtin_bit_cast(us2, tp.K4), S, false);
+            S = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, dw(3)),
+                                       __builtin_bit_cast(us2, (j & 1) ? K3hi : K3lo), S, false);
+            const bool simd = xg + j < bsimd_end;
+            const uint32_t val = (S + (simd ? 32767u + ((S >> 16) & 1u) : 32768u)) >> 16;
+            packed |= min(val, 255u) << (8 * j);
+        }
+        uint8_t* d = dblur + __umul24(Y0 + r, pitch) + xg;
+        if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = packed;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+    };
+    if constexpr (FULL) {
+#pragma unroll
+        for (int k = 0; k < LT_H * LT_GW / 256; ++k) col_item(tid + 256 * k);
+    } else {
+        for (int i = tid; i < n5; i += 256) col_item(i);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
                                                const uint8_t* __restrict__ ltab,
                                                const uint8_t* __restrict__ in0,
@@ -286,81 +398,20 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
 
     uint8_t* dlev = pyr + (size_t)b * g->pyr_bytes + L.off;
     uint8_t* dblur = blur + (size_t)b * g->pyr_bytes + L.off;
-    const int ng = (vw + 3) >> 2;
-    // ---- 3. level tile out (output x = X0 + 4g  <->  halo group g + 1) ----
-    for (int i = tid; i < vh * LT_GW; i += 256) {
-        const int r = i / LT_GW, gq = i - r * LT_GW;
-        if (gq >= ng) continue;
-        const uint32_t v = lvl[(r + 3) * LT_G + gq + 1];
-        uint8_t* d = dlev + __umul24(Y0 + r, L.pitch) + X0 + 4 * gq;
-        if (4 * gq + 4 <= vw) *(uint32_t*)d = v;
-        else
-            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
-    }
-    // ---- 4. blur row pass (RowFilter<uchar,int>: exact; sums <= 257*255 fit u16) ----
-    // pixel x = X0+4gq+j needs halo bytes 1+j .. 7+j: two v_dot4_u32_u8 over the byte runs
-    // 1+j..4+j (taps k0..k3) and 5+j..8+j (taps k4..k6, 0)
     const int k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3];
     const int k4 = g->taps[4], k5 = g->taps[5], k6 = g->taps[6];
-    const uint32_t tapA = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24;
-    const uint32_t tapB = (uint32_t)k4 | (uint32_t)k5 << 8 | (uint32_t)k6 << 16;
-    for (int i = tid; i < (vh + 6) * LT_GW; i += 256) {
-        const int r = i / LT_GW, gq = i - r * LT_GW;
-        if (gq >= ng) continue;
-        const uint32_t* s = lvl + r * LT_G + gq;   // bytes of x = X0 + 4gq - 4 .. + 7
-        const uint32_t d0 = s[0], d1 = s[1], d2 = s[2];
-        uint32_t sum[4];
-        sum[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tapA,
-                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), tapB, 0u, false), false);
-        sum[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tapA,
-                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), tapB, 0u, false), false);
-        sum[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tapA,
-                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tapB, 0u, false), false);
-        sum[3] = __builtin_amdgcn_udot4(d1, tapA, __builtin_amdgcn_udot4(d2, tapB, 0u, false), false);
-        const uint32_t lo = sum[0] | (sum[1] << 16), hi = sum[2] | (sum[3] << 16);
-        *(uint2*)(rows + r * LT_W + 4 * gq) = make_uint2(lo, hi);
-    }
+    const BlurTaps tp = {(uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24,
+                         (uint32_t)k4 | (uint32_t)k5 << 8 | (uint32_t)k6 << 16,
+                         (uint32_t)k4 * 0x10001u, (uint32_t)k5 * 0x10001u, (uint32_t)k6 * 0x10001u,
+                         (uint32_t)k3};
+    // full tiles (all but the right / bottom edge) run the fixed-trip-count form
+    const bool full = vw == LT_W && vh == LT_H;
+    if (full) tile_out_rows<true>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
+    else tile_out_rows<false>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     __syncthreads();
     STAMP(4);
-    // ---- 5. blur column pass (SymmColumnFilter / SymmColumnVec_32s8u) ----
-    // The SSE2 float form s = c0*f0 + p1*f1 + p2*f2 + p3*f3 (f = k/65536) is exact here:
-    // every product k*v is an integer < 2^24 scaled by a power of two, and every partial
-    // sum S = k3*c0 + k4*p1 + ... stays exact while S < 2^24 (partials only grow); at
-    // S >= 2^24 both forms give >= 256 and saturate to 255.  So rintf(S/65536) is
-    // round-half-even of the integer S, and the scalar tail is (S + 32768) >> 16.
-    // S_j = k3*c + k4*(r2+r4) + k5*(r1+r5) + k6*(r0+r6): per pixel three v_perm pair the
-    // symmetric rows' u16 sums and four v_dot2_u32_u16 accumulate (S < 2^24: exact).
-    const uint32_t K4 = (uint32_t)k4 * 0x10001u, K5 = (uint32_t)k5 * 0x10001u;
-    const uint32_t K6 = (uint32_t)k6 * 0x10001u, K3lo = (uint32_t)k3, K3hi = (uint32_t)k3 << 16;
-    for (int i = tid; i < vh * LT_GW; i += 256) {
-        const int r = i / LT_GW, gq = i - r * LT_GW;
-        if (gq >= ng) continue;
-        uint2 v[7];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) v[k] = *(const uint2*)(rows + (r + k) * LT_W + 4 * gq);
-        const int xg = X0 + 4 * gq;
-        uint32_t packed = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            auto dw = [&](int k) { return (j < 2) ? v[k].x : v[k].y; };
-            const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;   // (a.hi, b.hi) / (a.lo, b.lo)
-            const us2 p06 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(6), dw(0), sel));
-            const us2 p15 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(5), dw(1), sel));
-            const us2 p24 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(dw(4), dw(2), sel));
-            uint32_t S = __builtin_amdgcn_udot2(p06, __builtin_bit_cast(us2, K6), 0u, false);
-            S = __builtin_amdgcn_udot2(p15, __builtin_bit_cast(us2, K5), S, false);
-            S = __builtin_amdgcn_udot2(p24, __builtin_bit_cast(us2, K4), S, false);
-            S = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, dw(3)),
-                                       __builtin_bit_cast(us2, (j & 1) ? K3hi : K3lo), S, false);
-            const bool simd = xg + j < L.bsimd_end;
-            const uint32_t val = (S + (simd ? 32767u + ((S >> 16) & 1u) : 32768u)) >> 16;
-            packed |= min(val, 255u) << (8 * j);
-        }
-        uint8_t* d = dblur + __umul24(Y0 + r, L.pitch) + xg;
-        if (4 * gq + 4 <= vw) *(uint32_t*)d = packed;
-        else
-            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
-    }
+    if (full) tile_columns<true>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+    else tile_columns<false>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
     STAMP(5);
 }
 
