@@ -296,12 +296,11 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
     // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
-    int hr = tid / LT_G, q = tid - hr * LT_G;
-    for (int i = direct ? LT_HR * LT_G : tid; i < LT_HR * LT_G;
-         i += 256, hr += 7, q += 18, (q >= LT_G ? (q -= LT_G, ++hr) : 0)) {
+    const bool full_tile = vw == LT_W && vh == LT_H;   // every halo item is needed
+    auto level_item = [&](int hr, int q, bool all) {
         const int y = Y0 - 3 + hr, xg = X0 - 4 + 4 * q;
         uint32_t out = 0;
-        if (y >= ny0 && y <= ny1 && xg + 3 >= nx0 && xg <= nx1) {
+        if (all || (y >= ny0 && y <= ny1 && xg + 3 >= nx0 && xg <= nx1)) {
             const uint2 cg = cgrp[q];
             const uint32_t ci = cinf[q];
             const uint2 ri = rinf[hr];
@@ -392,6 +391,24 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
             }
         }
         lvl[hr * LT_G + q] = out;
+    };
+    if (!direct) {
+        int hr = tid / LT_G, q = tid - hr * LT_G;
+        if (full_tile) {
+            constexpr int KF = (LT_HR * LT_G) / 256, RF = (LT_HR * LT_G) % 256;
+#pragma unroll
+            for (int k = 0; k < KF; ++k) {
+                level_item(hr, q, true);
+                hr += 7;
+                q += 18;
+                if (q >= LT_G) { q -= LT_G; ++hr; }
+            }
+            if (tid < RF) level_item(hr, q, true);
+        } else {
+            for (int i = tid; i < LT_HR * LT_G;
+                 i += 256, hr += 7, q += 18, (q >= LT_G ? (q -= LT_G, ++hr) : 0))
+                level_item(hr, q, false);
+        }
     }
     __syncthreads();
     STAMP(3);
