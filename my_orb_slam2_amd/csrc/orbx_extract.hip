@@ -758,21 +758,26 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
 }
 
 // ----------------------------------------------------------------------------------------
-// Orientation + rBRIEF + assembly: one wave per OD_NK keypoints of one level.  The patch
-// loads of keypoint k+1 are in flight while keypoint k is computed from LDS; the per-lane
+// Orientation + rBRIEF + assembly: one wave per OD_NK keypoints of one level, two keypoints at
+// a time (one per half-wave: 32 lanes each), so the per-keypoint scalar work (moments
+// reduction, fastAtan2, sin/cos, outputs) is issued once for two keypoints.  The patch loads
+// of the next pair are in flight while the current pair is computed from LDS; the per-lane
 // patch offsets are the same for every keypoint of the level and are computed once.
 // ----------------------------------------------------------------------------------------
 #define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
 #define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
-#define OD_NLOAD 11    // dword loads per lane: (31 * 9 + 37 * 10) / 64, rounded up
+#define OD_PATCH_DW (31 * OD_RAW_DW + 37 * OD_BLR_DW)   // 649
+#define OD_NLOAD 21    // dword loads per lane per patch: 649 / 32, rounded up
 
-__device__ __forceinline__ int wave_sum_dpp(int v) {
+// Sum over each half-wave (lanes 0-31 / 32-63), returned to every lane of that half.
+__device__ __forceinline__ int half_sum_dpp(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
     v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);   // row_ror:4
     v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);   // row_ror:8
-    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
-           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+    const int lo = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
+    const int hi = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+    return (threadIdx.x & 32) ? hi : lo;
 }
 
 __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict__ g,
@@ -783,9 +788,10 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
                                                      float* __restrict__ kps,
                                                      uint8_t* __restrict__ desc,
                                                      int* __restrict__ nkp) {
-    __shared__ uint32_t patch[4][31 * OD_RAW_DW + 37 * OD_BLR_DW];
+    __shared__ uint32_t patch[4][2][OD_PATCH_DW];
     const int b = blockIdx.y, blk = blockIdx.x;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int half = lane >> 5, l32 = lane & 31;
     int level = 0;
     while (level + 1 < g->nlevels && blk >= g->orient_block_begin[level + 1]) ++level;
     const int i0 = ((blk - g->orient_block_begin[level]) * 4 + wid) * OD_NK;
@@ -806,12 +812,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
 
     // per-lane patch offsets (raw rows first, then blurred rows) relative to the patch bases
-    constexpr int n1 = 31 * OD_RAW_DW, n2 = 37 * OD_BLR_DW;
+    constexpr int n1 = 31 * OD_RAW_DW;
     uint32_t so[OD_NLOAD];
     uint32_t rawbits = 0;
 #pragma unroll
     for (int k = 0; k < OD_NLOAD; ++k) {
-        const int t = min(lane + 64 * k, n1 + n2 - 1);
+        const int t = min(l32 + 32 * k, OD_PATCH_DW - 1);
         const bool isr = t < n1;
         const int tt = isr ? t : t - n1;
         const int row = isr ? tt / OD_RAW_DW : tt / OD_BLR_DW;
@@ -821,8 +827,16 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     }
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
     const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
-    auto issue = [&](int k, uint32_t (&v)[OD_NLOAD]) {
-        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, k);
+    // keypoint of this half-wave in pair p: k = 2p + half (clamped: a lone last keypoint is
+    // computed by both halves, the upper half's results are not written)
+    auto kp_word = [&](int p) {
+        const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cw, k0);
+        const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)cw, k1);
+        return half ? c1 : c0;
+    };
+    auto issue = [&](int p, uint32_t (&v)[OD_NLOAD]) {
+        const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint8_t* pr = pyr_l + __umul24(y - 15, pitch) + ((x - 15) & ~3);
         const uint8_t* pb = blr_l + __umul24(y - 18, pitch) + ((x - 18) & ~3);
@@ -831,77 +845,90 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
             v[j] = *(const uint32_t*)(((rawbits >> j) & 1u ? pr : pb) + so[j]);
     };
 
-    // IC_Angle lane work (src/ORBextractor.cc:77-104): lane l31 < 31 is column u = l31 - 15;
-    // the lower half-wave takes rows v = 1..7 (and the m_10 centre row), the upper v = 8..15.
-    // umax decreases with v, so the rows with |u| <= umax[v] are a prefix [vb, vend).
-    const int half = lane >> 5, l31 = lane & 31;
-    const int u = l31 - 15, au = u < 0 ? -u : u;
-    const int vb = half ? 8 : 1, ve = half ? 16 : 8;
-    int vend = vb;
-    for (int v = vb; v < ve; ++v) vend += (l31 < 31 && au <= g->umax[v]) ? 1 : 0;
+    // IC_Angle lane work (src/ORBextractor.cc:77-104): lane l32 < 31 is column u = l32 - 15 of
+    // its half's keypoint, rows v = 1..15; umax decreases with v, so the rows with
+    // |u| <= umax[v] are a prefix [1, vend).
+    const int u = l32 - 15, au = u < 0 ? -u : u;
+    int vend = 1;
+    for (int v = 1; v < 16; ++v) vend += (l32 < 31 && au <= g->umax[v]) ? 1 : 0;
+
+    // this lane's 8 rBRIEF pairs (q = 32w + l32), converted once
+    float px1[8], py1[8], px2[8], py2[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int q = 32 * w + l32;
+        px1[w] = (float)c_pattern[4 * q];
+        py1[w] = (float)c_pattern[4 * q + 1];
+        px2[w] = (float)c_pattern[4 * q + 2];
+        py2[w] = (float)c_pattern[4 * q + 3];
+    }
 
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    uint32_t* P = patch[wid];
+    uint32_t* P = patch[wid][half];
     const uint8_t* raw = (const uint8_t*)P;                       // [31][36]
     const uint8_t* blr = (const uint8_t*)(P + n1);                // [37][40]
+    const int npair = (nk + 1) >> 1;
     uint32_t v[OD_NLOAD];
     issue(0, v);
-    for (int k = 0; k < nk; ++k) {
-        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cw, k);
+    for (int p = 0; p < npair; ++p) {
+        const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
 #pragma unroll
         for (int j = 0; j < OD_NLOAD; ++j) {
-            const int t = lane + 64 * j;
-            if (t < n1 + n2) P[t] = v[j];
+            const int t = l32 + 32 * j;
+            if (t < OD_PATCH_DW) P[t] = v[j];
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (k + 1 < nk) issue(k + 1, v);   // next patch in flight during this keypoint
+        if (p + 1 < npair) issue(p + 1, v);   // next pair's patches in flight
 
         const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ((x - 15) & ~3));
         int m10 = 0, m01 = 0;
-        if (l31 < 31) {
-            if (!half) m10 = __mul24(u, (int)center[u]);
-            for (int vv = vb; vv < vend; ++vv) {
+        if (l32 < 31) {
+            m10 = __mul24(u, (int)center[u]);
+            for (int vv = 1; vv < vend; ++vv) {
                 const int vp = center[u + vv * (OD_RAW_DW * 4)], vm = center[u - vv * (OD_RAW_DW * 4)];
                 m10 += __mul24(u, vp + vm);
                 m01 += __mul24(vv, vp - vm);
             }
         }
-        m10 = wave_sum_dpp(m10);
-        m01 = wave_sum_dpp(m01);
+        m10 = half_sum_dpp(m10);
+        m01 = half_sum_dpp(m01);
         const float angle = cv_fast_atan2((float)m01, (float)m10);
 
         // computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level.
         const float ang = angle * factorPI;
         const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
         const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ((x - 18) & ~3));
-        uint64_t words[4];
+        uint32_t words[8];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const int q = w * 64 + lane;
-            const float x1 = (float)c_pattern[4 * q], y1 = (float)c_pattern[4 * q + 1];
-            const float x2 = (float)c_pattern[4 * q + 2], y2 = (float)c_pattern[4 * q + 3];
-            const float r1a = x1 * sb, r1b = y1 * ca, c1a = x1 * ca, c1b = y1 * sb;
-            const float r2a = x2 * sb, r2b = y2 * ca, c2a = x2 * ca, c2b = y2 * sb;
+        for (int w = 0; w < 8; ++w) {
+            const float r1a = px1[w] * sb, r1b = py1[w] * ca, c1a = px1[w] * ca, c1b = py1[w] * sb;
+            const float r2a = px2[w] * sb, r2b = py2[w] * ca, c2a = px2[w] * ca, c2b = py2[w] * sb;
             const int t0 = bc[cv_round(r1a + r1b) * (OD_BLR_DW * 4) + cv_round(c1a - c1b)];
             const int t1 = bc[cv_round(r2a + r2b) * (OD_BLR_DW * 4) + cv_round(c2a - c2b)];
-            words[w] = __ballot(t0 < t1);
+            const uint64_t m = __ballot(t0 < t1);
+            words[w] = half ? (uint32_t)(m >> 32) : (uint32_t)m;
         }
-        const size_t o = (size_t)b * g->kp_cap + off + i0 + k;
-        if (lane == 0) {
-            float* kp = kps + o * 7;
-            const float sc = L.scale;
-            kp[0] = level ? (float)x * sc : (float)x;
-            kp[1] = level ? (float)y * sc : (float)y;
-            kp[2] = (float)L.patch_size;
-            kp[3] = angle;
-            kp[4] = (float)s;
-            ((int*)kp)[5] = level;
-            ((int*)kp)[6] = -1;
-        }
-        if (lane < 4) {
-            uint64_t wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-            *(uint64_t*)(desc + o * 32 + lane * 8) = wv;
+        const int k = 2 * p + half;
+        if (k < nk) {
+            const size_t o = (size_t)b * g->kp_cap + off + i0 + k;
+            if (l32 == 0) {
+                float* kp = kps + o * 7;
+                const float sc = L.scale;
+                kp[0] = level ? (float)x * sc : (float)x;
+                kp[1] = level ? (float)y * sc : (float)y;
+                kp[2] = (float)L.patch_size;
+                kp[3] = angle;
+                kp[4] = (float)s;
+                ((int*)kp)[5] = level;
+                ((int*)kp)[6] = -1;
+            }
+            if (l32 < 8) {
+                uint32_t wv = words[0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) wv = l32 == w ? words[w] : wv;
+                *(uint32_t*)(desc + o * 32 + l32 * 4) = wv;
+            }
         }
     }
 }
