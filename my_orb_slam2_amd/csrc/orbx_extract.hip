@@ -130,9 +130,10 @@ __device__ __forceinline__ u16x2 pair_u16(const uint32_t* A, int s_abs) {
 // FAST compass pre-test of 4 adjacent pixels (detection columns 4gx..4gx+3 of ROI row R):
 // a 9-pixel arc beyond the threshold contains two neighbouring compass pixels (circle
 // indices i, i+4) beyond it on the same side.  Packed 16-bit saturating arithmetic, two
-// pixels per instruction: bright_i = (n_i - (v + t))+ , dark_i = ((v - t)+ - n_i)+, and a
-// pixel passes when max over the four neighbouring pairs of min(.,.) is non-zero for either
-// polarity.  XO = the ROI's byte offset in its first LDS dword (roi row = dwords, aligned).
+// pixels per instruction: a pixel passes when, over the four neighbouring compass pairs,
+// max(min(n_i, n_j)) > v + t (both brighter) or min(max(n_i, n_j)) < (v - t)+ (both darker),
+// tested as non-zero saturating differences.  XO = the ROI's byte offset in its first LDS
+// dword (ROI rows are aligned dwords).
 // Returns 4 flag bits, bit j = pixel 4gx+j.
 template <int XO>
 __device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R, int gx, u16x2 T) {
@@ -155,14 +156,14 @@ __device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R,
         const u16x2 V = pair_u16(C, o), N12 = pair_u16(C, o - 3), N4 = pair_u16(C, o + 3);
         const u16x2 N0 = pair_u16(D, o), N8 = pair_u16(U, o);
         const u16x2 HI = V + T, LO = __builtin_elementwise_sub_sat(V, T);
-        const u16x2 b0 = __builtin_elementwise_sub_sat(N0, HI), b4 = __builtin_elementwise_sub_sat(N4, HI);
-        const u16x2 b8 = __builtin_elementwise_sub_sat(N8, HI), b12 = __builtin_elementwise_sub_sat(N12, HI);
-        const u16x2 d0 = __builtin_elementwise_sub_sat(LO, N0), d4 = __builtin_elementwise_sub_sat(LO, N4);
-        const u16x2 d8 = __builtin_elementwise_sub_sat(LO, N8), d12 = __builtin_elementwise_sub_sat(LO, N12);
 #define MN(a, b) __builtin_elementwise_min(a, b)
 #define MX(a, b) __builtin_elementwise_max(a, b)
-        const u16x2 pb = MX(MX(MN(b0, b4), MN(b4, b8)), MX(MN(b8, b12), MN(b12, b0)));
-        const u16x2 pd = MX(MX(MN(d0, d4), MN(d4, d8)), MX(MN(d8, d12), MN(d12, d0)));
+        // a neighbouring pair is all brighter iff its min exceeds v + t, all darker iff its max
+        // is below v - t: compare the best pair of each kind once
+        const u16x2 bmin = MX(MX(MN(N0, N4), MN(N4, N8)), MX(MN(N8, N12), MN(N12, N0)));
+        const u16x2 dmax = MN(MN(MX(N0, N4), MX(N4, N8)), MN(MX(N8, N12), MX(N12, N0)));
+        const u16x2 pb = __builtin_elementwise_sub_sat(bmin, HI);
+        const u16x2 pd = __builtin_elementwise_sub_sat(LO, dmax);
         const u16x2 one = {1, 1};
         w[h] = __builtin_bit_cast(uint32_t, MN(MX(pb, pd), one));   // 0/1 per pixel
 #undef MN
