@@ -496,7 +496,8 @@ def main_match(args):
     import torch
     import torch.distributed as dist
     from my_orb_slam2_amd import ORBmatcher
-    from my_orb_slam2_amd.distributed import all_gather_counts, broadcast_query, shard_range
+    from my_orb_slam2_amd.distributed import (all_gather_counts, broadcast_query,
+                                              gather_candidate_matches, gather_rows, shard_range)
     from my_orb_slam2_amd.features import FeatureSetC
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -529,7 +530,10 @@ def main_match(args):
                 broadcast_query([qdesc, qkeys])
             m.search_by_bow_kf_frame_batch_device(db, fc, out, cnt, st)
             if world > 1:
-                return all_gather_counts(cnt[:k1 - k0], args.kfs, world)
+                allc = all_gather_counts(cnt[:k1 - k0], args.kfs, world)
+                # the candidates' match lists travel to every rank (Tracking.cc:1503-1528)
+                gather_candidate_matches(out, allc, args.kfs, world)
+                return allc
             return cnt[:k1 - k0]
         units, unit_name = 1, "query frames/sec"
         work_ops = 16.0 * nvalid * F                   # 8 XOR + 8 BCNT per distance
@@ -537,7 +541,7 @@ def main_match(args):
         cfg = {"workload": "relocalisation_bf_vs_keyframes", "keyframes": args.kfs,
                "features_per_keyframe": F, "query_features": F, "nnratio": 0.75,
                "check_orientation": True, "featurevector": "single node (brute force)",
-               "parallelism": f"keyframe shards x{world}, RCCL broadcast + all-gather"}
+               "parallelism": f"keyframe shards x{world}, RCCL broadcast + all-gather of counts and candidate match lists"}
         metric = "relocalisation query frames/sec, 1000-descriptor frame vs 10k keyframes"
     else:
         from my_orb_slam2_amd import synth
@@ -564,10 +568,14 @@ def main_match(args):
         out = torch.empty(int(n1.sum()), dtype=torch.int32, device=dev)
         cnt = torch.empty(max(nj, 1), dtype=torch.int32, device=dev)
 
+        uniform = bool((n1 == n1[0]).all()) if nj else True
+
         def step():
             m.search_for_triangulation_batch_device(db.c, kf1, kf2, dF, dE, s2, s, job_off, out,
                                                     cnt, stream=st)
             if world > 1:
+                if uniform and nj:   # every job's match12 array to every rank
+                    gather_rows(out.view(nj, -1), args.jobs, world)
                 return all_gather_counts(cnt[:nj], args.jobs, world)
             return cnt[:nj]
         units, unit_name = args.jobs, "keyframe-pair jobs/sec"
@@ -575,7 +583,8 @@ def main_match(args):
         kern = "k_triangulate"
         cfg = {"workload": "batched_search_for_triangulation", "jobs": args.jobs,
                "features_per_keyframe": 2000, "vocabulary_nodes": 100, "only_stereo": False,
-               "check_orientation": False, "parallelism": f"job shards x{world}, RCCL all-gather"}
+               "check_orientation": False,
+               "parallelism": f"job shards x{world}, RCCL all-gather of counts and match arrays"}
         metric = "SearchForTriangulation keyframe-pair jobs/sec (512 jobs, 2000 features/KF)"
 
     for _ in range(args.warmup):

@@ -9,6 +9,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from my_orb_slam2_amd.distributed import (all_gather_counts, broadcast_query,
+                                          gather_candidate_matches, gather_rows,
                                           relocalisation_candidates, shard_range)
 
 
@@ -34,7 +35,15 @@ def _worker(rank, world, port, n_total, q):
         # each rank "matches" its shard: count = global keyframe id % 20
         local = torch.arange(b, e, dtype=torch.int32) % 20
         allc = all_gather_counts(local, n_total, world)
-        q.put((rank, desc.sum().item(), allc.numpy().tolist()))
+        # per-keyframe match rows: feature f of keyframe k matched to (k * 7 + f) % 11, or -1
+        F = 6
+        kf = torch.arange(b, e, dtype=torch.int32)[:, None]
+        feat = torch.arange(F, dtype=torch.int32)[None, :]
+        rows = torch.where(feat < 4, (kf * 7 + feat) % 11, torch.full_like(kf * feat, -1))
+        everything = gather_rows(rows, n_total, world)
+        cand = gather_candidate_matches(rows, allc, n_total, world)
+        q.put((rank, desc.sum().item(), allc.numpy().tolist(), everything.numpy().tolist(),
+               [(k, m.numpy().tolist()) for k, m in cand]))
     finally:
         dist.destroy_process_group()
 
@@ -52,8 +61,13 @@ def test_gloo_broadcast_and_gather():
         p.join(60)
         assert p.exitcode == 0
     expect = (np.arange(n_total) % 20).tolist()
-    for rank, s, allc in res:
+    F = 6
+    rows = [[(k * 7 + f) % 11 if f < 4 else -1 for f in range(F)] for k in range(n_total)]
+    want_cand = [(k, rows[k]) for k in range(n_total) if k % 20 >= 15]
+    for rank, s, allc, everything, cand in res:
         assert s == int(np.arange(160).sum())
         assert allc == expect
+        assert everything == rows
+        assert cand == want_cand
     cand = relocalisation_candidates(np.array(expect))
     np.testing.assert_array_equal(cand, [i for i in range(n_total) if i % 20 >= 15])
