@@ -13,6 +13,8 @@ import numpy as np
 
 PKG = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG / "liborbx.so"
+# tools/variants.py benchmarks alternative builds of the same sources (in-tree .so files)
+ORBX_LIB_ENV = "ORBX_LIB"
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -120,7 +122,8 @@ def load(path: pathlib.Path | str | None = None):
     """Load liborbx.so (raises OSError if it has not been built)."""
     global _lib
     if _lib is None or path is not None:
-        p = pathlib.Path(path) if path else LIB_PATH
+        import os
+        p = pathlib.Path(path or os.environ.get(ORBX_LIB_ENV) or LIB_PATH)
         # One HIP runtime per process: torch wheels bundle their own libamdhip64 (same
         # soname).  Loading torch first makes liborbx bind to that copy instead of pulling
         # in /opt/rocm's second runtime next to it.

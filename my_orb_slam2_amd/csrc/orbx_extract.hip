@@ -112,8 +112,18 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 }
 
 #define FAST_LIST 512
+#ifndef FAST_NC
 #define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
-#define FAST_PF 12     // prefetched ROI dwords per lane (larger ROIs are staged directly)
+#endif
+#ifndef FAST_PF
+#define FAST_PF 8      // prefetched ROI dwords per lane (larger ROIs are staged directly)
+#endif
+#ifndef FAST_WPE
+#define FAST_WPE 1     // minimum waves per SIMD requested from the register allocator
+#endif
+#ifndef OD_WPE
+#define OD_WPE 1
+#endif
 __device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
@@ -173,7 +183,7 @@ __device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R,
     return (f & 5u) | ((f >> 15) & 10u);
 }
 
-__global__ __launch_bounds__(256) void k_fast(const Geometry* __restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE))) void k_fast(const Geometry* __restrict__ g,
                                               const CellDesc* __restrict__ cells,
                                               const uint8_t* __restrict__ pyr,
                                               int* __restrict__ ccnt,
@@ -759,37 +769,44 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
 }
 
 // ----------------------------------------------------------------------------------------
-// Orientation + rBRIEF + assembly: one wave per OD_NK keypoints of one level, two keypoints at
-// a time (one per half-wave: 32 lanes each), so the per-keypoint scalar work (moments
-// reduction, fastAtan2, sin/cos, outputs) is issued once for two keypoints.  The patch loads
-// of the next pair are in flight while the current pair is computed from LDS; the per-lane
-// patch offsets are the same for every keypoint of the level and are computed once.
+// Orientation + rBRIEF + assembly: one wave per OD_NK keypoints of one level, in three phases.
+//   1. IC_Angle moments, two keypoints at a time (one per half-wave, 32 lanes each) from the
+//      31x31 raw patch staged in LDS; the next pair's patch loads are in flight meanwhile.
+//      Keypoint k's two sums end up in lane k.
+//   2. fastAtan2 and glibc cosf/sinf once for all OD_NK keypoints (lane k: keypoint k): the
+//      per-keypoint float / double work is issued once per wave, not once per pair.  Lane k
+//      also writes keypoint k's record.
+//   3. rBRIEF, two keypoints at a time from the 37x37 blurred patch, same pipelining.
+// The per-lane patch offsets are the same for every keypoint of the level, computed once.
 // ----------------------------------------------------------------------------------------
 #define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
 #define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
-#define OD_PATCH_DW (31 * OD_RAW_DW + 37 * OD_BLR_DW)   // 649
-#define OD_NLOAD 21    // dword loads per lane per patch: 649 / 32, rounded up
+#define OD_RAW_N (31 * OD_RAW_DW)                  // 279
+#define OD_BLR_N (37 * OD_BLR_DW)                  // 370
+#define OD_RL ((OD_RAW_N + 31) / 32)               // 9 dword loads per lane per raw patch
+#define OD_BL ((OD_BLR_N + 31) / 32)               // 12 per blurred patch
+static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
 
-// Sum over each half-wave (lanes 0-31 / 32-63), returned to every lane of that half.
-__device__ __forceinline__ int half_sum_dpp(int v) {
+// Sums over each half-wave (lanes 0-31 / 32-63) as two scalars.
+__device__ __forceinline__ void half_sums_dpp(int v, int& lo, int& hi) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
     v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);   // row_ror:4
     v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);   // row_ror:8
-    const int lo = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
-    const int hi = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
-    return (threadIdx.x & 32) ? hi : lo;
+    lo = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
+    hi = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
-__global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict__ g,
-                                                     const uint8_t* __restrict__ pyr,
-                                                     const uint8_t* __restrict__ blur,
-                                                     const int* __restrict__ ocnt,
-                                                     const uint32_t* __restrict__ okp,
-                                                     float* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc,
-                                                     int* __restrict__ nkp) {
-    __shared__ uint32_t patch[4][2][OD_PATCH_DW];
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) void k_orient_desc(
+    const Geometry* __restrict__ g, const uint8_t* __restrict__ pyr,
+    const uint8_t* __restrict__ blur, const int* __restrict__ ocnt,
+    const uint32_t* __restrict__ okp, float* __restrict__ kps, uint8_t* __restrict__ desc,
+    int* __restrict__ nkp) {
+    __shared__ uint32_t patch[4][2][OD_BLR_N];
     const int b = blockIdx.y, blk = blockIdx.x;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int half = lane >> 5, l32 = lane & 31;
@@ -809,50 +826,109 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
     for (int l = 0; l < level; ++l) off += oc[l];
     const LevelGeom& L = g->lv[level];
     const int pitch = L.pitch;
-    // every keypoint word of the wave in one load
+    // every keypoint word of the wave in one load: lane k holds keypoint k
     const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
 
-    // per-lane patch offsets (raw rows first, then blurred rows) relative to the patch bases
-    constexpr int n1 = 31 * OD_RAW_DW;
-    uint32_t so[OD_NLOAD];
-    uint32_t rawbits = 0;
+    // per-lane patch offsets relative to the patch bases
+    uint32_t sor[OD_RL], sob[OD_BL];
 #pragma unroll
-    for (int k = 0; k < OD_NLOAD; ++k) {
-        const int t = min(l32 + 32 * k, OD_PATCH_DW - 1);
-        const bool isr = t < n1;
-        const int tt = isr ? t : t - n1;
-        const int row = isr ? tt / OD_RAW_DW : tt / OD_BLR_DW;
-        const int col = tt - row * (isr ? OD_RAW_DW : OD_BLR_DW);
-        so[k] = __umul24(row, pitch) + 4 * col;
-        rawbits |= (uint32_t)isr << k;
+    for (int k = 0; k < OD_RL; ++k) {
+        const int t = min(l32 + 32 * k, OD_RAW_N - 1);
+        const int row = t / OD_RAW_DW;
+        sor[k] = __umul24(row, pitch) + 4 * (t - row * OD_RAW_DW);
+    }
+#pragma unroll
+    for (int k = 0; k < OD_BL; ++k) {
+        const int t = min(l32 + 32 * k, OD_BLR_N - 1);
+        const int row = t / OD_BLR_DW;
+        sob[k] = __umul24(row, pitch) + 4 * (t - row * OD_BLR_DW);
     }
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
     const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
     // keypoint of this half-wave in pair p: k = 2p + half (clamped: a lone last keypoint is
-    // computed by both halves, the upper half's results are not written)
+    // computed by both halves, the upper half's results are not used)
     auto kp_word = [&](int p) {
         const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
         const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)cw, k0);
         const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)cw, k1);
         return half ? c1 : c0;
     };
-    auto issue = [&](int p, uint32_t (&v)[OD_NLOAD]) {
+    uint32_t* P = patch[wid][half];
+    const int npair = (nk + 1) >> 1;
+    uint32_t v[OD_BL];
+    auto issue_raw = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint8_t* pr = pyr_l + __umul24(y - 15, pitch) + ((x - 15) & ~3);
+#pragma unroll
+        for (int j = 0; j < OD_RL; ++j) v[j] = *(const uint32_t*)(pr + sor[j]);
+    };
+    auto issue_blr = [&](int p) {
+        const uint32_t c = kp_word(p);
+        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint8_t* pb = blr_l + __umul24(y - 18, pitch) + ((x - 18) & ~3);
 #pragma unroll
-        for (int j = 0; j < OD_NLOAD; ++j)
-            v[j] = *(const uint32_t*)(((rawbits >> j) & 1u ? pr : pb) + so[j]);
+        for (int j = 0; j < OD_BL; ++j) v[j] = *(const uint32_t*)(pb + sob[j]);
     };
 
-    // IC_Angle lane work (src/ORBextractor.cc:77-104): lane l32 < 31 is column u = l32 - 15 of
-    // its half's keypoint, rows v = 1..15; umax decreases with v, so the rows with
-    // |u| <= umax[v] are a prefix [1, vend).
+    // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
+    //      u = l32 - 15 of its half's keypoint, rows v = 1..15; umax decreases with v, so the
+    //      rows with |u| <= umax[v] are a prefix [1, vend).
     const int u = l32 - 15, au = u < 0 ? -u : u;
+    const int uw = l32 < 31 ? u : 0;
     int vend = 1;
-    for (int v = 1; v < 16; ++v) vend += (l32 < 31 && au <= g->umax[v]) ? 1 : 0;
+    for (int vv = 1; vv < 16; ++vv) vend += (l32 < 31 && au <= g->umax[vv]) ? 1 : 0;
+    const uint8_t* raw = (const uint8_t*)P;   // [31][36]
+    int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
+    issue_raw(0);
+    for (int p = 0; p < npair; ++p) {
+        const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
+#pragma unroll
+        for (int j = 0; j < OD_RL; ++j) {
+            const int t = l32 + 32 * j;
+            if (t < OD_RAW_N) P[t] = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (p + 1 < npair) issue_raw(p + 1);   // next pair's patches in flight
+        else issue_blr(0);                     // phase 3's first patches in flight
+        const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ((x - 15) & ~3));
+        // fixed trip count (all 30 reads in flight at once); rows v >= vend contribute 0.  The
+        // reads stay inside the staged patch for every lane (lane 31: u = 16, weight 0).
+        int m10 = __mul24(uw, (int)center[u]), m01 = 0;
+#pragma unroll
+        for (int vv = 1; vv < 16; ++vv) {
+            const int vp = center[u + vv * (OD_RAW_DW * 4)], vm = center[u - vv * (OD_RAW_DW * 4)];
+            const bool on = vv < vend;
+            m10 += __mul24(uw, on ? vp + vm : 0);
+            m01 += __mul24(vv, on ? vp - vm : 0);
+        }
+        int a10, b10, a01, b01;
+        half_sums_dpp(m10, a10, b10);
+        half_sums_dpp(m01, a01, b01);
+        mk10 = lane == 2 * p ? a10 : (lane == 2 * p + 1 ? b10 : mk10);
+        mk01 = lane == 2 * p ? a01 : (lane == 2 * p + 1 ? b01 : mk01);
+    }
 
+    // ---- 2. angle, cos / sin (src/ORBextractor.cc:103, 113) and the keypoint record ----
+    const float angle = cv_fast_atan2((float)mk01, (float)mk10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float ca_l = glibc_cosf(ang), sb_l = glibc_sinf(ang);
+    if (lane < nk) {
+        const size_t o = (size_t)b * g->kp_cap + off + i0 + lane;
+        const int x = cand_x(cw) + ORBX_MIN_BORDER, y = cand_y(cw) + ORBX_MIN_BORDER;
+        float* kp = kps + o * 7;
+        const float sc = L.scale;
+        kp[0] = level ? (float)x * sc : (float)x;
+        kp[1] = level ? (float)y * sc : (float)y;
+        kp[2] = (float)L.patch_size;
+        kp[3] = angle;
+        kp[4] = (float)cand_s(cw);
+        ((int*)kp)[5] = level;
+        ((int*)kp)[6] = -1;
+    }
+
+    // ---- 3. computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level ----
     // this lane's 8 rBRIEF pairs (q = 32w + l32), converted once
     float px1[8], py1[8], px2[8], py2[8];
 #pragma unroll
@@ -863,42 +939,20 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
         px2[w] = (float)c_pattern[4 * q + 2];
         py2[w] = (float)c_pattern[4 * q + 3];
     }
-
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    uint32_t* P = patch[wid][half];
-    const uint8_t* raw = (const uint8_t*)P;                       // [31][36]
-    const uint8_t* blr = (const uint8_t*)(P + n1);                // [37][40]
-    const int npair = (nk + 1) >> 1;
-    uint32_t v[OD_NLOAD];
-    issue(0, v);
+    const uint8_t* blr = (const uint8_t*)P;   // [37][40]
     for (int p = 0; p < npair; ++p) {
-        const uint32_t c = kp_word(p);
-        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER, s = cand_s(c);
+        const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
+        const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
+        const float ca0 = readlane_f(ca_l, k0), ca1 = readlane_f(ca_l, k1);
+        const float sb0 = readlane_f(sb_l, k0), sb1 = readlane_f(sb_l, k1);
+        const float ca = half ? ca1 : ca0, sb = half ? sb1 : sb0;
 #pragma unroll
-        for (int j = 0; j < OD_NLOAD; ++j) {
+        for (int j = 0; j < OD_BL; ++j) {
             const int t = l32 + 32 * j;
-            if (t < OD_PATCH_DW) P[t] = v[j];
+            if (t < OD_BLR_N) P[t] = v[j];
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (p + 1 < npair) issue(p + 1, v);   // next pair's patches in flight
-
-        const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ((x - 15) & ~3));
-        int m10 = 0, m01 = 0;
-        if (l32 < 31) {
-            m10 = __mul24(u, (int)center[u]);
-            for (int vv = 1; vv < vend; ++vv) {
-                const int vp = center[u + vv * (OD_RAW_DW * 4)], vm = center[u - vv * (OD_RAW_DW * 4)];
-                m10 += __mul24(u, vp + vm);
-                m01 += __mul24(vv, vp - vm);
-            }
-        }
-        m10 = half_sum_dpp(m10);
-        m01 = half_sum_dpp(m01);
-        const float angle = cv_fast_atan2((float)m01, (float)m10);
-
-        // computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level.
-        const float ang = angle * factorPI;
-        const float ca = glibc_cosf(ang), sb = glibc_sinf(ang);
+        if (p + 1 < npair) issue_blr(p + 1);
         const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ((x - 18) & ~3));
         uint32_t words[8];
 #pragma unroll
@@ -911,25 +965,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(const Geometry* __restrict_
             words[w] = half ? (uint32_t)(m >> 32) : (uint32_t)m;
         }
         const int k = 2 * p + half;
-        if (k < nk) {
+        if (k < nk && l32 < 8) {
             const size_t o = (size_t)b * g->kp_cap + off + i0 + k;
-            if (l32 == 0) {
-                float* kp = kps + o * 7;
-                const float sc = L.scale;
-                kp[0] = level ? (float)x * sc : (float)x;
-                kp[1] = level ? (float)y * sc : (float)y;
-                kp[2] = (float)L.patch_size;
-                kp[3] = angle;
-                kp[4] = (float)s;
-                ((int*)kp)[5] = level;
-                ((int*)kp)[6] = -1;
-            }
-            if (l32 < 8) {
-                uint32_t wv = words[0];
+            uint32_t wv = words[0];
 #pragma unroll
-                for (int w = 1; w < 8; ++w) wv = l32 == w ? words[w] : wv;
-                *(uint32_t*)(desc + o * 32 + l32 * 4) = wv;
-            }
+            for (int w = 1; w < 8; ++w) wv = l32 == w ? words[w] : wv;
+            *(uint32_t*)(desc + o * 32 + l32 * 4) = wv;
         }
     }
 }

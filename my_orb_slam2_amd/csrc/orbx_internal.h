@@ -45,9 +45,13 @@ struct LevelGeom {
 };
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
-#define OD_NK 4               // keypoints per wave in k_orient_desc
+#ifndef OD_NK
+#define OD_NK 4               // keypoints per wave in k_orient_desc (<= 64)
+#endif
 #define LT_W 128              // output tile width  (32 groups of 4)
+#ifndef LT_H
 #define LT_H 32               // output tile height
+#endif
 #define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
 #define LT_HR (LT_H + 6)      // halo rows: y = Y0-3 .. Y0+LT_H+2
 
