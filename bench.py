@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="stereo pairs per step per GPU")
-    ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic pairs")
+    ap.add_argument("--distinct", type=int, default=32,
+                    help="synthetic base pairs / frames generated per rank (stereo: the batch "
+                         "slots are row-rolled copies of them, all distinct)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -100,9 +102,14 @@ def main():
     B = args.batch
     P = max(1, min(args.distinct, B))
     pairs = [synth.stereo_pair(1000 * rank + i, W, H) for i in range(P)]
-    idx = [i % P for i in range(B)]
-    Lh = np.stack([pairs[i][0] for i in idx])
-    Rh = np.stack([pairs[i][1] for i in idx])
+    # every slot of the batch holds a different pair: slot i is base pair i % P with both views
+    # rolled down by 37 * (i // P) rows (still rectified; generating B pairs from scratch
+    # would cost ~60 ms each on the host)
+    def slot(i, view):
+        return np.roll(pairs[i % P][view], 37 * (i // P), axis=0)
+    Lh = np.stack([slot(i, 0) for i in range(B)])
+    Rh = np.stack([slot(i, 1) for i in range(B)])
+    n_distinct = len({(i % P, (37 * (i // P)) % H) for i in range(B)})
     Ls = torch.from_numpy(Lh).to(dev)
     Rs = torch.from_numpy(Rh).to(dev)
     torch.cuda.synchronize(dev)
@@ -171,7 +178,8 @@ def main():
                "dtype": "u8", "data": "synthetic",
                "config": {"workload": "kitti_stereo_extract_match", "width": W, "height": H,
                           "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2,
-                          "pairs_per_step_per_gpu": B, "distinct_pairs": P,
+                          "pairs_per_step_per_gpu": B, "distinct_pairs": n_distinct,
+                          "base_pairs": P,
                           "parallelism": f"dp{world}"},
                "mean_keypoints_left": float(nkp.mean()),
                "mean_stereo_matches": float(nv.mean()),

@@ -66,6 +66,14 @@ __device__ __forceinline__ int block_sum(int v, int* tmp) {
 
 namespace orbx {
 
+// An explicit s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their maxima).  The staging loops
+// below wait for their loads only inside the guarded LDS stores, so on the path that skips a
+// store the compiler's wait analysis still counts that load as pending, and it then inserts
+// a vmcnt(0) at the next use of the register anywhere downstream -- for k_fast that was the
+// head of the compass loop, which drained the next cell's prefetch on every iteration.
+// Waiting once here (every load has landed by now anyway) clears that state.
+__device__ __forceinline__ void vmem_drained() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // Stage a rows x ndw-dword window (row r at gsrc + r*gpitch, 4-byte aligned rows) into LDS
 // (row r at lds + r*lpitch_dw dwords).  Each thread issues up to 8 loads before its first
 // LDS store, so a workgroup keeps NT*8 loads in flight instead of one per thread.  The
@@ -104,6 +112,7 @@ __device__ __forceinline__ void stage_dwords(const uint8_t* __restrict__ gsrc, s
         for (int k = 0; k < 8; ++k)
             if (at[k] >= 0) lds[at[k]] = v[k];
     }
+    vmem_drained();
 }
 
 // Same for an arbitrary byte window (no alignment), 16 loads in flight per thread.
@@ -138,6 +147,7 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, si
         for (int k = 0; k < 16; ++k)
             if (at[k] >= 0) lds[at[k]] = v[k];
     }
+    vmem_drained();
 }
 
 }  // namespace orbx
