@@ -49,29 +49,30 @@ __device__ __forceinline__ int fast_arc_score(const uint8_t* roi, int cols, int 
     d[13] = v - roi[(r + 1) * cols + c - 3];
     d[14] = v - roi[(r + 2) * cols + c - 2];
     d[15] = v - roi[(r + 3) * cols + c - 1];
-    // sliding min / max over 9 cyclic neighbours by doubling
-    int mn2[16], mx2[16];
+    // min / max over the 16 cyclic 9-runs as three 3-runs each: every step is one
+    // v_min3 / v_max3 (a 2-input v_min costs the same issue slot on gfx950)
+    int mn3[16], mx3[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        mn2[i] = min(d[i], d[(i + 1) & 15]);
-        mx2[i] = max(d[i], d[(i + 1) & 15]);
+        mn3[i] = min(min(d[i], d[(i + 1) & 15]), d[(i + 2) & 15]);
+        mx3[i] = max(max(d[i], d[(i + 1) & 15]), d[(i + 2) & 15]);
     }
-    int mn4[16], mx4[16];
+    int mn9[16], mx9[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        mn4[i] = min(mn2[i], mn2[(i + 2) & 15]);
-        mx4[i] = max(mx2[i], mx2[(i + 2) & 15]);
+        mn9[i] = min(min(mn3[i], mn3[(i + 3) & 15]), mn3[(i + 6) & 15]);
+        mx9[i] = max(max(mx3[i], mx3[(i + 3) & 15]), mx3[(i + 6) & 15]);
     }
-    int best_dark = -1000, best_min_max = 1000;
+    // 9 pixels all darker than v by > t: max_i mn9; all brighter: -min_i mx9
+    int best_dark = max(max(mn9[0], mn9[1]), mn9[2]);
+    int best_min_max = min(min(mx9[0], mx9[1]), mx9[2]);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int mn8 = min(mn4[i], mn4[(i + 4) & 15]);
-        const int mx8 = max(mx4[i], mx4[(i + 4) & 15]);
-        const int mn9 = min(mn8, d[(i + 8) & 15]);
-        const int mx9 = max(mx8, d[(i + 8) & 15]);
-        best_dark = max(best_dark, mn9);       // 9 pixels all darker than v by > t
-        best_min_max = min(best_min_max, mx9); // 9 pixels all brighter: -max(d) > t
+    for (int i = 3; i < 15; i += 2) {
+        best_dark = max(max(best_dark, mn9[i]), mn9[i + 1]);
+        best_min_max = min(min(best_min_max, mx9[i]), mx9[i + 1]);
     }
+    best_dark = max(best_dark, mn9[15]);
+    best_min_max = min(best_min_max, mx9[15]);
     return max(best_dark, -best_min_max);
 }
 

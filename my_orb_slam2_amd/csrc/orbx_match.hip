@@ -3,10 +3,10 @@
 // The matchers are integer/bit work (XOR + v_bcnt over 256-bit descriptors) with a greedy,
 // order-dependent claim step.  The kernels keep the reference's exact selection semantics
 // while moving the distance work off the sequential chain:
-//   k_bow<NPL>       one wave per (keyframe, frame) job, walking the shared FeatureVector
-//                    nodes; the node's candidate descriptors live in VGPRs (NPL per lane),
-//                    each greedy step is 8 XOR + 8 BCNT per candidate and two DPP wave-min
-//                    reductions over (distance, position) keys (first-min semantics).
+//   k_bow            one workgroup per (keyframe, frame) job, walking the shared FeatureVector
+//                    nodes: static best / second of every A feature (one thread each, B side
+//                    in LDS), then an in-order replay of the greedy claims that re-scans only
+//                    the A features whose static pair meets a claim.
 //   k_triangulate    one workgroup per keyframe pair, one wave per KF1 node; every idx1 is
 //                    independent (vbMatched2 is never set, :722), so each is a wave-min over
 //                    (distance, reversed position) keys = the reference's last-wins ties.
@@ -48,6 +48,13 @@ __device__ __forceinline__ Desc load_desc(const uint8_t* base, long long i) {
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     uint32_t r;
     asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+// median of three (one v_med3_u32; a 2-input v_min / v_max costs the same issue slot)
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
@@ -120,31 +127,56 @@ __device__ __forceinline__ int x86_int(float f) {
 // SearchByBoW (:182-319 and :563-696)
 // ---------------------------------------------------------------------------------------
 
-template <int NPL>
-__global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
-    extern __shared__ int lds[];
-    const int job = blockIdx.x, lane = threadIdx.x;
+// One workgroup (4 waves) per (keyframe, frame) job.  A B feature belongs to exactly one
+// FeatureVector node, so the greedy claims of different nodes never interact and each
+// shared node is an independent problem:
+//   1. the node's B descriptors (and a per-position key suffix: the position, or INF for a
+//      feature the reference skips statically) are staged in LDS;
+//   2. every A feature of the node gets its STATIC best and second key (distance << 20 |
+//      position) over all of them, one thread per A feature scanning the LDS copy (broadcast
+//      reads, no reductions);
+//   3. wave 0 replays the reference's loop over the A features in order, 64 at a time.  The
+//      claimed set only grows, so an A feature whose static best and second are both still
+//      unclaimed at its turn has exactly those as its dynamic best and second: it is decided
+//      without looking at the candidates again.  Only an A feature whose static pair meets a
+//      claim is re-scanned (all 64 lanes, against the claim bitmap).  Within a chunk, the
+//      lanes before the first one that claims or conflicts are decided together.
+// BLDS = false reads the B descriptors from global memory (nodes too large for LDS).
+#ifndef BOW_R
+#define BOW_R 4   // A features per thread in the static pass
+#endif
+#ifndef BOW_T
+#define BOW_T 256 // threads per job
+#endif
+template <bool BLDS>
+__global__ __launch_bounds__(BOW_T) void k_bow(BowLaunch g) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int job = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int ka = g.a_fixed ? 0 : job, kb = g.b_fixed ? 0 : job;
     const int fa0 = g.A.feat_off[ka], nA = g.A.feat_off[ka + 1] - fa0;
     const int fb0 = g.B.feat_off[kb], nBt = g.B.feat_off[kb + 1] - fb0;
     const int nOut = g.kf_kf ? nA : nBt;
     int32_t* out = g.out + (size_t)job * g.out_stride;
     if (nA < 0 || nBt < 0 || nA > g.A.max_feat || nBt > g.B.max_feat || nOut > g.out_stride) {
-        for (int i = lane; i < g.out_stride; i += 64) out[i] = -1;
-        if (lane == 0) {
+        for (int i = tid; i < g.out_stride; i += BOW_T) out[i] = -1;
+        if (tid == 0) {
             g.nmatches[job] = 0;
             atomicOr(g.err, 1);
         }
         return;
     }
-    const int smax = g.kf_kf ? g.A.max_feat : g.B.max_feat;
-    int* state = lds;                                    // match | bin << 24, or -1
-    uint32_t* claimed = (uint32_t*)(lds + smax);         // B features claimed (bitmap)
-    int* hist = (int*)(claimed + (g.B.max_feat + 31) / 32);
-    for (int i = lane; i < nOut; i += 64) state[i] = -1;
-    for (int i = lane; i < (nBt + 31) / 32; i += 64) claimed[i] = 0u;
-    if (lane < 32) hist[lane] = 0;
-    __syncthreads();
+    const int amax = g.A.max_feat, bmax = g.B.max_feat;
+    const int smax = g.kf_kf ? amax : bmax;
+    // LDS carve (bow_lds_bytes): B descriptors first (16-byte aligned)
+    uint4* bdesc = (uint4*)lds;                                    // [bmax][2] (BLDS)
+    uint32_t* pkey = (uint32_t*)(lds + (BLDS ? 8 * bmax : 0));     // [bmax]
+    uint32_t* top1 = pkey + bmax;                                  // [amax]
+    uint32_t* top2 = top1 + amax;                                  // [amax]
+    int* state = (int*)(top2 + amax);                              // [smax] match | bin << 24
+    uint32_t* claimed = (uint32_t*)(state + smax);                 // [(bmax + 31) / 32] per node
+    int* hist = (int*)(claimed + (bmax + 31) / 32);                // [32] + 8 scan scratch
+    for (int i = tid; i < nOut; i += BOW_T) state[i] = -1;
+    if (tid < 32) hist[tid] = 0;
 
     const bool kfkf = g.kf_kf != 0;
     const int na0 = g.A.node_off[ka], na1 = g.A.node_off[ka + 1];
@@ -157,123 +189,150 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
         while (bn < bn1 && g.B.node_id[bn] < id) ++bn;
         if (bn >= bn1) break;
         if (g.B.node_id[bn] != id) continue;
-        const int a0 = g.A.node_feat_off[ga], a1 = g.A.node_feat_off[ga + 1];
+        const int a0 = g.A.node_feat_off[ga], nAn = g.A.node_feat_off[ga + 1] - a0;
         const int b0 = g.B.node_feat_off[bn], nB = g.B.node_feat_off[bn + 1] - b0;
         ++bn;
-        if (nB <= 0) continue;
-        if (nB <= 64 * NPL) {
-            // Candidates resident in VGPRs for the whole node.  pm[c] is the candidate's
-            // position (the key's low bits) or INF once unavailable, so a key is one
-            // v_lshl_or: (dist << 20) | pm.  A distance of 256 needs no test: its key sorts
-            // below INF but d1 = 256 is rejected and d2 = 256 equals the reference's init.
-            Desc bd[NPL];
-            int bf[NPL];
-            uint32_t pm[NPL];
+        if (nB <= 0 || nAn <= 0) continue;
+        __syncthreads();   // the previous node's readers are done with the LDS arrays
+        // ---- 1. stage the node's B side ----
+        for (int p = tid; p < nB; p += BOW_T) {
+            const int f = g.B.node_feat[b0 + p];
+            const bool in = (unsigned)f < (unsigned)nBt;
+            const int fc = in ? f : 0;
+            // :240 skips claimed frame features only; KF-KF also needs a valid MapPoint (:633)
+            const bool ok = in && (!kfkf || g.B.flag[fb0 + fc]);
+            pkey[p] = ok ? (uint32_t)p : INF;
+            if (BLDS) {
+                const uint4* s = (const uint4*)(g.B.desc + 32 * ((size_t)fb0 + fc));
+                bdesc[2 * p] = s[0];
+                bdesc[2 * p + 1] = s[1];
+            }
+        }
+        for (int i = tid; i < (nB + 31) / 32; i += BOW_T) claimed[i] = 0u;
+        __syncthreads();
+        // ---- 2. static best / second of every A feature of the node: BOW_R rows per
+        //      thread (rows i, i + 256, ...), so one LDS read of a B descriptor feeds BOW_R
+        //      distances ----
+        for (int i0 = tid; i0 < nAn; i0 += BOW_T * BOW_R) {
+            Desc ad[BOW_R];
+            bool vl[BOW_R];
+            uint32_t k1[BOW_R], k2[BOW_R];
+            bool any = false;
 #pragma unroll
-            for (int c = 0; c < NPL; ++c) {
-                pm[c] = INF;
-                bf[c] = 0;
-                if (c * 64 < nB) {
-                    const int pos = c * 64 + lane;
-                    const int f = g.B.node_feat[b0 + min(pos, nB - 1)];
-                    const bool in = pos < nB && (unsigned)f < (unsigned)nBt;
-                    const int fc = in ? f : 0;
-                    bd[c] = load_desc(g.B.desc, (long long)fb0 + fc);
-                    bf[c] = fc;
-                    const bool ok = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
-                                    (!kfkf || g.B.flag[fb0 + fc]);
-                    pm[c] = ok ? (uint32_t)pos : INF;
+            for (int r = 0; r < BOW_R; ++r) {
+                const int i = i0 + BOW_T * r;
+                const int fa = i < nAn ? g.A.node_feat[a0 + i] : -1;
+                vl[r] = (unsigned)fa < (unsigned)nA && g.A.flag[fa0 + max(fa, 0)];
+                ad[r] = load_desc(g.A.desc, (long long)fa0 + (vl[r] ? fa : 0));
+                k1[r] = INF;
+                k2[r] = INF;
+                any |= vl[r];
+            }
+            if (any) {
+                for (int p = 0; p < nB; ++p) {
+                    Desc bd;
+                    if (BLDS) {
+                        const uint4 u0 = bdesc[2 * p], u1 = bdesc[2 * p + 1];
+                        bd = Desc{{u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w}};
+                    } else {
+                        const int f = g.B.node_feat[b0 + p];
+                        bd = load_desc(g.B.desc, (long long)fb0 + ((unsigned)f < (unsigned)nBt ? f : 0));
+                    }
+                    const uint32_t pk = pkey[p];
+#pragma unroll
+                    for (int r = 0; r < BOW_R; ++r) {
+                        const uint32_t key = ((uint32_t)hamming(ad[r], bd) << 20) | pk;
+                        k2[r] = med3_u32(k1[r], k2[r], key);   // k1 <= k2: the new second
+                        k1[r] = min(k1[r], key);
+                    }
                 }
             }
-            // A features of the node, 64 at a time: lane l loads step l's descriptor, the
-            // steps read it back with v_readlane (no load on the sequential chain)
-            for (int ib = a0; ib < a1; ib += 64) {
-                const int ial = ib + lane;
-                const int fal = ial < a1 ? g.A.node_feat[ial] : -1;
-                const bool vl = (unsigned)fal < (unsigned)nA && g.A.flag[fa0 + max(fal, 0)];
-                const Desc adl = load_desc(g.A.desc, (long long)fa0 + (vl ? fal : 0));
-                uint64_t todo = __ballot(vl);   // :224-228 / :599-603
-                while (todo) {
-                    const int t = __builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    Desc ad;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) ad.w[k] = (uint32_t)__builtin_amdgcn_readlane((int)adl.w[k], t);
-                    const int fa = __builtin_amdgcn_readlane(fal, t);
-                    uint32_t k1 = INF, k2 = INF;
-#pragma unroll
-                    for (int c = 0; c < NPL; ++c) {
-                        if (c * 64 < nB) {
-                            const uint32_t key = ((uint32_t)hamming(ad, bd[c]) << 20) | pm[c];
-                            k2 = min(k2, max(k1, key));
-                            k1 = min(k1, key);
-                        }
-                    }
-                    const uint32_t m1 = wave_min_u32(k1);
-                    const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
-                    const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
-                    const int d2 = m2 == INF ? 256 : min((int)(m2 >> 20), 256);
-                    const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
-                                     (float)d1 < g.ratio * (float)d2;
-                    if (acc) {
-                        const int pos = (int)(m1 & 0xFFFFFu);
-#pragma unroll
-                        for (int c = 0; c < NPL; ++c)
-                            if (pos == c * 64 + lane) {
-                                pm[c] = INF;
-                                const int fbm = bf[c];
-                                claimed[fbm >> 5] |= 1u << (fbm & 31);
-                                if (kfkf) state[fa] = fbm;
-                                else state[fbm] = fa;
+            for (int r = 0; r < BOW_R; ++r) {
+                const int i = i0 + BOW_T * r;
+                if (i < nAn) {
+                    top1[i] = vl[r] ? k1[r] : INF - 1;   // INF - 1: A feature skipped (:224-228 / :599-603)
+                    top2[i] = k2[r];
+                }
+            }
+        }
+        __syncthreads();
+        // ---- 3. greedy replay in A order (wave 0) ----
+        if (wid == 0) {
+            auto is_claimed = [&](uint32_t k) {
+                const uint32_t p = k & 0xFFFFFu;
+                return k < INF - 1 && ((claimed[p >> 5] >> (p & 31)) & 1u);
+            };
+            auto pass = [&](int d1, int d2) {
+                return (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) && (float)d1 < g.ratio * (float)d2;
+            };
+            for (int c0 = 0; c0 < nAn; c0 += 64) {
+                const int i = c0 + lane;
+                const bool inr = i < nAn;
+                const uint32_t k1 = inr ? top1[i] : INF - 1, k2 = inr ? top2[i] : INF;
+                const bool vl = k1 != INF - 1;
+                const int fa = inr ? g.A.node_feat[a0 + i] : 0;
+                const int d1 = k1 == INF ? 256 : (int)(k1 >> 20);
+                const int d2 = k2 == INF ? 256 : min((int)(k2 >> 20), 256);
+                const bool sacc = vl && pass(d1, d2);
+                int start = 0;
+                while (true) {
+                    const bool conflict = vl && (is_claimed(k1) || is_claimed(k2));
+                    const uint64_t ev = __ballot((conflict || sacc) && lane >= start);
+                    if (!ev) break;
+                    const int t = __builtin_ctzll(ev);
+                    const bool tconf = (__ballot(conflict) >> t) & 1u;
+                    uint32_t m1;
+                    bool tacc;
+                    if (tconf) {
+                        // dynamic best / second over the unclaimed candidates
+                        const int fat = __builtin_amdgcn_readlane(fa, t);
+                        const Desc ad = load_desc(g.A.desc, (long long)fa0 + fat);
+                        uint32_t q1 = INF, q2 = INF;
+                        for (int p = lane; p < nB; p += 64) {
+                            Desc bd;
+                            if (BLDS) {
+                                const uint4 u0 = bdesc[2 * p], u1 = bdesc[2 * p + 1];
+                                bd = Desc{{u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w}};
+                            } else {
+                                const int f = g.B.node_feat[b0 + p];
+                                bd = load_desc(g.B.desc, (long long)fb0 + ((unsigned)f < (unsigned)nBt ? f : 0));
                             }
+                            const bool cl = (claimed[p >> 5] >> (p & 31)) & 1u;
+                            const uint32_t key = cl ? INF : (((uint32_t)hamming(ad, bd) << 20) | pkey[p]);
+                            q2 = min(q2, max(q1, key));
+                            q1 = min(q1, key);
+                        }
+                        m1 = wave_min_u32(q1);
+                        const uint32_t m2 = wave_min_u32(q1 == m1 ? q2 : q1);
+                        const int e1 = m1 == INF ? 256 : (int)(m1 >> 20);
+                        const int e2 = m2 == INF ? 256 : min((int)(m2 >> 20), 256);
+                        tacc = pass(e1, e2);
+                    } else {
+                        m1 = (uint32_t)__builtin_amdgcn_readlane((int)k1, t);
+                        tacc = true;
                     }
-                }
-            }
-        } else {
-            // Large node: candidates re-read every step, claims from the LDS bitmap.
-            for (int ia = a0; ia < a1; ++ia) {
-                const int fa = g.A.node_feat[ia];
-                if ((unsigned)fa >= (unsigned)nA) continue;
-                if (!g.A.flag[fa0 + fa]) continue;
-                const Desc ad = load_desc(g.A.desc, (long long)fa0 + fa);
-                uint32_t k1 = INF, k2 = INF;
-                for (int base = 0; base < nB; base += 64) {
-                    const int pos = base + lane;
-                    const int f = g.B.node_feat[b0 + min(pos, nB - 1)];
-                    const bool in = pos < nB && (unsigned)f < (unsigned)nBt;
-                    const int fc = in ? f : 0;
-                    const Desc bdd = load_desc(g.B.desc, (long long)fb0 + fc);
-                    const bool okc = in && !((claimed[fc >> 5] >> (fc & 31)) & 1u) &&
-                                     (!kfkf || g.B.flag[fb0 + fc]);
-                    const int d = hamming(ad, bdd);
-                    const uint32_t key = (okc && d < 256) ? ((uint32_t)d << 20 | (uint32_t)pos) : INF;
-                    if (key < k1) { k2 = k1; k1 = key; }
-                    else if (key < k2) { k2 = key; }
-                }
-                const uint32_t m1 = wave_min_u32(k1);
-                const uint32_t m2 = wave_min_u32(k1 == m1 ? k2 : k1);
-                const int d1 = m1 == INF ? 256 : (int)(m1 >> 20);
-                const int d2 = m2 == INF ? 256 : (int)(m2 >> 20);
-                const bool acc = (kfkf ? d1 < TH_LOW : d1 <= TH_LOW) &&
-                                 (float)d1 < g.ratio * (float)d2;
-                if (acc) {
-                    const int pos = (int)(m1 & 0xFFFFFu);
-                    const int fbm = g.B.node_feat[b0 + pos];
-                    if (lane == 0) {
-                        claimed[fbm >> 5] |= 1u << (fbm & 31);
-                        if (kfkf) state[fa] = fbm;
-                        else state[fbm] = fa;
+                    if (tacc) {
+                        const int pos = (int)(m1 & 0xFFFFFu);
+                        if (lane == 0) {
+                            claimed[pos >> 5] |= 1u << (pos & 31);
+                            const int fbm = g.B.node_feat[b0 + pos];
+                            const int fat = __builtin_amdgcn_readlane(fa, t);
+                            if (kfkf) state[fat] = fbm;
+                            else state[fbm] = fat;
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     }
+                    start = t + 1;
                 }
             }
         }
     }
     __syncthreads();
     // Rotation consistency (:298-316 / :675-693) and the count.  The histogram only needs
-    // the bin of every match, so it is built here from the final state (loads in parallel)
-    // instead of on the sequential chain.
+    // the bin of every match, so it is built here from the final state.
     if (g.check_ori) {
-        for (int i = lane; i < nOut; i += 64) {
+        for (int i = tid; i < nOut; i += BOW_T) {
             const int s = state[i];
             if (s >= 0) {
                 const int ia = kfkf ? i : s, ib = kfkf ? s : i;
@@ -286,7 +345,7 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
     }
     const Top3 top = g.check_ori ? three_maxima(hist) : Top3{-1, -1, -1};
     int cnt = 0;
-    for (int i = lane; i < nOut; i += 64) {
+    for (int i = tid; i < nOut; i += BOW_T) {
         const int s = state[i];
         int r = -1;
         if (s >= 0) {
@@ -298,9 +357,9 @@ __global__ __launch_bounds__(64) void k_bow(BowLaunch g) {
         }
         out[i] = r;
     }
-    for (int i = nOut + lane; i < g.out_stride; i += 64) out[i] = -1;
-    cnt = wave_sum(cnt);
-    if (lane == 0) g.nmatches[job] = cnt;
+    for (int i = nOut + tid; i < g.out_stride; i += BOW_T) out[i] = -1;
+    cnt = block_sum<BOW_T / 64>(cnt, hist + 32);
+    if (tid == 0) g.nmatches[job] = cnt;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1002,20 +1061,24 @@ bool proj_mode_greedy(int mode) {
            mode == ORBX_PROJ_LAST_FRAME || mode == ORBX_PROJ_KEYFRAME || mode == PROJ_INIT;
 }
 
-static int bow_npl(int max_feat) { return max_feat <= 256 ? 4 : 16; }
-
-size_t bow_lds_bytes(const BowLaunch& a) {
-    const int smax = a.kf_kf ? a.A.max_feat : a.B.max_feat;
-    return 4 * ((size_t)smax + (a.B.max_feat + 31) / 32 + 32);
+static size_t bow_lds_raw(const BowLaunch& a, bool blds) {
+    const size_t am = (size_t)a.A.max_feat, bm = (size_t)a.B.max_feat;
+    const size_t sm = a.kf_kf ? am : bm;
+    return (blds ? 32 * bm : 0) + 4 * bm + 8 * am + 4 * sm + 4 * ((bm + 31) / 32) + 4 * 40;
 }
+
+static bool bow_blds(const BowLaunch& a) { return bow_lds_raw(a, true) <= MATCH_MAX_LDS; }
+
+size_t bow_lds_bytes(const BowLaunch& a) { return bow_lds_raw(a, bow_blds(a)); }
 
 hipError_t launch_bow(const BowLaunch& a, hipStream_t st) {
     if (a.njobs <= 0) return hipSuccess;
     const size_t lds = bow_lds_bytes(a);
-    if (bow_npl(a.B.max_feat) == 4)
-        hipLaunchKernelGGL(k_bow<4>, dim3(a.njobs), dim3(64), lds, st, a);
+    if (lds > MATCH_MAX_LDS) return hipErrorInvalidValue;
+    if (bow_blds(a))
+        hipLaunchKernelGGL(k_bow<true>, dim3(a.njobs), dim3(BOW_T), lds, st, a);
     else
-        hipLaunchKernelGGL(k_bow<16>, dim3(a.njobs), dim3(64), lds, st, a);
+        hipLaunchKernelGGL(k_bow<false>, dim3(a.njobs), dim3(BOW_T), lds, st, a);
     return hipGetLastError();
 }
 
@@ -1055,8 +1118,8 @@ hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer) 
 hipError_t prepare_match_kernels() {
     const int lds = (int)MATCH_MAX_LDS;
     hipError_t e;
-    if ((e = hipFuncSetAttribute((const void*)k_bow<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void*)k_bow<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_bow<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_bow<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_triangulate, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_distinctive, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)k_proj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
