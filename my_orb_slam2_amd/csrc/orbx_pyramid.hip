@@ -196,7 +196,10 @@ __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int 
     }
 }
 
-__global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
+#ifndef LEVEL_WPE
+#define LEVEL_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))) void k_level(const Geometry* __restrict__ g,
                                                const uint8_t* __restrict__ ltab,
                                                const uint8_t* __restrict__ in0,
                                                const uint8_t* __restrict__ in1, int split,
@@ -214,7 +217,10 @@ __global__ __launch_bounds__(256) void k_level(const Geometry* __restrict__ g,
     uint8_t* p = smem;
     auto take = [&](size_t n) { uint8_t* r = p; p += (n + 15) & ~(size_t)15; return r; };
     uint32_t* lvl = (uint32_t*)take((size_t)LT_HR * LT_G * 4);      // [38][34] dwords
-    uint16_t* rows = (uint16_t*)take((size_t)LT_HR * LT_W * 2);     // [38][128] row sums
+    // the blur's row sums (phases 3-4) share their LDS with the tables and the source window
+    // (phases 1-2, dead after the barrier that ends phase 2): a smaller footprint, so more
+    // workgroups -- and more window loads in flight -- per CU
+    uint16_t* rows = (uint16_t*)p;                                   // [38][128] row sums
     uint2* cgrp = (uint2*)take((size_t)LT_G * 8);                    // per group: 4 x sx (u16)
     uint32_t* cinf = (uint32_t*)take((size_t)LT_G * 4);              // per group: flags
     uint4* calp = (uint4*)take((size_t)LT_G * 16);                   // per group: 4 x (a0, a1)
@@ -436,9 +442,10 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     (void)ltw;
     (void)lth;
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    size_t s = r((size_t)LT_HR * LT_G * 4) + r((size_t)LT_HR * LT_W * 2) + r(LT_G * 8) +
-               r(LT_G * 4) + r(LT_G * 16) + r(LT_G * 16) + r(LT_HR * 8) + r(64);
-    return s + r((size_t)win_cap + 16);
+    const size_t tables = r(LT_G * 8) + r(LT_G * 4) + r(LT_G * 16) + r(LT_G * 16) + r(LT_HR * 8);
+    const size_t phase12 = tables + r((size_t)win_cap + 16);
+    const size_t phase34 = r((size_t)LT_HR * LT_W * 2);
+    return r((size_t)LT_HR * LT_G * 4) + (phase12 > phase34 ? phase12 : phase34) + r(64);
 }
 
 hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
