@@ -445,6 +445,10 @@ def euroc_cpu_baseline(frames, inputs, budget_s):
 # ---- matcher workloads (configs[3], configs[4]) ----------------------------------------------
 
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 128 lane-ops/clk x 2.4 GHz (guide)
+# Measured issue cost on gfx950 (profiles/r01_valu_issue_rates.txt): v_xor_b32 issues at 2
+# cycles per wave64 instruction, v_bcnt_u32_b32 at 4; a 256-bit distance is 8 of each, so one
+# SIMD retires at most 64 distances per 48 cycles.
+DIST_ISSUE_PEAK = 1024 * 2.4e9 * 64 / 48
 
 
 def _hash_bytes(torch, idx, salt):
@@ -624,10 +628,14 @@ def main_match(args):
         avg_s = tot_ms / 1000.0 / launches
         if work_ops is not None:
             ach = work_ops / avg_s / 1e12
+            dps = work_ops / 16 / avg_s   # 16 lane-ops per 256-bit distance
             roof = {"kernel": kern, "bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
                     "unit": "Tops/s (int32 lane-ops)", "frac": ach / VALU_PEAK_TOPS,
                     "traffic": None, "algorithmic_ops_per_launch": work_ops,
-                    "avg_launch_ms": avg_s * 1000.0}
+                    "avg_launch_ms": avg_s * 1000.0,
+                    "distances_per_s": dps,
+                    "issue_peak_distances_per_s": DIST_ISSUE_PEAK,
+                    "issue_frac": dps / DIST_ISSUE_PEAK}
         else:
             nbytes = float(sum(fs.n for fs in kfs) * (32 + 28 + 4 + 1))
             ach = nbytes / avg_s / 1e9

@@ -24,3 +24,7 @@ timeout -k 10 600 python bench.py --workload reloc --steps 10 --warmup 2 > $OUT/
 cat $OUT/reloc.json
 timeout -k 10 600 python bench.py --workload triangulation --steps 20 --warmup 3 > $OUT/tri.json 2> $OUT/tri.err || { echo "TRI BENCH FAILED"; tail -20 $OUT/tri.err; exit 1; }
 cat $OUT/tri.json
+# kernel traces of the matcher workloads (configs[3], configs[4])
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_reloc -o run --output-format csv -- python3 bench.py --workload reloc --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_reloc.log 2>&1 || { echo "RELOC TRACE FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_tri -o run --output-format csv -- python3 bench.py --workload triangulation --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_tri.log 2>&1 || { echo "TRI TRACE FAILED"; exit 1; }
+echo session done
