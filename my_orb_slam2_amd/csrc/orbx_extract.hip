@@ -138,6 +138,54 @@ __device__ __forceinline__ u16x2 pair_u16(const uint32_t* A, int s_abs) {
     return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(A[k + 1], A[k], sel));
 }
 
+// Pixels s_abs and s_abs+2 as two zero-extended u16s (one v_perm).
+__device__ __forceinline__ uint32_t pair_u16_stride2(const uint32_t* A, int s_abs) {
+    const int k = s_abs >> 2, s = s_abs & 3;
+    const uint32_t sel = (uint32_t)s | 0x0C00u | (uint32_t)(s + 2) << 16 | 0x0C000000u;
+    return __builtin_amdgcn_perm(A[k + 1], A[k], sel);
+}
+
+// Bit positions of pixels 0..3 in the compass4_fr flag word.
+#define CMP_B0 14
+#define CMP_B1 15
+#define CMP_B2 30
+#define CMP_B3 31
+
+// The compass pre-test below on full-rate 32-bit adds and logic only.  With two pixels per
+// dword as u16 halves (pixels j and j+2) and K = (0x4000 - t - 1) in each half:
+//   n > v + t  <=>  bit 14 of n + (K - v)       n < v - t  <=>  bit 14 of (K + v) - n
+// (every half stays inside (0, 0x8000), so no carry or borrow crosses a half), and "two
+// neighbouring compass pixels beyond t on one side" is (b0 | b8) & (b4 | b12) on those bits.
+// Returns the flags of pixels 0..3 at bits CMP_B0..CMP_B3 (all other bits zero).
+template <int XO>
+__device__ __forceinline__ uint32_t compass4_fr(const uint8_t* roi0, int rp, int R, int gx, uint32_t K) {
+    const uint32_t* rc = (const uint32_t*)(roi0 + R * rp) + gx;
+    const uint32_t* rd = (const uint32_t*)(roi0 + (R + 3) * rp) + gx;
+    const uint32_t* ru = (const uint32_t*)(roi0 + (R - 3) * rp) + gx;
+    constexpr int KC = (XO + 9) >> 2;
+    constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
+    uint32_t C[5], D[5], U[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        C[k] = k <= KC ? rc[k] : 0u;
+        D[k] = (k >= K0 && k <= K1) ? rd[k] : 0u;
+        U[k] = (k >= K0 && k <= K1) ? ru[k] : 0u;
+    }
+    uint32_t F[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int o = XO + 3 + h;                   // byte of pixel h (centre row): pixels h, h+2
+        const uint32_t V = pair_u16_stride2(C, o);
+        const uint32_t N12 = pair_u16_stride2(C, o - 3), N4 = pair_u16_stride2(C, o + 3);
+        const uint32_t N0 = pair_u16_stride2(D, o), N8 = pair_u16_stride2(U, o);
+        const uint32_t A = K - V, B = K + V;
+        const uint32_t bright = ((N0 + A) | (N8 + A)) & ((N4 + A) | (N12 + A));
+        const uint32_t dark = ((B - N0) | (B - N8)) & ((B - N4) | (B - N12));
+        F[h] = (bright | dark) & 0x40004000u;       // bits 14 (pixel h), 30 (pixel h + 2)
+    }
+    return F[0] | (F[1] << 1);
+}
+
 // FAST compass pre-test of 4 adjacent pixels (detection columns 4gx..4gx+3 of ROI row R):
 // a 9-pixel arc beyond the threshold contains two neighbouring compass pixels (circle
 // indices i, i+4) beyond it on the same side.  Packed 16-bit saturating arithmetic, two
@@ -204,7 +252,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     int16_t* corners = list + FAST_LIST + 64;   // pixels with M > min threshold, raster order
     const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
     const int tq = min(g->ini_th, g->min_th);
+#if FAST_COMPASS_PK
     const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
+#else
+    const uint32_t KT = (uint32_t)(0x4000 - tq - 1) * 0x10001u;
+#endif
 
     // ROI of a cell as aligned dwords, dense rows of ndw dwords: LDS dword t = lane + 64j
     uint32_t pf[FAST_PF];
@@ -270,7 +322,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
         const int rpp = 64 >> gsh;
         const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
-        const uint32_t colmask = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
+        const uint32_t colmask4 = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
+#if FAST_COMPASS_PK
+        const uint32_t colmask = colmask4;
+        constexpr int PB[4] = {0, 1, 2, 3};
+#else
+        const uint32_t colmask = ((colmask4 & 3u) << CMP_B0) | ((colmask4 & 12u) << (CMP_B2 - 2));
+        constexpr int PB[4] = {CMP_B0, CMP_B1, CMP_B2, CMP_B3};
+#endif
         const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
         int ncorner = 0;
         for (int rb = 0; rb < dh; rb += rows_blk) {
@@ -279,15 +338,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 const int rr = r0 + sub;
                 const int R = min(rr, dh - 1) + 3;
                 uint32_t f;
+#if FAST_COMPASS_PK
                 switch (xo) {
                     case 0: f = compass4<0>(roi0, rp, R, gx, T); break;
                     case 1: f = compass4<1>(roi0, rp, R, gx, T); break;
                     case 2: f = compass4<2>(roi0, rp, R, gx, T); break;
                     default: f = compass4<3>(roi0, rp, R, gx, T); break;
                 }
+#else
+                switch (xo) {
+                    case 0: f = compass4_fr<0>(roi0, rp, R, gx, KT); break;
+                    case 1: f = compass4_fr<1>(roi0, rp, R, gx, KT); break;
+                    case 2: f = compass4_fr<2>(roi0, rp, R, gx, KT); break;
+                    default: f = compass4_fr<3>(roi0, rp, R, gx, KT); break;
+                }
+#endif
                 f &= rr < dh ? colmask : 0u;
-                const uint64_t m0 = __ballot(f & 1u), m1 = __ballot(f & 2u);
-                const uint64_t m2 = __ballot(f & 4u), m3 = __ballot(f & 8u);
+                const uint64_t m0 = __ballot(f & (1u << PB[0])), m1 = __ballot(f & (1u << PB[1]));
+                const uint64_t m2 = __ballot(f & (1u << PB[2])), m3 = __ballot(f & (1u << PB[3]));
                 uint32_t below = __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u);
                 below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), below);
                 below = __builtin_amdgcn_mbcnt_lo((uint32_t)m1, below);
@@ -300,7 +368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 const int e0 = (rr << 6) | (4 * gx);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {   // unset bits write this lane's spare slot
-                    const int on = (f >> j) & 1u;
+                    const int on = (f >> PB[j]) & 1u;
                     list[on ? pos : FAST_LIST + lane] = (int16_t)(e0 + j);
                     pos += on;
                 }
