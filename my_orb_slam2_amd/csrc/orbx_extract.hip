@@ -353,6 +353,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                     default: f = compass4_fr<3>(roi0, rp, R, gx, KT); break;
                 }
 #endif
+#if FAST_DIAG >= 2   // diagnostic builds only (tools/variants.py): no compass survivors
+                f = 0u;
+#endif
                 f &= rr < dh ? colmask : 0u;
                 const uint64_t m0 = __ballot(f & (1u << PB[0])), m1 = __ballot(f & (1u << PB[1]));
                 const uint64_t m2 = __ballot(f & (1u << PB[2])), m3 = __ballot(f & (1u << PB[3]));
@@ -375,6 +378,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
             }
             lds_order();
+#if FAST_DIAG >= 1   // diagnostic builds only: skip the arc score
+            nlist = 0;
+#endif
             // 2. full arc score for the survivors only (dense across lanes); those above the
             //    lower threshold are appended to the corner list, keeping raster order
             for (int j0 = 0; j0 < nlist; j0 += 64) {
@@ -1023,13 +1029,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_blr(p + 1);
         const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ((x - 18) & ~3));
+        // cvRound (:118-120) by the round-to-nearest-even of a float add: for |v| < 2^22,
+        // v + 1.5*2^23 holds rint(v) in its low mantissa bits, so its bit pattern is
+        // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
+        // so one mad gives the patch offset up to a constant folded into the base.
+        const float MAGIC = 12582912.0f;
+        const uint8_t* bcm = bc - (0x400000u * (OD_BLR_DW * 4) + 0x4B400000u);
+        auto sample = [&](float ra, float rb, float cA, float cB) {
+            const uint32_t ro = __builtin_bit_cast(uint32_t, (ra + rb) + MAGIC);
+            const uint32_t co = __builtin_bit_cast(uint32_t, (cA - cB) + MAGIC);
+            return (int)bcm[__umul24(ro, OD_BLR_DW * 4) + co];
+        };
         uint32_t words[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             const float r1a = px1[w] * sb, r1b = py1[w] * ca, c1a = px1[w] * ca, c1b = py1[w] * sb;
             const float r2a = px2[w] * sb, r2b = py2[w] * ca, c2a = px2[w] * ca, c2b = py2[w] * sb;
-            const int t0 = bc[cv_round(r1a + r1b) * (OD_BLR_DW * 4) + cv_round(c1a - c1b)];
-            const int t1 = bc[cv_round(r2a + r2b) * (OD_BLR_DW * 4) + cv_round(c2a - c2b)];
+            const int t0 = sample(r1a, r1b, c1a, c1b);
+            const int t1 = sample(r2a, r2b, c2a, c2b);
             const uint64_t m = __ballot(t0 < t1);
             words[w] = half ? (uint32_t)(m >> 32) : (uint32_t)m;
         }

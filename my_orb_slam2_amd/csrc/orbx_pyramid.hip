@@ -196,6 +196,129 @@ __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int 
     }
 }
 
+#ifndef BLUR_F32
+#define BLUR_F32 1     // row sums kept as floats, column pass in float (exact, see below)
+#endif
+#ifndef BLUR_CVTPK
+#define BLUR_CVTPK 1   // round + saturate + pack with v_cvt_pk_u8_f32 (else magic-add rounding)
+#endif
+
+// ---- 4'. blur row pass with float row sums (BLUR_F32) ----
+// Same v_dot4 sums as tile_out_rows; each sum (<= 257 * 255) is stored as an exact float.
+template <bool FULL>
+__device__ __forceinline__ void tile_out_rows_f(const uint32_t* lvl, float* rows, int tid, int vw,
+                                                int vh, uint8_t* dlev, int X0, int Y0, int pitch,
+                                                const BlurTaps& tp) {
+    const int ng = FULL ? LT_GW : (vw + 3) >> 2;
+    const int n3 = FULL ? LT_H * LT_GW : vh * LT_GW;
+    auto out_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        const uint32_t v = lvl[(r + 3) * LT_G + gq + 1];
+        uint8_t* d = dlev + __umul24(Y0 + r, pitch) + X0 + 4 * gq;
+        if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = v;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(v >> (8 * j));
+    };
+    if constexpr (FULL) {
+#pragma unroll
+        for (int k = 0; k < LT_H * LT_GW / 256; ++k) out_item(tid + 256 * k);
+    } else {
+        for (int i = tid; i < n3; i += 256) out_item(i);
+    }
+    const int n4 = FULL ? (LT_H + 6) * LT_GW : (vh + 6) * LT_GW;
+    auto row_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        const uint32_t* s = lvl + r * LT_G + gq;
+        const uint32_t d0 = s[0], d1 = s[1], d2 = s[2];
+        float4 o;
+        o.x = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), tp.tapB, 0u, false), false);
+        o.y = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), tp.tapB, 0u, false), false);
+        o.z = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tp.tapB, 0u, false), false);
+        o.w = (float)__builtin_amdgcn_udot4(d1, tp.tapA, __builtin_amdgcn_udot4(d2, tp.tapB, 0u, false), false);
+        *(float4*)(rows + r * LT_W + 4 * gq) = o;
+    };
+    if constexpr (FULL) {
+        constexpr int K4 = ((LT_H + 6) * LT_GW) / 256, R4 = ((LT_H + 6) * LT_GW) % 256;
+#pragma unroll
+        for (int k = 0; k < K4; ++k) row_item(tid + 256 * k);
+        if (tid < R4) row_item(tid + 256 * K4);
+    } else {
+        for (int i = tid; i < n4; i += 256) row_item(i);
+    }
+}
+
+// ---- 5'. blur column pass in float (BLUR_F32) ----
+// S = k3*c + k4*(r2+r4) + k5*(r1+r5) + k6*(r0+r6) with integer taps and integer row sums:
+// every pairwise sum (< 2^17), product (< 2^23) and partial sum (< 2^24, see tile_columns)
+// is exact in float, so Sf == S.  SSE2 pixels take rint(S / 65536) saturated to u8
+// (v_cvt_pk_u8_f32 rounds to nearest even and clamps, as cvtps + packus do); the scalar
+// tail takes (S + 32768) >> 16 from the exact integer.
+template <bool FULL>
+__device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int vw, int vh,
+                                               uint8_t* dblur, int X0, int Y0, int pitch,
+                                               int bsimd_end, const BlurTaps& tp) {
+    const int ng = FULL ? LT_GW : (vw + 3) >> 2;
+    const int n5 = FULL ? LT_H * LT_GW : vh * LT_GW;
+    const float f3 = (float)tp.k3, f4 = (float)(tp.K4 & 0xFFFF), f5 = (float)(tp.K5 & 0xFFFF),
+                f6 = (float)(tp.K6 & 0xFFFF);
+    const float inv = 1.0f / 65536.0f;
+    // groups entirely left of bsimd_end take the SSE2 form only
+    const bool tile_simd = X0 + 4 * ng <= bsimd_end;
+    auto col_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        float4 v[7];
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) v[kk] = *(const float4*)(rows + (r + kk) * LT_W + 4 * gq);
+        const int xg = X0 + 4 * gq;
+        float S[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto c = [&](int kk) { return j == 0 ? v[kk].x : (j == 1 ? v[kk].y : (j == 2 ? v[kk].z : v[kk].w)); };
+            float a = (c(0) + c(6)) * f6;
+            a = __builtin_fmaf(c(1) + c(5), f5, a);
+            a = __builtin_fmaf(c(2) + c(4), f4, a);
+            S[j] = __builtin_fmaf(c(3), f3, a);
+        }
+        uint32_t packed = 0;
+        if (tile_simd || xg + 4 <= bsimd_end) {
+#if BLUR_CVTPK
+#pragma unroll
+            for (int j = 0; j < 4; ++j) packed = __builtin_amdgcn_cvt_pk_u8_f32(S[j] * inv, j, packed);
+#else
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_fmaf(S[j], inv, 12582912.0f)) - 0x4B400000u;
+                packed |= min(t, 255u) << (8 * j);
+            }
+#endif
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t Si = (uint32_t)S[j];
+                const bool simd = xg + j < bsimd_end;
+                const uint32_t val = (Si + (simd ? 32767u + ((Si >> 16) & 1u) : 32768u)) >> 16;
+                packed |= min(val, 255u) << (8 * j);
+            }
+        }
+        uint8_t* d = dblur + __umul24(Y0 + r, pitch) + xg;
+        if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = packed;
+        else
+            for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+    };
+    if constexpr (FULL) {
+#pragma unroll
+        for (int k = 0; k < LT_H * LT_GW / 256; ++k) col_item(tid + 256 * k);
+    } else {
+        for (int i = tid; i < n5; i += 256) col_item(i);
+    }
+}
+
 #ifndef LEVEL_WPE
 #define LEVEL_WPE 1
 #endif
@@ -429,12 +552,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                          (uint32_t)k3};
     // full tiles (all but the right / bottom edge) run the fixed-trip-count form
     const bool full = vw == LT_W && vh == LT_H;
+#if BLUR_F32
+    float* rowsf = (float*)rows;
+    if (full) tile_out_rows_f<true>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
+    else tile_out_rows_f<false>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
+    __syncthreads();
+    STAMP(4);
+    if (full) tile_columns_f<true>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+    else tile_columns_f<false>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+#else
     if (full) tile_out_rows<true>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     else tile_out_rows<false>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     __syncthreads();
     STAMP(4);
     if (full) tile_columns<true>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
     else tile_columns<false>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+#endif
     STAMP(5);
 }
 
@@ -444,7 +577,7 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
     const size_t tables = r(LT_G * 8) + r(LT_G * 4) + r(LT_G * 16) + r(LT_G * 16) + r(LT_HR * 8);
     const size_t phase12 = tables + r((size_t)win_cap + 16);
-    const size_t phase34 = r((size_t)LT_HR * LT_W * 2);
+    const size_t phase34 = r((size_t)LT_HR * LT_W * (BLUR_F32 ? 4 : 2));
     return r((size_t)LT_HR * LT_G * 4) + (phase12 > phase34 ? phase12 : phase34) + r(64);
 }
 
