@@ -4,6 +4,22 @@
 #include <stdint.h>
 
 namespace orbx {
+#ifndef ORBX_XCD_REMAP
+#define ORBX_XCD_REMAP 1
+#endif
+// Logical (x, y) block of a 2-D grid.  Consecutive linear blocks are dealt round-robin over
+// the 8 XCDs (MI355X_MICROARCH.md §Workgroup dispatch: blocks b and b + 8 share an XCD), so
+// linear block L runs logical block (L mod 8) * n/8 + L / 8: every XCD walks a contiguous
+// eighth of the logical order, and blocks that share halo rows, patches or an image share
+// that XCD's L2.  Results never depend on the mapping.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const uint32_t gx = gridDim.x, n = gx * gridDim.y;
+    uint32_t L = blockIdx.y * gx + blockIdx.x;
+    if (ORBX_XCD_REMAP && (n & 7u) == 0) L = (L & 7u) * (n >> 3) + (L >> 3);
+    by = (int)(L / gx);
+    bx = (int)(L - (uint32_t)by * gx);
+}
+
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 

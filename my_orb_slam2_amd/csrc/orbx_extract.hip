@@ -239,9 +239,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                                               uint32_t* __restrict__ cand) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
+    // linear block order (measured: the XCD remap does not help k_fast)
+    const int bx = blockIdx.x, b = blockIdx.y;
     // one wave owns FAST_NC consecutive cells; no block-level barriers: waves are independent
-    const int c_first = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * FAST_NC);
+    const int c_first = __builtin_amdgcn_readfirstlane((bx * 4 + wid) * FAST_NC);
     if (c_first >= g->n_cells) return;
     const int ncw = min(FAST_NC, g->n_cells - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
@@ -882,7 +883,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const uint32_t* __restrict__ okp, float* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkp) {
     __shared__ uint32_t patch[4][2][OD_BLR_N];
-    const int b = blockIdx.y, blk = blockIdx.x;
+    int blk, b;
+    xcd_block(blk, b);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int half = lane >> 5, l32 = lane & 31;
     int level = 0;

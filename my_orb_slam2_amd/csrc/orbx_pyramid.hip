@@ -330,10 +330,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                                                uint8_t* __restrict__ pyr,
                                                uint8_t* __restrict__ blur, int level) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int b = blockIdx.y, tid = threadIdx.x;
+    int bx, b;
+    xcd_block(bx, b);
+    const int tid = threadIdx.x;
     STAMP(0);
     const LevelGeom& L = g->lv[level];
-    const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
+    const int tx = bx % L.ntx, ty = bx / L.ntx;
     const int X0 = tx * LT_W, Y0 = ty * LT_H;
     const int vw = min(LT_W, L.w - X0), vh = min(LT_H, L.h - Y0);
 
