@@ -373,19 +373,19 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                 const bool contig = sx[1] == sx[0] + 1 && sx[2] == sx[0] + 2 &&
                                     sx[3] == sx[0] + 3 && (sx[0] & 3) == 0;
                 const int o0 = sx[0] & 3;
+                (void)o0;
                 const bool simple = sx[1] >= sx[0] && sx[2] >= sx[1] && sx[3] >= sx[2] &&
-                                    o0 + (sx[3] - sx[0]) + 1 <= 11;
+                                    sx[3] - sx[0] <= 6;
                 c.cgrp[2 * q] = (uint32_t)sx[0] | ((uint32_t)sx[1] << 16);
                 c.cgrp[2 * q + 1] = (uint32_t)sx[2] | ((uint32_t)sx[3] << 16);
-                uint32_t hi = 0;
+                const uint32_t hi = 0;
                 for (int j = 0; j < 4; ++j) {
-                    // simple groups: pixel j's taps are bytes k, k+1 of the 12 bytes from
-                    // (sx0 & ~3); v_perm picks them from dwords 0-1 (k <= 6) or 1-2 as u16s
-                    const int k = sx[j] - (sx[0] & ~3);
-                    const int kk = (k > 6) ? k - 4 : k;
-                    if (k > 6) hi |= 0x1000u << j;
-                    c.csel[4 * q + j] = (uint32_t)(kk & 7) | (0x0Cu << 8) |
-                                        ((uint32_t)((kk + 1) & 7) << 16) | (0x0Cu << 24);
+                    // simple groups: pixel j's taps are bytes k, k+1 of the 8 bytes from sx0
+                    // (the kernel aligns the window to sx0 with v_alignbyte); v_perm picks
+                    // them as u16s
+                    const int k = std::min(std::max(sx[j] - sx[0], 0), 6);
+                    c.csel[4 * q + j] = (uint32_t)k | (0x0Cu << 8) |
+                                        ((uint32_t)(k + 1) << 16) | (0x0Cu << 24);
                     // right of xmax HResizeLinear uses S[sx] * 2048: the same dot product
                     // with alphas (2048, 0)
                     if (mode == 3 && !((fl >> (2 * j)) & 1u)) al[j] = 2048u;

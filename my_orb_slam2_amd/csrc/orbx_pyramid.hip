@@ -449,26 +449,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                     // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
                     const uint4 sl = csel[q];
                     const uint32_t sels[4] = {sl.x, sl.y, sl.z, sl.w};
-                    const int base = xs[0] & ~3;
+                    const int base = xs[0] & ~3, o0 = xs[0] & 3;
                     const uint32_t* d0p = (const uint32_t*)(w0 + base);
                     const uint32_t* d1p = (const uint32_t*)(w1 + base);
                     const uint32_t a0 = d0p[0], a1 = d0p[1], a2 = d0p[2];
                     const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
+                    // 8-byte windows starting at the group's first tap column (span <= 7)
+                    const uint32_t wa0 = __builtin_amdgcn_alignbyte(a1, a0, o0);
+                    const uint32_t wa1 = __builtin_amdgcn_alignbyte(a2, a1, o0);
+                    const uint32_t wc0 = __builtin_amdgcn_alignbyte(c1, c0, o0);
+                    const uint32_t wc1 = __builtin_amdgcn_alignbyte(c2, c1, o0);
                     // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind; 24-bit
                     // multiplies (full rate): h < 2^19, b <= 2048.  Groups whose 4 pixels all
                     // take the SSE2 form (all but the right edge) skip the scalar form.
                     const bool all_simd = ((ci >> 1) & 0x55u) == 0x55u;
                     auto hsum = [&](int j, int& h0, int& h1) {
-                        const bool hi = (ci >> (12 + j)) & 1u;
-                        const uint32_t p0 = __builtin_amdgcn_perm(hi ? a2 : a1, hi ? a1 : a0, sels[j]);
-                        const uint32_t p1 = __builtin_amdgcn_perm(hi ? c2 : c1, hi ? c1 : c0, sels[j]);
+                        const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
+                        const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
                         const us2 al = __builtin_bit_cast(us2, als[j]);
                         h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
                         h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
                     };
+                    // no saturation: alphas and betas each sum to 2048, so both products
+                    // together are <= (255*2048 >> 4) * 2048 >> 16 = 1020 and the value <= 255
                     auto vsimd = [&](int h0, int h1) {
-                        return min(((int)(__umul24(h0 >> 4, b0) >> 16) +
-                                    (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2, 255);
+                        return ((int)(__umul24(h0 >> 4, b0) >> 16) +
+                                (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2;
                     };
                     if (all_simd) {
 #pragma unroll
