@@ -390,6 +390,11 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                     // with alphas (2048, 0)
                     if (mode == 3 && !((fl >> (2 * j)) & 1u)) al[j] = 2048u;
                 }
+                // simple groups carry 16 x the alphas (<= 32768 still a u16): the kernel's
+                // dot product then yields 16 h, whose low byte cleared is (h >> 4) << 8
+                if (mode == 3 && simple)
+                    for (int j = 0; j < 4; ++j)
+                        al[j] = ((al[j] & 0xFFFFu) << 4) | (((al[j] >> 16) << 4) << 16);
                 c.cinf[q] = fl | (contig ? 0x100u : 0u) | (simple ? 0x200u : 0u) | hi;
                 for (int j = 0; j < 4; ++j) c.calp[4 * q + j] = al[j];
             }

@@ -470,11 +470,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                         h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
                         h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
                     };
-                    // no saturation: alphas and betas each sum to 2048, so both products
-                    // together are <= (255*2048 >> 4) * 2048 >> 16 = 1020 and the value <= 255
-                    auto vsimd = [&](int h0, int h1) {
-                        return ((int)(__umul24(h0 >> 4, b0) >> 16) +
-                                (int)(__umul24(h1 >> 4, b1) >> 16) + 2) >> 2;
+                    // hsum returns H = 16 h (the table alphas are scaled by 16), so
+                    // ((h >> 4) * b) >> 16 = mulhi_u24(H & ~0xFF, b << 8): one v_and and one
+                    // v_mul_hi_u32_u24 per term.  No saturation: alphas and betas each sum to
+                    // 2048, so the two terms are <= (255*2048 >> 4) * 2048 >> 16 = 1020 and
+                    // the value <= 255.
+                    const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
+                    auto mulhi24 = [](uint32_t x, uint32_t y) {
+                        return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * (y & 0xFFFFFFu)) >> 32);
+                    };
+                    auto vsimd = [&](int H0, int H1) {
+                        return (int)((mulhi24((uint32_t)H0 & ~0xFFu, bs0) +
+                                      mulhi24((uint32_t)H1 & ~0xFFu, bs1) + 2u) >> 2);
                     };
                     if (all_simd) {
 #pragma unroll
@@ -489,6 +496,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                             int h0, h1;
                             hsum(j, h0, h1);
                             const int vs = vsimd(h0, h1);
+                            h0 >>= 4;
+                            h1 >>= 4;
                             const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
                             out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
                         }
