@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="stereo: batches in flight on separate HIP streams (step i uses handle "
+                         "and stream i %% inflight)")
     ap.add_argument("--workload", default="stereo",
                     choices=["stereo", "euroc", "reloc", "triangulation"],
                     help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
@@ -115,23 +118,29 @@ def main():
     torch.cuda.synchronize(dev)
 
     mb = float(np.float32(MBF) / np.float32(FX))
-    sb = orbx.StereoBatch(B, NFEAT, 1.2, 8, 20, 7, device=local)
-    stream = torch.cuda.current_stream(dev)
-    st = stream.cuda_stream
+    NI = max(1, args.inflight)
+    sbs = [orbx.StereoBatch(B, NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(NI)]
+    sb = sbs[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NI - 1)]
+    sts = [s_.cuda_stream for s_ in streams]
 
-    for _ in range(args.warmup):
-        sb(Ls, Rs, MBF, mb, stream=st)
+    def run_step(i):
+        sbs[i % NI](Ls, Rs, MBF, mb, stream=sts[i % NI])
+
+    for i in range(args.warmup):
+        run_step(i)
     torch.cuda.synchronize(dev)
     if not args.no_kernel_timing:
-        sb.profile(True)
-        sb.collect_profile()
+        for h in sbs:
+            h.profile(True)
+            h.collect_profile()
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sb(Ls, Rs, MBF, mb, stream=st)
+    for i in range(args.steps):
+        run_step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -141,7 +150,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    prof = sb.collect_profile() if not args.no_kernel_timing else {}
+    prof = {}
+    if not args.no_kernel_timing:
+        for h in sbs:
+            for k, (ms, n) in h.collect_profile().items():
+                t0_, n0_ = prof.get(k, (0.0, 0))
+                prof[k] = (t0_ + ms, n0_ + n)
 
     # sanity on the produced work (outside the timed region)
     nv = sb.nvalid.cpu().numpy()
@@ -179,7 +193,7 @@ def main():
                "config": {"workload": "kitti_stereo_extract_match", "width": W, "height": H,
                           "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2,
                           "pairs_per_step_per_gpu": B, "distinct_pairs": n_distinct,
-                          "base_pairs": P,
+                          "base_pairs": P, "inflight_batches": NI,
                           "parallelism": f"dp{world}"},
                "mean_keypoints_left": float(nkp.mean()),
                "mean_stereo_matches": float(nv.mean()),
