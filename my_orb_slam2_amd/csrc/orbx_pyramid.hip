@@ -264,9 +264,11 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
                                                int bsimd_end, const BlurTaps& tp) {
     const int ng = FULL ? LT_GW : (vw + 3) >> 2;
     const int n5 = FULL ? LT_H * LT_GW : vh * LT_GW;
-    const float f3 = (float)tp.k3, f4 = (float)(tp.K4 & 0xFFFF), f5 = (float)(tp.K5 & 0xFFFF),
-                f6 = (float)(tp.K6 & 0xFFFF);
+    // taps k / 65536 (the SSE2 path's own coefficients): power-of-two scaling keeps every
+    // product and partial sum exact, so Sf = S / 65536 exactly
     const float inv = 1.0f / 65536.0f;
+    const float f3 = (float)tp.k3 * inv, f4 = (float)(tp.K4 & 0xFFFF) * inv,
+                f5 = (float)(tp.K5 & 0xFFFF) * inv, f6 = (float)(tp.K6 & 0xFFFF) * inv;
     // groups entirely left of bsimd_end take the SSE2 form only
     const bool tile_simd = X0 + 4 * ng <= bsimd_end;
     auto col_item = [&](int i) {
@@ -289,18 +291,18 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
         if (tile_simd || xg + 4 <= bsimd_end) {
 #if BLUR_CVTPK
 #pragma unroll
-            for (int j = 0; j < 4; ++j) packed = __builtin_amdgcn_cvt_pk_u8_f32(S[j] * inv, j, packed);
+            for (int j = 0; j < 4; ++j) packed = __builtin_amdgcn_cvt_pk_u8_f32(S[j], j, packed);
 #else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_fmaf(S[j], inv, 12582912.0f)) - 0x4B400000u;
+                const uint32_t t = __builtin_bit_cast(uint32_t, S[j] + 12582912.0f) - 0x4B400000u;
                 packed |= min(t, 255u) << (8 * j);
             }
 #endif
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t Si = (uint32_t)S[j];
+                const uint32_t Si = (uint32_t)(S[j] * 65536.0f);
                 const bool simd = xg + j < bsimd_end;
                 const uint32_t val = (Si + (simd ? 32767u + ((Si >> 16) & 1u) : 32768u)) >> 16;
                 packed |= min(val, 255u) << (8 * j);
