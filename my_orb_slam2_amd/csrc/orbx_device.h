@@ -131,6 +131,37 @@ __device__ __forceinline__ void stage_dwords(const uint8_t* __restrict__ gsrc, s
     vmem_drained();
 }
 
+// Column-owner form for windows of at most 64 dwords per row and 4*MAXK rows (256 threads):
+// lane c of wave w owns column c and rows w, w + 4, ...  The per-lane source and LDS offsets
+// are fixed; row k's base is a uniform (scalar) address, so an element costs one load and one
+// LDS store and no per-element index arithmetic or exec-mask branch.  Returns false (nothing
+// staged) when the window does not fit the form.
+template <int MAXK>
+__device__ __forceinline__ bool stage_dwords_cols(const uint8_t* __restrict__ gsrc, size_t gpitch,
+                                                  int rows, int ndw, uint32_t* lds,
+                                                  int lpitch_dw, int tid) {
+    if (ndw > 64 || rows > 4 * MAXK) return false;
+    if (rows <= 0 || ndw <= 0) return true;
+    const int c = tid & 63, w = tid >> 6;
+    const bool colok = c < ndw;
+    const uint32_t voff = 4u * (uint32_t)(colok ? c : 0);
+    uint32_t v[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+        // rows past the window re-read the last row (uniform clamp, no branch)
+        const int r = min(w + 4 * k, rows - 1);
+        v[k] = *(const uint32_t*)(gsrc + (size_t)r * gpitch + voff);
+    }
+    if (colok) {
+        uint32_t* l = lds + w * lpitch_dw + c;
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k)
+            if (w + 4 * k < rows) l[4 * k * lpitch_dw] = v[k];
+    }
+    vmem_drained();
+    return true;
+}
+
 // Same for an arbitrary byte window (no alignment), 16 loads in flight per thread.
 template <int NT>
 __device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, size_t gpitch,

@@ -321,6 +321,9 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
     }
 }
 
+#ifndef STAGE_MAXK
+#define STAGE_MAXK 12  // column-owner window staging: up to 48 rows (0: always the generic form)
+#endif
 #ifndef LEVEL_WPE
 #define LEVEL_WPE 1
 #endif
@@ -408,12 +411,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         stage_bytes<256>(src + (size_t)wy0 * stride + wx0, stride, WH, WWb, win + wcol0, WP, tid);
     } else if (mode == 1) {
         const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;   // wx0 is a multiple of 4
-        stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, (WWb + 3) >> 2,
-                          (uint32_t*)(win + wcol0), WP / 4, tid);
+        if (!stage_dwords_cols<STAGE_MAXK>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH,
+                                           (WWb + 3) >> 2, (uint32_t*)(win + wcol0), WP / 4, tid))
+            stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, (WWb + 3) >> 2,
+                              (uint32_t*)(win + wcol0), WP / 4, tid);
     } else if (mode == 3) {
         const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;
-        stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4, (uint32_t*)win,
-                          WP / 4, tid);
+        if (!stage_dwords_cols<STAGE_MAXK>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4,
+                                           (uint32_t*)win, WP / 4, tid))
+            stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4,
+                              (uint32_t*)win, WP / 4, tid);
     }
     if (tid < LT_G) {
         cgrp[tid] = make_uint2(tc.x, tc.y);
