@@ -158,6 +158,9 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
         if (bestR < 0 || best >= 75) continue;   // thOrbDist = (TH_HIGH + TH_LOW) / 2
 
+#if ST_DIAG   // diagnostic builds only (tools/variants.py): descriptor search without the SAD
+        if (bestE >= 0) continue;
+#endif
         // ---- sliding-window SAD on the unblurred level of the left keypoint ----
         const LevelGeom& LV = g->lv[levelL];
         const float uR0 = __uint_as_float(rrec[bestE].x);
@@ -205,22 +208,45 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
 #pragma unroll
             for (int k = 0; k < 11; ++k) cR[k] = byte_of(rc, k + 5);
         }
+        // sum_x |(l_x - cL) - (r_{k+x} - cR_k)| = sum_x |(l_x + 256) - (r_{k+x} + 256 + cL - cR_k)|
+        // with every operand in [0, 1023]: v_sad_u16 takes two pixels per instruction (pixel
+        // pairs packed as u16 halves by v_perm), the 11th pixel one v_sad_u32-style |a - b|
         int acc[11];
+        uint32_t E[11];
 #pragma unroll
-        for (int k = 0; k < 11; ++k) acc[k] = 0;
+        for (int k = 0; k < 11; ++k) {
+            acc[k] = 0;
+            E[k] = (uint32_t)(256 + cL - cR[k]) * 0x10001u;
+        }
+        auto pair_sel = [](int s0) {   // bytes s0, s0 + 1 of an 8-byte (hi:lo) pair as u16s
+            return (uint32_t)(s0 & 7) | 0x0C00u | (uint32_t)((s0 + 1) & 7) << 16 | 0x0C000000u;
+        };
 #pragma unroll
         for (int r = 0; r < 11; ++r) {
             uint32_t lw[3], rw[6];
             lrow(r, lw);
             rrow(r, rw);
+            uint32_t LP[5];
 #pragma unroll
-            for (int xx = 0; xx < 11; ++xx) {
-                const int il = byte_of(lw, xx) - cL;
+            for (int j = 0; j < 5; ++j) {
+                const int b0 = 2 * j;   // bytes b0, b0 + 1 of lw
+                LP[j] = __builtin_amdgcn_perm(lw[(b0 >> 2) + 1 < 3 ? (b0 >> 2) + 1 : 2], lw[b0 >> 2],
+                                              pair_sel(b0 & 3)) + 0x01000100u;
+            }
+            const int l10 = byte_of(lw, 10) + 256;
+            // right pixel pairs starting at every byte 0..19: RP[m] = (r_m, r_{m+1})
+            uint32_t RP[20];
 #pragma unroll
-                for (int k = 0; k < 11; ++k) {
-                    const int d = il - (byte_of(rw, k + xx) - cR[k]);
-                    acc[k] += d < 0 ? -d : d;
-                }
+            for (int m = 0; m < 20; ++m)
+                RP[m] = __builtin_amdgcn_perm(rw[(m >> 2) + 1 < 6 ? (m >> 2) + 1 : 5], rw[m >> 2],
+                                              pair_sel(m & 3));
+#pragma unroll
+            for (int k = 0; k < 11; ++k) {
+                uint32_t a = (uint32_t)acc[k];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) a = __builtin_amdgcn_sad_u16(LP[j], RP[k + 2 * j] + E[k], a);
+                const int d = l10 - (byte_of(rw, k + 10) + (int)(E[k] & 0xFFFFu));
+                acc[k] = (int)a + (d < 0 ? -d : d);
             }
         }
         int bestDist = 0x7FFFFFFF;
