@@ -159,9 +159,11 @@ __device__ __forceinline__ uint32_t pair_u16_stride2(const uint32_t* A, int s_ab
 // Returns the flags of pixels 0..3 at bits CMP_B0..CMP_B3 (all other bits zero).
 template <int XO>
 __device__ __forceinline__ uint32_t compass4_fr(const uint8_t* roi0, int rp, int R, int gx, uint32_t K) {
-    const uint32_t* rc = (const uint32_t*)(roi0 + R * rp) + gx;
-    const uint32_t* rd = (const uint32_t*)(roi0 + (R + 3) * rp) + gx;
-    const uint32_t* ru = (const uint32_t*)(roi0 + (R - 3) * rp) + gx;
+    // R * rp as a 24-bit multiply (v_mul_lo_u32 is a quarter-rate instruction)
+    const uint8_t* row = roi0 + __umul24((uint32_t)R, (uint32_t)rp);
+    const uint32_t* rc = (const uint32_t*)row + gx;
+    const uint32_t* rd = (const uint32_t*)(row + 3 * rp) + gx;
+    const uint32_t* ru = (const uint32_t*)(row - 3 * rp) + gx;
     constexpr int KC = (XO + 9) >> 2;
     constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
     uint32_t C[5], D[5], U[5];
@@ -333,7 +335,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 #endif
         const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
         int ncorner = 0;
+#if FAST_DIAG >= 3   // diagnostic builds only: no detection work at all
+        for (int rb = 0; rb < 0; rb += rows_blk) {
+#else
         for (int rb = 0; rb < dh; rb += rows_blk) {
+#endif
             int nlist = 0;
             for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
                 const int rr = r0 + sub;
