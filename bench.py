@@ -184,9 +184,10 @@ def main():
                 # the matcher included), same definitions as the headline object
                 "per_kernel": per_kernel_hbm(prof, geo, args.traffic_csv, args.steps)}
 
-    cpu = None
+    cpu = cpu_tp = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(pairs, mb, args.cpu_seconds)
+        cpu_tp = cpu_baseline_throughput(pairs, mb, min(args.cpu_seconds, 6.0))
 
     if rank == 0:
         out = {"metric": METRIC, "value": fps, "unit": "frames/sec", "n_gpus": world,
@@ -200,7 +201,7 @@ def main():
                           "parallelism": f"dp{world}"},
                "mean_keypoints_left": float(nkp.mean()),
                "mean_stereo_matches": float(nv.mean()),
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -304,6 +305,42 @@ def cpu_baseline(pairs, mb, budget_s):
             "sample": f"{done} KITTI-size synthetic stereo pairs, L/R extraction on 2 threads + "
                       f"ComputeStereoMatches (Frame.cc:89-102), {el:.1f} s",
             "cpu_model": model, "host_cpus": os.cpu_count()}
+
+
+def cpu_baseline_throughput(pairs, mb, budget_s, workers=16):
+    """SURVEY §8(d) mode (ii): one stereo-frame pipeline per core (extract L, extract R,
+    ComputeStereoMatches, each worker with its own extractors), `workers` threads (the GPU box's
+    CPU share per GPU; ctypes releases the GIL inside the restatement)."""
+    try:
+        import oracle
+    except Exception:
+        return None
+    counts = [0] * workers
+    stop = [False]
+
+    def work(w):
+        ol = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
+        orr = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
+        i = w
+        while not stop[0]:
+            Lp, Rp = pairs[i % len(pairs)]
+            kl, _ = ol(Lp)
+            orr(Rp)
+            oracle.stereo_match(ol, orr, len(kl), MBF, mb)
+            counts[w] += 1
+            i += workers
+    ths = [threading.Thread(target=work, args=(w,)) for w in range(workers)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    time.sleep(budget_s)
+    stop[0] = True
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    return {"value": sum(counts) / el, "unit": "frames/sec", "cores": workers, "kind": "port",
+            "sample": f"{sum(counts)} KITTI-size synthetic stereo pairs on {workers} worker threads "
+                      f"(one pipeline per core, SURVEY §8d mode ii), {el:.1f} s"}
 
 
 # ---- EuRoC mono tracking (configs[2]) ----------------------------------------------------------
