@@ -964,7 +964,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const uint8_t* raw = (const uint8_t*)P;   // [31][36]
     int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
     issue_raw(0);
+#if OD_DIAG == 2   // diagnostic builds only: no moment phase (angle from zero moments)
+    for (int p = 0; p < 0; ++p) {
+#else
     for (int p = 0; p < npair; ++p) {
+#endif
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
 #pragma unroll
         for (int j = 0; j < OD_RL; ++j) {
@@ -1023,6 +1027,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         py2[w] = (float)c_pattern[4 * q + 3];
     }
     const uint8_t* blr = (const uint8_t*)P;   // [37][40]
+#if OD_DIAG == 1   // diagnostic builds only (tools/variants.py): no descriptor phase
+    if (npair > 0) return;
+#endif
     for (int p = 0; p < npair; ++p) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
         const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
