@@ -133,3 +133,42 @@ def test_blurred_levels_bitwise(oracle_mod, orbx_lib, gpu, simd):
             lvl = g.pyramid_level(l)
             want = oracle_mod.gaussian7(lvl, simd)
             assert_bytes_equal(g.blur_level(l), want, f"{name} simd={simd} blur L{l}")
+
+
+def test_large_batch_equals_single_images(oracle_mod, orbx_lib, gpu):
+    """Batch invariance at a bench-like batch: 48 stereo pairs (96 images: every kernel runs
+    its XCD-ordered grid) give, image by image, exactly the single-image outputs; two of them
+    are also checked against the CPU restatement (size-independent property, §8 parity)."""
+    import torch
+    import my_orb_slam2_amd as m
+    B = 48
+    base = [synth.stereo_pair(200 + i) for i in range(8)]
+    # distinct images: base pair i % 8 rolled down by 29 * (i // 8) rows (still rectified)
+    pairs = [tuple(np.roll(base[i % 8][v], 29 * (i // 8), axis=0) for v in (0, 1)) for i in range(B)]
+    Ls = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    sb = m.StereoBatch(B, 2000)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    uR, dep, nv = sb(Ls, Rs, KITTI_MBF, mb)
+    torch.cuda.synchronize()
+    nkp, kps, desc = sb.fetch("left")
+    nkpr, kpsr, descr = sb.fetch("right")
+    uRh, deph, nvh = uR.cpu().numpy(), dep.cpu().numpy(), nv.cpu().numpy()
+    gl, gr = m.ORBextractor(2000, 1.2, 8, 20, 7), m.ORBextractor(2000, 1.2, 8, 20, 7)
+    for i in range(B):
+        k1, d1 = gl(pairs[i][0])
+        k2, d2 = gr(pairs[i][1])
+        assert nkp[i] == len(k1) and nkpr[i] == len(k2), f"pair {i} keypoint counts"
+        assert_kps_equal(kps[i, :nkp[i]], k1, f"pair {i} left")
+        assert_bytes_equal(desc[i, :nkp[i]], d1, f"pair {i} left desc")
+        assert_kps_equal(kpsr[i, :nkpr[i]], k2, f"pair {i} right")
+        assert_bytes_equal(descr[i, :nkpr[i]], d2, f"pair {i} right desc")
+        u1, z1, n1 = m.compute_stereo_matches(gl, gr, KITTI_MBF, mb)
+        assert_f32_bits_equal(uRh[i, :nkp[i]], u1, f"pair {i} uRight")
+        assert_f32_bits_equal(deph[i, :nkp[i]], z1, f"pair {i} depth")
+        assert nvh[i] == n1
+    for i in (5, 41):
+        ol = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
+        k_o, d_o = ol(pairs[i][0])
+        assert_kps_equal(kps[i, :nkp[i]], k_o, f"pair {i} vs oracle")
+        assert_bytes_equal(desc[i, :nkp[i]], d_o, f"pair {i} desc vs oracle")
