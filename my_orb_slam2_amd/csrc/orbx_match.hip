@@ -393,6 +393,13 @@ __global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) F[k] = g.F12[9 * job + k];
     const float ex = g.epi[2 * job], ey = g.epi[2 * job + 1];
+    // Per shared node, lanes take the KF1 features (one idx1 per lane: every idx1 is
+    // independent, :722) and scan the node's KF2 features, staged once per 64 in this wave's
+    // LDS slice, in their order: the reference's `dist > bestDist` skip with bestDist updated
+    // on acceptance keeps the LAST accepted candidate of the smallest distance (:786-811).
+    __shared__ uint4 sBd[4][64][2];
+    __shared__ float sBx[4][64], sBy[4][64], sBa[4][64];
+    __shared__ int sBf[4][64];   // octave | stereo << 8 | valid << 9 | idx2 << 10
     const int na0 = db.node_off[k1], na1 = db.node_off[k1 + 1];
     const int nb0 = db.node_off[k2], nb1 = db.node_off[k2 + 1];
     for (int ga = na0 + w; ga < na1; ga += 4) {
@@ -405,55 +412,74 @@ __global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
         if (lo >= nb1 || db.node_id[lo] != id) continue;
         const int a0 = db.node_feat_off[ga], a1 = db.node_feat_off[ga + 1];
         const int b0 = db.node_feat_off[lo], nB = db.node_feat_off[lo + 1] - b0;
-        for (int ia = a0; ia < a1; ++ia) {
-            const int idx1 = db.node_feat[ia];
-            if ((unsigned)idx1 >= (unsigned)n1) continue;
-            if (db.flag[f10 + idx1]) continue;   // :749
-            const bool bStereo1 = (db.u_right ? db.u_right[f10 + idx1] : -1.0f) >= 0;
-            if (g.only_stereo && !bStereo1) continue;
-            const orbx_keypoint kp1 = db.keys[f10 + idx1];
+        for (int ac = a0; ac < a1; ac += 64) {
+            const int ia = ac + lane;
+            const int idx1 = ia < a1 ? db.node_feat[ia] : -1;
+            bool validA = (unsigned)idx1 < (unsigned)n1;
+            const int i1 = validA ? idx1 : 0;
+            validA = validA && !db.flag[f10 + i1];   // :749
+            const bool bStereo1 = (db.u_right ? db.u_right[f10 + i1] : -1.0f) >= 0;
+            if (g.only_stereo && !bStereo1) validA = false;
+            const orbx_keypoint kp1 = db.keys[f10 + i1];
             // CheckDistEpipolarLine's line coefficients depend on kp1 only.
             const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
             const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
             const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
             const float den = a * a + b * b;
-            const Desc d1 = load_desc(db.desc, (long long)f10 + idx1);
-            uint32_t key = INF;
-            for (int base = 0; base < nB; base += 64) {
-                const int pos = base + lane;
-                const int idx2 = db.node_feat[b0 + min(pos, nB - 1)];
-                if (pos >= nB || (unsigned)idx2 >= (unsigned)n2) continue;
-                if (db.flag[f20 + idx2]) continue;   // :773
-                const bool bStereo2 = (db.u_right ? db.u_right[f20 + idx2] : -1.0f) >= 0;
-                if (g.only_stereo && !bStereo2) continue;
-                const int dist = hamming(d1, load_desc(db.desc, (long long)f20 + idx2));
-                if (dist > TH_LOW) continue;   // :786 (the dist > bestDist half is the min)
-                const orbx_keypoint kp2 = db.keys[f20 + idx2];
-                const int o2 = min(max(kp2.octave, 0), MATCH_MAX_LEVELS - 1);
-                if (!bStereo1 && !bStereo2) {   // :791-798
-                    const float distex = ex - kp2.x;
-                    const float distey = ey - kp2.y;
-                    if (distex * distex + distey * distey < 100 * g.scale[o2]) continue;
+            const Desc d1 = load_desc(db.desc, (long long)f10 + i1);
+            int bestDist = TH_LOW, bestIdx2 = -1;
+            float bestAng = 0.f;
+            for (int bc = 0; bc < nB; bc += 64) {
+                const int cnt = min(64, nB - bc);
+                if (lane < cnt) {
+                    const int idx2 = db.node_feat[b0 + bc + lane];
+                    bool ok = (unsigned)idx2 < (unsigned)n2;
+                    const int i2 = ok ? idx2 : 0;
+                    ok = ok && !db.flag[f20 + i2];   // :773
+                    const bool st2 = (db.u_right ? db.u_right[f20 + i2] : -1.0f) >= 0;
+                    if (g.only_stereo && !st2) ok = false;
+                    const orbx_keypoint kp2 = db.keys[f20 + i2];
+                    const uint4* q = (const uint4*)(db.desc + 32 * ((long long)f20 + i2));
+                    sBd[w][lane][0] = q[0];
+                    sBd[w][lane][1] = q[1];
+                    sBx[w][lane] = kp2.x;
+                    sBy[w][lane] = kp2.y;
+                    sBa[w][lane] = kp2.angle;
+                    sBf[w][lane] = min(max(kp2.octave, 0), MATCH_MAX_LEVELS - 1) | (st2 ? 256 : 0) |
+                                   (ok ? 512 : 0) | (i2 << 10);
                 }
-                if (den == 0) continue;
-                const float num = a * kp2.x + b * kp2.y + c;
-                const float dsqr = num * num / den;
-                if (!((double)dsqr < 3.84 * (double)g.sigma2[o2])) continue;
-                // ties: the LAST accepted candidate wins (:786 skips only dist > bestDist)
-                key = min(key, (uint32_t)dist << 20 | (uint32_t)(0xFFFFF - pos));
-            }
-            const uint32_t m = wave_min_u32(key);
-            if (m != INF) {
-                const int pos = 0xFFFFF - (int)(m & 0xFFFFFu);
-                const int idx2 = db.node_feat[b0 + pos];
-                if (lane == 0) {
-                    int bin = 0;
-                    if (g.check_ori) {
-                        bin = rot_bin(kp1.angle, db.keys[f20 + idx2].angle);
-                        atomicAdd(&hist[bin], 1);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (int p = 0; p < cnt; ++p) {
+                    const int fl = sBf[w][p];
+                    if (!(fl & 512)) continue;   // uniform: a skipped KF2 feature
+                    const uint4 u0 = sBd[w][p][0], u1 = sBd[w][p][1];
+                    const Desc d2 = Desc{{u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w}};
+                    const int dist = hamming(d1, d2);
+                    if (dist > bestDist) continue;   // :786 (bestDist <= TH_LOW)
+                    const int o2 = fl & 255;
+                    const float x2 = sBx[w][p], y2 = sBy[w][p];
+                    if (!bStereo1 && !(fl & 256)) {   // :791-798
+                        const float distex = ex - x2;
+                        const float distey = ey - y2;
+                        if (distex * distex + distey * distey < 100 * g.scale[o2]) continue;
                     }
-                    state[idx1] = idx2 | (bin << 24);
+                    if (den == 0) continue;
+                    const float num = a * x2 + b * y2 + c;
+                    const float dsqr = num * num / den;
+                    if (!((double)dsqr < 3.84 * (double)g.sigma2[o2])) continue;
+                    bestDist = dist;
+                    bestIdx2 = fl >> 10;
+                    bestAng = sBa[w][p];
                 }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            if (validA && bestIdx2 >= 0) {
+                int bin = 0;
+                if (g.check_ori) {
+                    bin = rot_bin(kp1.angle, bestAng);
+                    atomicAdd(&hist[bin], 1);
+                }
+                state[idx1] = bestIdx2 | (bin << 24);
             }
         }
     }
@@ -1120,7 +1146,7 @@ hipError_t prepare_match_kernels() {
     hipError_t e;
     if ((e = hipFuncSetAttribute((const void*)k_bow<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_bow<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void*)k_triangulate, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_triangulate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRI_MAX_LDS)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void*)k_distinctive, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)k_proj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }

@@ -447,7 +447,7 @@ orbx_status orbx_search_for_triangulation(orbx_matcher* m, const orbx_featureset
     L.out = m->d_out.as<int32_t>() + 64;
     L.nmatches = m->d_out.as<int32_t>();
     L.err = m->d_err;
-    if (tri_lds_bytes(L.db.max_feat) > MATCH_MAX_LDS) return ORBX_ERR_UNSUPPORTED;
+    if (tri_lds_bytes(L.db.max_feat) > TRI_MAX_LDS) return ORBX_ERR_UNSUPPORTED;
     hipEvent_t e = m->timer.start(m->stream);
     if (!HIPOK(launch_triangulate(L, m->stream))) return ORBX_ERR_DEVICE;
     m->timer.stop(ORBX_MK_TRIANGULATE, e, m->stream);
@@ -621,7 +621,7 @@ orbx_status orbx_search_for_triangulation_batch_device(
     L.out = d_match12;
     L.nmatches = d_nmatches;
     L.err = m->d_err;
-    if (tri_lds_bytes(db->max_feat) > MATCH_MAX_LDS) return ORBX_ERR_UNSUPPORTED;
+    if (tri_lds_bytes(db->max_feat) > TRI_MAX_LDS) return ORBX_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
     hipEvent_t e = m->timer.start(st);
     if (!HIPOK(launch_triangulate(L, st))) return ORBX_ERR_DEVICE;

@@ -90,5 +90,7 @@ hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, i
 size_t distinctive_lds_bytes();
 // 160 KB of LDS per workgroup on gfx950, minus room for the kernels' static arrays
 constexpr size_t MATCH_MAX_LDS = 160 * 1024 - 256;
+// k_triangulate also holds 12 KiB of static LDS (one staged KF2 node slice per wave)
+constexpr size_t TRI_MAX_LDS = MATCH_MAX_LDS - 16 * 1024;
 
 }  // namespace orbx
