@@ -1,0 +1,62 @@
+"""Host-side checks of bench.py's measurement helpers against the committed profiles (no GPU).
+
+The headline roofline's `traffic` is FETCH_SIZE x2 + WRITE_SIZE from the rocprofv3 PMC passes
+(MI355X_MICROARCH.md §HBM); the committed bench line must agree with the committed CSVs."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _bench():
+    import bench
+    return bench
+
+
+def _latest(pattern):
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)),
+                   key=lambda p: int(os.path.basename(p).split("_v")[1].split("_")[0]))
+    return files[-1]
+
+
+def test_headline_traffic_matches_committed_pmc():
+    b = _bench()
+    line = json.load(open(_latest("r01_v*_bench.json")))
+    roof = line["roofline"]
+    t = b.traffic_from_csv(b.DEFAULT_PMC, roof["kernel"])
+    assert t is not None and t > 0
+    assert t == pytest.approx(roof["traffic"], rel=1e-9)
+    # the algorithmic bytes and the achieved rate are consistent with the launch time
+    assert roof["achieved"] == pytest.approx(
+        roof["algorithmic_bytes_per_launch"] / (roof["avg_launch_ms"] / 1000.0) / 1e9, rel=1e-9)
+    assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-9)
+
+
+def test_per_kernel_entries():
+    b = _bench()
+    prof = {"k_level": (16.0, 160), "k_fast": (10.0, 20), "k_missing": (1.0, 0)}
+    geo = {"k_level": 3.0e8, "k_fast": 7.0e8}
+    out = b.per_kernel_hbm(prof, geo, b.DEFAULT_PMC, 20)
+    assert set(out) == {"k_level", "k_fast"}
+    assert out["k_level"]["launches_per_step"] == 8
+    assert out["k_level"]["avg_launch_ms"] == pytest.approx(0.1)
+    assert out["k_level"]["achieved"] == pytest.approx(3.0e8 / 1e-4 / 1e9)
+    assert out["k_fast"]["frac"] == pytest.approx(out["k_fast"]["achieved"] / b.HBM_PEAK_GBS)
+
+
+def test_traffic_needs_both_passes(tmp_path):
+    b = _bench()
+    f = tmp_path / "fetch.csv"
+    f.write_text('"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+                 '1,"orbx::k_level(x)","FETCH_SIZE",100\n2,"orbx::k_level(x)","FETCH_SIZE",300\n')
+    assert b.traffic_from_csv(str(f), "k_level") is None   # WRITE_SIZE pass missing
+    w = tmp_path / "write.csv"
+    w.write_text('"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+                 '1,"orbx::k_level(x)","WRITE_SIZE",50\n')
+    # mean FETCH 200 KiB doubled + WRITE 50 KiB
+    assert b.traffic_from_csv(f"{f},{w}", "k_level") == pytest.approx((2 * 200 + 50) * 1024.0)
