@@ -122,6 +122,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_WPE
 #define FAST_WPE 1     // minimum waves per SIMD requested from the register allocator
 #endif
+#ifndef OCTREE_PACKED
+#define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
+#endif
 #ifndef OD_WPE
 #define OD_WPE 1
 #endif
@@ -607,6 +610,26 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         int Ctot, Stot, nToExpand = 0;
         if (!phase2) {
             // ---- phase 1 (src/ORBextractor.cc:608-667): expand every multi-key node ----
+            if (OCTREE_PACKED && S < 512) {
+                // one scan of packed (children | survivor << 11 | multi-key children << 20):
+                // every field's total stays below its width while S < 512 (children and
+                // multi-key children <= 4 S < 2048 < 4096, survivors < 512).  The thread that
+                // scans node i also writes it below, so no barrier is needed in between.
+                const uint32_t tot = (uint32_t)chunked_scan(
+                    S, tmp,
+                    [&](int i) {
+                        return cur.cnt[i] > 1 ? (int)((uint32_t)nonempty(i) | ((uint32_t)multi(i) << 20))
+                                              : (int)(1u << 11);
+                    },
+                    [&](int i, int ex) {
+                        sm.pord[i] = cur.cnt[i] > 1 ? (int16_t)i : (int16_t)-1;
+                        sm.pre[i] = (int)((uint32_t)ex & 0x7FFu);
+                        sm.pre2[i] = (int)(((uint32_t)ex >> 11) & 0x1FFu);
+                    });
+                Ctot = (int)(tot & 0x7FFu);
+                Stot = (int)((tot >> 11) & 0x1FFu);
+                nToExpand = (int)(tot >> 20);
+            } else {
             for (int i = tid; i < S; i += 256) sm.pord[i] = cur.cnt[i] > 1 ? (int16_t)i : (int16_t)-1;
             __syncthreads();
             Ctot = chunked_scan(
@@ -619,6 +642,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             int e = 0;
             for (int i = tid; i < S; i += 256) e += sm.pord[i] >= 0 ? multi(i) : 0;
             nToExpand = block_sum(e, tmp);
+            }
             for (int i = tid; i < S; i += 256) {
                 if (sm.pord[i] >= 0) {
                     const int c = nonempty(i);
