@@ -888,6 +888,7 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
 #define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
 #define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
 #define OD_RAW_N (31 * OD_RAW_DW)                  // 279
+static_assert(OD_RAW_DW == 9 && OD_BLR_DW == 10, "k_orient_desc row divisions are hard-coded");
 #define OD_BLR_N (37 * OD_BLR_DW)                  // 370
 #define OD_RL ((OD_RAW_N + 31) / 32)               // 9 dword loads per lane per raw patch
 #define OD_BL ((OD_BLR_N + 31) / 32)               // 12 per blurred patch
@@ -941,13 +942,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
     for (int k = 0; k < OD_RL; ++k) {
         const int t = min(l32 + 32 * k, OD_RAW_N - 1);
-        const int row = t / OD_RAW_DW;
+        const int row = (int)(__umul24((uint32_t)t, 7282u) >> 16);   // t / 9 for t < 1000 (24-bit multiply)
         sor[k] = __umul24(row, pitch) + 4 * (t - row * OD_RAW_DW);
     }
 #pragma unroll
     for (int k = 0; k < OD_BL; ++k) {
         const int t = min(l32 + 32 * k, OD_BLR_N - 1);
-        const int row = t / OD_BLR_DW;
+        const int row = (int)(__umul24((uint32_t)t, 6554u) >> 16);   // t / 10 for t < 1000
         sob[k] = __umul24(row, pitch) + 4 * (t - row * OD_BLR_DW);
     }
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
