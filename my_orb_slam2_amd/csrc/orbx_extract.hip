@@ -1110,12 +1110,12 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     KernelTimer& T = a.timer ? *a.timer : dummy;
     hipError_t err = launch_levels(a, st);
     if (err != hipSuccess) return err;
-    hipEvent_t e = T.start(st);
+    hipEvent_t e = T.start_after(st);
     hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch), dim3(256),
                        fast_lds_bytes(G), st,
                        a.dg, a.cells, a.pyr, a.ccnt, a.cand);
     T.stop(K_FAST, e, st);
-    e = T.start(st);
+    e = T.start_after(st);
     hipLaunchKernelGGL(k_octree, dim3(1, a.batch), dim3(256), a.octree_lds, st, a.dg, a.cells,
                        a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, a.ncap,
                        a.kcap, 0);
@@ -1124,7 +1124,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                            a.dg, a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch,
                            a.kscratch_per_image, a.ncap1, a.kcap1, 1);
     T.stop(K_OCTREE, e, st);
-    e = T.start(st);
+    e = T.start_after(st);
     hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,
                        a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp);
     T.stop(K_ORIENT, e, st);

@@ -42,7 +42,15 @@ struct KernelTimer {
         if (!b) return;
         (void)hipEventRecord(b, st);
         pending.push_back(Rec{id, a, b});
+        last = b;
     }
+    // Start of a kernel launched right after the previous timed one on the same stream: the
+    // previous stop event doubles as this start (one marker between two kernels, not two).
+    hipEvent_t start_after(hipStream_t st) {
+        if (!on) return nullptr;
+        return last ? last : start(st);
+    }
+    hipEvent_t last = nullptr;
     void collect() {
         for (auto& r : pending) {
             float t = 0.f;
@@ -53,6 +61,7 @@ struct KernelTimer {
         }
         pending.clear();
         used = 0;
+        last = nullptr;
     }
     void destroy() {
         for (auto e : pool) (void)hipEventDestroy(e);

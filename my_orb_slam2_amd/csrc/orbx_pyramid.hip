@@ -613,7 +613,7 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
     KernelTimer& T = a.timer ? *a.timer : dummy;
     for (int l = 0; l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
-        hipEvent_t e = T.start(st);
+        hipEvent_t e = l == 0 ? T.start(st) : T.start_after(st);
         hipLaunchKernelGGL(k_level, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
                            a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
                            a.blur, l);
