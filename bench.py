@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r01_pmc_fetch_b256.csv", "r01_pmc_write_b256.csv"))
+                       ("r01_pmc_fetch_b512.csv", "r01_pmc_write_b512.csv"))
 
 
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="stereo pairs per step per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="stereo pairs (default 512) or EuRoC frames (default 256) per step per GPU")
     ap.add_argument("--distinct", type=int, default=32,
                     help="synthetic base pairs / frames generated per rank (stereo: the batch "
                          "slots are row-rolled copies of them, all distinct)")
@@ -106,7 +107,7 @@ def main():
     import my_orb_slam2_amd as orbx
     from my_orb_slam2_amd import synth
 
-    B = args.batch
+    B = args.batch or 512
     P = max(1, min(args.distinct, B))
     pairs = [synth.stereo_pair(1000 * rank + i, W, H) for i in range(P)]
     # every slot of the batch holds a different pair: slot i is base pair i % P with both views
@@ -406,7 +407,7 @@ def main_euroc(args):
     dev = torch.device("cuda", local)
     st = torch.cuda.current_stream(dev).cuda_stream
     K4, distc = synth.EUROC_CAM
-    B = args.batch
+    B = args.batch or 256
     P = max(1, min(args.distinct, B))
     frames = [synth.frame(2000 * rank + 7 + i, EUROC_W, EUROC_H) for i in range(P)]
     idx = [i % P for i in range(B)]

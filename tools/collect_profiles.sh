@@ -4,11 +4,11 @@
 set -e
 V=gpurun_out/$1
 cp $V/bench.json profiles/r01_$1_bench.json
-cp $V/prof/trace/run_kernel_stats.csv profiles/r01_$1_kernel_stats_b256.csv
-cp $V/prof/pmc3/run_counter_collection.csv profiles/r01_pmc_fetch_b256.csv
-cp $V/prof/pmc4/run_counter_collection.csv profiles/r01_pmc_write_b256.csv
-cp $V/prof/pmc1/run_counter_collection.csv profiles/r01_pmc_insts_b256.csv
-cp $V/prof/pmc2/run_counter_collection.csv profiles/r01_pmc_waits_b256.csv
+cp $V/prof/trace/run_kernel_stats.csv profiles/r01_$1_kernel_stats_b512.csv
+cp $V/prof/pmc3/run_counter_collection.csv profiles/r01_pmc_fetch_b512.csv
+cp $V/prof/pmc4/run_counter_collection.csv profiles/r01_pmc_write_b512.csv
+cp $V/prof/pmc1/run_counter_collection.csv profiles/r01_pmc_insts_b512.csv
+cp $V/prof/pmc2/run_counter_collection.csv profiles/r01_pmc_waits_b512.csv
 cp $V/euroc.json profiles/r01_c3_euroc_bench.json
 cp $V/reloc.json profiles/r01_c4_reloc_bench.json
 cp $V/tri.json profiles/r01_c5_triangulation_bench.json
