@@ -76,6 +76,31 @@ __device__ __forceinline__ int fast_arc_score(const uint8_t* roi, int cols, int 
     return max(best_dark, -best_min_max);
 }
 
+// Exact necessary condition for M > t: the 9 circle indices of any arc include 4 or 5
+// consecutive even indices, so a corner at t has 4 cyclically consecutive even-index pixels
+// (0, 2, .., 14) all darker than v - t or all brighter than v + t.  8 reads instead of 16.
+__device__ __forceinline__ bool fast_even8(const uint8_t* roi, int cols, int r, int c, int t) {
+    const int v = roi[r * cols + c];
+    int e[8];
+    e[0] = v - roi[(r + 3) * cols + c];
+    e[1] = v - roi[(r + 2) * cols + c + 2];
+    e[2] = v - roi[(r)*cols + c + 3];
+    e[3] = v - roi[(r - 2) * cols + c + 2];
+    e[4] = v - roi[(r - 3) * cols + c];
+    e[5] = v - roi[(r - 2) * cols + c - 2];
+    e[6] = v - roi[(r)*cols + c - 3];
+    e[7] = v - roi[(r + 2) * cols + c - 2];
+    int dark = -256, bmax = 256;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int mn = min(min(min(e[k], e[(k + 1) & 7]), e[(k + 2) & 7]), e[(k + 3) & 7]);
+        const int mx = max(max(max(e[k], e[(k + 1) & 7]), e[(k + 2) & 7]), e[(k + 3) & 7]);
+        dark = max(dark, mn);
+        bmax = min(bmax, mx);
+    }
+    return max(dark, -bmax) > t;
+}
+
 // Keypoint test at threshold t on the M map (mb: (dh+2) x (dw+2), zero ring).
 __device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, int cc, int t,
                                             int& score) {
@@ -118,6 +143,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #endif
 #ifndef FAST_PF
 #define FAST_PF 8      // prefetched ROI dwords per lane (larger ROIs are staged directly)
+#endif
+#ifndef FAST_PRE8
+#define FAST_PRE8 0    // even-point segment test before the arc score (measured slower: off)
 #endif
 #ifndef FAST_WPE
 #define FAST_WPE 1     // minimum waves per SIMD requested from the register allocator
@@ -390,6 +418,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
             lds_order();
 #if FAST_DIAG >= 1   // diagnostic builds only: skip the arc score
             nlist = 0;
+#endif
+#if FAST_PRE8
+            // 1b. even-point segment test (exact filter, fast_even8), compacted in place: a
+            //     lane writes at or below the entry it read, so no unread entry is overwritten.
+            //     Survivors dropped here have M <= tq and keep 0 in the M map, which no NMS
+            //     test at a threshold >= tq distinguishes from their true M.
+            {
+                int n2 = 0;
+                for (int j0 = 0; j0 < nlist; j0 += 64) {
+                    const int j = j0 + lane;
+                    int pe = 0;
+                    bool pass = false;
+                    if (j < nlist) {
+                        pe = list[j];
+                        pass = fast_even8(roi, rp, (pe >> 6) + 3, (pe & 63) + 3, tq);
+                    }
+                    const uint64_t pm = __ballot(pass);
+                    if (pass) list[n2 + lanes_below(pm)] = (int16_t)pe;
+                    n2 += __popcll(pm);
+                }
+                nlist = n2;
+                lds_order();
+            }
 #endif
             // 2. full arc score for the survivors only (dense across lanes); those above the
             //    lower threshold are appended to the corner list, keeping raster order
