@@ -85,8 +85,29 @@ def algorithmic_bytes_fast(level_sizes, cells_area_read, ncand):
     return cells_area_read + 4 * ncand
 
 
+_RESULT_OUT = None
+
+
+def emit(line: str) -> None:
+    """The one JSON result line, on the process's original stdout."""
+    out = _RESULT_OUT or sys.stdout
+    out.write(line + "\n")
+    out.flush()
+
+
+def keep_stdout_for_result() -> None:
+    """Native libraries print to fd 1 (RCCL's version banner at communicator init): send fd 1
+    to stderr for the rest of the run and keep a handle on the original stdout, so that the
+    only thing on stdout is the result line."""
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main():
     args = parse()
+    keep_stdout_for_result()
     if args.traffic_csv is None:
         args.traffic_csv = DEFAULT_PMC if args.workload == "stereo" else DEFAULT_PMC_EUROC
     if args.workload == "euroc":
@@ -99,10 +120,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # ORBX_FORCE_DIST=1 takes the process-group path at world size 1 (torchrun
+    # --nproc-per-node 1), so the RCCL timing path can be exercised on a one-GPU box
+    dist_on = world > 1 or (os.environ.get("ORBX_FORCE_DIST") == "1" and "RANK" in os.environ)
+    if dist_on:   # bound to this rank's GPU, so RCCL's barrier never guesses the device
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
 
     import my_orb_slam2_amd as orbx
     from my_orb_slam2_amd import synth
@@ -171,17 +195,17 @@ def main():
             h.profile(True)
             h.collect_profile()
 
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         run_step(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -241,8 +265,8 @@ def main():
         if io is not None:
             out["metric"] = METRIC + " (PCIe-inclusive: host images in, host keypoints out)"
             out["config"]["host_io"] = io
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        emit(json.dumps(out))
+    if dist_on:
         dist.destroy_process_group()
 
 
@@ -401,10 +425,13 @@ def main_euroc(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # ORBX_FORCE_DIST=1 takes the process-group path at world size 1 (torchrun
+    # --nproc-per-node 1), so the RCCL timing path can be exercised on a one-GPU box
+    dist_on = world > 1 or (os.environ.get("ORBX_FORCE_DIST") == "1" and "RANK" in os.environ)
+    if dist_on:   # bound to this rank's GPU, so RCCL's barrier never guesses the device
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     K4, distc = synth.EUROC_CAM
     B = args.batch or 256
@@ -449,17 +476,17 @@ def main_euroc(args):
     mt.matcher.profile(prof_on)
     mt.ext.collect_profile()
     mt.matcher.collect_profile()
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -507,8 +534,8 @@ def main_euroc(args):
                     "mean_keypoints": float(nkp.mean()),
                     "mean_local_map_matches": float(counts.mean()),
                     "roofline": roof, "cpu_baseline": cpu}
-        print(json.dumps(out_line), flush=True)
-    if world > 1:
+        emit(json.dumps(out_line))
+    if dist_on:
         dist.destroy_process_group()
 
 
@@ -622,10 +649,13 @@ def main_match(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # ORBX_FORCE_DIST=1 takes the process-group path at world size 1 (torchrun
+    # --nproc-per-node 1), so the RCCL timing path can be exercised on a one-GPU box
+    dist_on = world > 1 or (os.environ.get("ORBX_FORCE_DIST") == "1" and "RANK" in os.environ)
+    if dist_on:   # bound to this rank's GPU, so RCCL's barrier never guesses the device
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
 
     if args.workload == "reloc":
@@ -645,10 +675,10 @@ def main_match(args):
         cnt = torch.empty(max(k1 - k0, 1), dtype=torch.int32, device=dev)
 
         def step():
-            if world > 1:
+            if dist_on:
                 broadcast_query([qdesc, qkeys])
             m.search_by_bow_kf_frame_batch_device(db, fc, out, cnt, st)
-            if world > 1:
+            if dist_on:
                 allc = all_gather_counts(cnt[:k1 - k0], args.kfs, world)
                 # the candidates' match lists travel to every rank (Tracking.cc:1503-1528)
                 gather_candidate_matches(out, allc, args.kfs, world)
@@ -693,7 +723,7 @@ def main_match(args):
         def step():
             m.search_for_triangulation_batch_device(db.c, kf1, kf2, dF, dE, s2, s, job_off, out,
                                                     cnt, stream=st)
-            if world > 1:
+            if dist_on:
                 if uniform and nj:   # every job's match12 array to every rank
                     gather_rows(out.view(nj, -1), args.jobs, world)
                 return all_gather_counts(cnt[:nj], args.jobs, world)
@@ -713,17 +743,17 @@ def main_match(args):
     m.sync(st)
     m.profile(not args.no_kernel_timing)
     m.collect_profile()
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    if dist_on:
+        dist.barrier(device_ids=[local])
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -778,8 +808,8 @@ def main_match(args):
                     "scaling": "strong", "vs_baseline": None, "dtype": "u8 (256-bit Hamming)",
                     "data": "synthetic", "config": cfg, **extra, "roofline": roof,
                     "cpu_baseline": cpu}
-        print(json.dumps(out_line), flush=True)
-    if world > 1:
+        emit(json.dumps(out_line))
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -60,3 +60,17 @@ def test_traffic_needs_both_passes(tmp_path):
                  '1,"orbx::k_level(x)","WRITE_SIZE",50\n')
     # mean FETCH 200 KiB doubled + WRITE 50 KiB
     assert b.traffic_from_csv(f"{f},{w}", "k_level") == pytest.approx((2 * 200 + 50) * 1024.0)
+
+
+def test_result_line_is_the_only_stdout():
+    """Native chatter on fd 1 (RCCL's version banner) goes to stderr; stdout holds only the
+    result line the driver parses."""
+    import subprocess
+    import sys
+    code = ("import os, bench; bench.keep_stdout_for_result(); "
+            "os.write(1, b'RCCL version : x\\n'); print('py noise'); bench.emit('{\"value\": 1}')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(ROOT), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == '{"value": 1}\n'
+    assert "RCCL version" in r.stderr and "py noise" in r.stderr
