@@ -137,7 +137,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
     k_lo = base && m > t_lo && supp <= t_lo;
 }
 
-#define FAST_LIST 512
+#ifndef FAST_LIST
+#define FAST_LIST 512    // compass survivors listed per row block (a multiple of 256)
+#endif
 #ifndef FAST_NC
 #define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
 #endif
