@@ -105,8 +105,26 @@ def keep_stdout_for_result() -> None:
     os.dup2(2, 1)
 
 
+def relaunch_if_needed(args) -> None:
+    """`--gpus N` must agree with the launcher's world size.  Run without a launcher
+    (no WORLD_SIZE) and N > 1, start torchrun with N ranks as a child process (nothing has
+    touched the GPU yet) and exit with its status; any other mismatch is an error."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus == world:
+        return
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={29500 + os.getpid() % 1000}",
+               os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE={world}")
+
+
 def main():
     args = parse()
+    relaunch_if_needed(args)
     keep_stdout_for_result()
     if args.traffic_csv is None:
         args.traffic_csv = DEFAULT_PMC if args.workload == "stereo" else DEFAULT_PMC_EUROC
@@ -232,12 +250,14 @@ def main():
         tot_ms, launches = prof[dom]
         avg_s = tot_ms / 1000.0 / max(launches, 1)
         geo = kernel_bytes(sb.ext, 2 * B, B)
-        alg = geo.get(dom)
+        traffic = traffic_from_csv(args.traffic_csv, dom)
+        alg = counted_bytes(geo.get(dom), traffic)
         achieved = (alg / avg_s / 1e9) if (alg and avg_s > 0) else None
         roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic_from_csv(args.traffic_csv, dom),
-                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg_s * 1000.0,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg,
+                "requested_bytes_per_launch": geo.get(dom), "avg_launch_ms": avg_s * 1000.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4)
                                        for k, v in prof.items()},
                 # every extraction / stereo kernel against the HBM roof (north_star: FAST and
@@ -270,17 +290,31 @@ def main():
         dist.destroy_process_group()
 
 
+def counted_bytes(requested, traffic):
+    """Bytes a roofline entry credits to one launch: the kernel's requested (algorithmic)
+    bytes, capped by the measured HBM traffic when a PMC pass holds it.  Requested bytes
+    count overlapping reads in full (k_orient_desc: every keypoint's 31x31 and 37x37
+    patches), which the caches serve once, so uncapped they would overstate the HBM
+    fraction."""
+    if not requested:
+        return requested
+    return min(requested, traffic) if traffic else requested
+
+
 def per_kernel_hbm(prof, geo, traffic_csv, steps):
     out = {}
     for k, (tot_ms, launches) in prof.items():
-        alg = geo.get(k)
-        if not alg or not launches or tot_ms <= 0:
+        req = geo.get(k)
+        if not req or not launches or tot_ms <= 0:
             continue
+        traffic = traffic_from_csv(traffic_csv, k)
+        alg = counted_bytes(req, traffic)
         avg_s = tot_ms / 1000.0 / launches
         ach = alg / avg_s / 1e9
         out[k] = {"achieved": ach, "frac": ach / HBM_PEAK_GBS, "unit": "GB/s",
-                  "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg_s * 1000.0,
-                  "launches_per_step": launches / max(steps, 1), "traffic": traffic_from_csv(traffic_csv, k)}
+                  "algorithmic_bytes_per_launch": alg, "requested_bytes_per_launch": req,
+                  "avg_launch_ms": avg_s * 1000.0,
+                  "launches_per_step": launches / max(steps, 1), "traffic": traffic}
     return out
 
 
@@ -658,6 +692,13 @@ def main_match(args):
         dist.init_process_group("nccl", init_method="env://", device_id=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
 
+    # every rank must own at least one unit, or its shard structures are empty while the
+    # other ranks wait in the collectives
+    units_total = args.kfs if args.workload == "reloc" else args.jobs
+    if units_total < world:
+        sys.exit(f"bench.py: {units_total} {'keyframes' if args.workload == 'reloc' else 'jobs'}"
+                 f" < world size {world}")
+
     if args.workload == "reloc":
         F = 1000
         k0, k1 = shard_range(args.kfs, rank, world)
@@ -718,13 +759,21 @@ def main_match(args):
         out = torch.empty(int(n1.sum()), dtype=torch.int32, device=dev)
         cnt = torch.empty(max(nj, 1), dtype=torch.int32, device=dev)
 
-        uniform = bool((n1 == n1[0]).all()) if nj else True
+        # whether the match12 arrays are gathered must be decided the same way on every
+        # rank (each rank makes the same collective calls): rows gather only when every job
+        # of every shard has the same KF1 feature count
+        row_len = int(n1[0])
+        uniform = bool((n1 == row_len).all())
+        if dist_on:
+            agree = torch.tensor([int(uniform), row_len, -row_len], dtype=torch.int64, device=dev)
+            dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+            uniform = bool(agree[0].item()) and int(agree[1].item()) == -int(agree[2].item())
 
         def step():
             m.search_for_triangulation_batch_device(db.c, kf1, kf2, dF, dE, s2, s, job_off, out,
                                                     cnt, stream=st)
             if dist_on:
-                if uniform and nj:   # every job's match12 array to every rank
+                if uniform:   # every job's match12 array to every rank
                     gather_rows(out.view(nj, -1), args.jobs, world)
                 return all_gather_counts(cnt[:nj], args.jobs, world)
             return cnt[:nj]

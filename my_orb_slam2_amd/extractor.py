@@ -202,6 +202,8 @@ class StereoBatch:
                                 cv_simd=cv_simd, max_batch=2 * batch, device=device)
         self.device = torch.device("cuda", device)
         self.uR = self.depth = self.nvalid = None
+        self._alloc_key = None    # (B, W, H, kp_cap) of the output buffers
+        self._last_b = None       # B of the last call: the right views start at image B
 
     def __call__(self, left_imgs, right_imgs, mbf: float, mb: float, stream=None):
         import torch
@@ -209,25 +211,32 @@ class StereoBatch:
         assert right_imgs.shape == left_imgs.shape
         assert left_imgs.stride() == right_imgs.stride(), "left/right tensors need equal strides"
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        if self.uR is None or self.uR.shape[0] != B:
-            kc = self._kp_cap(W, H)
-            self.uR = torch.empty((B, kc), dtype=torch.float32, device=self.device)
-            self.depth = torch.empty((B, kc), dtype=torch.float32, device=self.device)
-            self.nvalid = torch.empty((B,), dtype=torch.int32, device=self.device)
+        if self._alloc_key is None or self._alloc_key[:3] != (B, W, H):
+            # kp_cap follows W and H (the octree root count), so any shape change
+            # reallocates: k_stereo writes rows of kp_cap floats per pair
+            kc = self.ext.prepare(W, H, 2 * B)
+            if self._alloc_key is None or self._alloc_key[0] != B or self._alloc_key[3] != kc:
+                self.uR = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+                self.depth = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+                self.nvalid = torch.empty((B,), dtype=torch.int32, device=self.device)
+            self._alloc_key = (B, W, H, kc)
         stride = left_imgs.stride(1) * left_imgs.element_size()
         bstride = left_imgs.stride(0) * left_imgs.element_size()
         check("orbx_stereo_frames_device", self.ext._L.orbx_stereo_frames_device(
             self.ext._h, ptr(left_imgs), ptr(right_imgs), B, W, H, stride, bstride, mbf, mb,
             ptr(self.uR), ptr(self.depth), ptr(self.nvalid), ctypes.c_void_p(st)))
+        self._last_b = B
         return self.uR, self.depth, self.nvalid
 
-    def _kp_cap(self, W, H):
-        return self.ext.prepare(W, H, 2 * self.batch)
-
     def fetch(self, side: str = "left"):
-        """Host copies (nkp, keypoints, descriptors) of the left or right views."""
-        first = 0 if side == "left" else self.batch
-        return self.ext.batch_fetch(first, self.batch)
+        """Host copies (nkp, keypoints, descriptors) of the left or right views of the last
+        call (left view of pair i = image i, right view = image B + i)."""
+        if self._last_b is None:
+            raise RuntimeError("StereoBatch.fetch before any call")
+        if side not in ("left", "right"):
+            raise ValueError("side must be 'left' or 'right'")
+        B = self._last_b
+        return self.ext.batch_fetch(0 if side == "left" else B, B)
 
     def profile(self, on: bool = True):
         self.ext.profile(on)

@@ -74,3 +74,26 @@ def test_result_line_is_the_only_stdout():
     assert r.returncode == 0, r.stderr
     assert r.stdout == '{"value": 1}\n'
     assert "RCCL version" in r.stderr and "py noise" in r.stderr
+
+
+def test_counted_bytes_capped_by_traffic():
+    """Overlapping reads (k_orient_desc's patches) are credited at most the measured HBM
+    bytes, so the per-kernel fraction never exceeds what the PMC passes saw."""
+    b = _bench()
+    assert b.counted_bytes(4.95e9, 3.07e9) == 3.07e9
+    assert b.counted_bytes(6.1e8, 6.2e8) == 6.1e8
+    assert b.counted_bytes(6.1e8, None) == 6.1e8
+    prof = {"k_orient_desc": (13.6, 10)}
+    out = b.per_kernel_hbm(prof, {"k_orient_desc": 1e12}, b.DEFAULT_PMC, 10)
+    e = out["k_orient_desc"]
+    assert e["algorithmic_bytes_per_launch"] == e["traffic"] < e["requested_bytes_per_launch"]
+
+
+def test_gpus_flag_must_match_world_size():
+    """`--gpus 2` under a launcher that started one rank is an error, not a silent 1-GPU run."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       cwd=str(ROOT), capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert "does not match WORLD_SIZE=1" in r.stderr

@@ -172,3 +172,36 @@ def test_large_batch_equals_single_images(oracle_mod, orbx_lib, gpu):
         k_o, d_o = ol(pairs[i][0])
         assert_kps_equal(kps[i, :nkp[i]], k_o, f"pair {i} vs oracle")
         assert_bytes_equal(desc[i, :nkp[i]], d_o, f"pair {i} desc vs oracle")
+
+
+def test_stereo_batch_shape_and_size_changes(orbx_lib, gpu):
+    """One StereoBatch object across calls of different batch sizes and image shapes: the
+    output buffers follow (B, W, H, kp_cap) and fetch() reads the views of the last call
+    (right view of pair i = image B + i of that call), each equal to single-image runs."""
+    import torch
+    import my_orb_slam2_amd as m
+    sb = m.StereoBatch(2, 1000)
+    gl, gr = m.ORBextractor(1000, 1.2, 8, 20, 7), m.ORBextractor(1000, 1.2, 8, 20, 7)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    # small frames first (1 octree root), then wider ones (3 roots: a larger kp_cap), then a
+    # smaller batch of the wide shape
+    for seed, (w, h), B in ((300, (320, 240), 2), (310, (960, 300), 3), (320, (960, 300), 1)):
+        pairs = [synth.stereo_pair(seed + i, w, h) for i in range(B)]
+        Ls = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+        Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+        uR, dep, nv = sb(Ls, Rs, KITTI_MBF, mb)
+        torch.cuda.synchronize()
+        kc = sb.ext.batch_view().kp_cap
+        assert uR.shape == (B, kc) and dep.shape == (B, kc) and nv.shape == (B,)
+        nkp, kps, _ = sb.fetch("left")
+        nkpr, kpsr, _ = sb.fetch("right")
+        assert len(nkp) == B and len(nkpr) == B
+        uRh, nvh = uR.cpu().numpy(), nv.cpu().numpy()
+        for i in range(B):
+            k1, _ = gl(pairs[i][0])
+            k2, _ = gr(pairs[i][1])
+            assert_kps_equal(kps[i, :nkp[i]], k1, f"{w}x{h} B={B} pair {i} left")
+            assert_kps_equal(kpsr[i, :nkpr[i]], k2, f"{w}x{h} B={B} pair {i} right")
+            u1, _, n1 = m.compute_stereo_matches(gl, gr, KITTI_MBF, mb)
+            assert_f32_bits_equal(uRh[i, :nkp[i]], u1, f"{w}x{h} B={B} pair {i} uRight")
+            assert nvh[i] == n1
