@@ -46,7 +46,7 @@ struct LevelGeom {
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
 #ifndef OD_NK
-#define OD_NK 4               // keypoints per wave in k_orient_desc (<= 64)
+#define OD_NK 8               // keypoints per wave in k_orient_desc (<= 64)
 #endif
 #define LT_W 128              // output tile width  (32 groups of 4)
 #ifndef LT_H

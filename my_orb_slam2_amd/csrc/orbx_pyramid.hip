@@ -321,6 +321,9 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
     }
 }
 
+#ifndef LEVEL_COLQ
+#define LEVEL_COLQ 1   // mode-3 full tiles: a thread keeps one column group (tables read once)
+#endif
 #ifndef STAGE_MAXK
 #define STAGE_MAXK 12  // column-owner window staging: up to 48 rows (0: always the generic form)
 #endif
@@ -437,6 +440,94 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
     // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
     const bool full_tile = vw == LT_W && vh == LT_H;   // every halo item is needed
+    // mode 3 (generic INTER_LINEAR) on one 4-pixel group: halo row hr, the group's column
+    // tables (cg: source columns, ci: flags, al: alphas, sl: v_perm selectors)
+    auto item3 = [&](int hr, uint2 cg, uint32_t ci, uint4 al, uint4 sl) -> uint32_t {
+        uint32_t out = 0;
+        const uint2 ri = rinf[hr];
+        const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
+                           (int)(cg.y >> 16)};
+        const uint32_t als[4] = {al.x, al.y, al.z, al.w};
+        const int r0 = (int)(ri.x & 0xFFFF), r1 = (int)(ri.x >> 16);
+        const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
+        const uint8_t* w0 = win + __umul24(r0, WP);
+        const uint8_t* w1 = win + __umul24(r1, WP);
+        if (ci & 0x200u) {
+            // branch-free: v_perm gathers each pixel's two taps as u16s, v_dot2 applies
+            // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
+            const uint32_t sels[4] = {sl.x, sl.y, sl.z, sl.w};
+            const int base = xs[0] & ~3, o0 = xs[0] & 3;
+            const uint32_t* d0p = (const uint32_t*)(w0 + base);
+            const uint32_t* d1p = (const uint32_t*)(w1 + base);
+            const uint32_t a0 = d0p[0], a1 = d0p[1], a2 = d0p[2];
+            const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
+            // 8-byte windows starting at the group's first tap column (span <= 7)
+            const uint32_t wa0 = __builtin_amdgcn_alignbyte(a1, a0, o0);
+            const uint32_t wa1 = __builtin_amdgcn_alignbyte(a2, a1, o0);
+            const uint32_t wc0 = __builtin_amdgcn_alignbyte(c1, c0, o0);
+            const uint32_t wc1 = __builtin_amdgcn_alignbyte(c2, c1, o0);
+            // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind; 24-bit
+            // multiplies (full rate): h < 2^19, b <= 2048.  Groups whose 4 pixels all
+            // take the SSE2 form (all but the right edge) skip the scalar form.
+            const bool all_simd = ((ci >> 1) & 0x55u) == 0x55u;
+            auto hsum = [&](int j, int& h0, int& h1) {
+                const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
+                const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
+                const us2 al = __builtin_bit_cast(us2, als[j]);
+                h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
+                h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
+            };
+            // hsum returns H = 16 h (the table alphas are scaled by 16), so
+            // ((h >> 4) * b) >> 16 = mulhi_u24(H & ~0xFF, b << 8): one v_and and one
+            // v_mul_hi_u32_u24 per term.  No saturation: alphas and betas each sum to
+            // 2048, so the two terms are <= (255*2048 >> 4) * 2048 >> 16 = 1020 and
+            // the value <= 255.
+            const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
+            auto mulhi24 = [](uint32_t x, uint32_t y) {
+                return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * (y & 0xFFFFFFu)) >> 32);
+            };
+            auto vsimd = [&](int H0, int H1) {
+                return (int)((mulhi24((uint32_t)H0 & ~0xFFu, bs0) +
+                              mulhi24((uint32_t)H1 & ~0xFFu, bs1) + 2u) >> 2);
+            };
+            if (all_simd) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int h0, h1;
+                    hsum(j, h0, h1);
+                    out |= (uint32_t)vsimd(h0, h1) << (8 * j);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int h0, h1;
+                    hsum(j, h0, h1);
+                    const int vs = vsimd(h0, h1);
+                    h0 >>= 4;
+                    h1 >>= 4;
+                    const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+                    out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
+                }
+            }
+        } else {   // reflected border group: bytes one by one
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int sxj = xs[j];
+                const int f = (int)(ci >> (2 * j)) & 3;
+                int h0, h1;
+                if (f & 1) {
+                    const int aa = (int)(int16_t)(als[j] & 0xFFFF), ab = (int)(int16_t)(als[j] >> 16);
+                    h0 = w0[sxj] * aa + w0[sxj + 1] * ab;
+                    h1 = w1[sxj] * aa + w1[sxj + 1] * ab;
+                } else {
+                    h0 = w0[sxj] * 2048;
+                    h1 = w1[sxj] * 2048;
+                }
+                out |= (uint32_t)vresize(h0, h1, b0, b1, (f & 2) != 0) << (8 * j);
+            }
+        }
+        return out;
+    };
     auto level_item = [&](int hr, int q, bool all) {
         const int y = Y0 - 3 + hr, xg = X0 - 4 + 4 * q;
         uint32_t out = 0;
@@ -447,87 +538,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
                                (int)(cg.y >> 16)};
             if (mode == 3) {
-                const uint4 al = calp[q];
-                const uint32_t als[4] = {al.x, al.y, al.z, al.w};
-                const int r0 = (int)(ri.x & 0xFFFF), r1 = (int)(ri.x >> 16);
-                const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
-                const uint8_t* w0 = win + __umul24(r0, WP);
-                const uint8_t* w1 = win + __umul24(r1, WP);
-                if (ci & 0x200u) {
-                    // branch-free: v_perm gathers each pixel's two taps as u16s, v_dot2 applies
-                    // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
-                    const uint4 sl = csel[q];
-                    const uint32_t sels[4] = {sl.x, sl.y, sl.z, sl.w};
-                    const int base = xs[0] & ~3, o0 = xs[0] & 3;
-                    const uint32_t* d0p = (const uint32_t*)(w0 + base);
-                    const uint32_t* d1p = (const uint32_t*)(w1 + base);
-                    const uint32_t a0 = d0p[0], a1 = d0p[1], a2 = d0p[2];
-                    const uint32_t c0 = d1p[0], c1 = d1p[1], c2 = d1p[2];
-                    // 8-byte windows starting at the group's first tap column (span <= 7)
-                    const uint32_t wa0 = __builtin_amdgcn_alignbyte(a1, a0, o0);
-                    const uint32_t wa1 = __builtin_amdgcn_alignbyte(a2, a1, o0);
-                    const uint32_t wc0 = __builtin_amdgcn_alignbyte(c1, c0, o0);
-                    const uint32_t wc1 = __builtin_amdgcn_alignbyte(c2, c1, o0);
-                    // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind; 24-bit
-                    // multiplies (full rate): h < 2^19, b <= 2048.  Groups whose 4 pixels all
-                    // take the SSE2 form (all but the right edge) skip the scalar form.
-                    const bool all_simd = ((ci >> 1) & 0x55u) == 0x55u;
-                    auto hsum = [&](int j, int& h0, int& h1) {
-                        const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
-                        const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
-                        const us2 al = __builtin_bit_cast(us2, als[j]);
-                        h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), al, 0u, false);
-                        h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), al, 0u, false);
-                    };
-                    // hsum returns H = 16 h (the table alphas are scaled by 16), so
-                    // ((h >> 4) * b) >> 16 = mulhi_u24(H & ~0xFF, b << 8): one v_and and one
-                    // v_mul_hi_u32_u24 per term.  No saturation: alphas and betas each sum to
-                    // 2048, so the two terms are <= (255*2048 >> 4) * 2048 >> 16 = 1020 and
-                    // the value <= 255.
-                    const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
-                    auto mulhi24 = [](uint32_t x, uint32_t y) {
-                        return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * (y & 0xFFFFFFu)) >> 32);
-                    };
-                    auto vsimd = [&](int H0, int H1) {
-                        return (int)((mulhi24((uint32_t)H0 & ~0xFFu, bs0) +
-                                      mulhi24((uint32_t)H1 & ~0xFFu, bs1) + 2u) >> 2);
-                    };
-                    if (all_simd) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            int h0, h1;
-                            hsum(j, h0, h1);
-                            out |= (uint32_t)vsimd(h0, h1) << (8 * j);
-                        }
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            int h0, h1;
-                            hsum(j, h0, h1);
-                            const int vs = vsimd(h0, h1);
-                            h0 >>= 4;
-                            h1 >>= 4;
-                            const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
-                            out |= (uint32_t)(((ci >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
-                        }
-                    }
-                } else {   // reflected border group: bytes one by one
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int sxj = xs[j];
-                        const int f = (int)(ci >> (2 * j)) & 3;
-                        int h0, h1;
-                        if (f & 1) {
-                            const int aa = (int)(int16_t)(als[j] & 0xFFFF), ab = (int)(int16_t)(als[j] >> 16);
-                            h0 = w0[sxj] * aa + w0[sxj + 1] * ab;
-                            h1 = w1[sxj] * aa + w1[sxj + 1] * ab;
-                        } else {
-                            h0 = w0[sxj] * 2048;
-                            h1 = w1[sxj] * 2048;
-                        }
-                        out |= (uint32_t)vresize(h0, h1, b0, b1, (f & 2) != 0) << (8 * j);
-                    }
-                }
+                out = item3(hr, cg, ci, calp[q], csel[q]);
             } else if (mode == 2) {
                 const int yr = (int)ri.x;
 #pragma unroll
@@ -547,6 +558,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         }
         lvl[hr * LT_G + q] = out;
     };
+#if LEVEL_COLQ
+    if (!direct && mode == 3 && full_tile) {
+        // thread t < 7 LT_G keeps column group q = t % LT_G for halo rows t / LT_G + 7k: the
+        // group's tables are read once, not once per item
+        if (tid < 7 * LT_G) {
+            const int rs = (int)(__umul24((uint32_t)tid, 1928u) >> 16);   // tid / 34, tid < 256
+            const int q = tid - rs * LT_G;
+            const uint2 cg = cgrp[q];
+            const uint32_t ci = cinf[q];
+            const uint4 al = calp[q], sl = csel[q];
+#pragma unroll
+            for (int k = 0; k < (LT_HR + 6) / 7; ++k) {
+                const int hr = rs + 7 * k;
+                if (hr < LT_HR) lvl[hr * LT_G + q] = item3(hr, cg, ci, al, sl);
+            }
+        }
+    } else
+#endif
     if (!direct) {
         int hr = tid / LT_G, q = tid - hr * LT_G;
         if (full_tile) {
