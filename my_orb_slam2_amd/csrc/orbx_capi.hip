@@ -177,6 +177,10 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     memcpy(G.taps, h->taps, sizeof(G.taps));
     memcpy(G.umax, h->umax, sizeof(G.umax));
     G.stereo_win = (int)std::ceil(2.0f * h->scale[L - 1]) + 2;
+    // a left keypoint of level l only takes right keypoints of octaves l-1 .. l+1
+    // (src/Frame.cc:561-563), whose row bands (:522-530) reach at most 2 scale[l+1] rows
+    for (int l = 0; l < L; ++l)
+        G.lv[l].stereo_win = (int)std::ceil(2.0f * h->scale[std::min(l + 1, L - 1)]) + 2;
     long long off = 0, cand = 0;
     int out = 0, blur_tiles = 0, oblocks = 0;
     for (int l = 0; l < L; ++l) {
@@ -461,8 +465,8 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     for (int l = 0; l < L; ++l) h->kscratch_per_image += (long long)G.lv[l].cand_cap * 8;
     h->kscratch_per_image = (long long)align_up((size_t)std::max(h->kscratch_per_image, 16LL), 256);
     // octree LDS: node arrays for the largest list, candidate arrays up to kcap in LDS (a
-    // level with more candidates keeps them in global scratch).  Level 0 gets up to 96 KiB;
-    // levels 1.. run as a second launch sized to fit three workgroups per CU.
+    // level with more candidates keeps them in global scratch).  Level 0 gets up to OCT_LDS0_KB (two per CU);
+    // levels 1.. run as a second launch sized to fit four workgroups per CU (OCT_LDS1_KB).
     int ncand0 = 0, ncand1 = 0, oc1 = 16;
     {
         int c = 0;
@@ -477,14 +481,30 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     }
     h->ncap = (int)align_up((size_t)G.lv[0].out_cap, 16);
     int kcap = std::min(std::max(ncand0, 64), 8192);
-    while (kcap > 64 && octree_lds_bytes(h->ncap, kcap) > 96 * 1024) kcap -= 64;
+    while (kcap > 64 && octree_lds_bytes(h->ncap, kcap) > OCT_LDS0_KB * 1024) kcap -= 64;
     h->kcap = kcap;
     h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
     h->ncap1 = (int)align_up((size_t)oc1, 16);
     int kcap1 = std::min(std::max(ncand1, 64), 8192);
-    while (kcap1 > 64 && octree_lds_bytes(h->ncap1, kcap1) > 52 * 1024) kcap1 -= 64;
+    while (kcap1 > 64 && octree_lds_bytes(h->ncap1, kcap1) > OCT_LDS1_KB * 1024) kcap1 -= 64;
     h->kcap1 = kcap1;
     h->octree_lds1 = octree_lds_bytes(h->ncap1, h->kcap1);
+#if OCT_MERGED
+    {
+        // all levels in one launch: node arrays for the largest level, candidates in LDS up to
+        // the budget (the synthetic and KITTI-like frames stay far below it at every level)
+        int ocmax = 16;
+        for (int l = 0; l < L; ++l) ocmax = std::max(ocmax, G.lv[l].out_cap);
+        h->ncap = (int)align_up((size_t)ocmax, 16);
+        int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
+        while (kc > 64 && octree_lds_bytes(h->ncap, kc) > OCT_LDS_KB * 1024) kc -= 64;
+        h->kcap = kc;
+        h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
+        h->ncap1 = h->ncap;
+        h->kcap1 = h->kcap;
+        h->octree_lds1 = h->octree_lds;
+    }
+#endif
     h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h);
     if (h->octree_lds > 160 * 1024 || h->stereo_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     if (G.kp_cap > 32767) return ORBX_ERR_UNSUPPORTED;   // 16-bit keypoint indices in stereo

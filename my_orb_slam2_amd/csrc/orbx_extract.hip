@@ -587,6 +587,21 @@ __device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
     return carry;
 }
 
+#ifdef ORBX_OCT_STAMPS
+// Diagnostic build only (tools/octree_stamps.py): round clocks of one image's octrees.
+__device__ unsigned long long g_oct_stamps[16][64];
+#define OSTAMP(k)                                                                          \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && blockIdx.y == ORBX_OCT_STAMPS && (k) < 64)                   \
+            g_oct_stamps[level][(k)] = __builtin_readcyclecounter();                        \
+    } while (0)
+extern "C" int orbx_diag_octree_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_stamps), sizeof(g_oct_stamps));
+}
+#else
+#define OSTAMP(k) do { } while (0)
+#endif
+
 template <bool KEYS_LDS>
 __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
                              int level, int ncand, uint32_t* kdata, int16_t* knode, uint8_t* kq,
@@ -599,6 +614,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     const int Hh = L.h - 2 * ORBX_MIN_BORDER;
 
     // ---- roots (src/ORBextractor.cc:552-587) ----
+    OSTAMP(1);
     for (int i = tid; i < nIni; i += 256) sm.cc[i * 4] = 0;
     __syncthreads();
     for (int k = tid; k < ncand; k += 256) {
@@ -630,8 +646,10 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     int seq_base = 1;
     bool phase2 = false;
     NodeArrays cur = sm.A, nxt = sm.B;
+    OSTAMP(2);
     for (int guard = 0; guard < 100000; ++guard) {
         const int prevS = S;
+        OSTAMP(3 + 2 * guard);
         // ---- split every multi-key node: quadrant of each of its keys ----
         for (int i = tid; i < S; i += 256) {
             sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
@@ -842,9 +860,11 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         NodeArrays t2 = cur; cur = nxt; nxt = t2;
         S = Ctot + Stot;
         seq_base += Ctot;
+        OSTAMP(4 + 2 * guard);
         if (S >= N || S == prevS) break;
         if (!phase2 && S + nToExpand * 3 > N) phase2 = true;
     }
+    OSTAMP(60);
 
     // ---- retain the best keypoint of each node (src/ORBextractor.cc:743-762) ----
     uint32_t* best = (uint32_t*)sm.cc;
@@ -856,6 +876,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
     for (int i = tid; i < S; i += 256) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
     if (tid == 0) ocnt[b * g->nlevels + level] = S;
+    OSTAMP(61);
 }
 
 __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
@@ -869,6 +890,7 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int level = level_base + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const LevelGeom& L = g->lv[level];
+    OSTAMP(0);
     // carve LDS
     uint8_t* p = smem;
     auto take = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
@@ -916,9 +938,18 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
     chunked_scan(
         L.ncells, sm.tmp, [&](int c) { return cc[c]; },
         [&](int c, int ex) {
+            // 8 loads in flight per batch (addresses clamped into the cell's slot, so no load
+            // is guarded), then the stores: one memory round trip per 8 candidates of a cell
             const int n = cc[c];
             const uint32_t* s = cbase + lc[c].slot;
-            for (int e = 0; e < n; ++e) kdata[ex + e] = s[e];
+            for (int e0 = 0; e0 < n; e0 += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = s[min(e0 + j, n - 1)];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (e0 + j < n) kdata[ex + e0 + j] = v[j];
+            }
         });
     __syncthreads();
     if (in_lds)
@@ -1169,6 +1200,11 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                        a.dg, a.cells, a.pyr, a.ccnt, a.cand);
     T.stop(K_FAST, e, st);
     e = T.start_after(st);
+#if OCT_MERGED
+    hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
+                       a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
+                       a.ncap, a.kcap, 0);
+#else
     hipLaunchKernelGGL(k_octree, dim3(1, a.batch), dim3(256), a.octree_lds, st, a.dg, a.cells,
                        a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, a.ncap,
                        a.kcap, 0);
@@ -1176,6 +1212,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         hipLaunchKernelGGL(k_octree, dim3(G.nlevels - 1, a.batch), dim3(256), a.octree_lds1, st,
                            a.dg, a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch,
                            a.kscratch_per_image, a.ncap1, a.kcap1, 1);
+#endif
     T.stop(K_OCTREE, e, st);
     e = T.start_after(st);
     hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,

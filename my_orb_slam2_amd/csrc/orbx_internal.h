@@ -42,11 +42,27 @@ struct LevelGeom {
     int patch_size;         // (int)(31*scale)
     int ntx, nty;           // k_level tiles of this level
     int ctab, rowtab;       // k_level: byte offsets of the level's column / row tables
+    int stereo_win;         // k_stereo: row-bucket half-window for a left keypoint of this level
 };
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
 #ifndef OD_NK
 #define OD_NK 8               // keypoints per wave in k_orient_desc (<= 64)
+#endif
+// k_octree: one launch over all levels (OCT_MERGED) under one LDS budget per workgroup; a
+// level whose candidates exceed the budget's kcap keeps them in global scratch
+#ifndef OCT_MERGED
+#define OCT_MERGED 0   // measured slower (0.50 vs 0.46 ms at B = 512): the level-0 lists need
+                       // their large LDS footprint
+#endif
+#ifndef OCT_LDS0_KB
+#define OCT_LDS0_KB 76  // level 0 launch (OCT_MERGED = 0): two workgroups per CU (96: one)
+#endif
+#ifndef OCT_LDS1_KB
+#define OCT_LDS1_KB 40  // levels 1.. launch (OCT_MERGED = 0): four workgroups per CU
+#endif
+#ifndef OCT_LDS_KB
+#define OCT_LDS_KB 52
 #endif
 #define LT_W 128              // output tile width  (32 groups of 4)
 #ifndef LT_H

@@ -133,7 +133,9 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             dl1 = q[1];
         }
         int best = 100, bestR = -1;   // ORBmatcher::TH_HIGH, strict '<': first minimum wins
-        const int r0 = max(row - g->stereo_win, 0), r1 = min(row + g->stereo_win, H - 1);
+        // right keypoints of octaves levelL-1 .. levelL+1 sit within the level's window of rows
+        const int win = g->lv[levelL].stereo_win;
+        const int r0 = max(row - win, 0), r1 = min(row + win, H - 1);
         const int e1 = rowstart[r1 + 1];
         int bestE = -1;
         for (int e = rowstart[r0]; e < e1; ++e) {

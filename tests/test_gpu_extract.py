@@ -65,6 +65,16 @@ def test_edge_images(oracle_mod, orbx_lib, gpu, name):
     _check_extract(g, o, img, name)
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_dense_corners(oracle_mod, orbx_lib, gpu, seed):
+    """Uniform noise: thousands of FAST candidates per level, more than k_octree keeps in LDS,
+    so every level's DistributeOctTree runs on the global-scratch candidate arrays."""
+    g, o = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
+    img = np.random.default_rng(seed).integers(0, 256, (376, 1241), dtype=np.uint8)
+    assert len(o(img)[0]) > 0 and len(o.candidates(0)) > 8192
+    _check_extract(g, o, img, f"noise seed {seed}")
+
+
 def test_empty_image(orbx_lib, gpu):
     import my_orb_slam2_amd as m
     g = m.ORBextractor(1000, 1.2, 8, 20, 7)
