@@ -36,11 +36,11 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r01_pmc_fetch_b512.csv", "r01_pmc_write_b512.csv"))
+                       ("r02_pmc_fetch_b512.csv", "r02_pmc_write_b512.csv"))
 
 
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                             ("r01_pmc_fetch_euroc.csv", "r01_pmc_write_euroc.csv"))
+                             ("r02_pmc_fetch_euroc.csv", "r02_pmc_write_euroc.csv"))
 
 
 def parse():
