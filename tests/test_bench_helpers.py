@@ -19,14 +19,15 @@ def _bench():
 
 def _latest(pattern):
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)),
-                   key=lambda p: int(os.path.basename(p).split("_v")[1].split("_")[0]))
-    return files[-1]
+    def key(p):   # (round, version) of profiles/rNN_vM_*
+        name = os.path.basename(p)
+        return int(name[1:3]), int(name.split("_v")[1].split("_")[0])
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=key)[-1]
 
 
 def test_headline_traffic_matches_committed_pmc():
     b = _bench()
-    line = json.load(open(_latest("r01_v*_bench.json")))
+    line = json.load(open(_latest("r[0-9][0-9]_v*_bench.json")))
     roof = line["roofline"]
     t = b.traffic_from_csv(b.DEFAULT_PMC, roof["kernel"])
     assert t is not None and t > 0
