@@ -321,6 +321,13 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
     }
 }
 
+#ifndef LEVEL_DIAG
+#define LEVEL_DIAG 0   // diagnostic builds only: 1 no resize math, 2 no mode-3 staging, 4 no column pass, 8 no row pass,
+                       // 16 no level-0 loads, 32 no table loads
+#endif
+#ifndef LEVEL_FORCE_GENERIC
+#define LEVEL_FORCE_GENERIC 0   // diagnostic builds only: every tile on the partial-tile paths
+#endif
 #ifndef LEVEL_COLQ
 #define LEVEL_COLQ 1   // mode-3 full tiles: a thread keeps one column group (tables read once)
 #endif
@@ -372,7 +379,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     const int wx0 = CT->x0, WWb = CT->ww, wy0 = RT->y0, WH = RT->wh;
     // table loads issued before the window loads, so both land in one round trip
     uint4 tc = make_uint4(0, 0, 0, 0), ta = make_uint4(0, 0, 0, 0), ts = ta;
-    if (tid < LT_G) {
+    if (LEVEL_DIAG & 32) {
+        tc = make_uint4(tid, 0, 0, 0);
+    } else if (tid < LT_G) {
         tc = make_uint4(CT->cgrp[2 * tid], CT->cgrp[2 * tid + 1], CT->cinf[tid], 0);
         ta = *(const uint4*)&CT->calp[4 * tid];
         ts = *(const uint4*)&CT->csel[4 * tid];
@@ -386,7 +395,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     // into the level array (two aligned dwords + v_alignbyte per 4-pixel group)
     const bool direct = mode == 0 && X0 >= 4 && X0 + LT_W + 8 <= L.w && Y0 >= 3 &&
                         Y0 + LT_H + 3 <= L.h;
-    if (direct) {
+    if (direct && (LEVEL_DIAG & 16)) {
+        for (int i = tid; i < LT_HR * LT_G; i += 256) lvl[i] = (uint32_t)i;
+    } else if (direct) {
         const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
         constexpr int NI = (LT_HR * LT_G + 255) / 256;
         static_assert(256 / LT_G == 7 && 256 % LT_G == 18, "halo item stride");
@@ -418,7 +429,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                                            (WWb + 3) >> 2, (uint32_t*)(win + wcol0), WP / 4, tid))
             stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, (WWb + 3) >> 2,
                               (uint32_t*)(win + wcol0), WP / 4, tid);
-    } else if (mode == 3) {
+    } else if (mode == 3 && !(LEVEL_DIAG & 2)) {
         const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;
         if (!stage_dwords_cols<STAGE_MAXK>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4,
                                            (uint32_t*)win, WP / 4, tid))
@@ -439,11 +450,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
     // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
-    const bool full_tile = vw == LT_W && vh == LT_H;   // every halo item is needed
+    const bool full_tile = !LEVEL_FORCE_GENERIC && vw == LT_W && vh == LT_H;   // every halo item is needed
     // mode 3 (generic INTER_LINEAR) on one 4-pixel group: halo row hr, the group's column
     // tables (cg: source columns, ci: flags, al: alphas, sl: v_perm selectors)
     auto item3 = [&](int hr, uint2 cg, uint32_t ci, uint4 al, uint4 sl) -> uint32_t {
         uint32_t out = 0;
+        if (LEVEL_DIAG & 1) return cg.x ^ ci ^ al.x ^ sl.y ^ (uint32_t)hr;
         const uint2 ri = rinf[hr];
         const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
                            (int)(cg.y >> 16)};
@@ -606,13 +618,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                          (uint32_t)k4 * 0x10001u, (uint32_t)k5 * 0x10001u, (uint32_t)k6 * 0x10001u,
                          (uint32_t)k3};
     // full tiles (all but the right / bottom edge) run the fixed-trip-count form
-    const bool full = vw == LT_W && vh == LT_H;
+    const bool full = !LEVEL_FORCE_GENERIC && vw == LT_W && vh == LT_H;
 #if BLUR_F32
     float* rowsf = (float*)rows;
+    if (LEVEL_DIAG & 8) {} else
     if (full) tile_out_rows_f<true>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     else tile_out_rows_f<false>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     __syncthreads();
     STAMP(4);
+    if (LEVEL_DIAG & 4) {} else
     if (full) tile_columns_f<true>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
     else tile_columns_f<false>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
 #else
