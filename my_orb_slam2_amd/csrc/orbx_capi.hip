@@ -235,7 +235,8 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                     lcap += c.cap;
                     // k_fast stages the ROI as aligned dwords: <= cols + 6 bytes per row
                     G.max_roi_bytes = std::max(G.max_roi_bytes,
-                                               (int)c.rows * ((c.cols + 6 + 3) / 4) * 4);
+                                               (int)c.rows * std::max((c.cols + 6 + 3) / 4,
+                                                                      fast_lpitch((3 + c.cols + 3) / 4, dw)) * 4);
                     if (dh > 0 && dw > 0) {
                         G.max_mbuf_bytes = std::max(G.max_mbuf_bytes, ((dh + 2) * (dw + 2) + 3) & ~3);
                         G.max_cell_px = std::max(G.max_cell_px, dh * dw);

@@ -146,6 +146,15 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_PF
 #define FAST_PF 8      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
+#ifndef FAST_CMPONLY
+#define FAST_CMPONLY 0
+#endif
+#ifndef FAST_NOLDS
+#define FAST_NOLDS 0
+#endif
+#ifndef FAST_2PASS
+#define FAST_2PASS 1   // detect at iniThFAST first, minThFAST only for cells without a keypoint
+#endif
 #ifndef FAST_PRE8
 #define FAST_PRE8 0    // even-point segment test before the arc score (measured slower: off)
 #endif
@@ -200,12 +209,21 @@ __device__ __forceinline__ uint32_t compass4_fr(const uint8_t* roi0, int rp, int
     constexpr int KC = (XO + 9) >> 2;
     constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
     uint32_t C[5], D[5], U[5];
+#if FAST_NOLDS   // diagnostic builds only: compass operands without LDS reads
+    const uint32_t z = (uint32_t)(uintptr_t)rc ^ (uint32_t)(uintptr_t)rd ^ (uint32_t)(uintptr_t)ru;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        C[k] = z * (k + 3); D[k] = z * (k + 5); U[k] = z * (k + 7);
+        asm volatile("" : "+v"(C[k]), "+v"(D[k]), "+v"(U[k]));
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         C[k] = k <= KC ? rc[k] : 0u;
         D[k] = (k >= K0 && k <= K1) ? rd[k] : 0u;
         U[k] = (k >= K0 && k <= K1) ? ru[k] : 0u;
     }
+#endif
     uint32_t F[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -267,6 +285,53 @@ __device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R,
     return (f & 5u) | ((f >> 15) & 10u);
 }
 
+// The compass pre-test of 16 adjacent pixels (detection columns 16g .. 16g+15 of ROI row R),
+// the arithmetic of compass4_fr on four 4-pixel groups.  The centre row's 8 dwords and the
+// +-3 rows' 6 are read with 16-byte LDS loads (FAST_W16 rows are 16-byte aligned).  Returns
+// bit i = pixel 16g + i passes.
+template <int XO>
+__device__ __forceinline__ uint32_t compass16_fr(const uint8_t* roi0, int rp, int R, int g, uint32_t K) {
+    const uint8_t* row = roi0 + __umul24((uint32_t)R, (uint32_t)rp);
+    const uint4* rc = (const uint4*)row + g;
+    const uint4* rd = (const uint4*)(row + 3 * rp) + g;
+    const uint4* ru = (const uint4*)(row - 3 * rp) + g;
+    const uint4 c0 = rc[0], c1 = rc[1], d0 = rd[0], u0 = ru[0];
+    const uint2 d1 = *(const uint2*)(rd + 1), u1 = *(const uint2*)(ru + 1);
+    const uint32_t C[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const uint32_t D[6] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y};
+    const uint32_t U[6] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y};
+    uint32_t mask = 0;
+#pragma unroll
+    for (int h4 = 0; h4 < 4; ++h4) {
+        uint32_t F[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int o = XO + 3 + 4 * h4 + h;      // byte of pixel 4 h4 + h (centre row)
+            const uint32_t V = pair_u16_stride2(C, o);
+            const uint32_t N12 = pair_u16_stride2(C, o - 3), N4 = pair_u16_stride2(C, o + 3);
+            const uint32_t N0 = pair_u16_stride2(D, o), N8 = pair_u16_stride2(U, o);
+            const uint32_t A = K - V, B = K + V;
+            const uint32_t bright = ((N0 + A) | (N8 + A)) & ((N4 + A) | (N12 + A));
+            const uint32_t dark = ((B - N0) | (B - N8)) & ((B - N4) | (B - N12));
+            F[h] = (bright | dark) & 0x40004000u;    // bits 14 (pixel h), 30 (pixel h + 2)
+        }
+        const uint32_t f = F[0] | (F[1] << 1);       // bits 14, 15, 30, 31: pixels 0..3
+        mask |= (((f >> 14) & 3u) | ((f >> 28) & 12u)) << (4 * h4);
+    }
+    return mask;
+}
+
+// Inclusive prefix sum over the wave (DPP row shifts, then the row broadcasts).
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE))) void k_fast(const Geometry* __restrict__ g,
                                               const CellDesc* __restrict__ cells,
                                               const uint8_t* __restrict__ pyr,
@@ -282,17 +347,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     const int ncw = min(FAST_NC, g->n_cells - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
+#if FAST_W16
+    // one buffer: the corners found so far, then the current pass's survivor list (scored in
+    // place: a corner is written at or below the entry it was read from)
+    uint8_t* roi0 = smem + wid * (roi_cap + mb_cap + 64 * 2 + cl_cap);
+    uint8_t* mb = roi0 + roi_cap;
+    int16_t* list = (int16_t*)(mb + mb_cap);
+    int16_t* corners = list;
+#else
     uint8_t* roi0 = smem + wid * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
     uint8_t* mb = roi0 + roi_cap;
     int16_t* list = (int16_t*)(mb + mb_cap);
     int16_t* corners = list + FAST_LIST + 64;   // pixels with M > min threshold, raster order
-    const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
-    const int tq = min(g->ini_th, g->min_th);
-#if FAST_COMPASS_PK
-    const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
-#else
-    const uint32_t KT = (uint32_t)(0x4000 - tq - 1) * 0x10001u;
 #endif
+    const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
 
     // ROI of a cell as aligned dwords, dense rows of ndw dwords: LDS dword t = lane + 64j
     uint32_t pf[FAST_PF];
@@ -328,16 +396,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         int* cnt_out = ccnt + (size_t)b * g->n_cells + ci;
         const int xo = c.ini_x & 3;
         const int ndw = (xo + cols + 3) >> 2;
-        const int rp = ndw * 4;   // LDS row pitch of the ROI
+        const int lp = fast_lpitch(ndw, dw);   // LDS row pitch of the ROI, dwords
+        const int rp = lp * 4;
         if (dh > 0 && dw > 0) {
             if (pre) {
+                if (lp == ndw) {
 #pragma unroll
-                for (int j = 0; j < FAST_PF; ++j)
-                    if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lane + 64 * j] = pf[j];
+                    for (int j = 0; j < FAST_PF; ++j)
+                        if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lane + 64 * j] = pf[j];
+                } else {   // dense element t = lane + 64 j -> row t / ndw, column t % ndw
+                    const int dr = 64 / ndw, dc = 64 - dr * ndw;
+                    int r = lane / ndw, col = lane - r * ndw;
+                    int lo = r * lp + col;
+                    const int lstep = dr * lp + dc, lwrap = lp - ndw;
+#pragma unroll
+                    for (int j = 0; j < FAST_PF; ++j) {
+                        if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lo] = pf[j];
+                        col += dc;
+                        lo += lstep;
+                        if (col >= ndw) { col -= ndw; lo += lwrap; }
+                    }
+                }
             } else {
                 const LevelGeom& L = g->lv[c.level];
                 stage_dwords<64>(pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3),
-                                 L.pitch, rows, ndw, (uint32_t*)roi0, ndw, lane);
+                                 L.pitch, rows, ndw, (uint32_t*)roi0, lp, lane);
             }
         }
         if (k + 1 < ncw) {   // the next cell's ROI loads stay in flight during this cell
@@ -352,9 +435,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int mw = dw + 2;
         for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
         lds_order();
-        // 1. compass pre-test at the lower threshold, 4 pixels per lane: 2^gsh lanes per
-        //    detection row (groups of 4 columns), 64 >> gsh rows per pass, so lane order then
-        //    pixel order within a lane is raster order.
         const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
         const int rpp = 64 >> gsh;
         const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
@@ -366,7 +446,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const uint32_t colmask = ((colmask4 & 3u) << CMP_B0) | ((colmask4 & 12u) << (CMP_B2 - 2));
         constexpr int PB[4] = {CMP_B0, CMP_B1, CMP_B2, CMP_B3};
 #endif
+#if FAST_W16
+        // 16 pixels per lane: lpr lanes per detection row, 64 / lpr rows per pass; one pass
+        // is one block of the survivor list
+        const int lsh = dw > 32 ? 2 : 1;
+        const int rpp16 = 64 >> lsh;
+        const int sub16 = lane >> lsh, g16 = lane & ((1 << lsh) - 1);
+        const int rem16 = dw - 16 * g16;
+        const uint32_t colmask16 = rem16 >= 16 ? 0xFFFFu : (rem16 > 0 ? (1u << rem16) - 1u : 0u);
+        const int rows_blk = rpp16;
+        (void)colmask; (void)sub; (void)gx;
+#else
         const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
+#endif
+        uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
+        const int t_ini = g->ini_th, t_min = g->min_th;
+        int base = 0;
+        // FAST_2PASS: the cell is first detected at iniThFAST alone (compass test, arc scores
+        // and NMS at that threshold); only a cell with no keypoint there is detected again at
+        // minThFAST (:830-837).  Otherwise one pass at the lower threshold serves both.
+        for (int pass = 0; pass < (FAST_2PASS ? 2 : 1); ++pass) {
+        const int tq = FAST_2PASS ? (pass == 0 ? t_ini : t_min) : min(t_ini, t_min);
+#if FAST_COMPASS_PK
+        const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
+#else
+        const uint32_t KT = (uint32_t)(0x4000 - tq - 1) * 0x10001u;
+#endif
+        // 1. compass pre-test at tq, 4 pixels per lane: 2^gsh lanes per detection row (groups
+        //    of 4 columns), 64 >> gsh rows per pass, so lane order then pixel order within a
+        //    lane is raster order.
         int ncorner = 0;
 #if FAST_DIAG >= 3   // diagnostic builds only: no detection work at all
         for (int rb = 0; rb < 0; rb += rows_blk) {
@@ -374,6 +482,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         for (int rb = 0; rb < dh; rb += rows_blk) {
 #endif
             int nlist = 0;
+#if FAST_W16
+            {
+                const int rr = rb + sub16;
+                const int R = min(rr, dh - 1) + 3;
+                uint32_t f;
+                switch (xo) {
+                    case 0: f = compass16_fr<0>(roi0, rp, R, g16, KT); break;
+                    case 1: f = compass16_fr<1>(roi0, rp, R, g16, KT); break;
+                    case 2: f = compass16_fr<2>(roi0, rp, R, g16, KT); break;
+                    default: f = compass16_fr<3>(roi0, rp, R, g16, KT); break;
+                }
+#if FAST_DIAG >= 2
+                f = 0u;
+#endif
+#if FAST_CMPONLY
+                asm volatile("" ::"v"(f));
+                f = 0u;
+#endif
+                f &= rr < dh ? colmask16 : 0u;
+                // ordered compaction: lanes are in raster order, bits within a lane too
+                const int cnt = __builtin_popcount(f);
+                const int incl = wave_incl_scan_dpp(cnt);
+                int pos = incl - cnt;
+                const int e0 = (rr << 6) | (16 * g16);
+                int16_t* pl = list + ncorner;
+                while (f) {
+                    pl[pos++] = (int16_t)(e0 + __builtin_ctz(f));
+                    f &= f - 1u;
+                }
+                nlist = __builtin_amdgcn_readlane(incl, 63);
+            }
+#else
             for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
                 const int rr = r0 + sub;
                 const int R = min(rr, dh - 1) + 3;
@@ -394,6 +534,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 }
 #endif
 #if FAST_DIAG >= 2   // diagnostic builds only (tools/variants.py): no compass survivors
+                f = 0u;
+#endif
+#if FAST_CMPONLY   // diagnostic builds only: the compass test kept, no survivor list
+                asm volatile("" ::"v"(f));
                 f = 0u;
 #endif
                 f &= rr < dh ? colmask : 0u;
@@ -417,6 +561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 }
                 nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
             }
+#endif
             lds_order();
 #if FAST_DIAG >= 1   // diagnostic builds only: skip the arc score
             nlist = 0;
@@ -446,11 +591,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 #endif
             // 2. full arc score for the survivors only (dense across lanes); those above the
             //    lower threshold are appended to the corner list, keeping raster order
+            const int lb = FAST_W16 ? ncorner : 0;
             for (int j0 = 0; j0 < nlist; j0 += 64) {
                 const int j = j0 + lane;
                 int pe = 0, m = 0;
                 if (j < nlist) {
-                    pe = list[j];
+                    pe = list[lb + j];
                     const int rr = pe >> 6, cc = pe & 63;
                     m = fast_arc_score(roi, rp, rr + 3, cc + 3);
                     mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
@@ -464,16 +610,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         }
         // 3. cell-local NMS at iniThFAST, or at minThFAST when the cell has no keypoint at
         //    iniThFAST (:833-837); 4. ordered compaction (raster order, as cv::FAST emits).
-        //    Both thresholds are tested in one pass when the corners fit one wave.
-        uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
-        int base = 0;
-        const int t_ini = g->ini_th, t_min = g->min_th;
+        //    One pass tests both thresholds (FAST_2PASS = 0) or the pass's own.
+        const int th_hi = FAST_2PASS ? tq : t_ini, th_lo = FAST_2PASS ? tq : t_min;
         if (ncorner <= 64) {
             int sc = 0, pe = 0;
             bool k_hi = false, k_lo = false;
             if (lane < ncorner) {
                 pe = corners[lane];
-                fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+                fast_nms_kp2(mb, mw, pe >> 6, pe & 63, th_hi, th_lo, k_hi, k_lo, sc);
             }
             const uint64_t mh = __ballot(k_hi);
             const bool kk = mh ? k_hi : k_lo;
@@ -493,7 +637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 bool k_hi = false, k_lo = false;
                 if (j < ncorner) {
                     const int pe = corners[j];
-                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, th_hi, th_lo, k_hi, k_lo, sc);
                 }
                 found = __ballot(k_hi) != 0;
             }
@@ -503,7 +647,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 bool k_hi = false, k_lo = false;
                 if (j < ncorner) {
                     pe = corners[j];
-                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, t_ini, t_min, k_hi, k_lo, sc);
+                    fast_nms_kp2(mb, mw, pe >> 6, pe & 63, th_hi, th_lo, k_hi, k_lo, sc);
                 }
                 const bool kk = found ? k_hi : k_lo;
                 const uint64_t m = __ballot(kk);
@@ -516,6 +660,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 base += __popcll(m);
             }
         }
+        if (base > 0) break;   // wave-uniform: keypoints at this pass's threshold
+        lds_order();
+        }
         if (lane == 0) *cnt_out = min(base, c.cap);
         lds_order();
     }
@@ -524,7 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 size_t fast_lds_bytes(const Geometry& G) {
     const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (G.max_cell_px * 2 + 15) & ~15;
-    return (size_t)4 * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
+    return (size_t)4 * (roi_cap + mb_cap + (FAST_W16 ? 64 : FAST_LIST + 64) * 2 + cl_cap);
 }
 
 // ----------------------------------------------------------------------------------------

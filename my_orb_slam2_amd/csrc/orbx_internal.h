@@ -119,6 +119,24 @@ struct Geometry {
     LevelGeom lv[ORBX_MAX_LEVELS];
 };
 
+// k_fast ROI row pitch in dwords (FAST_W16): a multiple of 4 (16-byte aligned rows for the
+// compass's b128 reads) with room for the widest lane's reads (16 pixels per lane, 2 lanes
+// per detection row up to 32 columns, else 4).  A bank-conflict-free pitch (24 / 48 dwords)
+// was measured slower: the larger ROI costs a workgroup per CU.
+#ifndef FAST_W16
+#define FAST_W16 1
+#endif
+__host__ __device__ inline int fast_lpitch(int ndw, int dw) {
+#if FAST_W16
+    const int lpr = dw > 32 ? 4 : 2;
+    const int need = ndw > 4 * lpr + 4 ? ndw : 4 * lpr + 4;
+    return (need + 3) & ~3;
+#else
+    (void)dw;
+    return ndw;
+#endif
+}
+
 // Packed candidate / octree survivor: x, y relative to (minBorderX, minBorderY).
 __host__ __device__ inline uint32_t pack_cand(int x, int y, int score) {
     return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)score << 24);
