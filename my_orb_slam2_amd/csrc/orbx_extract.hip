@@ -144,7 +144,7 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
 #endif
 #ifndef FAST_PF
-#define FAST_PF 8      // prefetched ROI dwords per lane (larger ROIs are staged directly)
+#define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
 #ifndef FAST_CMPONLY
 #define FAST_CMPONLY 0
