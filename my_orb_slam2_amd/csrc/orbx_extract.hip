@@ -165,7 +165,7 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
 #endif
 #ifndef OD_WPE
-#define OD_WPE 1
+#define OD_WPE 5       // at most 96 VGPRs: five waves per SIMD (6: spills)
 #endif
 __device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
