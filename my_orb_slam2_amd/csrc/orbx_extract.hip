@@ -140,6 +140,12 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_LIST
 #define FAST_LIST 512    // compass survivors listed per row block (a multiple of 256)
 #endif
+#ifndef FAST_STAGE2D
+#define FAST_STAGE2D 1   // ROI prefetch on a 16-lanes-per-row grid (no index divisions)
+#endif
+#ifndef FAST_PF2D
+#define FAST_PF2D 10     // its rows per lane: ROIs up to 40 rows are prefetched
+#endif
 #ifndef FAST_NC
 #define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
 #endif
@@ -159,7 +165,7 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define FAST_PRE8 0    // even-point segment test before the arc score (measured slower: off)
 #endif
 #ifndef FAST_WPE
-#define FAST_WPE 1     // minimum waves per SIMD requested from the register allocator
+#define FAST_WPE 6     // minimum waves per SIMD requested from the register allocator (80 VGPRs)
 #endif
 #ifndef OCTREE_PACKED
 #define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
@@ -363,6 +369,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
 
     // ROI of a cell as aligned dwords, dense rows of ndw dwords: LDS dword t = lane + 64j
+#if FAST_STAGE2D
+    // ROI of a cell as a 2-D lane grid: lane (r = lane / 16, col = lane % 16) holds ROI dword
+    // col of rows r, r + 4, .., so an element costs one 24-bit multiply-add of address and no
+    // divisions (columns >= ndw idle)
+    uint32_t pf[FAST_PF2D];
+    const int lr2 = lane >> 4, lc2 = lane & 15;
+    auto prefetch = [&](const CellDesc& c) -> bool {
+        const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
+        if (ndw > 16 || c.rows > 4 * FAST_PF2D || c.rows <= 6 || c.cols <= 6) return false;
+        const LevelGeom& L = g->lv[c.level];
+        const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3) +
+                             4 * min(lc2, ndw - 1);
+        const uint32_t gp = (uint32_t)L.pitch;
+#pragma unroll
+        for (int j = 0; j < FAST_PF2D; ++j)
+            pf[j] = *(const uint32_t*)(src + __umul24((uint32_t)min(lr2 + 4 * j, c.rows - 1), gp));
+        return true;
+    };
+#else
     uint32_t pf[FAST_PF];
     auto prefetch = [&](const CellDesc& c) -> bool {
         const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
@@ -386,6 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         return true;
     };
 
+#endif
     CellDesc cn = cells[c_first];
     bool have = prefetch(cn);
     for (int k = 0; k < ncw; ++k) {
@@ -399,6 +425,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int lp = fast_lpitch(ndw, dw);   // LDS row pitch of the ROI, dwords
         const int rp = lp * 4;
         if (dh > 0 && dw > 0) {
+#if FAST_STAGE2D
+            if (pre) {
+                if (lc2 < ndw) {
+                    uint32_t* l = (uint32_t*)roi0 + lr2 * lp + lc2;
+#pragma unroll
+                    for (int j = 0; j < FAST_PF2D; ++j)
+                        if (lr2 + 4 * j < rows) l[4 * j * lp] = pf[j];
+                }
+            } else
+#endif
             if (pre) {
                 if (lp == ndw) {
 #pragma unroll
