@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "orbx_device.h"
 #include "orbx_internal.h"
 #include "orbx_kernels.h"
@@ -453,7 +455,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     const bool full_tile = !LEVEL_FORCE_GENERIC && vw == LT_W && vh == LT_H;   // every halo item is needed
     // mode 3 (generic INTER_LINEAR) on one 4-pixel group: halo row hr, the group's column
     // tables (cg: source columns, ci: flags, al: alphas, sl: v_perm selectors)
-    auto item3 = [&](int hr, uint2 cg, uint32_t ci, uint4 al, uint4 sl) -> uint32_t {
+    auto item3 = [&](int hr, uint2 cg, uint32_t ci, uint4 al, uint4 sl, auto fast_c) -> uint32_t {
+        constexpr bool FASTP = decltype(fast_c)::value;   // simple group, all four pixels SSE2
         uint32_t out = 0;
         if (LEVEL_DIAG & 1) return cg.x ^ ci ^ al.x ^ sl.y ^ (uint32_t)hr;
         const uint2 ri = rinf[hr];
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
         const uint8_t* w0 = win + __umul24(r0, WP);
         const uint8_t* w1 = win + __umul24(r1, WP);
-        if (ci & 0x200u) {
+        if (FASTP || (ci & 0x200u)) {
             // branch-free: v_perm gathers each pixel's two taps as u16s, v_dot2 applies
             // the alphas (HResizeLinear), then VResizeLinear (SSE2 or scalar form)
             const uint32_t sels[4] = {sl.x, sl.y, sl.z, sl.w};
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             // h <= 255*2048, betas in [0, 2048]: the SSE2 clamps never bind; 24-bit
             // multiplies (full rate): h < 2^19, b <= 2048.  Groups whose 4 pixels all
             // take the SSE2 form (all but the right edge) skip the scalar form.
-            const bool all_simd = ((ci >> 1) & 0x55u) == 0x55u;
+            const bool all_simd = FASTP || ((ci >> 1) & 0x55u) == 0x55u;
             auto hsum = [&](int j, int& h0, int& h1) {
                 const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
                 const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
                                (int)(cg.y >> 16)};
             if (mode == 3) {
-                out = item3(hr, cg, ci, calp[q], csel[q]);
+                out = item3(hr, cg, ci, calp[q], csel[q], std::false_type{});
             } else if (mode == 2) {
                 const int yr = (int)ri.x;
 #pragma unroll
@@ -580,10 +583,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             const uint2 cg = cgrp[q];
             const uint32_t ci = cinf[q];
             const uint4 al = calp[q], sl = csel[q];
+            // interior tiles: every group of the wave is simple and SSE2-only, so the wave takes
+            // the branch-free form with no per-item exec-mask branches
+            const bool fast = (ci & 0x200u) && ((ci >> 1) & 0x55u) == 0x55u;
+            if (__all(fast)) {
 #pragma unroll
-            for (int k = 0; k < (LT_HR + 6) / 7; ++k) {
-                const int hr = rs + 7 * k;
-                if (hr < LT_HR) lvl[hr * LT_G + q] = item3(hr, cg, ci, al, sl);
+                for (int k = 0; k < (LT_HR + 6) / 7; ++k) {
+                    const int hr = rs + 7 * k;
+                    if (hr < LT_HR) lvl[hr * LT_G + q] = item3(hr, cg, ci, al, sl, std::true_type{});
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < (LT_HR + 6) / 7; ++k) {
+                    const int hr = rs + 7 * k;
+                    if (hr < LT_HR) lvl[hr * LT_G + q] = item3(hr, cg, ci, al, sl, std::false_type{});
+                }
             }
         }
     } else
