@@ -201,6 +201,9 @@ __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int 
 #ifndef BLUR_F32
 #define BLUR_F32 1     // row sums kept as floats, column pass in float (exact, see below)
 #endif
+#ifndef BLUR_SLIDE
+#define BLUR_SLIDE 4   // full tiles: output rows per thread in the column pass (0: one row per item)
+#endif
 #ifndef BLUR_CVTPK
 #define BLUR_CVTPK 1   // round + saturate + pack with v_cvt_pk_u8_f32 (else magic-add rounding)
 #endif
@@ -273,14 +276,8 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
                 f5 = (float)(tp.K5 & 0xFFFF) * inv, f6 = (float)(tp.K6 & 0xFFFF) * inv;
     // groups entirely left of bsimd_end take the SSE2 form only
     const bool tile_simd = X0 + 4 * ng <= bsimd_end;
-    auto col_item = [&](int i) {
-        const int r = i / LT_GW, gq = i - r * LT_GW;
-        if (!FULL && gq >= ng) return;
-        float4 v[7];
-#pragma unroll
-        for (int kk = 0; kk < 7; ++kk) v[kk] = *(const float4*)(rows + (r + kk) * LT_W + 4 * gq);
-        const int xg = X0 + 4 * gq;
-        float S[4];
+    // S for the 4 pixels of one group from its 7 row sums v[0..6]
+    auto col_sums = [&](const float4* v, float* S) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             auto c = [&](int kk) { return j == 0 ? v[kk].x : (j == 1 ? v[kk].y : (j == 2 ? v[kk].z : v[kk].w)); };
@@ -289,6 +286,9 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
             a = __builtin_fmaf(c(2) + c(4), f4, a);
             S[j] = __builtin_fmaf(c(3), f3, a);
         }
+    };
+    auto col_store = [&](int r, int gq, const float* S) {
+        const int xg = X0 + 4 * gq;
         uint32_t packed = 0;
         if (tile_simd || xg + 4 <= bsimd_end) {
 #if BLUR_CVTPK
@@ -315,6 +315,34 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
     };
+    auto col_item = [&](int i) {
+        const int r = i / LT_GW, gq = i - r * LT_GW;
+        if (!FULL && gq >= ng) return;
+        float4 v[7];
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) v[kk] = *(const float4*)(rows + (r + kk) * LT_W + 4 * gq);
+        float S[4];
+        col_sums(v, S);
+        col_store(r, gq, S);
+    };
+#if BLUR_SLIDE
+    if constexpr (FULL) {
+        // a thread owns one group and BLUR_SLIDE consecutive output rows: it reads their
+        // BLUR_SLIDE + 6 row sums once (7 per output row in the item form)
+        static_assert(LT_GW == 32 && LT_H * LT_GW == 256 * BLUR_SLIDE, "column-slide mapping");
+        const int gq = tid & (LT_GW - 1), r0 = (tid >> 5) * BLUR_SLIDE;
+        float4 v[BLUR_SLIDE + 6];
+#pragma unroll
+        for (int kk = 0; kk < BLUR_SLIDE + 6; ++kk)
+            v[kk] = *(const float4*)(rows + (r0 + kk) * LT_W + 4 * gq);
+#pragma unroll
+        for (int o = 0; o < BLUR_SLIDE; ++o) {
+            float S[4];
+            col_sums(v + o, S);
+            col_store(r0 + o, gq, S);
+        }
+    } else
+#endif
     if constexpr (FULL) {
 #pragma unroll
         for (int k = 0; k < LT_H * LT_GW / 256; ++k) col_item(tid + 256 * k);
