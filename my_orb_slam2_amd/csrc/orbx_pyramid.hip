@@ -367,6 +367,9 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
 #ifndef LEVEL_WPE
 #define LEVEL_WPE 1
 #endif
+// MODE (host-chosen per level, one instantiation each): 0 level 0 (copy of the input), 1 scale
+// 1 copy, 2 exact 2:1 area, 3 INTER_LINEAR
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))) void k_level(const Geometry* __restrict__ g,
                                                const uint8_t* __restrict__ ltab,
                                                const uint8_t* __restrict__ in0,
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     uint2* rinf = (uint2*)take((size_t)LT_HR * 8);                   // per row: ry0, ry1, b0, b1
     uint8_t* win = p;                                                // source window
 
-    const int mode = level == 0 ? 0 : (L.copy ? 1 : (L.area2 ? 2 : 3));
+    constexpr int mode = MODE;
     const LevelGeom& S = g->lv[level > 0 ? level - 1 : 0];
     // needed halo ranges (level coordinates, before reflection)
     const int nx0 = X0 - 3, nx1 = X0 + vw + 2, ny0 = Y0 - 3, ny1 = Y0 + vh + 2;
@@ -411,6 +414,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     uint4 tc = make_uint4(0, 0, 0, 0), ta = make_uint4(0, 0, 0, 0), ts = ta;
     if (LEVEL_DIAG & 32) {
         tc = make_uint4(tid, 0, 0, 0);
+    } else if (mode == 0) {
+        // level 0 reads no tables
     } else if (tid < LT_G) {
         tc = make_uint4(CT->cgrp[2 * tid], CT->cgrp[2 * tid + 1], CT->cinf[tid], 0);
         ta = *(const uint4*)&CT->calp[4 * tid];
@@ -421,38 +426,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     // window row pitch; modes 0/1 place x at column x - (X0 - 4) so that groups are dword-aligned
     const int WP = (mode == 3) ? ((WWb + 3) & ~3) : LT_G * 4;
     const int wcol0 = (mode == 3) ? 0 : wx0 - (X0 - 4);
-    // level 0 away from the image border: the halo tile is the input itself, loaded straight
-    // into the level array (two aligned dwords + v_alignbyte per 4-pixel group)
-    const bool direct = mode == 0 && X0 >= 4 && X0 + LT_W + 8 <= L.w && Y0 >= 3 &&
-                        Y0 + LT_H + 3 <= L.h;
+    // level 0: the halo tile is the input itself, loaded straight into the level array: two
+    // aligned dwords + v_alignbyte per 4-pixel group, or on border tiles four byte loads per
+    // group (rows and columns reflected per item)
+    constexpr bool direct = mode == 0;
     if (direct && (LEVEL_DIAG & 16)) {
         for (int i = tid; i < LT_HR * LT_G; i += 256) lvl[i] = (uint32_t)i;
     } else if (direct) {
         const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
+        const int W = L.w, H = L.h;
         constexpr int NI = (LT_HR * LT_G + 255) / 256;
         static_assert(256 / LT_G == 7 && 256 % LT_G == 18, "halo item stride");
         uint32_t d0[NI], d1[NI], sh[NI];
-        int hr = tid / LT_G, q = tid - hr * LT_G;
+        // inner tiles: every group's aligned dword pair inside its image row (xg >= 4 keeps the
+        // aligned base after the row start, xg + 8 <= W its second dword before the row end)
+        const bool inner = X0 >= 8 && X0 + LT_W + 8 <= W && Y0 >= 3 && Y0 + LT_H + 3 <= H;
+        auto load_items = [&](auto inner_c) {
+            constexpr bool IN = decltype(inner_c)::value;
+            int hr = tid / LT_G, q = tid - hr * LT_G;
 #pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const int hrc = min(hr, LT_HR - 1);
-            const uintptr_t a = (uintptr_t)(src + __umul24(Y0 - 3 + hrc, (uint32_t)stride) + (X0 - 4 + 4 * q));
-            const uint32_t* ab = (const uint32_t*)(a & ~(uintptr_t)3);
-            sh[k] = (uint32_t)(a & 3);
-            d0[k] = ab[0];
-            d1[k] = ab[1];
-            hr += 7;
-            q += 18;
-            if (q >= LT_G) { q -= LT_G; ++hr; }
-        }
+            for (int k = 0; k < NI; ++k) {
+                const int hrc = min(hr, LT_HR - 1);
+                int y = Y0 - 3 + hrc;
+                if (!IN) {   // BORDER_REFLECT_101; rows past the needed halo: any row
+                    y = y < 0 ? -y : (y >= H ? 2 * H - 2 - y : y);
+                    y = min(max(y, 0), H - 1);
+                }
+                const uint8_t* row = src + __umul24(y, (uint32_t)stride);
+                const int xg = X0 - 4 + 4 * q;
+                if constexpr (IN) {
+                    const uintptr_t a = (uintptr_t)(row + xg);
+                    const uint32_t* ab = (const uint32_t*)(a & ~(uintptr_t)3);
+                    sh[k] = (uint32_t)(a & 3);
+                    d0[k] = ab[0];
+                    d1[k] = ab[1];
+                } else {
+                    // border tiles: four byte loads per group, branch-free, all in flight
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        int x = xg + j;
+                        x = x < 0 ? -x : (x >= W ? 2 * W - 2 - x : x);
+                        x = min(max(x, 0), W - 1);   // pixels past the needed halo: any in-row value
+                        v |= (uint32_t)row[x] << (8 * j);
+                    }
+                    d0[k] = v;
+                    d1[k] = 0;
+                    sh[k] = 0;
+                }
+                hr += 7;
+                q += 18;
+                if (q >= LT_G) { q -= LT_G; ++hr; }
+            }
+        };
+        if (inner) load_items(std::true_type{});
+        else load_items(std::false_type{});
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             const int i = tid + 256 * k;
             if (i < LT_HR * LT_G) lvl[i] = __builtin_amdgcn_alignbyte(d1[k], d0[k], sh[k]);
         }
-    } else if (mode == 0) {
-        const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
-        stage_bytes<256>(src + (size_t)wy0 * stride + wx0, stride, WH, WWb, win + wcol0, WP, tid);
     } else if (mode == 1) {
         const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;   // wx0 is a multiple of 4
         if (!stage_dwords_cols<STAGE_MAXK>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH,
@@ -466,7 +499,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4,
                               (uint32_t*)win, WP / 4, tid);
     }
-    if (tid < LT_G) {
+    if (mode == 0) {
+    } else if (tid < LT_G) {
         cgrp[tid] = make_uint2(tc.x, tc.y);
         cinf[tid] = tc.z;
         calp[tid] = ta;
@@ -692,6 +726,21 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     return r((size_t)LT_HR * LT_G * 4) + (phase12 > phase34 ? phase12 : phase34) + r(64);
 }
 
+static int level_mode(const LevelGeom& L, int l) {
+    return l == 0 ? 0 : (L.copy ? 1 : (L.area2 ? 2 : 3));
+}
+
+typedef void (*LevelKernel)(const Geometry*, const uint8_t*, const uint8_t*, const uint8_t*, int,
+                            size_t, size_t, uint8_t*, uint8_t*, int);
+static LevelKernel level_kernel(int mode) {
+    switch (mode) {
+        case 0: return k_level<0>;
+        case 1: return k_level<1>;
+        case 2: return k_level<2>;
+        default: return k_level<3>;
+    }
+}
+
 hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
     const Geometry& G = *a.hg;
     KernelTimer dummy;
@@ -699,7 +748,8 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
     for (int l = 0; l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
         hipEvent_t e = l == 0 ? T.start(st) : T.start_after(st);
-        hipLaunchKernelGGL(k_level, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
+        auto kern = level_kernel(level_mode(L, l));
+        hipLaunchKernelGGL(kern, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
                            a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
                            a.blur, l);
         T.stop(K_LEVEL, e, st);
@@ -714,8 +764,11 @@ extern "C" int orbx_diag_level_stamps(unsigned long long* out) {
 #endif
 
 hipError_t prepare_level(size_t lds) {
-    return hipFuncSetAttribute((const void*)k_level, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds);
+    hipError_t e = hipSuccess;
+    for (int m = 0; m < 4 && e == hipSuccess; ++m)
+        e = hipFuncSetAttribute((const void*)level_kernel(m),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    return e;
 }
 
 }  // namespace orbx
