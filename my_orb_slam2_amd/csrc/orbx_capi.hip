@@ -159,6 +159,80 @@ int vresize_simd_end(int width) {
     return x;
 }
 
+#ifndef LEVEL_STRIP
+#define LEVEL_STRIP 1  // 0: every level on the tiled k_level
+#endif
+// k_level_strip tables of level l (StripLane per half-strip lane, rows -3 .. h+2); the level
+// keeps the tiled kernel (strip = 0) for modes 1 / 2 or when a group's taps do not fit the
+// 8-byte window the strip kernel reads
+void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
+                        const int16_t* alpha, const int16_t* yofs, const int16_t* beta) {
+    Geometry& G = h->hg;
+    LevelGeom& lv = G.lv[l];
+    lv.strip = 0;
+    if (!LEVEL_STRIP || (mode != 0 && mode != 3)) return;
+    const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
+    lv.sth = STRIP_TH;
+    lv.snh = (lv.w + SW_PX - 1) / SW_PX;
+    lv.snw = (lv.snh + 1) / 2;
+    lv.sns = (lv.h + lv.sth - 1) / lv.sth;
+    std::vector<StripLane> sl((size_t)lv.snh * 32);
+    for (int hs = 0; hs < lv.snh; ++hs)
+        for (int q = 0; q < 32; ++q) {
+            StripLane& e = sl[(size_t)hs * 32 + q];
+            memset(&e, 0, sizeof(e));
+            int xr[4];
+            const int xg = hs * SW_PX - 4 + 4 * q;
+            for (int j = 0; j < 4; ++j)   // groups past every output's halo: any in-row column
+                xr[j] = xg > lv.w + 3 ? lv.w - 1 : reflect101_h(xg + j, lv.w);
+            if (mode == 0) {
+                const int mn = std::min(std::min(xr[0], xr[1]), std::min(xr[2], xr[3]));
+                e.base = (uint32_t)mn;
+                for (int j = 0; j < 4; ++j) {
+                    if (xr[j] - mn > 4) return;   // + the row address's low 2 bits <= 7
+                    e.sel |= (uint32_t)(xr[j] - mn) << (8 * j);
+                }
+            } else {
+                int sx[4];
+                for (int j = 0; j < 4; ++j) sx[j] = xofs[xr[j]];
+                const int mn = std::min(std::min(sx[0], sx[1]), std::min(sx[2], sx[3]));
+                e.base = (uint32_t)mn;
+                for (int j = 0; j < 4; ++j) {
+                    const int k = sx[j] - mn;
+                    // taps k, k+1 of the 8 bytes from the first tap column (o0 + 11 < 16 read)
+                    if (k > 6) return;
+                    e.psel[j] = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(k + 1) << 16) | (0x0Cu << 24);
+                    uint32_t a0 = (uint16_t)alpha[2 * xr[j]], a1 = (uint16_t)alpha[2 * xr[j] + 1];
+                    if (xr[j] >= lv.xmax) { a0 = 2048; a1 = 0; }   // HResizeLinear: S[sx] * 2048
+                    e.alp[j] = (a0 << 4) | ((a1 << 4) << 16);
+                    e.flags |= (uint32_t)((xr[j] < lv.xmax ? 1 : 0) | (xr[j] < lv.rsimd_end ? 2 : 0))
+                               << (2 * j);
+                }
+            }
+        }
+    std::vector<uint32_t> rt((size_t)2 * (lv.h + 6));
+    for (int k = 0; k < lv.h + 6; ++k) {
+        const int yr = reflect101_h(k - 3, lv.h);
+        if (mode == 0) {
+            rt[2 * k] = (uint32_t)yr;
+        } else {
+            const int sy = yofs[yr];
+            const uint32_t r0 = (uint32_t)std::min(std::max(sy, 0), S.h - 1);
+            const uint32_t r1 = (uint32_t)std::min(std::max(sy + 1, 0), S.h - 1);
+            rt[2 * k] = r0 | (r1 << 16);
+            rt[2 * k + 1] = (uint32_t)(uint16_t)beta[2 * yr] | ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16);
+        }
+    }
+    h->ltab.resize(align_up(h->ltab.size(), 16));
+    lv.stab = (int)h->ltab.size();
+    h->ltab.insert(h->ltab.end(), (const uint8_t*)sl.data(), (const uint8_t*)(sl.data() + sl.size()));
+    h->ltab.resize(align_up(h->ltab.size(), 16));
+    lv.srow = (int)h->ltab.size();
+    h->ltab.insert(h->ltab.end(), (const uint8_t*)rt.data(), (const uint8_t*)(rt.data() + rt.size()));
+    h->ltab.resize(align_up(h->ltab.size(), 16));
+    lv.strip = 1;
+}
+
 // Per-size geometry.  Returns ORBX_OK or ORBX_ERR_UNSUPPORTED.
 orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     Geometry& G = h->hg;
@@ -447,6 +521,7 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         lv.rowtab = (int)h->ltab.size();
         h->ltab.insert(h->ltab.end(), (const uint8_t*)rt.data(),
                        (const uint8_t*)(rt.data() + rt.size()));
+        build_strip_tables(h, l, mode, xofs, alpha, yofs, beta);
     }
     h->level_lds = level_lds_bytes(G.ltw, G.lth, G.win_cap);
     if (h->level_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;

@@ -43,6 +43,12 @@ struct LevelGeom {
     int ntx, nty;           // k_level tiles of this level
     int ctab, rowtab;       // k_level: byte offsets of the level's column / row tables
     int stereo_win;         // k_stereo: row-bucket half-window for a left keypoint of this level
+    // k_level_strip (orbx_pyramid.hip): column strips walked row by row
+    int strip;              // 1: this level runs k_level_strip, 0: the tiled k_level
+    int snh;                // half-wave strips across (SW_PX output pixels each)
+    int snw, sns;           // waves across (ceil(snh / 2)) / strip rows
+    int sth;                // output rows per strip
+    int stab, srow;         // byte offsets of the strip lane table / row table in ltab
 };
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
@@ -86,6 +92,27 @@ struct LevelColTab {
 struct LevelRowTab {
     int32_t y0, wh, pad0, pad1;
     uint32_t rinf[2 * LT_HR]; // (ry0 | ry1 << 16, beta0 | beta1 << 16)
+};
+
+// k_level_strip: a wave walks two half-strips (lanes 0-31, 32-63) down the level, one row per
+// step.  Lane q of a half-strip at X0 holds the 4-pixel group x = X0 - 4 + 4q; lanes 1..SW_OUT
+// write output.  Per lane (host-built, reflection and clamping folded in):
+//   mode 0 (level 0): base = the group's smallest reflected input column, sel = 4 byte
+//     offsets from base;
+//   mode 3 (INTER_LINEAR): base = smallest source tap column, psel = per-pixel v_perm selectors
+//     of the two taps relative to base, alp = 16 x alphas ((2048, 0) right of xmax), flags =
+//     2 bits per pixel (right tap in range, SSE2 vertical form).
+// Row table per level: rows y = -3 .. h + 2, (ry0 | ry1 << 16, beta0 | beta1 << 16) with ry
+// absolute source rows (mode 0: ry0 = the reflected input row).
+#ifndef STRIP_TH
+#define STRIP_TH 64   // output rows per strip (<= 122: the row table sits in two registers)
+#endif
+#define SW_OUT 30
+#define SW_PX (4 * SW_OUT)
+struct StripLane {
+    uint32_t base, flags, sel, pad;
+    uint32_t alp[4];
+    uint32_t psel[4];
 };
 
 struct CellDesc {

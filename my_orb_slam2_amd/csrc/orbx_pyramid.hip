@@ -716,6 +716,233 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     STAMP(5);
 }
 
+// ---- k_level_strip: level l and its blur by column strips, one row per step ----
+// A wave owns two half-strips (lanes 0-31 / 32-63) of SW_PX output pixels each and walks
+// them down STRIP rows (+3 halo rows above and below).  Per step, row y: every lane computes
+// its 4-pixel group of level l at row y (source bytes loaded STRIP_PF steps ahead), writes
+// it, takes its neighbours' groups with DPP wave shifts and forms the row sums of the
+// blur; the last 7 rows' sums stay in registers, so the blurred row y - 3 is one
+// symmetric column sum.  No LDS, no barriers: the loads of later rows are in flight while
+// the wave computes.  The arithmetic is item3's (resize, mode 3) and tile_out_rows_f /
+// tile_columns_f's (blur), bit for bit.
+#ifndef STRIP_PF
+#define STRIP_PF 2   // rows of source loads in flight ahead of the row being computed
+#endif
+#ifndef STRIP_WPE0
+#define STRIP_WPE0 6
+#endif
+#ifndef STRIP_WPE3
+#define STRIP_WPE3 5
+#endif
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? STRIP_WPE0 : STRIP_WPE3))) void k_level_strip(const Geometry* __restrict__ g,
+                                                     const uint8_t* __restrict__ ltab,
+                                                     const uint8_t* __restrict__ in0,
+                                                     const uint8_t* __restrict__ in1, int split,
+                                                     size_t stride, size_t bstride,
+                                                     uint8_t* __restrict__ pyr,
+                                                     uint8_t* __restrict__ blur, int level) {
+    static_assert(MODE == 0 || MODE == 3, "strip kernel: level 0 or INTER_LINEAR levels");
+    int bx, b;
+    xcd_block(bx, b);
+    const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+    const LevelGeom& L = g->lv[level];
+    const int wv = bx * 4 + (threadIdx.x >> 6);   // wave of this image
+    if (wv >= L.snw * L.sns) return;              // whole waves only
+    const int swx = wv % L.snw, sy = wv / L.snw;
+    const int hs = 2 * swx + half;
+    const bool hvalid = hs < L.snh;
+    const int hsc = min(hs, L.snh - 1);
+    const int W = L.w, H = L.h, pitch = L.pitch;
+    const int x = hsc * SW_PX - 4 + 4 * l32;      // this lane's group
+    const int Y0 = sy * L.sth, vh = min(L.sth, H - Y0);
+    const bool out_lane = hvalid && l32 >= 1 && l32 <= SW_OUT && x < W;
+    const StripLane* T = (const StripLane*)(ltab + L.stab) + hsc * 32 + l32;
+    const uint4 t0 = *(const uint4*)T;
+    const uint4 al = *(const uint4*)T->alp;
+    const uint4 ps = *(const uint4*)T->psel;
+    const uint2* RT = (const uint2*)(ltab + L.srow) + Y0;   // step i <-> row y = Y0 - 3 + i
+    const int n = vh + 6;
+
+    // source of this lane's bytes
+    const uint8_t* src;
+    size_t spitch;
+    if (MODE == 0) {
+        src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
+        spitch = stride;
+    } else {
+        const LevelGeom& S = g->lv[level - 1];
+        src = pyr + (size_t)b * g->pyr_bytes + S.off + (t0.x & ~3u);
+        spitch = (size_t)S.pitch;
+    }
+    const uint32_t o0 = t0.x & 3u;   // mode 3: first tap's byte offset in the aligned dword
+
+    // per-wave forms: every needed lane SSE2 in the vertical resize / the blur's columns
+    const bool lane_rsimd = ((t0.y >> 1) & 0x55u) == 0x55u;
+    const bool wave_rsimd = __all(!hvalid || lane_rsimd);
+    const bool wave_bsimd = __all(!out_lane || x + 4 <= L.bsimd_end);
+
+    // row sums of the blur (exact integers as floats), last 7 rows
+    const BlurTaps tp = {(uint32_t)g->taps[0] | (uint32_t)g->taps[1] << 8 | (uint32_t)g->taps[2] << 16 |
+                             (uint32_t)g->taps[3] << 24,
+                         (uint32_t)g->taps[4] | (uint32_t)g->taps[5] << 8 | (uint32_t)g->taps[6] << 16,
+                         0u, 0u, 0u, (uint32_t)g->taps[3]};
+    const float inv = 1.0f / 65536.0f;
+    const float f3 = (float)g->taps[3] * inv, f4 = (float)g->taps[4] * inv,
+                f5 = (float)g->taps[5] * inv, f6 = (float)g->taps[6] * inv;
+
+    // loads of one step: mode 0 two dwords of the input row (+ the row address's low bits),
+    // mode 3 three dwords of each of the two source rows
+    uint32_t A[2][3], C[2][3];
+    // the strip's row table in registers (lane k: steps k and 64 + k; n <= STRIP_TH + 6 <= 128),
+    // read with v_readlane: no scalar loads (and their waits) inside the walk
+    static_assert(STRIP_TH + 6 <= 128, "row table in two registers");
+    const uint2 rtl = RT[min(lane, n - 1)], rth = RT[min(64 + lane, n - 1)];
+    auto row_info = [&](int i) {
+        const uint2 v = i < 64 ? rtl : rth;
+        return make_uint2((uint32_t)__builtin_amdgcn_readlane((int)v.x, i & 63),
+                          (uint32_t)__builtin_amdgcn_readlane((int)v.y, i & 63));
+    };
+    auto issue = [&](int slot, int i) {
+        const int ic = min(i, n - 1);
+        const uint2 ri = row_info(ic);
+        if (MODE == 0) {
+            // pointer arithmetic only (global loads, not flat: a flat load would also hold
+            // every later scalar wait)
+            const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;
+            const uint8_t* a = rowp + t0.x;
+            const uint32_t o = (uint32_t)(uintptr_t)a & 3u;
+            const uint32_t* ab = (const uint32_t*)(a - o);
+            const uint8_t* lastb = rowp + (W - 1);
+            const uint32_t* last = (const uint32_t*)(lastb - ((uint32_t)(uintptr_t)lastb & 3u));
+            A[slot][0] = ab[0];
+            A[slot][1] = *(ab + 1 <= last ? ab + 1 : last);
+            A[slot][2] = o;
+        } else {
+            const uint32_t* p0 = (const uint32_t*)(src + (size_t)(ri.x & 0xFFFFu) * spitch);
+            const uint32_t* p1 = (const uint32_t*)(src + (size_t)(ri.x >> 16) * spitch);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                A[slot][k] = p0[k];
+                C[slot][k] = p1[k];
+            }
+        }
+    };
+    auto mulhi24 = [](uint32_t a, uint32_t c) {
+        return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (c & 0xFFFFFFu)) >> 32);
+    };
+    // this lane's group of level l at step i, from load slot `slot`
+    auto level_group = [&](int slot, int i, auto simd_c) -> uint32_t {
+        if (MODE == 0)
+            return __builtin_amdgcn_perm(A[slot][1], A[slot][0], t0.z + A[slot][2] * 0x01010101u);
+        constexpr bool SIMD = decltype(simd_c)::value;
+        const uint2 ri = row_info(i);
+        const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
+        const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
+        const uint32_t wa0 = __builtin_amdgcn_alignbyte(A[slot][1], A[slot][0], o0);
+        const uint32_t wa1 = __builtin_amdgcn_alignbyte(A[slot][2], A[slot][1], o0);
+        const uint32_t wc0 = __builtin_amdgcn_alignbyte(C[slot][1], C[slot][0], o0);
+        const uint32_t wc1 = __builtin_amdgcn_alignbyte(C[slot][2], C[slot][1], o0);
+        const uint32_t sels[4] = {ps.x, ps.y, ps.z, ps.w};
+        const uint32_t als[4] = {al.x, al.y, al.z, al.w};
+        uint32_t out = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
+            const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
+            const us2 a2 = __builtin_bit_cast(us2, als[j]);
+            int h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), a2, 0u, false);
+            int h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), a2, 0u, false);
+            const int vs = (int)((mulhi24((uint32_t)h0 & ~0xFFu, bs0) +
+                                  mulhi24((uint32_t)h1 & ~0xFFu, bs1) + 2u) >> 2);
+            if (SIMD) {
+                out |= (uint32_t)vs << (8 * j);
+            } else {
+                h0 >>= 4;
+                h1 >>= 4;
+                const int vc = min((int)((__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22), 255);
+                out |= (uint32_t)(((t0.y >> (2 * j + 1)) & 1u) ? vs : vc) << (8 * j);
+            }
+        }
+        return out;
+    };
+    float4 R[7];
+    // Stores without branches (a branch per store would cost the walk its counted vmcnt
+    // waits): row r's group as one dword (the image's last, partial group spills into the
+    // row's >= 4 bytes of padding, pitch >= w + 4); lanes or steps with nothing to write
+    // store into the padding dword of the level's row 0.
+    uint8_t* const lev0 = pyr + (size_t)b * g->pyr_bytes + L.off;
+    uint8_t* const blr0 = blur + (size_t)b * g->pyr_bytes + L.off;
+    auto store_row = [&](uint8_t* base, int r, bool ok, uint32_t v) {
+        const bool w = ok && out_lane;
+        *(uint32_t*)(base + (size_t)(ok ? r : 0) * pitch + (w ? x : pitch - 4)) = v;
+    };
+    // step i (k = i mod 14: the load slot k & 1, the row-sum register k mod 7)
+    auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c) {
+        constexpr int k = decltype(k_c)::value;
+        constexpr bool BSIMD = decltype(bsimd_c)::value;
+        const uint32_t v = level_group(k & 1, i, rsimd_c);
+        issue(k & 1, i + STRIP_PF);
+        store_row(lev0, Y0 + i - 3, i >= 3 && i < vh + 3, v);
+        // row sums: the groups left and right of this lane's
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        float4 o;
+        o.x = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 1), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 1), tp.tapB, 0u, false), false);
+        o.y = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 2), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 2), tp.tapB, 0u, false), false);
+        o.z = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 3), tp.tapA,
+                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 3), tp.tapB, 0u, false), false);
+        o.w = (float)__builtin_amdgcn_udot4(v, tp.tapA, __builtin_amdgcn_udot4(d2, tp.tapB, 0u, false), false);
+        R[k % 7] = o;
+        {
+            // blurred row y - 3 from the row sums of steps i-6 .. i (every lane computes it;
+            // only output lanes of steps 6 .. n-1 store it)
+            auto r = [&](int t) -> const float4& { return R[(k - t + 14) % 7]; };
+            float S[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                auto c = [&](int t) { const float4& q = r(t); return j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w)); };
+                float a = (c(6) + c(0)) * f6;
+                a = __builtin_fmaf(c(5) + c(1), f5, a);
+                a = __builtin_fmaf(c(4) + c(2), f4, a);
+                S[j] = __builtin_fmaf(c(3), f3, a);
+            }
+            uint32_t packed = 0;
+            if (BSIMD) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) packed = __builtin_amdgcn_cvt_pk_u8_f32(S[j], j, packed);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t Si = (uint32_t)(S[j] * 65536.0f);
+                    const bool simd = x + j < L.bsimd_end;
+                    const uint32_t val = (Si + (simd ? 32767u + ((Si >> 16) & 1u) : 32768u)) >> 16;
+                    packed |= min(val, 255u) << (8 * j);
+                }
+            }
+            store_row(blr0, Y0 + i - 6, i >= 6 && i < n, packed);
+        }
+    };
+    auto walk = [&](auto rsimd_c, auto bsimd_c) {
+#pragma unroll
+        for (int i = 0; i < STRIP_PF; ++i) issue(i & 1, i);
+        // whole blocks of 14 steps (no per-step exits: steps past n load clamped rows and
+        // store nothing)
+        for (int i0 = 0; i0 < n; i0 += 14) {
+            static_assert(STRIP_PF <= 2, "two load slots");
+#define STRIP_STEP(K) step(std::integral_constant<int, K>{}, i0 + K, rsimd_c, bsimd_c);
+            STRIP_STEP(0) STRIP_STEP(1) STRIP_STEP(2) STRIP_STEP(3) STRIP_STEP(4) STRIP_STEP(5) STRIP_STEP(6)
+            STRIP_STEP(7) STRIP_STEP(8) STRIP_STEP(9) STRIP_STEP(10) STRIP_STEP(11) STRIP_STEP(12) STRIP_STEP(13)
+#undef STRIP_STEP
+        }
+    };
+    // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
+    if ((MODE == 0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
+    else walk(std::false_type{}, std::false_type{});
+}
+
 size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     (void)ltw;
     (void)lth;
@@ -748,10 +975,17 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
     for (int l = 0; l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
         hipEvent_t e = l == 0 ? T.start(st) : T.start_after(st);
-        auto kern = level_kernel(level_mode(L, l));
-        hipLaunchKernelGGL(kern, dim3(L.ntx * L.nty, a.batch), dim3(256), a.level_lds, st, a.dg,
-                           a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride, a.pyr,
-                           a.blur, l);
+        const int mode = level_mode(L, l);
+        if (L.strip) {
+            hipLaunchKernelGGL(mode == 0 ? k_level_strip<0> : k_level_strip<3>,
+                               dim3((L.snw * L.sns + 3) / 4, a.batch), dim3(256), 0, st, a.dg,
+                               a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
+                               a.pyr, a.blur, l);
+        } else {
+            hipLaunchKernelGGL(level_kernel(mode), dim3(L.ntx * L.nty, a.batch), dim3(256),
+                               a.level_lds, st, a.dg, a.ltab, a.d_imgs, a.d_imgs2, a.split,
+                               a.stride, a.batch_stride, a.pyr, a.blur, l);
+        }
         T.stop(K_LEVEL, e, st);
     }
     return hipGetLastError();
