@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "orbx_device.h"
 #include "orbx_internal.h"
@@ -51,6 +52,7 @@ __device__ __forceinline__ int reflect101_i(int p, int len) {
 __device__ __forceinline__ int sat8(int v) { return min(max(v, 0), 255); }
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 // min / max of reflect101(p) over p in [lo, hi].
 __device__ __forceinline__ void reflected_range(int lo, int hi, int len, int& mn, int& mx) {
@@ -726,8 +728,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 // the wave computes.  The arithmetic is item3's (resize, mode 3) and tile_out_rows_f /
 // tile_columns_f's (blur), bit for bit.
 #ifndef STRIP_PF
-#define STRIP_PF 2   // rows of source loads in flight ahead of the row being computed
+#define STRIP_PF 2   // mode 3: rows of source loads in flight ahead of the row being computed
 #endif
+#ifndef STRIP_BUFST
+#define STRIP_BUFST 1
+#endif
+#ifndef STRIP_DIAG
+#define STRIP_DIAG 0   // diagnostic builds only: 1 no stores (every store dropped)
+#endif
+#if STRIP_BUFST
+#define STRIP_LEV rlev
+#define STRIP_BLR rblr
+#else
+#define STRIP_LEV lev0
+#define STRIP_BLR blr0
+#endif
+#ifndef STRIP_PRO_STORES
+#define STRIP_PRO_STORES 1
+#endif
+#ifndef STRIP_NS0
+#define STRIP_NS0 7  // mode 0: load slots (1, 2 or 7)
+#endif
+#ifndef STRIP_PF0
+#define STRIP_PF0 6  // mode 0: rows in flight (<= STRIP_NS0)
+#endif
+template <typename F, int... K>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, K...>) {
+    (f(std::integral_constant<int, K>{}), ...);
+}
 #ifndef STRIP_WPE0
 #define STRIP_WPE0 6
 #endif
@@ -747,7 +775,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     xcd_block(bx, b);
     const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
     const LevelGeom& L = g->lv[level];
-    const int wv = bx * 4 + (threadIdx.x >> 6);   // wave of this image
+    // wave of this image; readfirstlane makes it (and the strip row, the row counters and the
+    // row addresses derived from it) scalar for the compiler, not per-lane VALU work
+    const int wv = bx * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (wv >= L.snw * L.sns) return;              // whole waves only
     const int swx = wv % L.snw, sy = wv / L.snw;
     const int hs = 2 * swx + half;
@@ -764,18 +794,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     const uint2* RT = (const uint2*)(ltab + L.srow) + Y0;   // step i <-> row y = Y0 - 3 + i
     const int n = vh + 6;
 
-    // source of this lane's bytes
-    const uint8_t* src;
+    // Addresses are a wave-uniform row base (SGPRs) + a lane offset that is constant over the
+    // walk, so loads and stores take the saddr forms and a step spends no VALU on 64-bit
+    // address arithmetic.
+    const uint8_t* src;   // mode 0: 4 bytes before the image (lane offsets stay unsigned)
     size_t spitch;
     if (MODE == 0) {
-        src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
+        src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride) - 4;
         spitch = stride;
     } else {
         const LevelGeom& S = g->lv[level - 1];
-        src = pyr + (size_t)b * g->pyr_bytes + S.off + (t0.x & ~3u);
+        src = pyr + (size_t)b * g->pyr_bytes + S.off;
         spitch = (size_t)S.pitch;
     }
-    const uint32_t o0 = t0.x & 3u;   // mode 3: first tap's byte offset in the aligned dword
+    const uint32_t o0 = t0.x & 3u;         // mode 3: first tap's byte offset in its dword
+    const uint32_t boff = t0.x & ~3u;      // mode 3: lane offset of the aligned dwords
+    const uint32_t xoff4 = t0.x + 4u;      // mode 0: lane offset of its first byte
 
     // per-wave forms: every needed lane SSE2 in the vertical resize / the blur's columns
     const bool lane_rsimd = ((t0.y >> 1) & 0x55u) == 0x55u;
@@ -791,53 +825,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     const float f3 = (float)g->taps[3] * inv, f4 = (float)g->taps[4] * inv,
                 f5 = (float)g->taps[5] * inv, f6 = (float)g->taps[6] * inv;
 
-    // loads of one step: mode 0 two dwords of the input row (+ the row address's low bits),
-    // mode 3 three dwords of each of the two source rows
-    uint32_t A[2][3], C[2][3];
     // the strip's row table in registers (lane k: steps k and 64 + k; n <= STRIP_TH + 6 <= 128),
     // read with v_readlane: no scalar loads (and their waits) inside the walk
     static_assert(STRIP_TH + 6 <= 128, "row table in two registers");
     const uint2 rtl = RT[min(lane, n - 1)], rth = RT[min(64 + lane, n - 1)];
     auto row_info = [&](int i) {
-        const uint2 v = i < 64 ? rtl : rth;
-        return make_uint2((uint32_t)__builtin_amdgcn_readlane((int)v.x, i & 63),
-                          (uint32_t)__builtin_amdgcn_readlane((int)v.y, i & 63));
+        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)rtl.x, i & 63);
+        const uint32_t hx = (uint32_t)__builtin_amdgcn_readlane((int)rth.x, i & 63);
+        const uint32_t ly = (uint32_t)__builtin_amdgcn_readlane((int)rtl.y, i & 63);
+        const uint32_t hy = (uint32_t)__builtin_amdgcn_readlane((int)rth.y, i & 63);
+        return i < 64 ? make_uint2(lx, ly) : make_uint2(hx, hy);
     };
+    // load slots (a ring of NS; step i consumes slot i mod NS, then refills it with row i+PF
+    // ... PF <= NS): mode 0 two dwords of the input row + the perm selector for the row's
+    // alignment, mode 3 three dwords of each of the two source rows + the row's betas
+    constexpr int NS = MODE == 0 ? STRIP_NS0 : 2;
+    constexpr int PF = MODE == 0 ? STRIP_PF0 : STRIP_PF;
+    static_assert(PF <= NS && (NS == 1 || NS == 2 || NS == 7), "slot ring");
+    uint32_t A[NS][3], C[NS][3], RB[NS];
     auto issue = [&](int slot, int i) {
         const int ic = min(i, n - 1);
         const uint2 ri = row_info(ic);
         if (MODE == 0) {
-            // pointer arithmetic only (global loads, not flat: a flat load would also hold
-            // every later scalar wait)
-            const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;
-            const uint8_t* a = rowp + t0.x;
-            const uint32_t o = (uint32_t)(uintptr_t)a & 3u;
-            const uint32_t* ab = (const uint32_t*)(a - o);
-            const uint8_t* lastb = rowp + (W - 1);
-            const uint32_t* last = (const uint32_t*)(lastb - ((uint32_t)(uintptr_t)lastb & 3u));
-            A[slot][0] = ab[0];
-            A[slot][1] = *(ab + 1 <= last ? ab + 1 : last);
-            A[slot][2] = o;
+            const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;   // row - 4
+            const uint32_t rlo = (uint32_t)(uintptr_t)rowp;
+            const uint32_t o = (rlo + xoff4) & 3u;
+            const uint32_t aoff = xoff4 - o;
+            // the last dword holding a byte of the row (no read past the image)
+            const uint32_t last = ((rlo + 4u + (uint32_t)(W - 1)) & ~3u) - rlo;
+            A[slot][0] = *(const uint32_t*)(rowp + aoff);
+            A[slot][1] = *(const uint32_t*)(rowp + min(aoff + 4u, last));
+            A[slot][2] = t0.z + o * 0x01010101u;
         } else {
-            const uint32_t* p0 = (const uint32_t*)(src + (size_t)(ri.x & 0xFFFFu) * spitch);
-            const uint32_t* p1 = (const uint32_t*)(src + (size_t)(ri.x >> 16) * spitch);
+            const uint8_t* ra = src + (size_t)(ri.x & 0xFFFFu) * spitch;
+            const uint8_t* rc = src + (size_t)(ri.x >> 16) * spitch;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                A[slot][k] = p0[k];
-                C[slot][k] = p1[k];
+                A[slot][k] = *(const uint32_t*)(ra + boff + 4 * k);
+                C[slot][k] = *(const uint32_t*)(rc + boff + 4 * k);
             }
+            RB[slot] = ri.y;
         }
     };
     auto mulhi24 = [](uint32_t a, uint32_t c) {
         return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (c & 0xFFFFFFu)) >> 32);
     };
-    // this lane's group of level l at step i, from load slot `slot`
-    auto level_group = [&](int slot, int i, auto simd_c) -> uint32_t {
-        if (MODE == 0)
-            return __builtin_amdgcn_perm(A[slot][1], A[slot][0], t0.z + A[slot][2] * 0x01010101u);
+    // this lane's group of level l from load slot `slot`
+    auto level_group = [&](int slot, auto simd_c) -> uint32_t {
+        if (MODE == 0) return __builtin_amdgcn_perm(A[slot][1], A[slot][0], A[slot][2]);
         constexpr bool SIMD = decltype(simd_c)::value;
-        const uint2 ri = row_info(i);
-        const int b0 = (int)(int16_t)(ri.y & 0xFFFF), b1 = (int)(int16_t)(ri.y >> 16);
+        const uint32_t rb = RB[slot];
+        const int b0 = (int)(int16_t)(rb & 0xFFFF), b1 = (int)(int16_t)(rb >> 16);
         const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
         const uint32_t wa0 = __builtin_amdgcn_alignbyte(A[slot][1], A[slot][0], o0);
         const uint32_t wa1 = __builtin_amdgcn_alignbyte(A[slot][2], A[slot][1], o0);
@@ -873,17 +911,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // store into the padding dword of the level's row 0.
     uint8_t* const lev0 = pyr + (size_t)b * g->pyr_bytes + L.off;
     uint8_t* const blr0 = blur + (size_t)b * g->pyr_bytes + L.off;
-    auto store_row = [&](uint8_t* base, int r, bool ok, uint32_t v) {
-        const bool w = ok && out_lane;
-        *(uint32_t*)(base + (size_t)(ok ? r : 0) * pitch + (w ? x : pitch - 4)) = v;
+#if STRIP_BUFST
+    // buffer stores: a lane or step with nothing to write gets an offset past num_records,
+    // which the hardware drops (no branch, no write)
+    const int nrec = pitch * H;
+    const __amdgpu_buffer_rsrc_t rlev = __builtin_amdgcn_make_buffer_rsrc(lev0, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc(blr0, 0, nrec, 0x00020000);
+    // the row's byte offset rides in soffset (scalar), the lane's column in voffset: in range
+    // or not whether or not the hardware adds soffset into its range check
+    const uint32_t lane_off = (out_lane && !(STRIP_DIAG & 1)) ? (uint32_t)x : 0x80000000u;
+    auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, int r, bool ok, uint32_t v) {
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, 0);
     };
-    // step i (k = i mod 14: the load slot k & 1, the row-sum register k mod 7)
+#else
+    const uint32_t pad_off = (uint32_t)(pitch - 4);
+    const uint32_t lane_off = out_lane ? (uint32_t)x : pad_off;
+    auto store_row = [&](uint8_t* base, int r, bool ok, uint32_t v) {
+        *(uint32_t*)(base + (size_t)(ok ? r : 0) * pitch + (ok ? lane_off : pad_off)) = v;
+    };
+#endif
+    // step i (k = i mod U: the load slot k mod NS, the row-sum register k mod 7)
     auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c) {
         constexpr int k = decltype(k_c)::value;
         constexpr bool BSIMD = decltype(bsimd_c)::value;
-        const uint32_t v = level_group(k & 1, i, rsimd_c);
-        issue(k & 1, i + STRIP_PF);
-        store_row(lev0, Y0 + i - 3, i >= 3 && i < vh + 3, v);
+        const uint32_t v = level_group(k % NS, rsimd_c);
+        issue((k + PF) % NS, i + PF);
+        store_row(STRIP_LEV, Y0 + i - 3, i >= 3 && i < vh + 3, v);
         // row sums: the groups left and right of this lane's
         const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
         const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
@@ -899,15 +952,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         {
             // blurred row y - 3 from the row sums of steps i-6 .. i (every lane computes it;
             // only output lanes of steps 6 .. n-1 store it)
+            // two pixels per packed-f32 op (v_pk_add / v_pk_mul / v_pk_fma: per element the
+            // same IEEE operations as the scalar form)
             auto r = [&](int t) -> const float4& { return R[(k - t + 14) % 7]; };
             float S[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                auto c = [&](int t) { const float4& q = r(t); return j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w)); };
-                float a = (c(6) + c(0)) * f6;
-                a = __builtin_fmaf(c(5) + c(1), f5, a);
-                a = __builtin_fmaf(c(4) + c(2), f4, a);
-                S[j] = __builtin_fmaf(c(3), f3, a);
+            for (int hp = 0; hp < 2; ++hp) {
+                auto c = [&](int t) {
+                    const float4& q = r(t);
+                    return hp == 0 ? f2v{q.x, q.y} : f2v{q.z, q.w};
+                };
+                const f2v F6 = {f6, f6}, F5 = {f5, f5}, F4 = {f4, f4}, F3 = {f3, f3};
+                f2v a = (c(6) + c(0)) * F6;
+                a = __builtin_elementwise_fma(c(5) + c(1), F5, a);
+                a = __builtin_elementwise_fma(c(4) + c(2), F4, a);
+                a = __builtin_elementwise_fma(c(3), F3, a);
+                S[2 * hp] = a.x;
+                S[2 * hp + 1] = a.y;
             }
             uint32_t packed = 0;
             if (BSIMD) {
@@ -922,21 +983,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
                     packed |= min(val, 255u) << (8 * j);
                 }
             }
-            store_row(blr0, Y0 + i - 6, i >= 6 && i < n, packed);
+            store_row(STRIP_BLR, Y0 + i - 6, i >= 6 && i < n, packed);
         }
     };
+    constexpr int U = NS == 2 ? 14 : 7;   // steps per block: a multiple of NS and of 7
     auto walk = [&](auto rsimd_c, auto bsimd_c) {
 #pragma unroll
-        for (int i = 0; i < STRIP_PF; ++i) issue(i & 1, i);
-        // whole blocks of 14 steps (no per-step exits: steps past n load clamped rows and
-        // store nothing)
-        for (int i0 = 0; i0 < n; i0 += 14) {
-            static_assert(STRIP_PF <= 2, "two load slots");
-#define STRIP_STEP(K) step(std::integral_constant<int, K>{}, i0 + K, rsimd_c, bsimd_c);
-            STRIP_STEP(0) STRIP_STEP(1) STRIP_STEP(2) STRIP_STEP(3) STRIP_STEP(4) STRIP_STEP(5) STRIP_STEP(6)
-            STRIP_STEP(7) STRIP_STEP(8) STRIP_STEP(9) STRIP_STEP(10) STRIP_STEP(11) STRIP_STEP(12) STRIP_STEP(13)
-#undef STRIP_STEP
+        for (int i = 0; i < PF; ++i) {
+            issue(i % NS, i);
+#if STRIP_PRO_STORES
+            // the same memory-op sequence as a block's last steps (two stores after each
+            // issue), so the loop header sees one pending-load state from both edges
+            store_row(STRIP_LEV, 0, false, 0u);
+            store_row(STRIP_BLR, 0, false, 0u);
+#endif
         }
+        // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
+        // store nothing)
+        for (int i0 = 0; i0 < n; i0 += U)
+            unroll_seq([&](auto k_c) { step(k_c, i0 + decltype(k_c)::value, rsimd_c, bsimd_c); },
+                       std::make_integer_sequence<int, U>{});
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
     if ((MODE == 0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});

@@ -12,7 +12,7 @@ def trace(path):
         n = short(r["Kernel_Name"])
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         key = n
-        if n == "k_level":
+        if n.startswith(("k_level", "void k_level")):
             key = f"k_level[grid={r.get('Grid_Size_X', r.get('Grid_Size', '?'))}]"
         per[key].append(d)
     print("== kernel trace (us per dispatch, mean) ==")

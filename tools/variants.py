@@ -23,6 +23,8 @@ def build(specs):
     from my_orb_slam2_amd import build as b
     out = {}
     procs = []
+    for old in b.PKG.glob("liborbx_*.so"):   # stale variants would travel with every gpurun
+        old.unlink()
     for spec in specs:
         name, _, defs = spec.partition("=")
         flags = [d for d in defs.split(",") if d]
