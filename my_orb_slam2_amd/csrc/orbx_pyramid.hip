@@ -746,6 +746,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_PRO_STORES
 #define STRIP_PRO_STORES 1
 #endif
+#ifndef STRIP_ROWDOT
+#define STRIP_ROWDOT 1   // row pass as 10 v_dot4 with shifted tap words (no v_alignbyte)
+#endif
+#ifndef STRIP_SROW
+#define STRIP_SROW 1     // row table entries by scalar loads (else v_readlane from registers)
+#endif
+#ifndef STRIP_SCHEDB
+#define STRIP_SCHEDB 1
+#endif
+#ifndef STRIP_UNALIGNED
+#define STRIP_UNALIGNED 0   // mode 3: one unaligned dwordx2 per source row (no v_alignbyte)
+#endif
+#ifndef STRIP_NS3
+#define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
+#endif
 #ifndef STRIP_NS0
 #define STRIP_NS0 7  // mode 0: load slots (1, 2 or 7)
 #endif
@@ -824,12 +839,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     const float inv = 1.0f / 65536.0f;
     const float f3 = (float)g->taps[3] * inv, f4 = (float)g->taps[4] * inv,
                 f5 = (float)g->taps[5] * inv, f6 = (float)g->taps[6] * inv;
+    // row-pass tap words for pixel j of the group over the dwords left / own / right (byte b
+    // of a dword is the pixel at its position b)
+    const uint32_t k0 = g->taps[0], k1 = g->taps[1], k2 = g->taps[2], k3 = g->taps[3],
+                   k4 = g->taps[4], k5 = g->taps[5], k6 = g->taps[6];
+    const uint32_t W00 = k0 << 8 | k1 << 16 | k2 << 24, W01 = k3 | k4 << 8 | k5 << 16 | k6 << 24;
+    const uint32_t W10 = k0 << 16 | k1 << 24, W11 = k2 | k3 << 8 | k4 << 16 | k5 << 24, W12 = k6;
+    const uint32_t W20 = k0 << 24, W21 = k1 | k2 << 8 | k3 << 16 | k4 << 24, W22 = k5 | k6 << 8;
+    (void)W00; (void)W01; (void)W10; (void)W11; (void)W12; (void)W20; (void)W21; (void)W22;
 
     // the strip's row table in registers (lane k: steps k and 64 + k; n <= STRIP_TH + 6 <= 128),
     // read with v_readlane: no scalar loads (and their waits) inside the walk
     static_assert(STRIP_TH + 6 <= 128, "row table in two registers");
     const uint2 rtl = RT[min(lane, n - 1)], rth = RT[min(64 + lane, n - 1)];
     auto row_info = [&](int i) {
+#if STRIP_SROW
+        return RT[i];   // wave-uniform address: a scalar load
+#endif
         const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)rtl.x, i & 63);
         const uint32_t hx = (uint32_t)__builtin_amdgcn_readlane((int)rth.x, i & 63);
         const uint32_t ly = (uint32_t)__builtin_amdgcn_readlane((int)rtl.y, i & 63);
@@ -839,9 +865,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // load slots (a ring of NS; step i consumes slot i mod NS, then refills it with row i+PF
     // ... PF <= NS): mode 0 two dwords of the input row + the perm selector for the row's
     // alignment, mode 3 three dwords of each of the two source rows + the row's betas
-    constexpr int NS = MODE == 0 ? STRIP_NS0 : 2;
+    constexpr int NS = MODE == 0 ? STRIP_NS0 : STRIP_NS3;
     constexpr int PF = MODE == 0 ? STRIP_PF0 : STRIP_PF;
-    static_assert(PF <= NS && (NS == 1 || NS == 2 || NS == 7), "slot ring");
+    static_assert(PF <= NS && (NS == 1 || NS == 2 || NS == 3 || NS == 7), "slot ring");
     uint32_t A[NS][3], C[NS][3], RB[NS];
     auto issue = [&](int slot, int i) {
         const int ic = min(i, n - 1);
@@ -859,11 +885,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         } else {
             const uint8_t* ra = src + (size_t)(ri.x & 0xFFFFu) * spitch;
             const uint8_t* rc = src + (size_t)(ri.x >> 16) * spitch;
+#if STRIP_UNALIGNED
+            // the 8 bytes from the first tap column, one unaligned dwordx2 per row
+            typedef uint32_t u2a __attribute__((ext_vector_type(2), aligned(1)));
+            const u2a va = *(const u2a*)(ra + t0.x), vc = *(const u2a*)(rc + t0.x);
+            A[slot][0] = va.x;
+            A[slot][1] = va.y;
+            C[slot][0] = vc.x;
+            C[slot][1] = vc.y;
+#else
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 A[slot][k] = *(const uint32_t*)(ra + boff + 4 * k);
                 C[slot][k] = *(const uint32_t*)(rc + boff + 4 * k);
             }
+#endif
             RB[slot] = ri.y;
         }
     };
@@ -877,10 +913,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         const uint32_t rb = RB[slot];
         const int b0 = (int)(int16_t)(rb & 0xFFFF), b1 = (int)(int16_t)(rb >> 16);
         const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
+#if STRIP_UNALIGNED
+        const uint32_t wa0 = A[slot][0], wa1 = A[slot][1], wc0 = C[slot][0], wc1 = C[slot][1];
+#else
         const uint32_t wa0 = __builtin_amdgcn_alignbyte(A[slot][1], A[slot][0], o0);
         const uint32_t wa1 = __builtin_amdgcn_alignbyte(A[slot][2], A[slot][1], o0);
         const uint32_t wc0 = __builtin_amdgcn_alignbyte(C[slot][1], C[slot][0], o0);
         const uint32_t wc1 = __builtin_amdgcn_alignbyte(C[slot][2], C[slot][1], o0);
+#endif
         const uint32_t sels[4] = {ps.x, ps.y, ps.z, ps.w};
         const uint32_t als[4] = {al.x, al.y, al.z, al.w};
         uint32_t out = 0;
@@ -934,6 +974,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c) {
         constexpr int k = decltype(k_c)::value;
         constexpr bool BSIMD = decltype(bsimd_c)::value;
+#if STRIP_SCHEDB
+        // keep each step's memory operations in its step: the scheduler would otherwise sink
+        // the prefetch loads toward their use (shorter live ranges), shortening the prefetch
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         const uint32_t v = level_group(k % NS, rsimd_c);
         issue((k + PF) % NS, i + PF);
         store_row(STRIP_LEV, Y0 + i - 3, i >= 3 && i < vh + 3, v);
@@ -941,6 +986,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
         const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
         float4 o;
+#if STRIP_ROWDOT
+        // taps shifted onto the three dwords (10 v_dot4, no v_alignbyte)
+        auto dot4 = [](uint32_t a, uint32_t w, uint32_t c) { return __builtin_amdgcn_udot4(a, w, c, false); };
+        o.x = (float)dot4(d0, W00, dot4(v, W01, 0u));
+        o.y = (float)dot4(d0, W10, dot4(v, W11, dot4(d2, W12, 0u)));
+        o.z = (float)dot4(d0, W20, dot4(v, W21, dot4(d2, W22, 0u)));
+        o.w = (float)dot4(v, tp.tapA, dot4(d2, tp.tapB, 0u));
+#else
         o.x = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 1), tp.tapA,
                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 1), tp.tapB, 0u, false), false);
         o.y = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 2), tp.tapA,
@@ -948,6 +1001,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         o.z = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 3), tp.tapA,
                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 3), tp.tapB, 0u, false), false);
         o.w = (float)__builtin_amdgcn_udot4(v, tp.tapA, __builtin_amdgcn_udot4(d2, tp.tapB, 0u, false), false);
+#endif
         R[k % 7] = o;
         {
             // blurred row y - 3 from the row sums of steps i-6 .. i (every lane computes it;
@@ -986,7 +1040,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
             store_row(STRIP_BLR, Y0 + i - 6, i >= 6 && i < n, packed);
         }
     };
-    constexpr int U = NS == 2 ? 14 : 7;   // steps per block: a multiple of NS and of 7
+    constexpr int U = NS == 7 ? 7 : 7 * NS;   // steps per block: a multiple of NS and of 7
     auto walk = [&](auto rsimd_c, auto bsimd_c) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
