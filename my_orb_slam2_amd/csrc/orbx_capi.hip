@@ -210,17 +210,18 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
                 }
             }
         }
-    std::vector<uint32_t> rt((size_t)2 * (lv.h + 6));
+    std::vector<uint32_t> rt((size_t)4 * (lv.h + 6));
     for (int k = 0; k < lv.h + 6; ++k) {
         const int yr = reflect101_h(k - 3, lv.h);
         if (mode == 0) {
-            rt[2 * k] = (uint32_t)yr;
+            rt[4 * k] = (uint32_t)yr;
         } else {
             const int sy = yofs[yr];
             const uint32_t r0 = (uint32_t)std::min(std::max(sy, 0), S.h - 1);
             const uint32_t r1 = (uint32_t)std::min(std::max(sy + 1, 0), S.h - 1);
-            rt[2 * k] = r0 | (r1 << 16);
-            rt[2 * k + 1] = (uint32_t)(uint16_t)beta[2 * yr] | ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16);
+            rt[4 * k] = r0 * (uint32_t)S.pitch;       // byte offsets of the two source rows
+            rt[4 * k + 1] = r1 * (uint32_t)S.pitch;
+            rt[4 * k + 2] = (uint32_t)(uint16_t)beta[2 * yr] | ((uint32_t)(uint16_t)beta[2 * yr + 1] << 16);
         }
     }
     h->ltab.resize(align_up(h->ltab.size(), 16));

@@ -102,8 +102,8 @@ struct LevelRowTab {
 //   mode 3 (INTER_LINEAR): base = smallest source tap column, psel = per-pixel v_perm selectors
 //     of the two taps relative to base, alp = 16 x alphas ((2048, 0) right of xmax), flags =
 //     2 bits per pixel (right tap in range, SSE2 vertical form).
-// Row table per level: rows y = -3 .. h + 2, (ry0 | ry1 << 16, beta0 | beta1 << 16) with ry
-// absolute source rows (mode 0: ry0 = the reflected input row).
+// Row table per level: rows y = -3 .. h + 2, 4 dwords each: mode 3 the byte offsets of the
+// two source rows in level l-1 and (beta0 | beta1 << 16); mode 0 the reflected input row.
 #ifndef STRIP_TH
 #define STRIP_TH 64   // output rows per strip (<= 122: the row table sits in two registers)
 #endif

@@ -749,9 +749,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_ROWDOT
 #define STRIP_ROWDOT 1   // row pass as 10 v_dot4 with shifted tap words (no v_alignbyte)
 #endif
-#ifndef STRIP_SROW
-#define STRIP_SROW 1     // row table entries by scalar loads (else v_readlane from registers)
-#endif
 #ifndef STRIP_SCHEDB
 #define STRIP_SCHEDB 1
 #endif
@@ -806,7 +803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     const uint4 t0 = *(const uint4*)T;
     const uint4 al = *(const uint4*)T->alp;
     const uint4 ps = *(const uint4*)T->psel;
-    const uint2* RT = (const uint2*)(ltab + L.srow) + Y0;   // step i <-> row y = Y0 - 3 + i
+    const uint4* RT = (const uint4*)(ltab + L.srow) + Y0;   // step i <-> row y = Y0 - 3 + i
     const int n = vh + 6;
 
     // Addresses are a wave-uniform row base (SGPRs) + a lane offset that is constant over the
@@ -848,20 +845,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     const uint32_t W20 = k0 << 24, W21 = k1 | k2 << 8 | k3 << 16 | k4 << 24, W22 = k5 | k6 << 8;
     (void)W00; (void)W01; (void)W10; (void)W11; (void)W12; (void)W20; (void)W21; (void)W22;
 
-    // the strip's row table in registers (lane k: steps k and 64 + k; n <= STRIP_TH + 6 <= 128),
-    // read with v_readlane: no scalar loads (and their waits) inside the walk
-    static_assert(STRIP_TH + 6 <= 128, "row table in two registers");
-    const uint2 rtl = RT[min(lane, n - 1)], rth = RT[min(64 + lane, n - 1)];
-    auto row_info = [&](int i) {
-#if STRIP_SROW
-        return RT[i];   // wave-uniform address: a scalar load
-#endif
-        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)rtl.x, i & 63);
-        const uint32_t hx = (uint32_t)__builtin_amdgcn_readlane((int)rth.x, i & 63);
-        const uint32_t ly = (uint32_t)__builtin_amdgcn_readlane((int)rtl.y, i & 63);
-        const uint32_t hy = (uint32_t)__builtin_amdgcn_readlane((int)rth.y, i & 63);
-        return i < 64 ? make_uint2(lx, ly) : make_uint2(hx, hy);
-    };
+    // the strip's row table entry of step i: a wave-uniform address, so a scalar load
+    auto row_info = [&](int i) { return RT[i]; };
     // load slots (a ring of NS; step i consumes slot i mod NS, then refills it with row i+PF
     // ... PF <= NS): mode 0 two dwords of the input row + the perm selector for the row's
     // alignment, mode 3 three dwords of each of the two source rows + the row's betas
@@ -871,7 +856,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     uint32_t A[NS][3], C[NS][3], RB[NS];
     auto issue = [&](int slot, int i) {
         const int ic = min(i, n - 1);
-        const uint2 ri = row_info(ic);
+        const uint4 ri = row_info(ic);
         if (MODE == 0) {
             const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;   // row - 4
             const uint32_t rlo = (uint32_t)(uintptr_t)rowp;
@@ -883,8 +868,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
             A[slot][1] = *(const uint32_t*)(rowp + min(aoff + 4u, last));
             A[slot][2] = t0.z + o * 0x01010101u;
         } else {
-            const uint8_t* ra = src + (size_t)(ri.x & 0xFFFFu) * spitch;
-            const uint8_t* rc = src + (size_t)(ri.x >> 16) * spitch;
+            const uint8_t* ra = src + ri.x;
+            const uint8_t* rc = src + ri.y;
 #if STRIP_UNALIGNED
             // the 8 bytes from the first tap column, one unaligned dwordx2 per row
             typedef uint32_t u2a __attribute__((ext_vector_type(2), aligned(1)));
@@ -900,7 +885,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
                 C[slot][k] = *(const uint32_t*)(rc + boff + 4 * k);
             }
 #endif
-            RB[slot] = ri.y;
+            RB[slot] = ri.z;
         }
     };
     auto mulhi24 = [](uint32_t a, uint32_t c) {
