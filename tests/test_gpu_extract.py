@@ -128,6 +128,35 @@ def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
         assert nvh[i] == n_o
 
 
+def test_strided_unaligned_views(oracle_mod, orbx_lib, gpu):
+    """Input rows at an odd stride (1249 B) from a base 3 bytes past an aligned address: every
+    row of level 0 starts at a different alignment, which the level-0 strip walk folds into its
+    per-row byte selection."""
+    import torch
+    import my_orb_slam2_amd as m
+    B, W, H, pad = 3, 1241, 376, 8
+    pairs = [synth.stereo_pair(200 + i) for i in range(B)]
+    bigL = torch.zeros((B, H, W + pad), dtype=torch.uint8)
+    bigR = torch.zeros((B, H, W + pad), dtype=torch.uint8)
+    for i, (l, r) in enumerate(pairs):
+        bigL[i, :, 3:3 + W] = torch.from_numpy(l)
+        bigR[i, :, 3:3 + W] = torch.from_numpy(r)
+    Ls, Rs = bigL.to(gpu)[:, :, 3:3 + W], bigR.to(gpu)[:, :, 3:3 + W]
+    assert Ls.stride(1) == W + pad and Ls.storage_offset() == 3
+    sb = m.StereoBatch(B, 2000)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    sb(Ls, Rs, KITTI_MBF, mb)
+    torch.cuda.synchronize()
+    nkp, kps, desc = sb.fetch("left")
+    nkpr, kpsr, descr = sb.fetch("right")
+    for i in range(B):
+        for side, (n, k, d) in (("left", (nkp, kps, desc)), ("right", (nkpr, kpsr, descr))):
+            o = oracle_mod.OracleExtractor(2000, 1.2, 8, 20, 7)
+            k_o, d_o = o(pairs[i][0 if side == "left" else 1])
+            assert_kps_equal(k[i, :n[i]], k_o, f"strided item {i} {side}")
+            assert_bytes_equal(d[i, :n[i]], d_o, f"strided item {i} {side} desc")
+
+
 @pytest.mark.parametrize("simd", [0, 1])
 def test_blurred_levels_bitwise(oracle_mod, orbx_lib, gpu, simd):
     """Every blurred level vs GaussianBlur(7x7, sigma 2) restated on the same level, including
