@@ -752,8 +752,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_SCHEDB
 #define STRIP_SCHEDB 1
 #endif
-#ifndef STRIP_UNALIGNED
-#define STRIP_UNALIGNED 0   // mode 3: one unaligned dwordx2 per source row (no v_alignbyte)
+#ifndef STRIP_HREUSE
+#define STRIP_HREUSE 1   // mode 3: reuse the previous step's HResize of a shared source row
 #endif
 #ifndef STRIP_NS3
 #define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
@@ -854,6 +854,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     constexpr int PF = MODE == 0 ? STRIP_PF0 : STRIP_PF;
     static_assert(PF <= NS && (NS == 1 || NS == 2 || NS == 3 || NS == 7), "slot ring");
     uint32_t A[NS][3], C[NS][3], RB[NS];
+    // mode 3: the source rows' byte offsets of each slot, and the last step's horizontal sums
+    // of its second source row (HResize of a row is the same for every output row that
+    // reads it: 4 of 5 steps at scale 1.2 take the previous step's second row as their first)
+    uint32_t RAo[NS], RCo[NS], HCp[4] = {0u, 0u, 0u, 0u};
+    uint32_t prevRC = 0xFFFFFFFFu;
     auto issue = [&](int slot, int i) {
         const int ic = min(i, n - 1);
         const uint4 ri = row_info(ic);
@@ -870,22 +875,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         } else {
             const uint8_t* ra = src + ri.x;
             const uint8_t* rc = src + ri.y;
-#if STRIP_UNALIGNED
-            // the 8 bytes from the first tap column, one unaligned dwordx2 per row
-            typedef uint32_t u2a __attribute__((ext_vector_type(2), aligned(1)));
-            const u2a va = *(const u2a*)(ra + t0.x), vc = *(const u2a*)(rc + t0.x);
-            A[slot][0] = va.x;
-            A[slot][1] = va.y;
-            C[slot][0] = vc.x;
-            C[slot][1] = vc.y;
-#else
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 A[slot][k] = *(const uint32_t*)(ra + boff + 4 * k);
                 C[slot][k] = *(const uint32_t*)(rc + boff + 4 * k);
             }
-#endif
             RB[slot] = ri.z;
+            RAo[slot] = ri.x;
+            RCo[slot] = ri.y;
         }
     };
     auto mulhi24 = [](uint32_t a, uint32_t c) {
@@ -898,24 +895,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         const uint32_t rb = RB[slot];
         const int b0 = (int)(int16_t)(rb & 0xFFFF), b1 = (int)(int16_t)(rb >> 16);
         const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
-#if STRIP_UNALIGNED
-        const uint32_t wa0 = A[slot][0], wa1 = A[slot][1], wc0 = C[slot][0], wc1 = C[slot][1];
-#else
-        const uint32_t wa0 = __builtin_amdgcn_alignbyte(A[slot][1], A[slot][0], o0);
-        const uint32_t wa1 = __builtin_amdgcn_alignbyte(A[slot][2], A[slot][1], o0);
-        const uint32_t wc0 = __builtin_amdgcn_alignbyte(C[slot][1], C[slot][0], o0);
-        const uint32_t wc1 = __builtin_amdgcn_alignbyte(C[slot][2], C[slot][1], o0);
-#endif
         const uint32_t sels[4] = {ps.x, ps.y, ps.z, ps.w};
         const uint32_t als[4] = {al.x, al.y, al.z, al.w};
+        // HResizeLinear of one source row (3 aligned dwords) for this lane's 4 pixels
+        auto hrow = [&](const uint32_t* D, uint32_t* hs) {
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(D[1], D[0], o0);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(D[2], D[1], o0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                hs[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(w1, w0, sels[j])),
+                                               __builtin_bit_cast(us2, als[j]), 0u, false);
+        };
+        uint32_t hA[4], hC[4];
+        if (STRIP_HREUSE && RAo[slot] == prevRC) {   // wave-uniform
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hA[j] = HCp[j];
+        } else {
+            hrow(A[slot], hA);
+        }
+        hrow(C[slot], hC);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) HCp[j] = hC[j];
+        prevRC = RCo[slot];
         uint32_t out = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t p0 = __builtin_amdgcn_perm(wa1, wa0, sels[j]);
-            const uint32_t p1 = __builtin_amdgcn_perm(wc1, wc0, sels[j]);
-            const us2 a2 = __builtin_bit_cast(us2, als[j]);
-            int h0 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), a2, 0u, false);
-            int h1 = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), a2, 0u, false);
+            int h0 = (int)hA[j];
+            int h1 = (int)hC[j];
             const int vs = (int)((mulhi24((uint32_t)h0 & ~0xFFu, bs0) +
                                   mulhi24((uint32_t)h1 & ~0xFFu, bs1) + 2u) >> 2);
             if (SIMD) {
