@@ -871,7 +871,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
             const uint32_t last = ((rlo + 4u + (uint32_t)(W - 1)) & ~3u) - rlo;
             A[slot][0] = *(const uint32_t*)(rowp + aoff);
             A[slot][1] = *(const uint32_t*)(rowp + min(aoff + 4u, last));
-            A[slot][2] = t0.z + o * 0x01010101u;
+            // t0.z + o in every byte (no carries: bytes <= 4 + 3): o replicated by one v_perm
+            A[slot][2] = t0.z + __builtin_amdgcn_perm(0u, o, 0u);
         } else {
             const uint8_t* ra = src + ri.x;
             const uint8_t* rc = src + ri.y;
@@ -974,8 +975,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         issue((k + PF) % NS, i + PF);
         store_row(STRIP_LEV, Y0 + i - 3, i >= 3 && i < vh + 3, v);
         // row sums: the groups left and right of this lane's
-        const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
-        const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);  // wave_shr:1 (bound_ctrl: lane 0 reads 0)
+        const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);  // wave_shl:1
         float4 o;
 #if STRIP_ROWDOT
         // taps shifted onto the three dwords (10 v_dot4, no v_alignbyte)
