@@ -1289,10 +1289,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     }
 
     // ---- 2. angle, cos / sin (src/ORBextractor.cc:103, 113) and the keypoint record ----
+#if OD_DIAG == 3   // diagnostic builds only: no angle / sincos work
+    const float angle = (float)(mk01 ^ mk10), ca_l = angle, sb_l = -angle;
+#else
     const float angle = cv_fast_atan2((float)mk01, (float)mk10);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float ca_l = glibc_cosf(ang), sb_l = glibc_sinf(ang);
+#endif
     if (lane < nk) {
         const size_t o = (size_t)b * g->kp_cap + off + i0 + lane;
         const int x = cand_x(cw) + ORBX_MIN_BORDER, y = cand_y(cw) + ORBX_MIN_BORDER;
