@@ -309,9 +309,12 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                     cand += c.cap;
                     lcap += c.cap;
                     // k_fast stages the ROI as aligned dwords: <= cols + 6 bytes per row
-                    G.max_roi_bytes = std::max(G.max_roi_bytes,
-                                               (int)c.rows * std::max((c.cols + 6 + 3) / 4,
-                                                                      fast_lpitch((3 + c.cols + 3) / 4, dw)) * 4);
+                    {
+                        const int lpc = std::max((c.cols + 6 + 3) / 4, fast_lpitch((3 + c.cols + 3) / 4, dw));
+                        // FAST_PFU: a prefetched ROI writes all 4 * FAST_PF2D rows
+                        const int rows_w = (FAST_PFU && FAST_STAGE2D) ? std::max((int)c.rows, 4 * FAST_PF2D) : (int)c.rows;
+                        G.max_roi_bytes = std::max(G.max_roi_bytes, rows_w * lpc * 4);
+                    }
                     if (dh > 0 && dw > 0) {
                         G.max_mbuf_bytes = std::max(G.max_mbuf_bytes, ((dh + 2) * (dw + 2) + 3) & ~3);
                         G.max_cell_px = std::max(G.max_cell_px, dh * dw);
@@ -618,7 +621,9 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     if (batch > h->cap_batch) {
         const Geometry& G = h->hg;
         const size_t B = (size_t)batch;
-        bool ok = h->d_pyr.ensure(B * G.pyr_bytes) && h->d_blur.ensure(B * G.pyr_bytes) &&
+        // k_fast (FAST_PFU) reads up to 4 * FAST_PF2D rows past a cell's ROI
+        const size_t pyr_slack = (size_t)4 * FAST_PF2D * G.lv[0].pitch + 256;
+        bool ok = h->d_pyr.ensure(B * G.pyr_bytes + pyr_slack) && h->d_blur.ensure(B * G.pyr_bytes) &&
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
                   h->d_cand.ensure(B * G.cand_words * 4) &&
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&

@@ -140,12 +140,6 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_LIST
 #define FAST_LIST 512    // compass survivors listed per row block (a multiple of 256)
 #endif
-#ifndef FAST_STAGE2D
-#define FAST_STAGE2D 1   // ROI prefetch on a 16-lanes-per-row grid (no index divisions)
-#endif
-#ifndef FAST_PF2D
-#define FAST_PF2D 10     // its rows per lane: ROIs up to 40 rows are prefetched
-#endif
 #ifndef FAST_NC
 #define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
 #endif
@@ -379,12 +373,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
         if (ndw > 16 || c.rows > 4 * FAST_PF2D || c.rows <= 6 || c.cols <= 6) return false;
         const LevelGeom& L = g->lv[c.level];
+#if FAST_PFU
+        // every lane reads its 10 rows unclamped (rows past the ROI land in the LDS buffer's
+        // spare rows; the pyramid buffer has FAST_PF2D * 4 rows of slack after the last
+        // image): a wave-uniform row base per load plus one lane offset, no per-load VALU
+        const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3);
+        const uint32_t lane_off = __umul24((uint32_t)lr2, (uint32_t)L.pitch) + 4u * (uint32_t)min(lc2, ndw - 1);
+#pragma unroll
+        for (int j = 0; j < FAST_PF2D; ++j)
+            pf[j] = *(const uint32_t*)(src + (size_t)(4 * j) * L.pitch + lane_off);
+#else
         const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3) +
                              4 * min(lc2, ndw - 1);
         const uint32_t gp = (uint32_t)L.pitch;
 #pragma unroll
         for (int j = 0; j < FAST_PF2D; ++j)
             pf[j] = *(const uint32_t*)(src + __umul24((uint32_t)min(lr2 + 4 * j, c.rows - 1), gp));
+#endif
         return true;
     };
 #else
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                     uint32_t* l = (uint32_t*)roi0 + lr2 * lp + lc2;
 #pragma unroll
                     for (int j = 0; j < FAST_PF2D; ++j)
-                        if (lr2 + 4 * j < rows) l[4 * j * lp] = pf[j];
+                        if (FAST_PFU || lr2 + 4 * j < rows) l[4 * j * lp] = pf[j];
                 }
             } else
 #endif

@@ -151,6 +151,15 @@ struct Geometry {
 // compass's b128 reads) with room for the widest lane's reads (16 pixels per lane, 2 lanes
 // per detection row up to 32 columns, else 4).  A bank-conflict-free pitch (24 / 48 dwords)
 // was measured slower: the larger ROI costs a workgroup per CU.
+#ifndef FAST_STAGE2D
+#define FAST_STAGE2D 1   // k_fast ROI prefetch on a 16-lanes-per-row grid (no index divisions)
+#endif
+#ifndef FAST_PF2D
+#define FAST_PF2D 10     // its rows per lane: ROIs up to 40 rows are prefetched
+#endif
+#ifndef FAST_PFU
+#define FAST_PFU 1       // prefetch all 4 * FAST_PF2D rows unclamped (LDS and pyramid slack)
+#endif
 #ifndef FAST_W16
 #define FAST_W16 1
 #endif
