@@ -116,11 +116,16 @@ struct StripLane {
     uint32_t psel[4];
 };
 
-struct CellDesc {
+// 32 bytes, 16-byte aligned: a wave-uniform cells[i] is two scalar dwordx4 loads (a 20-byte
+// record had one field fetched by a vector load, whose vmcnt(0) wait also drained the wave's
+// in-flight ROI prefetch and stores)
+struct alignas(16) CellDesc {
     int16_t level, ini_x, ini_y, cols, rows, pad;
     int32_t slot;           // u32 offset of this cell's candidate slot (per image block)
     int32_t cap;            // slot capacity
+    int32_t pad2[3];
 };
+static_assert(sizeof(CellDesc) == 32, "CellDesc layout");
 
 struct Geometry {
     int width, height, nlevels;
