@@ -146,6 +146,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_PF
 #define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
+#ifndef FAST_XCD
+#define FAST_XCD 0   // XCD block order for k_fast: measured slower (1.445-1.456 vs 1.434-1.439 ms)
+#endif
 #ifndef FAST_CMPONLY
 #define FAST_CMPONLY 0
 #endif
@@ -339,8 +342,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                                               uint32_t* __restrict__ cand) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // linear block order (measured: the XCD remap does not help k_fast)
+#if FAST_XCD
+    // XCD block order: an XCD walks a contiguous range of (image, cell block), so the ROI
+    // borders shared with the neighbouring cells (left / right and the next cell row) hit its L2
+    int bx, b;
+    xcd_block(bx, b);
+#else
     const int bx = blockIdx.x, b = blockIdx.y;
+#endif
     // one wave owns FAST_NC consecutive cells; no block-level barriers: waves are independent
     const int c_first = __builtin_amdgcn_readfirstlane((bx * 4 + wid) * FAST_NC);
     if (c_first >= g->n_cells) return;
@@ -474,7 +483,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         }
         const uint8_t* roi = roi0 + xo;
         const int mw = dw + 2;
-        for (int i = lane; i < ((dh + 2) * mw + 3) >> 2; i += 64) ((uint32_t*)mb)[i] = 0u;
+        // zero the score map 16 bytes per lane (mb is 16-byte aligned, mb_cap a multiple of 16)
+        for (int i = lane; i < ((dh + 2) * mw + 15) >> 4; i += 64) ((uint4*)mb)[i] = make_uint4(0u, 0u, 0u, 0u);
         lds_order();
         const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
         const int rpp = 64 >> gsh;
