@@ -251,11 +251,10 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     G.min_th = std::min(std::max(h->prm.min_th_fast, 0), 255);
     memcpy(G.taps, h->taps, sizeof(G.taps));
     memcpy(G.umax, h->umax, sizeof(G.umax));
-    G.stereo_win = (int)std::ceil(2.0f * h->scale[L - 1]) + 2;
-    // a left keypoint of level l only takes right keypoints of octaves l-1 .. l+1
-    // (src/Frame.cc:561-563), whose row bands (:522-530) reach at most 2 scale[l+1] rows
+    // k_stereo buckets right keypoints by (octave, row); a keypoint of octave o lists itself
+    // in the rows of its band [floor(y - 2 scale[o]), ceil(y + 2 scale[o])] (src/Frame.cc:522-530)
     for (int l = 0; l < L; ++l)
-        G.lv[l].stereo_win = (int)std::ceil(2.0f * h->scale[std::min(l + 1, L - 1)]) + 2;
+        G.lv[l].stereo_win = (int)std::ceil(2.0f * h->scale[l]) + 2;
     long long off = 0, cand = 0;
     int out = 0, blur_tiles = 0, oblocks = 0;
     for (int l = 0; l < L; ++l) {
@@ -585,7 +584,12 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         h->octree_lds1 = h->octree_lds;
     }
 #endif
-    h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h);
+    G.stereo_ob = G.nlevels;
+    h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h, G.stereo_ob);
+    if (h->stereo_lds > 160 * 1024) {   // row buckets only (octaves tested per candidate)
+        G.stereo_ob = 1;
+        h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h, G.stereo_ob);
+    }
     if (h->octree_lds > 160 * 1024 || h->stereo_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     if (G.kp_cap > 32767) return ORBX_ERR_UNSUPPORTED;   // 16-bit keypoint indices in stereo
     return ORBX_OK;

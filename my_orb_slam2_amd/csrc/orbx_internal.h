@@ -42,7 +42,7 @@ struct LevelGeom {
     int patch_size;         // (int)(31*scale)
     int ntx, nty;           // k_level tiles of this level
     int ctab, rowtab;       // k_level: byte offsets of the level's column / row tables
-    int stereo_win;         // k_stereo: row-bucket half-window for a left keypoint of this level
+    int stereo_win;         // k_stereo: row half-window of the octave-l buckets (ceil(2 scale) + 2)
     // k_level_strip (orbx_pyramid.hip): column strips walked row by row
     int strip;              // 1: this level runs k_level_strip, 0: the tiled k_level
     int snh;                // half-wave strips across (SW_PX output pixels each)
@@ -146,7 +146,7 @@ struct Geometry {
     int taps[7];            // cvRound(getGaussianKernel(7, 2, CV_32F) * 256)
     int umax[16];           // src/ORBextractor.cc:454-469
     int ini_th, min_th;     // FAST thresholds, clamped to [0, 255]
-    int stereo_win;         // row-bucket search half-window: ceil(2*max scale) + 2
+    int stereo_ob;          // k_stereo bucket groups: nlevels (octave, row), or 1 (row) if LDS is short
     int ltw, lth;           // k_level output tile
     int win_cap;            // k_level: largest staged source window (bytes)
     LevelGeom lv[ORBX_MAX_LEVELS];

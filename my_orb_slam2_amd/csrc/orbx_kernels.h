@@ -125,6 +125,6 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap);
 size_t fast_lds_bytes(const Geometry& g);
 size_t octree_lds_bytes(int ncap, int kcap);
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st);
-size_t stereo_lds_bytes(int kp_cap, int height);
+size_t stereo_lds_bytes(int kp_cap, int height, int ob);  // ob: octave bucket groups
 
 }  // namespace orbx

@@ -1,10 +1,11 @@
 // orbx_stereo.hip — Frame::ComputeStereoMatches (src/Frame.cc:496-686) as one gfx950
-// workgroup (512 threads) per stereo pair, batched over pairs.
+// workgroup (1024 threads) per stereo pair, batched over pairs.
 //
-//   1. right keypoints bucketed by image row (LDS counting sort) and their descriptors staged
-//      in LDS; the reference's vRowIndices lists are recovered exactly by testing each
-//      bucketed keypoint's [floor(y-2s), ceil(y+2s)] band, and its "first candidate wins"
-//      rule becomes a lexicographic (distance, right index) minimum, so bucket order is free;
+//   1. right keypoints bucketed by (octave, image row) (LDS counting sort) and their
+//      descriptors staged in LDS; the reference's vRowIndices lists are recovered exactly by
+//      testing each bucketed keypoint's [floor(y-2s), ceil(y+2s)] band over the rows of the
+//      three octaves a left keypoint may match, and its "first candidate wins" rule becomes a
+//      lexicographic (distance, right index) minimum, so bucket order is free;
 //   2. one lane per left keypoint: band / octave / disparity-range filters + 256-bit Hamming
 //      from LDS (v_xor + v_bcnt); if the best distance is < 75 the same lane runs the 11x11
 //      SAD at 11 shifts on the unblurred pyramids (rows read as aligned dwords, realigned
@@ -20,7 +21,9 @@
 
 namespace orbx {
 
+#ifndef ST_THREADS
 #define ST_THREADS 1024
+#endif
 #define ST_WAVES (ST_THREADS / 64)
 
 // N bytes of a pyramid row starting at x, as ceil(N/4) dwords realigned to x (bytes of
@@ -60,10 +63,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     uint8_t* p = smem;
     auto take = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
     int* tmp = (int*)take(32 * 4);
-    uint4* rdesc = (uint4*)take((size_t)KC * 32);   // in row-bucket order
-    int* rowstart = (int*)take((size_t)(H + 1) * 4);
-    int* cursor = (int*)take((size_t)(H + 1) * 4);
-    // per right keypoint, in row-bucket order: (uR bits, rmin | rmax << 16, oct | iR << 16)
+    // (octave, row) buckets, or row buckets alone (stereo_ob = 1) when the octave buckets
+    // would not fit in LDS beside the descriptors
+    const int OB = g->stereo_ob, NB = OB * H;
+    uint4* rdesc = (uint4*)take((size_t)KC * 32);   // in bucket order
+    // bucket k: counts, then (scan) its start, then (fill) its end = the start of bucket k+1
+    int* bend = (int*)take((size_t)NB * 4);
+    // per right keypoint, in bucket order: (uR bits, rmin | rmax << 16, oct | iR << 16)
     uint3* rrec = (uint3*)take((size_t)KC * 12);
     int* vsad = (int*)take((size_t)KC * 4);
     int16_t* vidx = (int16_t*)take((size_t)KC * 2);
@@ -74,25 +80,29 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     const float* kR = kpsR + (size_t)b * KC * 7;
     float* uR = uRight + (size_t)b * KC;
     float* dep = depth + (size_t)b * KC;
-    for (int i = tid; i <= H; i += ST_THREADS) rowstart[i] = 0;
+    for (int i = tid; i < NB; i += ST_THREADS) bend[i] = 0;
     if (tid == 0) tmp[16] = 0;
     __syncthreads();
 
-    // 1. right keypoints -> rows (src/Frame.cc:516-531): counts, a scan, then each keypoint's
-    //    record and descriptor written at its bucket position
-    for (int iR = tid; iR < NR; iR += ST_THREADS) {
-        const float ky = kR[iR * 7 + 1];
-        atomicAdd(&rowstart[min(max((int)ky, 0), H - 1)], 1);
-    }
+    // 1. right keypoints -> (octave, row) buckets (src/Frame.cc:516-531): counts, a scan, then
+    //    each keypoint's record and descriptor written at its bucket position.  A left
+    //    keypoint of level l only matches octaves l-1 .. l+1 (:561-563), and a right keypoint
+    //    of octave o lists itself in the rows within 2*scale[o] of its own (:522-530), so the
+    //    search reads three bucket windows instead of every octave's keypoints in its rows
+    auto rkey = [&](int iR) {
+        const int o = OB == 1 ? 0 : min(max(((const int*)kR)[iR * 7 + 5], 0), g->nlevels - 1);
+        return o * H + min(max((int)kR[iR * 7 + 1], 0), H - 1);
+    };
+    for (int iR = tid; iR < NR; iR += ST_THREADS) atomicAdd(&bend[rkey(iR)], 1);
     __syncthreads();
     {
         int carry = 0;
-        for (int c0 = 0; c0 < H + 1; c0 += ST_THREADS) {
+        for (int c0 = 0; c0 < NB; c0 += ST_THREADS) {
             const int i = c0 + tid;
-            const int v = i < H + 1 ? rowstart[i] : 0;
+            const int v = i < NB ? bend[i] : 0;
             int tot;
             const int ex = block_excl_scan<ST_WAVES>(v, tmp, tot);
-            if (i < H + 1) { rowstart[i] = carry + ex; cursor[i] = carry + ex; }
+            if (i < NB) bend[i] = carry + ex;
             carry += tot;
         }
     }
@@ -105,7 +115,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             const int oct = ((const int*)kR)[iR * 7 + 5];
             const float r = 2.0f * g->lv[oct].scale;
             const int mx = (int)ceilf(ky + r), mn = (int)floorf(ky - r);
-            const int pos = atomicAdd(&cursor[min(max((int)ky, 0), H - 1)], 1);
+            const int pos = atomicAdd(&bend[rkey(iR)], 1);
             rrec[pos] = make_uint3(__float_as_uint(kx),
                                    (uint32_t)(uint16_t)mn | ((uint32_t)(uint16_t)mx << 16),
                                    (uint32_t)oct | ((uint32_t)iR << 16));
@@ -118,6 +128,9 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     // 2. per left keypoint: descriptor search (src/Frame.cc:542-587) + SAD (:591-667)
     const float maxD = mbf / mb;   // minZ = mb, maxD = mbf/minZ (Frame.cc:534-536)
     const float minD = 0;
+#if ST_DIAG >= 3   // diagnostic builds only: phase 1 alone
+    if (NL >= 0) return;
+#endif
     for (int iL = tid; iL < NL; iL += ST_THREADS) {
         uR[iL] = -1.0f;
         dep[iL] = -1.0f;
@@ -133,28 +146,38 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             dl1 = q[1];
         }
         int best = 100, bestR = -1;   // ORBmatcher::TH_HIGH, strict '<': first minimum wins
-        // right keypoints of octaves levelL-1 .. levelL+1 sit within the level's window of rows
-        const int win = g->lv[levelL].stereo_win;
-        const int r0 = max(row - win, 0), r1 = min(row + win, H - 1);
-        const int e1 = rowstart[r1 + 1];
         int bestE = -1;
-        for (int e = rowstart[r0]; e < e1; ++e) {
-            const uint3 rc = rrec[e];
-            const int mn = (int)(int16_t)(rc.y & 0xFFFF), mx = (int)(int16_t)(rc.y >> 16);
-            if (mn > row || mx < row) continue;
-            const int o = (int)(rc.z & 0xFFFF);
-            if (o < levelL - 1 || o > levelL + 1) continue;
-            const float u = __uint_as_float(rc.x);
-            if (u >= minU && u <= maxU) {
-                const int iR = (int)(rc.z >> 16);
-                const uint4 a = rdesc[2 * e], c = rdesc[2 * e + 1];
-                const int dist = __popc(dl0.x ^ a.x) + __popc(dl0.y ^ a.y) + __popc(dl0.z ^ a.z) +
-                                 __popc(dl0.w ^ a.w) + __popc(dl1.x ^ c.x) + __popc(dl1.y ^ c.y) +
-                                 __popc(dl1.z ^ c.z) + __popc(dl1.w ^ c.w);
-                if (dist < best || (dist == best && bestR >= 0 && iR < bestR)) {
-                    best = dist;
-                    bestR = iR;
-                    bestE = e;
+#if ST_DIAG >= 2   // diagnostic builds only: no descriptor search (and so no SAD)
+        if (row >= 0) continue;
+#endif
+        // octaves levelL-1 .. levelL+1: a right keypoint of octave o whose band
+        // [floor(y - 2s), ceil(y + 2s)] holds `row` has int(y) within ceil(2s) + 1 rows of it
+        // (one group of every octave when OB = 1: the window of the largest scale, octaves
+        // tested per candidate)
+        const int o0 = max(levelL - 1, 0), o1 = min(levelL + 1, g->nlevels - 1);
+        for (int o = OB == 1 ? 0 : o0; o <= (OB == 1 ? 0 : o1); ++o) {
+            const int win = g->lv[OB == 1 ? o1 : o].stereo_win;
+            const int r0 = max(row - win, 0), r1 = min(row + win, H - 1);
+            const int k0 = o * H + r0;
+            const int e1 = bend[o * H + r1];
+            for (int e = k0 > 0 ? bend[k0 - 1] : 0; e < e1; ++e) {
+                const uint3 rc = rrec[e];
+                const int mn = (int)(int16_t)(rc.y & 0xFFFF), mx = (int)(int16_t)(rc.y >> 16);
+                if (mn > row || mx < row) continue;
+                const int oc = (int)(rc.z & 0xFFFF);
+                if (oc < levelL - 1 || oc > levelL + 1) continue;
+                const float u = __uint_as_float(rc.x);
+                if (u >= minU && u <= maxU) {
+                    const int iR = (int)(rc.z >> 16);
+                    const uint4 a = rdesc[2 * e], c = rdesc[2 * e + 1];
+                    const int dist = __popc(dl0.x ^ a.x) + __popc(dl0.y ^ a.y) + __popc(dl0.z ^ a.z) +
+                                     __popc(dl0.w ^ a.w) + __popc(dl1.x ^ c.x) + __popc(dl1.y ^ c.y) +
+                                     __popc(dl1.z ^ c.z) + __popc(dl1.w ^ c.w);
+                    if (dist < best || (dist == best && bestR >= 0 && iR < bestR)) {
+                        best = dist;
+                        bestR = iR;
+                        bestE = e;
+                    }
                 }
             }
         }
@@ -340,9 +363,9 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     if (tid == 0 && nvalid) nvalid[b] = nv - dropped;
 }
 
-size_t stereo_lds_bytes(int kp_cap, int height) {
+size_t stereo_lds_bytes(int kp_cap, int height, int ob) {
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    size_t s = r(32 * 4) + r((size_t)kp_cap * 32) + 2 * r((size_t)(height + 1) * 4);
+    size_t s = r(32 * 4) + r((size_t)kp_cap * 32) + r((size_t)ob * height * 4);
     s += r((size_t)kp_cap * 12);
     s += r((size_t)kp_cap * 4) + r((size_t)kp_cap * 2) + r(256 * 4);
     return s;

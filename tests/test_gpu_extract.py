@@ -81,12 +81,10 @@ def test_empty_image(orbx_lib, gpu):
     assert g(np.zeros((0, 0), np.uint8)) == (None, None)
 
 
-@pytest.mark.parametrize("seed", [0, 3])
-def test_kitti_stereo_parity(oracle_mod, orbx_lib, gpu, seed):
+def _check_stereo(oracle_mod, L, R, params):
     import my_orb_slam2_amd as m
-    L, R = synth.stereo_pair(seed)
-    gl, ol = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
-    gr, orr = _pair(oracle_mod, 2000, 1.2, 8, 20, 7)
+    gl, ol = _pair(oracle_mod, *params)
+    gr, orr = _pair(oracle_mod, *params)
     kl, _ = _check_extract(gl, ol, L, "left")
     _check_extract(gr, orr, R, "right")
     mb = np.float32(KITTI_MBF) / np.float32(KITTI_FX)
@@ -95,7 +93,24 @@ def test_kitti_stereo_parity(oracle_mod, orbx_lib, gpu, seed):
     assert_f32_bits_equal(u_g, u_o, "uRight")
     assert_f32_bits_equal(d_g, d_o, "depth")
     assert n_g == n_o
-    assert n_g > 100
+    return n_g
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_kitti_stereo_parity(oracle_mod, orbx_lib, gpu, seed):
+    L, R = synth.stereo_pair(seed)
+    assert _check_stereo(oracle_mod, L, R, (2000, 1.2, 8, 20, 7)) > 100
+
+
+@pytest.mark.parametrize("params,size", [((3000, 1.2, 8, 20, 7), (800, 600)),
+                                         ((1500, 1.1, 12, 20, 7), (752, 480)),
+                                         ((1000, 2.0, 3, 20, 7), (640, 480))])
+def test_stereo_param_sweep(oracle_mod, orbx_lib, gpu, params, size):
+    """k_stereo's right-keypoint buckets: (octave, row) buckets for the usual sizes; 3000
+    features at 800x600 take the row-bucket fallback (the octave buckets and the descriptors
+    would exceed the 160 KB of LDS), 12 and 3 levels the octave windows at their edges."""
+    L, R = synth.stereo_pair(7, *size)
+    assert _check_stereo(oracle_mod, L, R, params) > 50
 
 
 def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
