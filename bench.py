@@ -46,8 +46,8 @@ DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="stereo pairs (default 512) or EuRoC frames (default 256) per step per GPU")
     ap.add_argument("--distinct", type=int, default=32,

@@ -10,6 +10,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -162,6 +163,21 @@ int vresize_simd_end(int width) {
 #ifndef LEVEL_STRIP
 #define LEVEL_STRIP 1  // 0: every level on the tiled k_level
 #endif
+// Output rows per strip of level l: STRIP_TH, or ORBX_STRIP_TH="h0,h1,..." (tuning runs only;
+// 0 or a missing entry keeps the default)
+static int strip_height(int l) {
+    int th = STRIP_TH;
+    if (const char* e = getenv("ORBX_STRIP_TH")) {
+        for (int i = 0; i <= l && e; ++i) {
+            const int v = atoi(e);
+            if (i == l && v > 0) th = std::min(v, 4096);
+            e = strchr(e, ',');
+            if (e) ++e;
+        }
+    }
+    return th;
+}
+
 // k_level_strip tables of level l (StripLane per half-strip lane, rows -3 .. h+2); the level
 // keeps the tiled kernel (strip = 0) for modes 1 / 2 or when a group's taps do not fit the
 // 8-byte window the strip kernel reads
@@ -172,7 +188,7 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
     lv.strip = 0;
     if (!LEVEL_STRIP || (mode != 0 && mode != 3)) return;
     const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
-    lv.sth = STRIP_TH;
+    lv.sth = strip_height(l);
     lv.snh = (lv.w + SW_PX - 1) / SW_PX;
     lv.snw = (lv.snh + 1) / 2;
     lv.sns = (lv.h + lv.sth - 1) / lv.sth;

@@ -755,6 +755,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_HREUSE
 #define STRIP_HREUSE 1   // mode 3: reuse the previous step's HResize of a shared source row
 #endif
+#ifndef STRIP_HMASK
+#define STRIP_HMASK 1   // mode 3, SSE2 waves: horizontal sums masked once per source row
+#endif
 #ifndef STRIP_NS3
 #define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
 #endif
@@ -903,9 +906,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
             const uint32_t w0 = __builtin_amdgcn_alignbyte(D[1], D[0], o0);
             const uint32_t w1 = __builtin_amdgcn_alignbyte(D[2], D[1], o0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j) {
                 hs[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(w1, w0, sels[j])),
                                                __builtin_bit_cast(us2, als[j]), 0u, false);
+                // SSE2 form: the row's sums enter the vertical pass as (sum >> 4) << 8, masked
+                // once per source row here (a reused row is not masked again)
+                if (SIMD && STRIP_HMASK) hs[j] &= ~0xFFu;
+            }
         };
         uint32_t hA[4], hC[4];
         if (STRIP_HREUSE && RAo[slot] == prevRC) {   // wave-uniform
@@ -923,8 +930,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         for (int j = 0; j < 4; ++j) {
             int h0 = (int)hA[j];
             int h1 = (int)hC[j];
-            const int vs = (int)((mulhi24((uint32_t)h0 & ~0xFFu, bs0) +
-                                  mulhi24((uint32_t)h1 & ~0xFFu, bs1) + 2u) >> 2);
+            const uint32_t hm = (SIMD && STRIP_HMASK) ? ~0u : ~0xFFu;
+            const int vs = (int)((mulhi24((uint32_t)h0 & hm, bs0) +
+                                  mulhi24((uint32_t)h1 & hm, bs1) + 2u) >> 2);
             if (SIMD) {
                 out |= (uint32_t)vs << (8 * j);
             } else {
