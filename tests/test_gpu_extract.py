@@ -104,13 +104,14 @@ def test_kitti_stereo_parity(oracle_mod, orbx_lib, gpu, seed):
 
 @pytest.mark.parametrize("params,size", [((3000, 1.2, 8, 20, 7), (800, 600)),
                                          ((1500, 1.1, 12, 20, 7), (752, 480)),
-                                         ((1000, 2.0, 3, 20, 7), (640, 480))])
+                                         ((1000, 2.0, 3, 20, 7), (640, 480)),
+                                         ((500, 1.2, 8, 20, 7), (333, 97))])
 def test_stereo_param_sweep(oracle_mod, orbx_lib, gpu, params, size):
     """k_stereo's right-keypoint buckets: (octave, row) buckets for the usual sizes; 3000
     features at 800x600 take the row-bucket fallback (the octave buckets and the descriptors
     would exceed the 160 KB of LDS), 12 and 3 levels the octave windows at their edges."""
     L, R = synth.stereo_pair(7, *size)
-    assert _check_stereo(oracle_mod, L, R, params) > 50
+    assert _check_stereo(oracle_mod, L, R, params) > (50 if size[1] > 200 else 5)
 
 
 def test_batched_equals_single(oracle_mod, orbx_lib, gpu):
