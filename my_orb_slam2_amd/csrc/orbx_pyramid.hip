@@ -758,6 +758,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_HMASK
 #define STRIP_HMASK 1   // mode 3, SSE2 waves: horizontal sums masked once per source row
 #endif
+#ifndef STRIP_PEEL
+#define STRIP_PEEL 1   // interior blocks of a walk without store predicates
+#endif
 #ifndef STRIP_NS3
 #define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
 #endif
@@ -971,8 +974,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     };
 #endif
     // step i (k = i mod U: the load slot k mod NS, the row-sum register k mod 7)
-    auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c) {
+    // ALL: every step of this block stores both rows (no per-step store predicates)
+    auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c, auto all_c) {
         constexpr int k = decltype(k_c)::value;
+        constexpr bool ALL = decltype(all_c)::value;
         constexpr bool BSIMD = decltype(bsimd_c)::value;
 #if STRIP_SCHEDB
         // keep each step's memory operations in its step: the scheduler would otherwise sink
@@ -981,7 +986,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
 #endif
         const uint32_t v = level_group(k % NS, rsimd_c);
         issue((k + PF) % NS, i + PF);
-        store_row(STRIP_LEV, Y0 + i - 3, i >= 3 && i < vh + 3, v);
+        store_row(STRIP_LEV, Y0 + i - 3, ALL || (i >= 3 && i < vh + 3), v);
         // row sums: the groups left and right of this lane's
         const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);  // wave_shr:1 (bound_ctrl: lane 0 reads 0)
         const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);  // wave_shl:1
@@ -1037,7 +1042,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
                     packed |= min(val, 255u) << (8 * j);
                 }
             }
-            store_row(STRIP_BLR, Y0 + i - 6, i >= 6 && i < n, packed);
+            store_row(STRIP_BLR, Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
         }
     };
     constexpr int U = NS == 7 ? 7 : 7 * NS;   // steps per block: a multiple of NS and of 7
@@ -1054,9 +1059,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         }
         // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
         // store nothing)
-        for (int i0 = 0; i0 < n; i0 += U)
-            unroll_seq([&](auto k_c) { step(k_c, i0 + decltype(k_c)::value, rsimd_c, bsimd_c); },
+        auto block = [&](int i0, auto all_c) {
+            unroll_seq([&](auto k_c) { step(k_c, i0 + decltype(k_c)::value, rsimd_c, bsimd_c, all_c); },
                        std::make_integer_sequence<int, U>{});
+        };
+        int i0 = 0;
+#if STRIP_PEEL
+        // the first block (the 6 halo steps), then the blocks that store every step (a copy
+        // without the store predicates), then the rest
+        static_assert(U >= 6, "the first block holds the halo steps");
+        block(0, std::false_type{});
+        for (i0 = U; i0 + U <= vh + 3; i0 += U) block(i0, std::true_type{});
+#endif
+        for (; i0 < n; i0 += U) block(i0, std::false_type{});
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
     if ((MODE == 0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
