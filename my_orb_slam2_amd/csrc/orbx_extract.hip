@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         for (int l = 0; l < g->nlevels; ++l) tot += oc[l];
         nkp[b] = tot;
     }
-    const int n = oc[level];
+    const int n = __builtin_amdgcn_readfirstlane(oc[level]);   // wave-uniform trip counts
     if (i0 >= n) return;
     const int nk = min(OD_NK, n - i0);
     int off = 0;
@@ -1253,12 +1253,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_RL; ++j) v[j] = *(const uint32_t*)(pr + sor[j]);
     };
+    // buffer loads: one 32-bit offset add per dword instead of a 64-bit address
+    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc((void*)blr_l, 0, 0x7FFFFFFF, 0x00020000);
     auto issue_blr = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
-        const uint8_t* pb = blr_l + __umul24(y - 18, pitch) + ((x - 18) & ~3);
+        const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
 #pragma unroll
-        for (int j = 0; j < OD_BL; ++j) v[j] = *(const uint32_t*)(pb + sob[j]);
+        for (int j = 0; j < OD_BL; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rblr, vo + sob[j], 0, 0);
     };
 
     // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
