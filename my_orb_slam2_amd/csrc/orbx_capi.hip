@@ -163,10 +163,10 @@ int vresize_simd_end(int width) {
 #ifndef LEVEL_STRIP
 #define LEVEL_STRIP 1  // 0: every level on the tiled k_level
 #endif
-// Output rows per strip of level l: STRIP_TH, or ORBX_STRIP_TH="h0,h1,..." (tuning runs only;
+// Output rows per strip of level l: `def`, or ORBX_STRIP_TH="h0,h1,..." (tuning runs only;
 // 0 or a missing entry keeps the default)
-static int strip_height(int l) {
-    int th = STRIP_TH;
+static int strip_height(int l, int def) {
+    int th = def;
     if (const char* e = getenv("ORBX_STRIP_TH")) {
         for (int i = 0; i <= l && e; ++i) {
             const int v = atoi(e);
@@ -176,6 +176,36 @@ static int strip_height(int l) {
         }
     }
     return th;
+}
+
+// Strip height of a level for a batch of nimg images: STRIP_TH rows while the level's strip
+// walks give every SIMD of the chip (256 CUs x 4) two waves, else the tallest of 32 / 16 / 8
+// rows that does (8 at most).  A strip walk is a serial chain of rows, so a small batch (one
+// stereo frame at a time: the tracking thread's case) is latency-bound on the few long walks
+// of each level: 8-row strips take one stereo pair's pyramid from 0.218 to 0.082 ms (the
+// halo rows cost more work, which only large batches would notice).
+static int strip_default(const LevelGeom& lv, int nimg) {
+    const long long target = 2LL * 256 * 4;
+    int th = STRIP_TH;
+    while (th > 8 && (long long)lv.snw * ((lv.h + th - 1) / th) * nimg < target) th /= 2;
+    return th;
+}
+
+// Sets every strip level's height for a batch of nimg images; true if any changed (the
+// device Geometry must then be re-uploaded).
+static bool apply_strip_heights(orbx_extractor* h, int nimg) {
+    bool changed = false;
+    for (int l = 0; l < h->hg.nlevels; ++l) {
+        LevelGeom& lv = h->hg.lv[l];
+        if (!lv.strip) continue;
+        const int th = strip_height(l, strip_default(lv, nimg));
+        if (th != lv.sth) {
+            lv.sth = th;
+            lv.sns = (lv.h + th - 1) / th;
+            changed = true;
+        }
+    }
+    return changed;
 }
 
 // k_level_strip tables of level l (StripLane per half-strip lane, rows -3 .. h+2); the level
@@ -188,7 +218,7 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
     lv.strip = 0;
     if (!LEVEL_STRIP || (mode != 0 && mode != 3)) return;
     const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
-    lv.sth = strip_height(l);
+    lv.sth = strip_height(l, STRIP_TH);   // apply_strip_heights sets the batch's height
     lv.snh = (lv.w + SW_PX - 1) / SW_PX;
     lv.snw = (lv.snh + 1) / 2;
     lv.sns = (lv.h + lv.sth - 1) / lv.sth;
@@ -618,6 +648,7 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     if (!same) {
         orbx_status s = build_geometry(h, W, H);
         if (s != ORBX_OK) { h->have_geom = false; return s; }
+        apply_strip_heights(h, batch);
         if (!h->d_geom.ensure(sizeof(Geometry))) return ORBX_ERR_DEVICE;
         if (!h->d_cells.ensure(std::max<size_t>(h->cells.size(), 1) * sizeof(CellDesc))) return ORBX_ERR_DEVICE;
         if (!h->d_rtab.ensure(std::max<size_t>(h->rtab.size(), 1) * 2)) return ORBX_ERR_DEVICE;
@@ -637,6 +668,11 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
             return ORBX_ERR_DEVICE;
         h->have_geom = true;
         h->cap_batch = 0;
+    } else if (apply_strip_heights(h, batch)) {
+        // the previous call's kernels may still read the Geometry on the handle's stream
+        if (!HIPOK(hipStreamSynchronize(h->stream)) ||
+            !HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
+            return ORBX_ERR_DEVICE;
     }
     if (batch > h->cap_batch) {
         const Geometry& G = h->hg;
