@@ -730,6 +730,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_PF
 #define STRIP_PF 2   // mode 3: rows of source loads in flight ahead of the row being computed
 #endif
+#ifndef STRIP_ST_POLICY
+#define STRIP_ST_POLICY 0   // cache-policy bits of the strip walk stores: nt (2) 1.99 ms, sc1 (16) 1.88 ms vs 1.71 ms
+#endif
 #ifndef STRIP_BUFST
 #define STRIP_BUFST 1
 #endif
@@ -964,7 +967,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // or not whether or not the hardware adds soffset into its range check
     const uint32_t lane_off = (out_lane && !(STRIP_DIAG & 1)) ? (uint32_t)x : 0x80000000u;
     auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, int r, bool ok, uint32_t v) {
-        __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, STRIP_ST_POLICY);
     };
 #else
     const uint32_t pad_off = (uint32_t)(pitch - 4);
