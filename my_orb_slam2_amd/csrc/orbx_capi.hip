@@ -59,7 +59,7 @@ struct orbx_extractor {
     size_t octree_lds = 0, octree_lds1 = 0, stereo_lds = 0, level_lds = 0;
     int cap_batch = 0;
     DevBuf d_geom, d_cells, d_rtab, d_ltab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
-        d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv;
+        d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv, d_sscr;
     long long kscratch_per_image = 0;
     KernelTimer timer;
     // last extraction
@@ -763,6 +763,27 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
     a.nvalid = d_nv;
     a.lds = L->stereo_lds;
     a.timer = &L->timer;
+    a.scnt = nullptr;
+    a.ssad = nullptr;
+    a.sidx = nullptr;
+    if (stereo_split(batch) > 1) {
+        // split path scratch: counters (zeroed when allocated; k_stereo_cut leaves them zero),
+        // then per pair kp_cap SADs and left indices
+        // (a fixed counter block: one slot per pair of the largest split batch, so a later
+        // call with another batch finds its counters zero)
+        const size_t cnt_bytes = 256 * 4;
+        if (batch > 256) return ORBX_ERR_INVALID;
+        const size_t need = cnt_bytes + (size_t)batch * KC * 6;
+        const void* before = L->d_sscr.p;
+        if (!L->d_sscr.ensure(need)) return ORBX_ERR_DEVICE;
+        if (L->d_sscr.p != before &&
+            !HIPOK(hipMemsetAsync(L->d_sscr.p, 0, L->d_sscr.n, st)))
+            return ORBX_ERR_DEVICE;
+        uint8_t* base = L->d_sscr.as<uint8_t>();
+        a.scnt = (int*)base;
+        a.ssad = (int*)(base + cnt_bytes);
+        a.sidx = (int16_t*)(base + cnt_bytes + (size_t)batch * KC * 4);
+    }
     return HIPOK(launch_stereo(a, st)) ? ORBX_OK : ORBX_ERR_DEVICE;
 }
 
@@ -842,7 +863,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_in, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
-                      &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv};
+                      &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
     if (h->done) (void)hipEventDestroy(h->done);

@@ -117,6 +117,11 @@ struct StereoLaunch {
     int* nvalid;
     size_t lds;
     KernelTimer* timer;
+    // split path (stereo_split(batch) > 1): per pair an accepted-SAD count (zero on entry,
+    // left zero) and kp_cap (SAD, left index) slots
+    int* scnt;
+    int* ssad;
+    int16_t* sidx;
 };
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
@@ -125,6 +130,7 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap);
 size_t fast_lds_bytes(const Geometry& g);
 size_t octree_lds_bytes(int ncap, int kcap);
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st);
+int stereo_split(int batch);   // workgroups per pair of a launch_stereo over `batch` pairs
 size_t stereo_lds_bytes(int kp_cap, int height, int ob);  // ob: octave bucket groups
 
 }  // namespace orbx

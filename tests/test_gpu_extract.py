@@ -232,6 +232,34 @@ def test_large_batch_equals_single_images(oracle_mod, orbx_lib, gpu):
         assert_bytes_equal(desc[i, :nkp[i]], d_o, f"pair {i} desc vs oracle")
 
 
+def test_stereo_split_equals_unsplit(orbx_lib, gpu):
+    """k_stereo splits a pair's left keypoints over two workgroups (median in k_stereo_cut)
+    when a call has at most 128 pairs, and keeps one workgroup per pair above that: 136 pairs
+    in one call (one workgroup per pair) give bit for bit the uRight / depth / counts of the
+    same pairs in calls of 8 (split; those are checked against the oracle elsewhere)."""
+    import torch
+    import my_orb_slam2_amd as m
+    B, C = 136, 8
+    base = [synth.stereo_pair(400 + i, 640, 200) for i in range(8)]
+    pairs = [tuple(np.roll(base[i % 8][v], 13 * (i // 8), axis=0) for v in (0, 1)) for i in range(B)]
+    Ls = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    big = m.StereoBatch(B, 1000)
+    uR, dep, nv = (t.cpu().numpy() for t in big(Ls, Rs, KITTI_MBF, mb))
+    nkp = big.fetch("left")[0]
+    small = m.StereoBatch(C, 1000)
+    for c0 in range(0, B, C):
+        u2, d2, n2 = (t.cpu().numpy() for t in small(Ls[c0:c0 + C], Rs[c0:c0 + C], KITTI_MBF, mb))
+        assert np.array_equal(small.fetch("left")[0], nkp[c0:c0 + C]), f"pairs {c0}.. keypoints"
+        assert np.array_equal(n2, nv[c0:c0 + C]), f"pairs {c0}.. valid counts"
+        for i in range(C):
+            n = nkp[c0 + i]
+            assert_f32_bits_equal(u2[i, :n], uR[c0 + i, :n], f"pair {c0 + i} uRight")
+            assert_f32_bits_equal(d2[i, :n], dep[c0 + i, :n], f"pair {c0 + i} depth")
+    assert nv.sum() > 0
+
+
 def test_stereo_batch_shape_and_size_changes(orbx_lib, gpu):
     """One StereoBatch object across calls of different batch sizes and image shapes: the
     output buffers follow (B, W, H, kp_cap) and fetch() reads the views of the last call
