@@ -164,6 +164,14 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_WPE
 #define FAST_WPE 6     // minimum waves per SIMD requested from the register allocator (80 VGPRs)
 #endif
+#ifndef OCT_NT
+#define OCT_NT 256         // k_octree threads per list (64 / 128 / 256 / 512); 512 pairs per step:
+                           // 64 0.537, 128 0.377, 256 0.323 ms
+#endif
+#ifndef OCT_NT_SMALL
+#define OCT_NT_SMALL 256   // ... when batch * levels <= 256; one stereo pair: 128 0.112, 256 0.081,
+                           // 1024 0.101 ms
+#endif
 #ifndef OCTREE_PACKED
 #define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
 #endif
@@ -771,14 +779,14 @@ __device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1
 
 // Chunked exclusive scan over n items (n may exceed 256).  f(i) gives the value; g(i, excl)
 // consumes the exclusive prefix.  Returns the total.  All threads must call.
-template <class F, class G>
+template <int NT, class F, class G>
 __device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
     int carry = 0;
-    for (int c0 = 0; c0 < n; c0 += 256) {
+    for (int c0 = 0; c0 < n; c0 += NT) {
         const int i = c0 + threadIdx.x;
         const int v = (i < n) ? f(i) : 0;
         int tot;
-        const int ex = block_excl_scan(v, tmp, tot);
+        const int ex = block_excl_scan<NT / 64>(v, tmp, tot);
         if (i < n) gcb(i, carry + ex);
         carry += tot;
     }
@@ -800,7 +808,7 @@ extern "C" int orbx_diag_octree_stamps(unsigned long long* out) {
 #define OSTAMP(k) do { } while (0)
 #endif
 
-template <bool KEYS_LDS>
+template <int NT, bool KEYS_LDS>
 __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
                              int level, int ncand, uint32_t* kdata, int16_t* knode, uint8_t* kq,
                              OctreeSmem& sm, int* __restrict__ ocnt, uint32_t* __restrict__ okp) {
@@ -813,9 +821,9 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
 
     // ---- roots (src/ORBextractor.cc:552-587) ----
     OSTAMP(1);
-    for (int i = tid; i < nIni; i += 256) sm.cc[i * 4] = 0;
+    for (int i = tid; i < nIni; i += NT) sm.cc[i * 4] = 0;
     __syncthreads();
-    for (int k = tid; k < ncand; k += 256) {
+    for (int k = tid; k < ncand; k += NT) {
         const int x = cand_x(kdata[k]);
         int r = (int)((float)x / hX);
         r = min(r, nIni - 1);
@@ -823,7 +831,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         atomicAdd(&sm.cc[r * 4], 1);
     }
     __syncthreads();
-    int S = chunked_scan(
+    int S = chunked_scan<NT>(
         nIni, tmp, [&](int i) { return sm.cc[i * 4] > 0 ? 1 : 0; },
         [&](int i, int ex) {
             const int c = sm.cc[i * 4];
@@ -838,7 +846,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             sm.npos[i] = (int16_t)ex;
         });
     __syncthreads();
-    for (int k = tid; k < ncand; k += 256) knode[k] = sm.npos[knode[k]];
+    for (int k = tid; k < ncand; k += NT) knode[k] = sm.npos[knode[k]];
     __syncthreads();
 
     int seq_base = 1;
@@ -849,13 +857,13 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         const int prevS = S;
         OSTAMP(3 + 2 * guard);
         // ---- split every multi-key node: quadrant of each of its keys ----
-        for (int i = tid; i < S; i += 256) {
+        for (int i = tid; i < S; i += NT) {
             sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
             sm.cc[i * 4 + 2] = 0; sm.cc[i * 4 + 3] = 0;
             sm.pord[i] = -1;
         }
         __syncthreads();
-        for (int k = tid; k < ncand; k += 256) {
+        for (int k = tid; k < ncand; k += NT) {
             const int n = knode[k];
             if (cur.cnt[n] > 1) {
                 int sx, sy;
@@ -884,7 +892,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 // every field's total stays below its width while S < 512 (children and
                 // multi-key children <= 4 S < 2048 < 4096, survivors < 512).  The thread that
                 // scans node i also writes it below, so no barrier is needed in between.
-                const uint32_t tot = (uint32_t)chunked_scan(
+                const uint32_t tot = (uint32_t)chunked_scan<NT>(
                     S, tmp,
                     [&](int i) {
                         return cur.cnt[i] > 1 ? (int)((uint32_t)nonempty(i) | ((uint32_t)multi(i) << 20))
@@ -899,20 +907,20 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 Stot = (int)((tot >> 11) & 0x1FFu);
                 nToExpand = (int)(tot >> 20);
             } else {
-            for (int i = tid; i < S; i += 256) sm.pord[i] = cur.cnt[i] > 1 ? (int16_t)i : (int16_t)-1;
+            for (int i = tid; i < S; i += NT) sm.pord[i] = cur.cnt[i] > 1 ? (int16_t)i : (int16_t)-1;
             __syncthreads();
-            Ctot = chunked_scan(
+            Ctot = chunked_scan<NT>(
                 S, tmp, [&](int i) { return sm.pord[i] >= 0 ? nonempty(i) : 0; },
                 [&](int i, int ex) { sm.pre[i] = ex; });
-            Stot = chunked_scan(
+            Stot = chunked_scan<NT>(
                 S, tmp, [&](int i) { return sm.pord[i] >= 0 ? 0 : 1; },
                 [&](int i, int ex) { sm.pre2[i] = ex; });
             // nToExpand: children with more than one key
             int e = 0;
-            for (int i = tid; i < S; i += 256) e += sm.pord[i] >= 0 ? multi(i) : 0;
-            nToExpand = block_sum(e, tmp);
+            for (int i = tid; i < S; i += NT) e += sm.pord[i] >= 0 ? multi(i) : 0;
+            nToExpand = block_sum<NT / 64>(e, tmp);
             }
-            for (int i = tid; i < S; i += 256) {
+            for (int i = tid; i < S; i += NT) {
                 if (sm.pord[i] >= 0) {
                     const int c = nonempty(i);
                     const int start = Ctot - sm.pre[i] - c;
@@ -944,7 +952,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             }
         } else {
             // ---- phase 2 (src/ORBextractor.cc:675-740): split largest (size, seq) first ----
-            const int nV = chunked_scan(
+            const int nV = chunked_scan<NT>(
                 S, tmp, [&](int i) { return cur.cnt[i] > 1 ? 1 : 0; },
                 [&](int i, int ex) {
                     if (cur.cnt[i] > 1)
@@ -952,7 +960,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                                        ((uint64_t)(uint32_t)cur.seq[i] << 16) | (uint64_t)i;
                 });
             __syncthreads();
-            if (nV <= 4 * 256) {
+            if (nV <= 4 * NT) {
                 // rank sort, descending: a key's position is the number of larger keys (keys
                 // are unique: they end in the node index); two barriers instead of bitonic's
                 // log^2 stages
@@ -960,7 +968,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 int rank[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int i = tid + 256 * u;
+                    const int i = tid + NT * u;
                     key[u] = i < nV ? sm.sortb[i] : 0;
                     rank[u] = 0;
                 }
@@ -972,15 +980,15 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 __syncthreads();
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (tid + 256 * u < nV) sm.sortb[rank[u]] = key[u];
+                    if (tid + NT * u < nV) sm.sortb[rank[u]] = key[u];
             } else {
                 int P = 1;
                 while (P < nV) P <<= 1;
-                for (int i = nV + tid; i < P; i += 256) sm.sortb[i] = 0;
+                for (int i = nV + tid; i < P; i += NT) sm.sortb[i] = 0;
                 __syncthreads();
                 for (int k2 = 2; k2 <= P; k2 <<= 1) {
                     for (int j = k2 >> 1; j > 0; j >>= 1) {
-                        for (int i = tid; i < P; i += 256) {
+                        for (int i = tid; i < P; i += NT) {
                             const int ixj = i ^ j;
                             if (ixj > i) {
                                 const uint64_t a = sm.sortb[i], c = sm.sortb[ixj];
@@ -993,21 +1001,21 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 }
             }
             // running size after processing j (descending order); stop once >= N
-            if (tid == 0) tmp[8] = nV - 1;
+            if (tid == 0) tmp[24] = nV - 1;   // past the scan's NT / 64 partials
             __syncthreads();
-            chunked_scan(
+            chunked_scan<NT>(
                 nV, tmp,
                 [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1; },
                 [&](int j, int ex) {
                     const int delta = nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1;
-                    if (S + ex + delta >= N) atomicMin(&tmp[8], j);
+                    if (S + ex + delta >= N) atomicMin(&tmp[24], j);
                 });
             __syncthreads();
-            const int J = tmp[8];
+            const int J = tmp[24];
             __syncthreads();
             const int nP = J + 1;
             // children-before prefix in processing order, over processed nodes only
-            Ctot = chunked_scan(
+            Ctot = chunked_scan<NT>(
                 nP, tmp, [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)); },
                 [&](int j, int ex) {
                     const int n = (int)(sm.sortb[j] & 0xFFFF);
@@ -1015,10 +1023,10 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     sm.pord[n] = (int16_t)j;
                 });
             __syncthreads();
-            Stot = chunked_scan(
+            Stot = chunked_scan<NT>(
                 S, tmp, [&](int i) { return sm.pord[i] >= 0 ? 0 : 1; },
                 [&](int i, int ex) { sm.pre2[i] = ex; });
-            for (int i = tid; i < S; i += 256) {
+            for (int i = tid; i < S; i += NT) {
                 if (sm.pord[i] >= 0) {
                     const int c = nonempty(i);
                     const int start = Ctot - sm.pre[i] - c;
@@ -1050,7 +1058,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             }
         }
         __syncthreads();
-        for (int k = tid; k < ncand; k += 256) {
+        for (int k = tid; k < ncand; k += NT) {
             const int n = knode[k];
             knode[k] = sm.pord[n] >= 0 ? sm.cpos[n * 4 + kq[k]] : sm.npos[n];
         }
@@ -1066,18 +1074,19 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
 
     // ---- retain the best keypoint of each node (src/ORBextractor.cc:743-762) ----
     uint32_t* best = (uint32_t*)sm.cc;
-    for (int i = tid; i < S; i += 256) best[i] = 0;
+    for (int i = tid; i < S; i += NT) best[i] = 0;
     __syncthreads();
-    for (int k = tid; k < ncand; k += 256)
+    for (int k = tid; k < ncand; k += NT)
         atomicMax(&best[knode[k]], ((uint32_t)cand_s(kdata[k]) << 24) | (uint32_t)(0xFFFFFF - k));
     __syncthreads();
     uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
-    for (int i = tid; i < S; i += 256) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
+    for (int i = tid; i < S; i += NT) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
     if (tid == 0) ocnt[b * g->nlevels + level] = S;
     OSTAMP(61);
 }
 
-__global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                                                 const CellDesc* __restrict__ cells,
                                                 const int* __restrict__ ccnt,
                                                 const uint32_t* __restrict__ cand,
@@ -1095,7 +1104,7 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
     OctreeSmem sm;
     int NP2 = 1;
     while (NP2 < NCAP) NP2 <<= 1;
-    sm.tmp = (int*)take(16 * sizeof(int));
+    sm.tmp = (int*)take(32 * sizeof(int));
     sm.sortb = (uint64_t*)take((size_t)NP2 * 8);
     sm.A.x0 = (int16_t*)take(NCAP * 2); sm.A.y0 = (int16_t*)take(NCAP * 2);
     sm.A.x1 = (int16_t*)take(NCAP * 2); sm.A.y1 = (int16_t*)take(NCAP * 2);
@@ -1116,8 +1125,8 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
     // count the level's candidates
     const int* cc = ccnt + (size_t)b * g->n_cells + L.cell_begin;
     int part = 0;
-    for (int c = tid; c < L.ncells; c += 256) part += cc[c];
-    const int ncand = block_sum(part, sm.tmp);
+    for (int c = tid; c < L.ncells; c += NT) part += cc[c];
+    const int ncand = block_sum<NT / 64>(part, sm.tmp);
     if (ncand == 0 || L.n_ini < 1 || L.nfeat <= 0) {
         if (tid == 0) ocnt[b * g->nlevels + level] = 0;
         return;
@@ -1133,7 +1142,7 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
     // gather candidates in cell order (cell-major, raster inside a cell)
     const uint32_t* cbase = cand + (size_t)b * g->cand_words;
     const CellDesc* lc = cells + L.cell_begin;
-    chunked_scan(
+    chunked_scan<NT>(
         L.ncells, sm.tmp, [&](int c) { return cc[c]; },
         [&](int c, int ex) {
             // 8 loads in flight per batch (addresses clamped into the cell's slot, so no load
@@ -1151,9 +1160,9 @@ __global__ __launch_bounds__(256) void k_octree(const Geometry* __restrict__ g,
         });
     __syncthreads();
     if (in_lds)
-        octree_level<true>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+        octree_level<NT, true>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
     else
-        octree_level<false>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+        octree_level<NT, false>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1404,18 +1413,24 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                        a.dg, a.cells, a.pyr, a.ccnt, a.cand);
     T.stop(K_FAST, e, st);
     e = T.start_after(st);
+    // threads per list: OCT_NT, or OCT_NT_SMALL while the batch's lists fit one round on the
+    // CUs (each list is a serial chain of rounds with a few barriers each)
+    const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
+    auto oct = [&](dim3 grid, size_t lds, int ncap, int kcap, int level_base) {
+#define ORBX_OCT_LAUNCH(T)                                                                   \
+        hipLaunchKernelGGL(k_octree<T>, grid, dim3(T), lds, st, a.dg, a.cells, a.ccnt, a.cand, \
+                           a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
+        if (nt == 64) ORBX_OCT_LAUNCH(64);
+        else if (nt == 128) ORBX_OCT_LAUNCH(128);
+        else if (nt == 512) ORBX_OCT_LAUNCH(512);
+        else ORBX_OCT_LAUNCH(256);
+#undef ORBX_OCT_LAUNCH
+    };
 #if OCT_MERGED
-    hipLaunchKernelGGL(k_octree, dim3(G.nlevels, a.batch), dim3(256), a.octree_lds, st, a.dg,
-                       a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image,
-                       a.ncap, a.kcap, 0);
+    oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0);
 #else
-    hipLaunchKernelGGL(k_octree, dim3(1, a.batch), dim3(256), a.octree_lds, st, a.dg, a.cells,
-                       a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, a.ncap,
-                       a.kcap, 0);
-    if (G.nlevels > 1)
-        hipLaunchKernelGGL(k_octree, dim3(G.nlevels - 1, a.batch), dim3(256), a.octree_lds1, st,
-                           a.dg, a.cells, a.ccnt, a.cand, a.ocnt, a.okp, a.kscratch,
-                           a.kscratch_per_image, a.ncap1, a.kcap1, 1);
+    oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0);
+    if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1);
 #endif
     T.stop(K_OCTREE, e, st);
     e = T.start_after(st);
@@ -1429,7 +1444,7 @@ size_t octree_lds_bytes(int ncap, int kcap) {
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
     int np2 = 1;
     while (np2 < ncap) np2 <<= 1;
-    size_t s = r(16 * 4) + r((size_t)np2 * 8);
+    size_t s = r(32 * 4) + r((size_t)np2 * 8);
     s += 2 * (4 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4));
     s += r((size_t)ncap * 16) + r((size_t)ncap * 8) + 2 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4);
     s += r((size_t)kcap * 4) + r((size_t)kcap * 2) + r((size_t)kcap);
@@ -1444,8 +1459,11 @@ hipError_t prepare_level(size_t lds);
 // Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).
 hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
                            size_t fast_lds) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_octree,
+    hipError_t e = hipFuncSetAttribute((const void*)k_octree<256>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
+    for (const void* k : {(const void*)k_octree<64>, (const void*)k_octree<128>, (const void*)k_octree<512>})
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)fast_lds);
