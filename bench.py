@@ -41,6 +41,15 @@ DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
 
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
                              ("r02_pmc_fetch_euroc.csv", "r02_pmc_write_euroc.csv"))
+# SQ_INSTS_VALU passes (the VALU issue entry beside the HBM roofline)
+DEFAULT_INSTS = os.path.join(HERE, "profiles", "r02_pmc_insts_b512.csv")
+DEFAULT_INSTS_EUROC = os.path.join(HERE, "profiles", "r02_pmc_insts_euroc.csv")
+# VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
+# 2 cycles per SIMD for the full-rate class (add / logic / shifts / f32 mul-add), per 4 cycles
+# for the rest (v_dot*, v_perm, v_pk_*, v_bcnt, 32-bit min / max, conversions), measured by
+# tools/valu_rates.hip (profiles/r01_valu_issue_rates.txt)
+VALU_PEAK_2CYC = 1024 * 2.4e9 / 2
+VALU_PEAK_4CYC = 1024 * 2.4e9 / 4
 
 
 def parse():
@@ -73,6 +82,9 @@ def parse():
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
     ap.add_argument("--queries", type=int, default=2000,
                     help="euroc: projected local-map MapPoints per frame")
+    ap.add_argument("--insts-csv", default=None,
+                    help="rocprofv3 --pmc CSV holding SQ_INSTS_VALU for the roofline's VALU issue "
+                         "entry (default: the committed profiles/r02_pmc_insts_*.csv)")
     ap.add_argument("--traffic-csv", default=None,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"
@@ -128,6 +140,8 @@ def main():
     keep_stdout_for_result()
     if args.traffic_csv is None:
         args.traffic_csv = DEFAULT_PMC if args.workload == "stereo" else DEFAULT_PMC_EUROC
+    if args.insts_csv is None:
+        args.insts_csv = DEFAULT_INSTS if args.workload == "stereo" else DEFAULT_INSTS_EUROC
     if args.workload == "euroc":
         return main_euroc(args)
     if args.workload != "stereo":
@@ -263,6 +277,10 @@ def main():
                 # every extraction / stereo kernel against the HBM roof (north_star: FAST and
                 # the matcher included), same definitions as the headline object
                 "per_kernel": per_kernel_hbm(prof, geo, args.traffic_csv, args.steps)}
+        # the integer kernels are bound by VALU issue, not HBM: the same launches against
+        # the issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
+        for k, e in [(dom, roof)] + list(roof["per_kernel"].items()):
+            e["valu"] = valu_entry(args.insts_csv, k, e["avg_launch_ms"] / 1000.0)
 
     cpu = cpu_tp = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -337,6 +355,34 @@ def kernel_bytes(ext, n, B):
         # both views' keypoints + descriptors in, 11x11 + 11x21 SAD windows, 8 B out
         "k_stereo": B * kc * (2 * (28 + 32) + 11 * 11 + 11 * 21 + 8),
     }
+
+
+def valu_from_csv(paths, kernel):
+    """SQ_INSTS_VALU (wave instructions) per launch of `kernel`, averaged over its dispatches
+    in rocprofv3 --pmc CSVs, or None."""
+    import csv
+    import glob
+    tot, ids = 0.0, set()
+    for p in (paths or "").split(","):
+        for path in (sorted(glob.glob(p.strip())) if p.strip() else []):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == "SQ_INSTS_VALU":
+                        tot += float(row["Counter_Value"])
+                        ids.add((path, row.get("Dispatch_Id")))
+    return tot / len(ids) if ids else None
+
+
+def valu_entry(paths, kernel, avg_s):
+    """A launch's VALU issue rate against the chip's 2-cycle and 4-cycle class peaks."""
+    v = valu_from_csv(paths, kernel)
+    if not v or avg_s <= 0:
+        return None
+    rate = v / avg_s
+    return {"bound": "valu", "wave_instr_per_launch": v, "achieved": rate / 1e12,
+            "unit": "T wave-instr/s", "peak_2cycle": VALU_PEAK_2CYC / 1e12,
+            "peak_4cycle": VALU_PEAK_4CYC / 1e12, "frac_2cycle": rate / VALU_PEAK_2CYC,
+            "frac_4cycle": rate / VALU_PEAK_4CYC}
 
 
 def traffic_from_csv(paths, kernel):
@@ -549,7 +595,8 @@ def main_euroc(args):
                 "traffic": traffic_from_csv(args.traffic_csv, dom),
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg_s * 1000.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4)
-                                       for k, v in prof.items() if v[1]}}
+                                       for k, v in prof.items() if v[1]},
+                "valu": valu_entry(args.insts_csv, dom, avg_s)}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = euroc_cpu_baseline(frames, [per[p] for p in range(P)], args.cpu_seconds)

@@ -98,3 +98,33 @@ def test_gpus_flag_must_match_world_size():
                        cwd=str(ROOT), capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0
     assert "does not match WORLD_SIZE=1" in r.stderr
+
+
+def test_valu_entry_from_pmc(tmp_path):
+    """The roofline's VALU issue entry: SQ_INSTS_VALU averaged over a kernel's dispatches,
+    per launch duration, against the 2- and 4-cycle issue peaks of 1024 SIMDs at 2.4 GHz."""
+    b = _bench()
+    f = tmp_path / "insts.csv"
+    f.write_text('"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+                 '1,"orbx::k_level_strip<0>(x)","SQ_INSTS_VALU",100\n'
+                 '2,"orbx::k_level_strip<3>(x)","SQ_INSTS_VALU",300\n'
+                 '3,"orbx::k_fast(x)","SQ_INSTS_VALU",999\n'
+                 '3,"orbx::k_fast(x)","SQ_INSTS_SALU",5\n')
+    assert b.valu_from_csv(str(f), "k_level") == pytest.approx(200.0)
+    e = b.valu_entry(str(f), "k_fast", 1e-6)
+    assert e["wave_instr_per_launch"] == pytest.approx(999.0)
+    assert e["frac_4cycle"] == pytest.approx(999.0 / 1e-6 / (1024 * 2.4e9 / 4))
+    assert e["frac_2cycle"] == pytest.approx(e["frac_4cycle"] / 2)
+    assert b.valu_entry(str(f), "k_stereo", 1e-6) is None
+
+
+def test_headline_valu_entry_matches_committed_pmc():
+    """The committed headline line's VALU entry is the committed SQ_INSTS_VALU pass over the
+    line's own average launch duration."""
+    b = _bench()
+    roof = json.load(open(_latest("r[0-9][0-9]_v*_bench.json")))["roofline"]
+    if "valu" not in roof:
+        pytest.skip("headline line predates the VALU entry")
+    v = b.valu_from_csv(b.DEFAULT_INSTS, roof["kernel"])
+    assert roof["valu"]["wave_instr_per_launch"] == pytest.approx(v)
+    assert roof["valu"]["achieved"] == pytest.approx(v / (roof["avg_launch_ms"] / 1000.0) / 1e12)
