@@ -646,6 +646,8 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     if (!HIPOK(hipSetDevice(h->device))) return ORBX_ERR_DEVICE;
     const bool same = h->have_geom && h->hg.width == W && h->hg.height == H;
     if (!same) {
+        // a previous call's kernels may still read the old tables on the caller's stream
+        if (h->have_geom && !HIPOK(hipDeviceSynchronize())) return ORBX_ERR_DEVICE;
         orbx_status s = build_geometry(h, W, H);
         if (s != ORBX_OK) { h->have_geom = false; return s; }
         apply_strip_heights(h, batch);
@@ -669,8 +671,9 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         h->have_geom = true;
         h->cap_batch = 0;
     } else if (apply_strip_heights(h, batch)) {
-        // the previous call's kernels may still read the Geometry on the handle's stream
-        if (!HIPOK(hipStreamSynchronize(h->stream)) ||
+        // the previous call's kernels may still read the Geometry, on whatever stream the
+        // caller named (batched calls run on the caller's stream)
+        if (!HIPOK(hipDeviceSynchronize()) ||
             !HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
             return ORBX_ERR_DEVICE;
     }
