@@ -1371,11 +1371,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
         // so one mad gives the patch offset up to a constant folded into the base.
         const float MAGIC = 12582912.0f;
-        const uint8_t* bcm = bc - (0x400000u * (OD_BLR_DW * 4) + 0x4B400000u);
+        // (the constant is folded into a wrapping u32 offset from the patch start, not into
+        // the pointer: a pointer that far outside the LDS object is undefined behaviour, which
+        // the compiler may turn into a constant descriptor)
+        const uint32_t bko = (uint32_t)(bc - blr) - (0x400000u * (OD_BLR_DW * 4) + 0x4B400000u);
         auto sample = [&](float ra, float rb, float cA, float cB) {
             const uint32_t ro = __builtin_bit_cast(uint32_t, (ra + rb) + MAGIC);
             const uint32_t co = __builtin_bit_cast(uint32_t, (cA - cB) + MAGIC);
-            return (int)bcm[__umul24(ro, OD_BLR_DW * 4) + co];
+            return (int)blr[__umul24(ro, OD_BLR_DW * 4) + co + bko];
         };
         uint32_t words[8];
 #pragma unroll
