@@ -500,10 +500,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const uint32_t colmask4 = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
 #if FAST_COMPASS_PK
         const uint32_t colmask = colmask4;
-        constexpr int PB[4] = {0, 1, 2, 3};
+        [[maybe_unused]] constexpr int PB[4] = {0, 1, 2, 3};
 #else
         const uint32_t colmask = ((colmask4 & 3u) << CMP_B0) | ((colmask4 & 12u) << (CMP_B2 - 2));
-        constexpr int PB[4] = {CMP_B0, CMP_B1, CMP_B2, CMP_B3};
+        [[maybe_unused]] constexpr int PB[4] = {CMP_B0, CMP_B1, CMP_B2, CMP_B3};
 #endif
 #if FAST_W16
         // 16 pixels per lane: lpr lanes per detection row, 64 / lpr rows per pass; one pass
