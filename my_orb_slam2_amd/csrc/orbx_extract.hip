@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         for (int i = lane; i < ((dh + 2) * mw + 15) >> 4; i += 64) ((uint4*)mb)[i] = make_uint4(0u, 0u, 0u, 0u);
         lds_order();
         const int gsh = ((dw + 3) >> 2) <= 8 ? 3 : 4;
-        const int rpp = 64 >> gsh;
+        [[maybe_unused]] const int rpp = 64 >> gsh;
         const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
         const uint32_t colmask4 = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
 #if FAST_COMPASS_PK
