@@ -73,11 +73,14 @@ def parse():
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
     ap.add_argument("--workload", default="stereo",
-                    choices=["stereo", "euroc", "reloc", "triangulation"],
+                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin"],
                     help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
                          "extract + SearchByProjection vs the local map); reloc = configs[3] "
                          "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
-                         "(512 SearchForTriangulation jobs, sharded)")
+                         "(512 SearchForTriangulation jobs, sharded); dropin = the host-image "
+                         "drop-in path one stereo frame at a time (per-frame latency)")
+    ap.add_argument("--frames", type=int, default=300,
+                    help="dropin: timed stereo frames (after --warmup frames, at least 20)")
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
     ap.add_argument("--queries", type=int, default=2000,
@@ -90,6 +93,65 @@ def parse():
                          " and WRITE_SIZE for the roofline traffic field (default: the"
                          " committed profiles/ summaries of this workload)")
     return ap.parse_args()
+
+
+# ---- the timed workloads' inputs (also built by tests/test_gpu_bench_geometry.py, which checks
+# parity at exactly the sizes and geometries timed here) ----------------------------------------
+
+def stereo_inputs(rank: int, B: int, P: int):
+    """configs[1] inputs of one rank: B host stereo pairs (left [B,H,W], right [B,H,W]) built
+    from P generated base pairs; slot i is base pair i % P with both views rolled down by
+    37 * (i // P) rows (still rectified; generating B pairs from scratch would cost ~60 ms
+    each on the host).  Returns (Lh, Rh, base_pairs, distinct_slots)."""
+    from my_orb_slam2_amd import synth
+    P = max(1, min(P, B))
+    pairs = [synth.stereo_pair(1000 * rank + i, W, H) for i in range(P)]
+
+    def slot(i, view):
+        return np.roll(pairs[i % P][view], 37 * (i // P), axis=0)
+    Lh = np.stack([slot(i, 0) for i in range(B)])
+    Rh = np.stack([slot(i, 1) for i in range(B)])
+    n_distinct = len({(i % P, (37 * (i // P)) % H) for i in range(B)})
+    return Lh, Rh, pairs, n_distinct
+
+
+def euroc_frames(rank: int, B: int, P: int):
+    """configs[2] frames of one rank: P generated EuRoC-size frames, slot i = frame i % P."""
+    from my_orb_slam2_amd import synth
+    P = max(1, min(P, B))
+    frames = [synth.frame(2000 * rank + 7 + i, EUROC_W, EUROC_H) for i in range(P)]
+    return frames, [i % P for i in range(B)]
+
+
+def euroc_queries(idx, nkp, ku, desc, queries: int, kp_cap: int):
+    """Per distinct frame p: `queries` projected local-map MapPoints built from the frame's own
+    undistorted features (Frame::isInFrustum output: u, v, radius, predicted level), their
+    descriptors, and the motion-model pre-claimed mask (20 % of the features).  Returns
+    {p: (q, d, claimed)} over the frames that slots `idx` reference (first slot of each)."""
+    from my_orb_slam2_amd import synth
+    per = {}
+    for b, p in enumerate(idx):
+        if p not in per:
+            n = int(nkp[b])
+            q, d = synth.local_map_queries(p, ku[b, :n], desc[b, :n], queries, EUROC_W, EUROC_H)
+            cl = np.random.default_rng(p).random(kp_cap) < 0.2
+            per[p] = (q, d, cl.astype(np.uint8))
+    return per
+
+
+def triangulation_jobs(j0: int, j1: int):
+    """configs[4] jobs [j0, j1): keyframe pairs of 2000 features each over a 100-node synthetic
+    vocabulary, 30 % of the features with a MapPoint; returns (kfs, flags, F12s, epipoles)."""
+    from my_orb_slam2_amd import synth
+    kfs, flags, F12, epi = [], [], [], []
+    for j in range(j0, j1):
+        k1f, k2f, F, e, _ = synth.keyframe_pair(10000 + j, n1=2000, n2=2000, nodes=100)
+        rng = np.random.default_rng(j)
+        kfs += [k1f, k2f]
+        flags += [rng.random(k1f.n) < 0.3, rng.random(k2f.n) < 0.3]
+        F12.append(F.reshape(9))
+        epi.append(e)
+    return kfs, flags, F12, epi
 
 
 def algorithmic_bytes_fast(level_sizes, cells_area_read, ncand):
@@ -144,6 +206,8 @@ def main():
         args.insts_csv = DEFAULT_INSTS if args.workload == "stereo" else DEFAULT_INSTS_EUROC
     if args.workload == "euroc":
         return main_euroc(args)
+    if args.workload == "dropin":
+        return main_dropin(args)
     if args.workload != "stereo":
         return main_match(args)
     import torch
@@ -161,19 +225,11 @@ def main():
         dist.init_process_group("nccl", init_method="env://", device_id=dev)
 
     import my_orb_slam2_amd as orbx
-    from my_orb_slam2_amd import synth
 
     B = args.batch or 512
     P = max(1, min(args.distinct, B))
-    pairs = [synth.stereo_pair(1000 * rank + i, W, H) for i in range(P)]
-    # every slot of the batch holds a different pair: slot i is base pair i % P with both views
-    # rolled down by 37 * (i // P) rows (still rectified; generating B pairs from scratch
-    # would cost ~60 ms each on the host)
-    def slot(i, view):
-        return np.roll(pairs[i % P][view], 37 * (i // P), axis=0)
-    Lh = np.stack([slot(i, 0) for i in range(B)])
-    Rh = np.stack([slot(i, 1) for i in range(B)])
-    n_distinct = len({(i % P, (37 * (i // P)) % H) for i in range(B)})
+    # every slot of the batch holds a different pair (stereo_inputs)
+    Lh, Rh, pairs, n_distinct = stereo_inputs(rank, B, P)
     Ls = torch.from_numpy(Lh).to(dev)
     Rs = torch.from_numpy(Rh).to(dev)
     torch.cuda.synchronize(dev)
@@ -413,41 +469,66 @@ def traffic_from_csv(paths, kernel):
     return (2.0 * fetch + write) * 1024.0
 
 
-def cpu_baseline(pairs, mb, budget_s):
-    """The CPU restatement timed on this host: reference-faithful mode (src/Frame.cc:89-102:
-    left and right extraction on two threads, then ComputeStereoMatches on one)."""
+def cpu_model() -> str:
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return model
+
+
+def latency_stats(ms) -> dict:
+    """Median / mean of per-frame latencies, as Examples/Stereo/stereo_kitti.cc:115-123 prints
+    them (sorted vector, element n/2; plain mean)."""
+    v = sorted(ms)
+    return {"median_ms": v[len(v) // 2], "mean_ms": sum(v) / len(v), "p90_ms": v[int(0.9 * len(v))],
+            "frames": len(v)}
+
+
+def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20):
+    """The CPU restatement timed on this host in the reference's own mode (src/Frame.cc:89-102:
+    left and right extraction on two threads, then ComputeStereoMatches on one), per stereo
+    frame: `warmup` untimed frames, then at least `min_frames` timed ones (more while the
+    budget lasts); median and mean latency like stereo_kitti.cc:115-123, value = frames/s over
+    the timed frames."""
     try:
         import oracle
     except Exception:
         return None
     ol = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
     orr = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
-    done = 0
-    t0 = time.perf_counter()
+    ms = []
+    t_start = None
+    f = 0
     while True:
-        Lp, Rp = pairs[done % len(pairs)]
+        Lp, Rp = pairs[f % len(pairs)]
+        t0 = time.perf_counter()
         res = {}
         th = threading.Thread(target=lambda: res.__setitem__("r", orr(Rp)))
         th.start()
         kl, _ = ol(Lp)
         th.join()
         oracle.stereo_match(ol, orr, len(kl), MBF, mb)
-        done += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    el = time.perf_counter() - t0
-    model = platform.processor() or ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
+        t1 = time.perf_counter()
+        f += 1
+        if f == warmup:
+            t_start = t1
+        elif f > warmup:
+            ms.append(1000.0 * (t1 - t0))
+            if len(ms) >= min_frames and t1 - t_start >= budget_s:
                 break
-    except OSError:
-        pass
-    return {"value": done / el, "unit": "frames/sec", "cores": 2, "kind": "port",
-            "sample": f"{done} KITTI-size synthetic stereo pairs, L/R extraction on 2 threads + "
-                      f"ComputeStereoMatches (Frame.cc:89-102), {el:.1f} s",
-            "cpu_model": model, "host_cpus": os.cpu_count()}
+    el = time.perf_counter() - t_start
+    out = {"value": len(ms) / el, "unit": "frames/sec", "cores": 2, "kind": "port",
+           "sample": f"{len(ms)} KITTI-size synthetic stereo pairs after {warmup} warm-up pairs, "
+                     f"L/R extraction on 2 threads + ComputeStereoMatches (Frame.cc:89-102), "
+                     f"{el:.1f} s",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+           "build": "g++ -O3 -march=x86-64-v3 -ffp-contract=off (oracle/Makefile)"}
+    out.update(latency_stats(ms))
+    return out
 
 
 def cpu_baseline_throughput(pairs, mb, budget_s, workers=16):
@@ -486,6 +567,54 @@ def cpu_baseline_throughput(pairs, mb, budget_s, workers=16):
                       f"(one pipeline per core, SURVEY §8d mode ii), {el:.1f} s"}
 
 
+# ---- the drop-in host path, one stereo frame at a time ---------------------------------------
+
+def main_dropin(args):
+    """The path INTEGRATION.md installs into ORB-SLAM2, timed as its Tracking thread runs it:
+    per stereo frame, two std::threads call orbx_extract on the left and right host images
+    (src/Frame.cc:89-92), then orbx_stereo_match (:102); host memory in and out (PCIe
+    included).  The loop runs in C++ (tests/native/boundary_test.cpp `bench`, compiled against
+    include/orbx*.h only), so no Python overhead enters the latency.  Per-frame median and mean
+    over --frames frames after --warmup (>= 20) frames, beside the CPU restatement run the same
+    way on the same pairs."""
+    import subprocess
+    import tempfile
+    B = max(1, args.distinct)
+    Lh, Rh, pairs, _ = stereo_inputs(0, B, args.distinct)
+    mb = float(np.float32(MBF) / np.float32(FX))
+    warm = max(20, args.warmup)
+    binp = os.path.join(ROOT, "tests", "native", "boundary_test")
+    with tempfile.TemporaryDirectory() as d:
+        for i in range(B):
+            Lh[i].tofile(os.path.join(d, f"pair_{i}_left.raw"))
+            Rh[i].tofile(os.path.join(d, f"pair_{i}_right.raw"))
+        with open(os.path.join(d, "params.txt"), "w") as f:
+            f.write(f"{W} {H} {NFEAT} {MBF!r} {mb!r} {B}\n")
+        r = subprocess.run([binp, "bench", d, str(args.frames), str(warm)], capture_output=True,
+                           text=True, timeout=600)
+    if r.returncode != 0:
+        sys.exit(f"bench.py: {binp} failed ({r.returncode}): {r.stderr[-2000:]}")
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    lat = latency_stats(res["latency_ms"])
+    cpu = None
+    if args.cpu_seconds > 0:
+        cpu = cpu_baseline(pairs, mb, min(args.cpu_seconds, 6.0))
+    out = {"metric": "per-stereo-frame latency of the drop-in host path (orbx_extract x2 on 2 "
+                     "threads + orbx_stereo_match), KITTI 1241x376",
+           "value": 1000.0 / lat["mean_ms"], "unit": "frames/sec", "n_gpus": 1,
+           "steps": args.frames, "warmup": warm, "ms_per_step": lat["mean_ms"],
+           "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic",
+           "config": {"workload": "kitti_stereo_dropin_host_path", "width": W, "height": H,
+                      "nfeatures": NFEAT, "distinct_pairs": B, "threads": 2,
+                      "io": "host images in, host keypoints/descriptors/uRight/depth out"},
+           "latency": lat, "mean_keypoints_left": res["mean_keypoints_left"],
+           "mean_stereo_matches": res["mean_stereo_matches"], "cpu_baseline": cpu}
+    if cpu:
+        out["speedup_vs_cpu_median"] = cpu["median_ms"] / lat["median_ms"]
+    emit(json.dumps(out))
+
+
 # ---- EuRoC mono tracking (configs[2]) ----------------------------------------------------------
 
 EUROC_W, EUROC_H, EUROC_NFEAT = 752, 480, 1000     # Examples/Monocular/EuRoC.yaml
@@ -516,24 +645,17 @@ def main_euroc(args):
     K4, distc = synth.EUROC_CAM
     B = args.batch or 256
     P = max(1, min(args.distinct, B))
-    frames = [synth.frame(2000 * rank + 7 + i, EUROC_W, EUROC_H) for i in range(P)]
-    idx = [i % P for i in range(B)]
+    frames, idx = euroc_frames(rank, B, P)
     d_imgs = torch.from_numpy(np.stack([frames[i] for i in idx])).to(dev)
     mt = MonoTrackBatch(B, EUROC_W, EUROC_H, K4, distc, EUROC_NFEAT, device=local)
 
     # inputs: the local map projected into each frame (built from the frame's own features)
     mt.frames(d_imgs, st)
     nkp, ku, desc = mt.fetch_undistorted()
-    per = {}
+    per = euroc_queries(idx, nkp, ku, desc, args.queries, mt.kp_cap)
     qs, ds, cls = [], [], []
     for b in range(B):
         p = idx[b]
-        if p not in per:
-            n = int(nkp[b])
-            q, d = synth.local_map_queries(p, ku[b, :n], desc[b, :n], args.queries,
-                                           EUROC_W, EUROC_H)
-            cl = np.random.default_rng(p).random(mt.kp_cap) < 0.2
-            per[p] = (q, d, cl.astype(np.uint8))
         qs.append(per[p][0])
         ds.append(per[p][1])
         cls.append(per[p][2])
@@ -785,14 +907,7 @@ def main_match(args):
         from my_orb_slam2_amd import synth
         from my_orb_slam2_amd.matcher import DeviceKfDb
         j0, j1 = shard_range(args.jobs, rank, world)
-        kfs, flags, F12, epi = [], [], [], []
-        for j in range(j0, j1):
-            k1f, k2f, F, e, _ = synth.keyframe_pair(10000 + j, n1=2000, n2=2000, nodes=100)
-            rng = np.random.default_rng(j)
-            kfs += [k1f, k2f]
-            flags += [rng.random(k1f.n) < 0.3, rng.random(k2f.n) < 0.3]
-            F12.append(F.reshape(9))
-            epi.append(e)
+        kfs, flags, F12, epi = triangulation_jobs(j0, j1)
         db = DeviceKfDb(kfs, flags, dev)
         nj = j1 - j0
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)

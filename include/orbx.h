@@ -3,9 +3,11 @@
  * Drop-in boundary for the hot path of the reference (zackLiuzz/MY_ORB_SLAM2).  Each entry
  * point names the reference interface it replaces (file:line relative to the reference
  * root).  Plain pointers and sizes only; no OpenCV, no torch types.  All functions return
- * an orbx_status (0 = ok, < 0 = error) and are safe to call from several host threads as
- * long as each thread uses its own extractor handle (an ORBextractor is not re-entrant in
- * the reference either: its pyramid is mutable state, include/ORBextractor.h:85).
+ * an orbx_status (0 = ok, < 0 = error) and are safe to call from several host threads: a
+ * handle serialises its own calls (an ORBextractor is not re-entrant in the reference either:
+ * its pyramid is mutable state, include/ORBextractor.h:85), and a call waits only for its own
+ * handle's work, never for the whole device (Tracking, LocalMapping and LoopClosing call the
+ * hot path concurrently, src/System.cc:91-101).
  *
  * Numerics: bit-exact with the CPU restatement in oracle/ (same keypoints, angles,
  * descriptors, pyramid bytes, stereo outputs); see DESIGN.md for the OpenCV 3.2 conventions.
@@ -158,7 +160,16 @@ orbx_status orbx_profile_enable(orbx_extractor* h, int on);
 orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* launches);
 const char* orbx_kernel_name(int id);
 
-/* Library / device information. */
+/* The launch geometry a batched call of `batch` images would use after
+ * orbx_extractor_prepare (diagnostics; the parity tests pin the benchmarked geometry with
+ * it): strip_rows[nlevels] = output rows per k_level strip walk of each level (0: the level
+ * runs the tiled kernel), *stereo_split = workgroups per pair of a stereo launch over batch/2
+ * pairs (orbx_stereo_frames_device). */
+orbx_status orbx_extractor_launch_info(const orbx_extractor* h, int batch, int* strip_rows,
+                                       int* stereo_split);
+
+/* Library / device information.  orbx_version() ends in "orbx-src:<hash>", the hash of the
+ * sources the library was built from (my_orb_slam2_amd/build.py). */
 const char* orbx_version(void);
 /* Text of the last failing HIP call on this thread ("" if none). */
 const char* orbx_last_error(void);

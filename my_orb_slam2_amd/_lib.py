@@ -71,6 +71,7 @@ SIGNATURES = {
     "orbx_profile_enable": (_i, [_vp, _i]),
     "orbx_profile_collect": (_i, [_vp, _vp, _vp]),
     "orbx_kernel_name": (ctypes.c_char_p, [_i]),
+    "orbx_extractor_launch_info": (_i, [_vp, _i, _vp, ctypes.POINTER(_i)]),
     # include/orbx_match.h
     "orbx_matcher_create": (_i, [_vp, ctypes.POINTER(_vp)]),
     "orbx_matcher_destroy": (_i, [_vp]),

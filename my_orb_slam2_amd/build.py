@@ -4,9 +4,15 @@
 
 hipcc cross-compiles for gfx950 without a GPU.  The .so lands next to this file so it
 travels with the repo snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+
+Staleness is decided by content, not by file times: the build embeds a hash of every source
+and header (``orbx-src:<hash>`` in the binary, also reported by ``orbx_version()``), and a
+library whose embedded hash differs from the tree's is rebuilt.  A snapshot copied to another
+machine keeps a fresh library fresh whatever the copy does to modification times.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import pathlib
 import subprocess
@@ -16,10 +22,13 @@ PKG = pathlib.Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "liborbx.so"
 SOURCES = ["orbx_pyramid.hip", "orbx_extract.hip", "orbx_stereo.hip", "orbx_match.hip",
-           "orbx_capi.hip", "orbx_match_capi.hip", "orbx_vocab.hip", "orbx_frame.hip"]
+           "orbx_capi.hip", "orbx_match_capi.hip", "orbx_vocab.hip", "orbx_frame.hip",
+           "orbx_kfdb.hip"]
 HEADERS = ["orbx_internal.h", "orbx_device.h", "orbx_math.h", "orbx_kernels.h", "orbx_host.h",
            "orbx_match_kernels.h", "orbx_pattern.inc", "../../include/orbx.h",
-           "../../include/orbx_match.h", "../../include/orbx_vocab.h", "../../include/orbx_frame.h"]
+           "../../include/orbx_match.h", "../../include/orbx_vocab.h", "../../include/orbx_frame.h",
+           "../../include/orbx_kfdb.h"]
+HASH_TAG = b"orbx-src:"
 
 # -ffp-contract=off: every float a*b+c in the path is two roundings, as in the x86 reference
 # (hipcc defaults to fast contraction).  No -ffast-math: IEEE division/rounding throughout.
@@ -35,26 +44,75 @@ def hipcc() -> str:
     return "hipcc"
 
 
+def source_hash(extra_flags=()) -> str:
+    """16 hex digits over the sources, headers and compile flags of the library."""
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        p = CSRC / name
+        h.update(name.encode() + b"\0")
+        h.update(p.read_bytes() if p.exists() else b"<missing>")
+    h.update(" ".join(FLAGS[:-1] + list(extra_flags)).encode())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path: pathlib.Path = LIB) -> str | None:
+    """The source hash a built library carries, or None."""
+    try:
+        data = path.read_bytes()
+    except OSError:
+        return None
+    i = data.find(HASH_TAG)
+    if i < 0:
+        return None
+    return data[i + len(HASH_TAG):i + len(HASH_TAG) + 16].decode("ascii", "replace")
+
+
 def stale() -> bool:
-    if not LIB.exists():
-        return True
-    t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES] + [CSRC / h for h in HEADERS]
-    return any(p.exists() and p.stat().st_mtime > t for p in deps)
+    return embedded_hash() != source_hash()
 
 
-def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
-    if not force and not stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, extra_flags=(),
+          out: pathlib.Path | None = None) -> pathlib.Path:
+    """Compile the library (if stale, or always with force).  `extra_flags` / `out` build a
+    tuning variant (tools/variants.py) next to the product library."""
+    target = pathlib.Path(out) if out else LIB
+    digest = source_hash(extra_flags)
+    if not force and embedded_hash(target) == digest:
+        return target
     srcs = [str(CSRC / s) for s in SOURCES if (CSRC / s).exists()]
-    cmd = [hipcc()] + FLAGS + srcs + ["-o", str(LIB) + ".tmp"]
+    cmd = ([hipcc()] + FLAGS + list(extra_flags) + [f'-DORBX_SRC_HASH="{digest}"'] + srcs +
+           ["-o", str(target) + ".tmp"])
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(str(LIB) + ".tmp", LIB)
-    return LIB
+    os.replace(str(target) + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
-    print(LIB)
+    print(LIB, source_hash())
+
+
+# ---- the C++ boundary consumer (tests/native/boundary_test.cpp) -------------------------------
+BOUNDARY_SRC = PKG.parent / "tests" / "native" / "boundary_test.cpp"
+BOUNDARY_BIN = PKG.parent / "tests" / "native" / "boundary_test"
+
+
+def build_boundary_test(force: bool = False, verbose: bool = False) -> pathlib.Path:
+    """g++ against include/orbx*.h only, linked to the in-tree liborbx.so (found at run time
+    through the binary's RUNPATH, $ORIGIN-relative, so the tree can move)."""
+    hdrs = sorted((PKG.parent / "include").glob("*.h"))
+    newest = max([BOUNDARY_SRC.stat().st_mtime] + [h.stat().st_mtime for h in hdrs])
+    if not force and BOUNDARY_BIN.exists() and BOUNDARY_BIN.stat().st_mtime >= newest:
+        return BOUNDARY_BIN
+    build(verbose=verbose)
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-I" + str(PKG.parent / "include"),
+           str(BOUNDARY_SRC), "-L" + str(PKG), "-lorbx", "-L/opt/rocm/lib",
+           "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,-rpath,$ORIGIN/../../my_orb_slam2_amd",
+           "-pthread", "-o", str(BOUNDARY_BIN) + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(BOUNDARY_BIN) + ".tmp", BOUNDARY_BIN)
+    return BOUNDARY_BIN

@@ -19,7 +19,11 @@
 #include "orbx_internal.h"
 #include "orbx_kernels.h"
 
-#define ORBX_VERSION "orbx 0.1.0 (gfx950)"
+#ifndef ORBX_SRC_HASH
+#define ORBX_SRC_HASH "0000000000000000"   // my_orb_slam2_amd/build.py passes the real one
+#endif
+// "orbx-src:<hash>" is also how build.py finds the hash in the binary (staleness check)
+#define ORBX_VERSION "orbx 0.3.0 (gfx950) orbx-src:" ORBX_SRC_HASH
 
 namespace orbx {
 hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
@@ -42,8 +46,19 @@ bool hip_ok(hipError_t e, const char* what) {
 struct orbx_extractor {
     orbx_extractor_params prm;
     int device = 0;
+    int ncu = 256;                // compute units of the device (strip-height heuristic)
     hipStream_t stream = nullptr;
+    // `done` is recorded after the last work issued for this handle (on `done_stream`): a
+    // later call on another stream waits for it, and table updates / buffer growth / host
+    // fetches wait on it instead of on the whole device
     hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    bool have_done = false;
+    // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
+    uint8_t* h_in = nullptr;
+    size_t h_in_n = 0;
+    uint8_t* h_out = nullptr;
+    size_t h_out_n = 0;
     // ORBextractor tables
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> nfeat;
@@ -163,10 +178,12 @@ int vresize_simd_end(int width) {
 #ifndef LEVEL_STRIP
 #define LEVEL_STRIP 1  // 0: every level on the tiled k_level
 #endif
-// Output rows per strip of level l: `def`, or ORBX_STRIP_TH="h0,h1,..." (tuning runs only;
-// 0 or a missing entry keeps the default)
+// Output rows per strip of level l: `def`; tuning builds (-DORBX_TUNING, tools/strip_sweep.py)
+// also read ORBX_STRIP_TH="h0,h1,..." (0 or a missing entry keeps the default).  The product
+// library never reads the environment.
 static int strip_height(int l, int def) {
     int th = def;
+#ifdef ORBX_TUNING
     if (const char* e = getenv("ORBX_STRIP_TH")) {
         for (int i = 0; i <= l && e; ++i) {
             const int v = atoi(e);
@@ -175,37 +192,65 @@ static int strip_height(int l, int def) {
             if (e) ++e;
         }
     }
+#else
+    (void)l;
+#endif
     return th;
 }
 
 // Strip height of a level for a batch of nimg images: STRIP_TH rows while the level's strip
-// walks give every SIMD of the chip (256 CUs x 4) two waves, else the tallest of 32 / 16 / 8
+// walks give every SIMD of the device (ncu CUs x 4) two waves, else the tallest of 32 / 16 / 8
 // rows that does (8 at most).  A strip walk is a serial chain of rows, so a small batch (one
 // stereo frame at a time: the tracking thread's case) is latency-bound on the few long walks
 // of each level: 8-row strips take one stereo pair's pyramid from 0.218 to 0.082 ms (the
 // halo rows cost more work, which only large batches would notice).
-static int strip_default(const LevelGeom& lv, int nimg) {
-    const long long target = 2LL * 256 * 4;
+static int strip_default(const LevelGeom& lv, int nimg, int ncu) {
+    const long long target = 2LL * ncu * 4;
     int th = STRIP_TH;
     while (th > 8 && (long long)lv.snw * ((lv.h + th - 1) / th) * nimg < target) th /= 2;
     return th;
 }
 
-// Sets every strip level's height for a batch of nimg images; true if any changed (the
-// device Geometry must then be re-uploaded).
-static bool apply_strip_heights(orbx_extractor* h, int nimg) {
-    bool changed = false;
+// Every strip level's height for a batch of nimg images (a launch argument of k_level_strip,
+// so a batch-size change touches no device state).
+static void strip_heights(const orbx_extractor* h, int nimg, int* sth) {
+    for (int l = 0; l < ORBX_MAX_LEVELS; ++l) sth[l] = STRIP_TH;
     for (int l = 0; l < h->hg.nlevels; ++l) {
-        LevelGeom& lv = h->hg.lv[l];
-        if (!lv.strip) continue;
-        const int th = strip_height(l, strip_default(lv, nimg));
-        if (th != lv.sth) {
-            lv.sth = th;
-            lv.sns = (lv.h + th - 1) / th;
-            changed = true;
-        }
+        const LevelGeom& lv = h->hg.lv[l];
+        if (lv.strip) sth[l] = strip_height(l, strip_default(lv, nimg, h->ncu));
     }
-    return changed;
+}
+
+static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
+
+// Orders stream st after all work issued so far for this handle (on whatever stream).
+static bool order_after_last(orbx_extractor* h, hipStream_t st) {
+    if (h->have_done && h->done_stream != st) return HIPOK(hipStreamWaitEvent(st, h->done, 0));
+    return true;
+}
+
+// Marks the end of the work just issued for this handle on st.
+static bool mark_done(orbx_extractor* h, hipStream_t st) {
+    h->done_stream = st;
+    h->have_done = true;
+    return HIPOK(hipEventRecord(h->done, st));
+}
+
+// Waits (host) until the handle's issued work has finished: its tables may then change and
+// its buffers grow.  Other streams and handles on the device keep running.
+static bool wait_idle(orbx_extractor* h) {
+    return !h->have_done || HIPOK(hipEventSynchronize(h->done));
+}
+
+// Host staging buffer (pinned) of at least n bytes.
+static bool ensure_pinned(uint8_t*& p, size_t& cap, size_t n) {
+    if (p && cap >= n) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (!HIPOK(hipHostMalloc((void**)&p, n, hipHostMallocDefault))) { p = nullptr; return false; }
+    cap = n;
+    return true;
 }
 
 // k_level_strip tables of level l (StripLane per half-strip lane, rows -3 .. h+2); the level
@@ -218,10 +263,8 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
     lv.strip = 0;
     if (!LEVEL_STRIP || (mode != 0 && mode != 3)) return;
     const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
-    lv.sth = strip_height(l, STRIP_TH);   // apply_strip_heights sets the batch's height
     lv.snh = (lv.w + SW_PX - 1) / SW_PX;
     lv.snw = (lv.snh + 1) / 2;
-    lv.sns = (lv.h + lv.sth - 1) / lv.sth;
     std::vector<StripLane> sl((size_t)lv.snh * 32);
     for (int hs = 0; hs < lv.snh; ++hs)
         for (int q = 0; q < 32; ++q) {
@@ -646,38 +689,35 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     if (!HIPOK(hipSetDevice(h->device))) return ORBX_ERR_DEVICE;
     const bool same = h->have_geom && h->hg.width == W && h->hg.height == H;
     if (!same) {
-        // a previous call's kernels may still read the old tables on the caller's stream
-        if (h->have_geom && !HIPOK(hipDeviceSynchronize())) return ORBX_ERR_DEVICE;
+        // this handle's earlier calls may still read the old tables (on their streams)
+        if (!wait_idle(h)) return ORBX_ERR_DEVICE;
         orbx_status s = build_geometry(h, W, H);
         if (s != ORBX_OK) { h->have_geom = false; return s; }
-        apply_strip_heights(h, batch);
         if (!h->d_geom.ensure(sizeof(Geometry))) return ORBX_ERR_DEVICE;
         if (!h->d_cells.ensure(std::max<size_t>(h->cells.size(), 1) * sizeof(CellDesc))) return ORBX_ERR_DEVICE;
         if (!h->d_rtab.ensure(std::max<size_t>(h->rtab.size(), 1) * 2)) return ORBX_ERR_DEVICE;
         if (!h->d_ltab.ensure(std::max<size_t>(h->ltab.size(), 16))) return ORBX_ERR_DEVICE;
-        if (!HIPOK(hipMemcpy(h->d_ltab.p, h->ltab.data(), h->ltab.size(), hipMemcpyHostToDevice)))
-            return ORBX_ERR_DEVICE;
-        if (!HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
+        // uploads on the handle's own (non-blocking) stream: nothing else on the device waits
+        hipStream_t st = h->stream;
+        if (!HIPOK(hipMemcpyAsync(h->d_ltab.p, h->ltab.data(), h->ltab.size(), hipMemcpyHostToDevice, st)) ||
+            !HIPOK(hipMemcpyAsync(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice, st)))
             return ORBX_ERR_DEVICE;
         if (!h->cells.empty() &&
-            !HIPOK(hipMemcpy(h->d_cells.p, h->cells.data(), h->cells.size() * sizeof(CellDesc),
-                      hipMemcpyHostToDevice)))
+            !HIPOK(hipMemcpyAsync(h->d_cells.p, h->cells.data(), h->cells.size() * sizeof(CellDesc),
+                                  hipMemcpyHostToDevice, st)))
             return ORBX_ERR_DEVICE;
         if (!h->rtab.empty() &&
-            !HIPOK(hipMemcpy(h->d_rtab.p, h->rtab.data(), h->rtab.size() * 2, hipMemcpyHostToDevice)))
+            !HIPOK(hipMemcpyAsync(h->d_rtab.p, h->rtab.data(), h->rtab.size() * 2, hipMemcpyHostToDevice, st)))
             return ORBX_ERR_DEVICE;
+        if (!HIPOK(hipStreamSynchronize(st))) return ORBX_ERR_DEVICE;
         if (!HIPOK(prepare_kernels(h->octree_lds, h->stereo_lds, h->level_lds, fast_lds_bytes(h->hg))))
             return ORBX_ERR_DEVICE;
         h->have_geom = true;
         h->cap_batch = 0;
-    } else if (apply_strip_heights(h, batch)) {
-        // the previous call's kernels may still read the Geometry, on whatever stream the
-        // caller named (batched calls run on the caller's stream)
-        if (!HIPOK(hipDeviceSynchronize()) ||
-            !HIPOK(hipMemcpy(h->d_geom.p, &h->hg, sizeof(Geometry), hipMemcpyHostToDevice)))
-            return ORBX_ERR_DEVICE;
     }
     if (batch > h->cap_batch) {
+        // growing frees the old buffers: the handle's work in flight must be done
+        if (!wait_idle(h)) return ORBX_ERR_DEVICE;
         const Geometry& G = h->hg;
         const size_t B = (size_t)batch;
         // k_fast (FAST_PFU) reads up to 4 * FAST_PF2D rows past a cell's ROI
@@ -729,7 +769,9 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.desc = h->d_desc.as<uint8_t>();
     a.nkp = h->d_nkp.as<int>();
     a.timer = &h->timer;
-    if (!HIPOK(launch_extract(a, st))) return ORBX_ERR_DEVICE;
+    strip_heights(h, batch, a.sth);
+    if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
+    if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
     h->last_valid = true;
     return ORBX_OK;
@@ -774,20 +816,26 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
         // then per pair kp_cap SADs and left indices
         // (a fixed counter block: one slot per pair of the largest split batch, so a later
         // call with another batch finds its counters zero)
+        // (stereo_split(batch) > 1 only for batch <= 128, so 256 counters always suffice)
         const size_t cnt_bytes = 256 * 4;
-        if (batch > 256) return ORBX_ERR_INVALID;
         const size_t need = cnt_bytes + (size_t)batch * KC * 6;
-        const void* before = L->d_sscr.p;
+        // a reallocation (detected by capacity: the allocator may hand back the same
+        // address) starts from zeroed counters
+        const size_t cap_before = L->d_sscr.n;
+        if (need > cap_before && !wait_idle(L)) return ORBX_ERR_DEVICE;
         if (!L->d_sscr.ensure(need)) return ORBX_ERR_DEVICE;
-        if (L->d_sscr.p != before &&
-            !HIPOK(hipMemsetAsync(L->d_sscr.p, 0, L->d_sscr.n, st)))
+        if (L->d_sscr.n != cap_before &&
+            !HIPOK(hipMemsetAsync(L->d_sscr.p, 0, cnt_bytes, st)))
             return ORBX_ERR_DEVICE;
         uint8_t* base = L->d_sscr.as<uint8_t>();
         a.scnt = (int*)base;
         a.ssad = (int*)(base + cnt_bytes);
         a.sidx = (int16_t*)(base + cnt_bytes + (size_t)batch * KC * 4);
     }
-    return HIPOK(launch_stereo(a, st)) ? ORBX_OK : ORBX_ERR_DEVICE;
+    if (!order_after_last(L, st) || (R != L && !order_after_last(R, st))) return ORBX_ERR_DEVICE;
+    if (!HIPOK(launch_stereo(a, st)) || !mark_done(L, st) || (R != L && !mark_done(R, st)))
+        return ORBX_ERR_DEVICE;
+    return ORBX_OK;
 }
 
 }  // namespace
@@ -822,6 +870,18 @@ orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* l
     return ORBX_OK;
 }
 
+orbx_status orbx_extractor_launch_info(const orbx_extractor* h, int batch, int* strip_rows,
+                                       int* stereo_split) {
+    if (!h || batch < 1) return ORBX_ERR_INVALID;
+    if (!h->have_geom) return ORBX_ERR_STATE;
+    int sth[ORBX_MAX_LEVELS];
+    strip_heights(h, batch, sth);
+    if (strip_rows)
+        for (int l = 0; l < h->hg.nlevels; ++l) strip_rows[l] = h->hg.lv[l].strip ? sth[l] : 0;
+    if (stereo_split) *stereo_split = stereo_split_of(std::max(batch / 2, 1));
+    return ORBX_OK;
+}
+
 orbx_status orbx_device_count(int* n) {
     if (!n) return ORBX_ERR_INVALID;
     int c = 0;
@@ -850,12 +910,15 @@ orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor
     if (h->prm.max_batch < 1) h->prm.max_batch = 1;
     h->device = p->device;
     compute_tables(h);
-    if (!HIPOK(hipSetDevice(h->device)) ||
+    hipDeviceProp_t prop;
+    if (!HIPOK(hipSetDevice(h->device)) || !HIPOK(hipGetDeviceProperties(&prop, h->device)) ||
         !HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) ||
         !HIPOK(hipEventCreateWithFlags(&h->done, hipEventDisableTiming))) {
+        if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         return ORBX_ERR_DEVICE;
     }
+    h->ncu = std::max(prop.multiProcessorCount, 1);
     *out = h;
     return ORBX_OK;
 }
@@ -863,7 +926,10 @@ orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor
 orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (!h) return ORBX_ERR_INVALID;
     (void)hipSetDevice(h->device);
+    (void)wait_idle(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->h_in) (void)hipHostFree(h->h_in);
+    if (h->h_out) (void)hipHostFree(h->h_out);
     DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_in, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
@@ -901,23 +967,38 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     orbx_status s = ensure_workspace(h, width, height, 1);
     if (s != ORBX_OK) return s;
     hipStream_t st = h->stream;
-    if (!HIPOK(hipMemcpy2DAsync(h->d_in.p, width, img, stride, width, height, hipMemcpyHostToDevice, st)))
+    // The image goes through the handle's pinned staging (a true async DMA, no pageable
+    // bounce), and every output comes back in one pinned block: one host wait per call.
+    const size_t img_bytes = (size_t)width * height;
+    const size_t KC = (size_t)h->hg.kp_cap;
+    const size_t o_kps = 256, o_desc = o_kps + KC * sizeof(orbx_keypoint);
+    if (!ensure_pinned(h->h_in, h->h_in_n, img_bytes) ||
+        !ensure_pinned(h->h_out, h->h_out_n, o_desc + KC * 32))
         return ORBX_ERR_DEVICE;
-    s = run_extract(h, h->d_in.as<uint8_t>(), nullptr, 1, 1, width, (size_t)width * height, st);
+    if (stride == (size_t)width) {
+        std::memcpy(h->h_in, img, img_bytes);
+    } else {
+        for (int y = 0; y < height; ++y)
+            std::memcpy(h->h_in + (size_t)y * width, img + (size_t)y * stride, width);
+    }
+    if (!order_after_last(h, st) ||
+        !HIPOK(hipMemcpyAsync(h->d_in.p, h->h_in, img_bytes, hipMemcpyHostToDevice, st)))
+        return ORBX_ERR_DEVICE;
+    s = run_extract(h, h->d_in.as<uint8_t>(), nullptr, 1, 1, width, img_bytes, st);
     if (s != ORBX_OK) return s;
-    int n = 0;
-    if (!HIPOK(hipMemcpyAsync(&n, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipStreamSynchronize(st)))
+    if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(h->h_out + o_kps, h->d_kps.p, KC * sizeof(orbx_keypoint),
+                              hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(h->h_out + o_desc, h->d_desc.p, KC * 32, hipMemcpyDeviceToHost, st)) ||
+        !mark_done(h, st) || !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
+    int n = 0;
+    std::memcpy(&n, h->h_out, 4);
     *n_out = n;
     const int m = std::min(n, kp_cap);
     if (m > 0) {
-        if (kps && !HIPOK(hipMemcpyAsync(kps, h->d_kps.p, (size_t)m * sizeof(orbx_keypoint),
-                                  hipMemcpyDeviceToHost, st)))
-            return ORBX_ERR_DEVICE;
-        if (desc && !HIPOK(hipMemcpyAsync(desc, h->d_desc.p, (size_t)m * 32, hipMemcpyDeviceToHost, st)))
-            return ORBX_ERR_DEVICE;
-        if (!HIPOK(hipStreamSynchronize(st))) return ORBX_ERR_DEVICE;
+        if (kps) std::memcpy(kps, h->h_out + o_kps, (size_t)m * sizeof(orbx_keypoint));
+        if (desc) std::memcpy(desc, h->h_out + o_desc, (size_t)m * 32);
     }
     return n > kp_cap ? ORBX_ERR_CAPACITY : ORBX_OK;
 }
@@ -934,7 +1015,8 @@ static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, i
     std::lock_guard<std::mutex> lk(h->mu);
     (void)hipSetDevice(h->device);
     const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
-    if (!HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
+    if (!order_after_last(h, h->stream) ||
+        !HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
         !HIPOK(hipStreamSynchronize(h->stream)))
         return ORBX_ERR_DEVICE;
     return ORBX_OK;
@@ -997,50 +1079,55 @@ orbx_status orbx_batch_fetch(orbx_extractor* h, int first, int count, int32_t* n
         return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(h->mu);
     (void)hipSetDevice(h->device);
-    if (!HIPOK(hipDeviceSynchronize())) return ORBX_ERR_DEVICE;
+    // after the handle's last launches (on whatever stream), on the handle's own stream
+    hipStream_t st = h->stream;
+    if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     const size_t KC = (size_t)h->hg.kp_cap;
-    if (nkp && !HIPOK(hipMemcpy(nkp, h->d_nkp.as<int32_t>() + first, (size_t)count * 4,
-                                hipMemcpyDeviceToHost)))
+    if (nkp && !HIPOK(hipMemcpyAsync(nkp, h->d_nkp.as<int32_t>() + first, (size_t)count * 4,
+                                     hipMemcpyDeviceToHost, st)))
         return ORBX_ERR_DEVICE;
-    if (kps && !HIPOK(hipMemcpy(kps, h->d_kps.as<orbx_keypoint>() + first * KC,
-                                (size_t)count * KC * sizeof(orbx_keypoint), hipMemcpyDeviceToHost)))
+    if (kps && !HIPOK(hipMemcpyAsync(kps, h->d_kps.as<orbx_keypoint>() + first * KC,
+                                     (size_t)count * KC * sizeof(orbx_keypoint),
+                                     hipMemcpyDeviceToHost, st)))
         return ORBX_ERR_DEVICE;
-    if (desc && !HIPOK(hipMemcpy(desc, h->d_desc.as<uint8_t>() + first * KC * 32,
-                                 (size_t)count * KC * 32, hipMemcpyDeviceToHost)))
+    if (desc && !HIPOK(hipMemcpyAsync(desc, h->d_desc.as<uint8_t>() + first * KC * 32,
+                                      (size_t)count * KC * 32, hipMemcpyDeviceToHost, st)))
         return ORBX_ERR_DEVICE;
-    return ORBX_OK;
+    return HIPOK(hipStreamSynchronize(st)) ? ORBX_OK : ORBX_ERR_DEVICE;
 }
 
 orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float mbf, float mb,
                               float* uRight, float* depth, int n_left, int* n_valid) {
     if (!left || !right || left == right) return ORBX_ERR_INVALID;
+    // both handles: the right pyramid is read, so neither may be re-extracted meanwhile
+    std::scoped_lock lk(left->mu, right->mu);
     if (!left->last_valid || !right->last_valid || left->last_batch != 1 || right->last_batch != 1)
         return ORBX_ERR_STATE;
-    std::lock_guard<std::mutex> lk(left->mu);
     (void)hipSetDevice(left->device);
     const size_t KC = (size_t)left->hg.kp_cap;
     if (!left->d_uR.ensure(KC * 4) || !left->d_dep.ensure(KC * 4) || !left->d_nv.ensure(16))
         return ORBX_ERR_DEVICE;
+    // results come back in one pinned block: [nkp, nvalid | uRight[KC] | depth[KC]]
+    const size_t o_u = 256, o_d = o_u + KC * 4;
+    if (!ensure_pinned(left->h_out, left->h_out_n, o_d + KC * 4)) return ORBX_ERR_DEVICE;
     hipStream_t st = left->stream;
-    if (!HIPOK(hipEventRecord(right->done, right->stream)) ||
-        !HIPOK(hipStreamWaitEvent(st, right->done, 0)))
-        return ORBX_ERR_DEVICE;
     orbx_status s = run_stereo(left, right, 1, 0, 0, mbf, mb, left->d_uR.as<float>(),
                                left->d_dep.as<float>(), left->d_nv.as<int>(), st);
     if (s != ORBX_OK) return s;
-    int n = 0, nv = 0;
-    if (!HIPOK(hipMemcpyAsync(&n, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(&nv, left->d_nv.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipStreamSynchronize(st)))
+    uint8_t* ho = left->h_out;
+    if (!HIPOK(hipMemcpyAsync(ho, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(ho + 4, left->d_nv.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(ho + o_u, left->d_uR.p, KC * 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(ho + o_d, left->d_dep.p, KC * 4, hipMemcpyDeviceToHost, st)) ||
+        !mark_done(left, st) || !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
+    int n = 0, nv = 0;
+    std::memcpy(&n, ho, 4);
+    std::memcpy(&nv, ho + 4, 4);
     const int m = std::min(n, n_left);
     if (m > 0) {
-        if ((uRight && !HIPOK(hipMemcpyAsync(uRight, left->d_uR.p, (size_t)m * 4, hipMemcpyDeviceToHost,
-                                      st))) ||
-            (depth && !HIPOK(hipMemcpyAsync(depth, left->d_dep.p, (size_t)m * 4, hipMemcpyDeviceToHost,
-                                     st))) ||
-            !HIPOK(hipStreamSynchronize(st)))
-            return ORBX_ERR_DEVICE;
+        if (uRight) std::memcpy(uRight, ho + o_u, (size_t)m * 4);
+        if (depth) std::memcpy(depth, ho + o_d, (size_t)m * 4);
     }
     if (n_valid) *n_valid = nv;
     return n > n_left ? ORBX_ERR_CAPACITY : ORBX_OK;
@@ -1050,6 +1137,7 @@ orbx_status orbx_stereo_match_batch_device(orbx_extractor* left, orbx_extractor*
                                            float mb, float* d_uRight, float* d_depth,
                                            int32_t* d_nvalid, void* stream) {
     if (!left || !right || left == right || !d_uRight || !d_depth) return ORBX_ERR_INVALID;
+    std::scoped_lock lk(left->mu, right->mu);
     (void)hipSetDevice(left->device);
     if (left->last_batch != right->last_batch) return ORBX_ERR_INVALID;
     return run_stereo(left, right, left->last_batch, 0, 0, mbf, mb, d_uRight, d_depth, d_nvalid,

@@ -9,6 +9,8 @@
 // float (fastAtan2, the BRIEF rotation, the blur's SSE2 column pass); the library is built
 // with -ffp-contract=off so each of those is a separately rounded v_mul/v_add, as on x86.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 #include "orbx_device.h"
@@ -1459,19 +1461,35 @@ size_t octree_lds_bytes(int ncap, int kcap) {
 namespace orbx {
 hipError_t prepare_stereo(size_t lds);
 hipError_t prepare_level(size_t lds);
-// Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).
+// Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).  The
+// attribute is process-wide and only ever raised (to the largest size any handle needs), under
+// a lock: handles on several host threads may prepare concurrently.
 hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
                            size_t fast_lds) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_octree<256>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
-    for (const void* k : {(const void*)k_octree<64>, (const void*)k_octree<128>, (const void*)k_octree<512>})
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
-    if (e == hipSuccess)
+    static std::mutex mu;
+    static size_t have[4] = {0, 0, 0, 0};
+    std::lock_guard<std::mutex> lk(mu);
+    hipError_t e = hipSuccess;
+    if (octree_lds > have[0]) {
+        for (const void* k : {(const void*)k_octree<256>, (const void*)k_octree<64>,
+                              (const void*)k_octree<128>, (const void*)k_octree<512>})
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)octree_lds);
+        if (e == hipSuccess) have[0] = octree_lds;
+    }
+    if (e == hipSuccess && fast_lds > have[1]) {
         e = hipFuncSetAttribute((const void*)k_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)fast_lds);
-    if (e == hipSuccess) e = prepare_level(level_lds);
-    if (e != hipSuccess) return e;
-    return prepare_stereo(stereo_lds);
+        if (e == hipSuccess) have[1] = fast_lds;
+    }
+    if (e == hipSuccess && level_lds > have[2]) {
+        e = prepare_level(level_lds);
+        if (e == hipSuccess) have[2] = level_lds;
+    }
+    if (e == hipSuccess && stereo_lds > have[3]) {
+        e = prepare_stereo(stereo_lds);
+        if (e == hipSuccess) have[3] = stereo_lds;
+    }
+    return e;
 }
 }  // namespace orbx

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <mutex>
+#include <vector>
 
 #include "../../include/orbx_frame.h"
 #include "orbx_device.h"
@@ -176,6 +178,47 @@ __global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ src, i
     for (int j = 0; j < nx; ++j) d[j] = (uint8_t)(out >> (8 * j));
 }
 
+// Device staging of the host-array entry points: a pool of (device, non-blocking stream,
+// growable buffer) slots taken for the length of one call.  After warm-up a call allocates
+// nothing, and it waits only for its own stream, never for the device (the reference calls
+// these from the Tracking thread while LocalMapping / LoopClosing run matchers).
+struct Scratch {
+    int device = -1;
+    hipStream_t st = nullptr;
+    DevBuf buf;
+};
+std::mutex g_scratch_mu;
+std::vector<Scratch*> g_scratch_free;
+
+struct ScratchLease {
+    Scratch* s = nullptr;
+    explicit ScratchLease(int device) {
+        {
+            std::lock_guard<std::mutex> lk(g_scratch_mu);
+            for (size_t i = 0; i < g_scratch_free.size(); ++i)
+                if (g_scratch_free[i]->device == device) {
+                    s = g_scratch_free[i];
+                    g_scratch_free.erase(g_scratch_free.begin() + i);
+                    break;
+                }
+        }
+        if (!s) {
+            Scratch* n = new Scratch();
+            n->device = device;
+            if (!HIPOK(hipStreamCreateWithFlags(&n->st, hipStreamNonBlocking))) {
+                delete n;
+                return;
+            }
+            s = n;
+        }
+    }
+    ~ScratchLease() {
+        if (!s) return;
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        g_scratch_free.push_back(s);   // slots live for the process (no teardown-order hazards)
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -202,20 +245,21 @@ orbx_status orbx_cvt_color(const uint8_t* src, int32_t width, int32_t height, si
         return ORBX_ERR_INVALID;
     if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
     const size_t sb = (size_t)width * channels * height, db = (size_t)width * height;
-    DevBuf buf;
-    if (!buf.ensure(sb + db)) return ORBX_ERR_DEVICE;
-    uint8_t* ds = buf.as<uint8_t>();
+    ScratchLease L(device);
+    if (!L.s || !L.s->buf.ensure(sb + db)) return ORBX_ERR_DEVICE;
+    hipStream_t st = L.s->st;
+    uint8_t* ds = L.s->buf.as<uint8_t>();
     orbx_status s = ORBX_OK;
-    if (!HIPOK(hipMemcpy2D(ds, (size_t)width * channels, src, src_stride, (size_t)width * channels,
-                           height, hipMemcpyHostToDevice)))
+    if (!HIPOK(hipMemcpy2DAsync(ds, (size_t)width * channels, src, src_stride,
+                                (size_t)width * channels, height, hipMemcpyHostToDevice, st)))
         s = ORBX_ERR_DEVICE;
     if (s == ORBX_OK)
         s = orbx_cvt_color_device(ds, width, height, (size_t)width * channels, channels, rgb,
-                                  ds + sb, width, nullptr);
-    if (s == ORBX_OK && !HIPOK(hipMemcpy2D(dst, dst_stride, ds + sb, width, width, height,
-                                           hipMemcpyDeviceToHost)))
+                                  ds + sb, width, st);
+    if (s == ORBX_OK && !HIPOK(hipMemcpy2DAsync(dst, dst_stride, ds + sb, width, width, height,
+                                                hipMemcpyDeviceToHost, st)))
         s = ORBX_ERR_DEVICE;
-    buf.release();
+    if (!HIPOK(hipStreamSynchronize(st))) s = ORBX_ERR_DEVICE;
     return s;
 }
 
@@ -240,14 +284,17 @@ orbx_status orbx_undistort_keypoints(const float* K4, const float* dist, int32_t
         return ORBX_ERR_INVALID;
     if (n == 0) return ORBX_OK;
     if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
-    orbx_keypoint* d = nullptr;
     const size_t bytes = sizeof(orbx_keypoint) * (size_t)n;
-    if (!HIPOK(hipMalloc((void**)&d, bytes))) return ORBX_ERR_DEVICE;
+    ScratchLease L(device);
+    if (!L.s || !L.s->buf.ensure(bytes)) return ORBX_ERR_DEVICE;
+    hipStream_t st = L.s->st;
+    orbx_keypoint* d = L.s->buf.as<orbx_keypoint>();
     orbx_status s = ORBX_OK;
-    if (!HIPOK(hipMemcpy(d, kps, bytes, hipMemcpyHostToDevice))) s = ORBX_ERR_DEVICE;
-    if (s == ORBX_OK) s = orbx_undistort_keypoints_device(K4, dist, ndist, d, n, d, nullptr);
-    if (s == ORBX_OK && !HIPOK(hipMemcpy(kps_un, d, bytes, hipMemcpyDeviceToHost))) s = ORBX_ERR_DEVICE;
-    (void)hipFree(d);
+    if (!HIPOK(hipMemcpyAsync(d, kps, bytes, hipMemcpyHostToDevice, st))) s = ORBX_ERR_DEVICE;
+    if (s == ORBX_OK) s = orbx_undistort_keypoints_device(K4, dist, ndist, d, n, d, st);
+    if (s == ORBX_OK && !HIPOK(hipMemcpyAsync(kps_un, d, bytes, hipMemcpyDeviceToHost, st)))
+        s = ORBX_ERR_DEVICE;
+    if (!HIPOK(hipStreamSynchronize(st))) s = ORBX_ERR_DEVICE;
     return s;
 }
 

@@ -46,8 +46,8 @@ struct LevelGeom {
     // k_level_strip (orbx_pyramid.hip): column strips walked row by row
     int strip;              // 1: this level runs k_level_strip, 0: the tiled k_level
     int snh;                // half-wave strips across (SW_PX output pixels each)
-    int snw, sns;           // waves across (ceil(snh / 2)) / strip rows
-    int sth;                // output rows per strip
+    int snw;                // waves across (ceil(snh / 2)); the strip height (rows per strip)
+                            // is a launch argument chosen per call from its batch size
     int stab, srow;         // byte offsets of the strip lane table / row table in ltab
 };
 

@@ -98,6 +98,9 @@ struct ExtractLaunch {
     uint8_t* desc;
     int* nkp;
     KernelTimer* timer;
+    // k_level_strip output rows per strip of each level for this call's batch (a kernel
+    // argument: a batch-size change needs no device-side table update)
+    int sth[ORBX_MAX_LEVELS];
 };
 
 struct StereoLaunch {

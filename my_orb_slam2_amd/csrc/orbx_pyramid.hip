@@ -790,7 +790,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
                                                      const uint8_t* __restrict__ in1, int split,
                                                      size_t stride, size_t bstride,
                                                      uint8_t* __restrict__ pyr,
-                                                     uint8_t* __restrict__ blur, int level) {
+                                                     uint8_t* __restrict__ blur, int level,
+                                                     int sth) {
     static_assert(MODE == 0 || MODE == 3, "strip kernel: level 0 or INTER_LINEAR levels");
     int bx, b;
     xcd_block(bx, b);
@@ -799,14 +800,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // wave of this image; readfirstlane makes it (and the strip row, the row counters and the
     // row addresses derived from it) scalar for the compiler, not per-lane VALU work
     const int wv = bx * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (wv >= L.snw * L.sns) return;              // whole waves only
+    const int sns = (L.h + sth - 1) / sth;        // strip rows of this call's height
+    if (wv >= L.snw * sns) return;                // whole waves only
     const int swx = wv % L.snw, sy = wv / L.snw;
     const int hs = 2 * swx + half;
     const bool hvalid = hs < L.snh;
     const int hsc = min(hs, L.snh - 1);
     const int W = L.w, H = L.h, pitch = L.pitch;
     const int x = hsc * SW_PX - 4 + 4 * l32;      // this lane's group
-    const int Y0 = sy * L.sth, vh = min(L.sth, H - Y0);
+    const int Y0 = sy * sth, vh = min(sth, H - Y0);
     const bool out_lane = hvalid && l32 >= 1 && l32 <= SW_OUT && x < W;
     const StripLane* T = (const StripLane*)(ltab + L.stab) + hsc * 32 + l32;
     const uint4 t0 = *(const uint4*)T;
@@ -818,10 +820,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // Addresses are a wave-uniform row base (SGPRs) + a lane offset that is constant over the
     // walk, so loads and stores take the saddr forms and a step spends no VALU on 64-bit
     // address arithmetic.
-    const uint8_t* src;   // mode 0: 4 bytes before the image (lane offsets stay unsigned)
+    const uint8_t* src;   // mode 0: the image (a row's loads start 4 bytes before the row)
     size_t spitch;
     if (MODE == 0) {
-        src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride) - 4;
+        src = b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride;
         spitch = stride;
     } else {
         const LevelGeom& S = g->lv[level - 1];
@@ -872,14 +874,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         const int ic = min(i, n - 1);
         const uint4 ri = row_info(ic);
         if (MODE == 0) {
-            const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;   // row - 4
-            const uint32_t rlo = (uint32_t)(uintptr_t)rowp;
+            // offsets relative to row - 4 (unsigned); the pointers formed are the load
+            // addresses themselves: the aligned dwords holding the group's bytes, which start
+            // before the tensor only when its first row does not start on a dword
+            const uint8_t* rowp = src + (size_t)(ri.x & 0xFFFFu) * spitch;
+            const uint32_t rlo = (uint32_t)(uintptr_t)rowp - 4u;
             const uint32_t o = (rlo + xoff4) & 3u;
             const uint32_t aoff = xoff4 - o;
             // the last dword holding a byte of the row (no read past the image)
             const uint32_t last = ((rlo + 4u + (uint32_t)(W - 1)) & ~3u) - rlo;
-            A[slot][0] = *(const uint32_t*)(rowp + aoff);
-            A[slot][1] = *(const uint32_t*)(rowp + min(aoff + 4u, last));
+            A[slot][0] = *(const uint32_t*)(rowp + aoff - 4);
+            A[slot][1] = *(const uint32_t*)(rowp + min(aoff + 4u, last) - 4);
             // t0.z + o in every byte (no carries: bytes <= 4 + 3): o replicated by one v_perm
             A[slot][2] = t0.z + __builtin_amdgcn_perm(0u, o, 0u);
         } else {
@@ -1115,10 +1120,11 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
         hipEvent_t e = l == 0 ? T.start(st) : T.start_after(st);
         const int mode = level_mode(L, l);
         if (L.strip) {
+            const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;
             hipLaunchKernelGGL(mode == 0 ? k_level_strip<0> : k_level_strip<3>,
-                               dim3((L.snw * L.sns + 3) / 4, a.batch), dim3(256), 0, st, a.dg,
+                               dim3((L.snw * sns + 3) / 4, a.batch), dim3(256), 0, st, a.dg,
                                a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
-                               a.pyr, a.blur, l);
+                               a.pyr, a.blur, l, sth);
         } else {
             hipLaunchKernelGGL(level_kernel(mode), dim3(L.ntx * L.nty, a.batch), dim3(256),
                                a.level_lds, st, a.dg, a.ltab, a.d_imgs, a.d_imgs2, a.split,

@@ -321,9 +321,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
                 vsad[pos] = bestDist;
                 vidx[pos] = (int16_t)iL;
             } else {
+                // a pair has at most KC accepted SADs; the guard keeps a corrupted counter from
+                // writing past the pair's slots
                 const int pos = atomicAdd(&scnt[b], 1);
-                ssad[(size_t)b * KC + pos] = bestDist;
-                sidx[(size_t)b * KC + pos] = (int16_t)iL;
+                if (pos < KC) {
+                    ssad[(size_t)b * KC + pos] = bestDist;
+                    sidx[(size_t)b * KC + pos] = (int16_t)iL;
+                }
             }
         }
     }
@@ -399,7 +403,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo_cut(const Geometry* __res
     __shared__ int tmp[32];
     const int b = blockIdx.x;
     const size_t KC = (size_t)g->kp_cap;
-    const int nv = scnt[b];
+    const int nv = min(scnt[b], (int)KC);
     __syncthreads();
     if (threadIdx.x == 0) scnt[b] = 0;
     median_cut(nv, ssad + b * KC, sidx + b * KC, hist, tmp, uRight + b * KC, depth + b * KC,

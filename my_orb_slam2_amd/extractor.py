@@ -163,6 +163,15 @@ class ORBextractor:
                                                             ptr(kps), ptr(desc)))
         return nkp, kps, desc
 
+    def launch_info(self, batch: int):
+        """(strip rows per level, stereo workgroups per pair) of a batched call of `batch`
+        images at the prepared size (include/orbx.h orbx_extractor_launch_info)."""
+        rows = np.zeros(self.nlevels, np.int32)
+        split = ctypes.c_int(0)
+        check("orbx_extractor_launch_info", self._L.orbx_extractor_launch_info(
+            self._h, batch, ptr(rows), ctypes.byref(split)))
+        return rows, split.value
+
     def batch_view(self) -> BatchView:
         v = BatchView()
         check("orbx_batch_view_get", self._L.orbx_batch_view_get(self._h, ctypes.byref(v)))

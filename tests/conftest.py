@@ -22,12 +22,17 @@ def oracle_mod():
 
 @pytest.fixture(scope="session")
 def orbx_lib():
-    """liborbx.so, built in-tree if missing (hipcc cross-compiles without a GPU)."""
+    """liborbx.so, rebuilt in-tree when missing or stale (hipcc cross-compiles without a GPU).
+    Staleness is by content: the library carries a hash of the sources it was built from, so
+    a library that does not match the tree under test is never tested."""
     from my_orb_slam2_amd import build as b
-    if not b.LIB.exists():
+    if b.stale():
+        print(f"{b.LIB} is missing or stale: rebuilding", file=sys.stderr, flush=True)
         b.build()
     from my_orb_slam2_amd import _lib
-    return _lib.load()
+    L = _lib.load()
+    assert b.source_hash() in L.orbx_version().decode(), "loaded library is not this tree's"
+    return L
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,315 @@
+// boundary_test.cpp — a C++ consumer of the drop-in boundary, compiled by g++ against
+// include/orbx*.h only and linked to liborbx.so (no HIP headers, no torch, no ctypes).
+//
+//   boundary_test layout        struct sizes / field offsets as JSON (no GPU; the CPU suite
+//                               compares them with the Python ctypes mirrors)
+//   boundary_test run DIR       the sequence INTEGRATION.md installs into ORB-SLAM2, on the GPU:
+//     * two ORBextractor handles, the left and right images extracted on two std::threads
+//       (Frame::Frame stereo, src/Frame.cc:89-92) through orbx_extract;
+//     * Frame::ComputeStereoMatches (src/Frame.cc:102) through orbx_stereo_match;
+//     * ORBmatcher(0.75, true).SearchByBoW(KF = right view, F = left view) (src/ORBmatcher.cc:
+//       182-319, single-node FeatureVector: the brute-force anchor of SURVEY 8c);
+//     * ORBmatcher(0.6, false).SearchForTriangulation(left, right, F12) (:702-872).
+//   DIR holds left.raw / right.raw (W*H bytes) and params.txt ("W H nfeatures mbf mb ex ey
+//   F12[9]"); the outputs are written back to DIR as raw little-endian arrays.
+#include <algorithm>
+#include <chrono>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "orbx.h"
+#include "orbx_frame.h"
+#include "orbx_match.h"
+#include "orbx_vocab.h"
+
+// cv::KeyPoint as OpenCV 3.2 lays it out (core/types.hpp: Point2f pt; float size, angle,
+// response; int octave, class_id): the facade of INTEGRATION.md hands a
+// std::vector<cv::KeyPoint>'s buffer to orbx_extract, so the layouts must agree byte for byte.
+struct CvPoint2f { float x, y; };
+struct CvKeyPointShape {
+    CvPoint2f pt;
+    float size, angle, response;
+    int octave, class_id;
+};
+static_assert(sizeof(orbx_keypoint) == 28, "orbx_keypoint is 28 bytes");
+static_assert(sizeof(orbx_keypoint) == sizeof(CvKeyPointShape), "cv::KeyPoint size");
+static_assert(offsetof(orbx_keypoint, x) == offsetof(CvKeyPointShape, pt) + offsetof(CvPoint2f, x), "pt.x");
+static_assert(offsetof(orbx_keypoint, y) == offsetof(CvKeyPointShape, pt) + offsetof(CvPoint2f, y), "pt.y");
+static_assert(offsetof(orbx_keypoint, size) == offsetof(CvKeyPointShape, size), "size");
+static_assert(offsetof(orbx_keypoint, angle) == offsetof(CvKeyPointShape, angle), "angle");
+static_assert(offsetof(orbx_keypoint, response) == offsetof(CvKeyPointShape, response), "response");
+static_assert(offsetof(orbx_keypoint, octave) == offsetof(CvKeyPointShape, octave), "octave");
+static_assert(offsetof(orbx_keypoint, class_id) == offsetof(CvKeyPointShape, class_id), "class_id");
+static_assert(alignof(orbx_keypoint) == alignof(CvKeyPointShape), "alignment");
+
+#define FIELD(T, f) std::printf("%s\"%s\": [%zu, %zu]", first ? "" : ", ", #f, offsetof(T, f), sizeof(((T*)0)->f)), first = false
+#define STRUCT(T, ...)                                                     \
+    do {                                                                   \
+        std::printf("%s\"%s\": {\"size\": %zu, \"fields\": {", nfirst ? "" : ", ", #T, sizeof(T)); \
+        bool first = true;                                                 \
+        __VA_ARGS__;                                                       \
+        std::printf("}}");                                                 \
+        nfirst = false;                                                    \
+    } while (0)
+
+static int layout() {
+    bool nfirst = true;
+    std::printf("{");
+    STRUCT(orbx_keypoint, FIELD(orbx_keypoint, x); FIELD(orbx_keypoint, y); FIELD(orbx_keypoint, size);
+           FIELD(orbx_keypoint, angle); FIELD(orbx_keypoint, response); FIELD(orbx_keypoint, octave);
+           FIELD(orbx_keypoint, class_id));
+    STRUCT(orbx_extractor_params, FIELD(orbx_extractor_params, nfeatures);
+           FIELD(orbx_extractor_params, scale_factor); FIELD(orbx_extractor_params, nlevels);
+           FIELD(orbx_extractor_params, ini_th_fast); FIELD(orbx_extractor_params, min_th_fast);
+           FIELD(orbx_extractor_params, cv_simd); FIELD(orbx_extractor_params, max_batch);
+           FIELD(orbx_extractor_params, device));
+    STRUCT(orbx_batch_view, FIELD(orbx_batch_view, batch); FIELD(orbx_batch_view, kp_cap);
+           FIELD(orbx_batch_view, kps); FIELD(orbx_batch_view, desc); FIELD(orbx_batch_view, nkp);
+           FIELD(orbx_batch_view, pyramid); FIELD(orbx_batch_view, pyr_bytes);
+           FIELD(orbx_batch_view, level_w); FIELD(orbx_batch_view, level_h);
+           FIELD(orbx_batch_view, level_pitch); FIELD(orbx_batch_view, level_off));
+    STRUCT(orbx_featureset, FIELD(orbx_featureset, n); FIELD(orbx_featureset, keys);
+           FIELD(orbx_featureset, desc); FIELD(orbx_featureset, u_right);
+           FIELD(orbx_featureset, n_nodes); FIELD(orbx_featureset, node_id);
+           FIELD(orbx_featureset, node_off); FIELD(orbx_featureset, node_feat);
+           FIELD(orbx_featureset, grid_cols); FIELD(orbx_featureset, grid_rows);
+           FIELD(orbx_featureset, grid_off); FIELD(orbx_featureset, grid_feat);
+           FIELD(orbx_featureset, min_x); FIELD(orbx_featureset, min_y);
+           FIELD(orbx_featureset, max_x); FIELD(orbx_featureset, max_y);
+           FIELD(orbx_featureset, grid_inv_w); FIELD(orbx_featureset, grid_inv_h));
+    STRUCT(orbx_matcher_params, FIELD(orbx_matcher_params, nnratio);
+           FIELD(orbx_matcher_params, check_orientation); FIELD(orbx_matcher_params, device));
+    STRUCT(orbx_kf_db, FIELD(orbx_kf_db, nkf); FIELD(orbx_kf_db, max_feat); FIELD(orbx_kf_db, feat_off);
+           FIELD(orbx_kf_db, keys); FIELD(orbx_kf_db, desc); FIELD(orbx_kf_db, u_right);
+           FIELD(orbx_kf_db, flag); FIELD(orbx_kf_db, node_off); FIELD(orbx_kf_db, node_id);
+           FIELD(orbx_kf_db, node_feat_off); FIELD(orbx_kf_db, node_feat));
+    STRUCT(orbx_proj_query, FIELD(orbx_proj_query, u); FIELD(orbx_proj_query, v);
+           FIELD(orbx_proj_query, ur); FIELD(orbx_proj_query, radius);
+           FIELD(orbx_proj_query, min_level); FIELD(orbx_proj_query, max_level);
+           FIELD(orbx_proj_query, pred_level); FIELD(orbx_proj_query, angle));
+    std::printf("}\n");
+    return 0;
+}
+
+static bool read_file(const std::string& path, std::vector<uint8_t>& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize((size_t)n);
+    const bool ok = std::fread(out.data(), 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok;
+}
+
+static bool write_file(const std::string& path, const void* p, size_t n) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = n == 0 || std::fwrite(p, 1, n, f) == n;
+    std::fclose(f);
+    return ok;
+}
+
+#define CHECK(call)                                                                      \
+    do {                                                                                 \
+        const orbx_status s_ = (call);                                                   \
+        if (s_ != ORBX_OK) {                                                             \
+            std::fprintf(stderr, "%s failed: %d [%s]\n", #call, (int)s_, orbx_last_error()); \
+            return 1;                                                                    \
+        }                                                                                \
+    } while (0)
+
+// One view as ORB_SLAM2::Frame holds it after ExtractORB (mvKeys, mDescriptors).
+struct View {
+    std::vector<orbx_keypoint> kps;
+    std::vector<uint8_t> desc;
+    int n = 0;
+    orbx_status st = ORBX_OK;
+};
+
+static void extract(orbx_extractor* h, const uint8_t* img, int w, int hgt, View* v) {
+    // the facade's ORBextractor::operator(): size the vectors from the call's count
+    int n = 0;
+    v->kps.resize(4096);
+    v->desc.resize(4096 * 32);
+    v->st = orbx_extract(h, img, w, hgt, (size_t)w, v->kps.data(), 4096, v->desc.data(), &n);
+    if (v->st == ORBX_ERR_CAPACITY) {
+        v->kps.resize((size_t)n);
+        v->desc.resize((size_t)n * 32);
+        v->st = orbx_extract(h, img, w, hgt, (size_t)w, v->kps.data(), n, v->desc.data(), &n);
+    }
+    v->n = n;
+    v->kps.resize((size_t)std::max(n, 0));
+    v->desc.resize((size_t)std::max(n, 0) * 32);
+}
+
+static orbx_featureset single_node(const View& v, std::vector<int32_t>& feat, const uint32_t* id,
+                                   const int32_t* off) {
+    orbx_featureset f;
+    std::memset(&f, 0, sizeof(f));
+    feat.resize((size_t)v.n);
+    for (int i = 0; i < v.n; ++i) feat[(size_t)i] = i;
+    f.n = v.n;
+    f.keys = v.kps.data();
+    f.desc = v.desc.data();
+    f.u_right = nullptr;
+    f.n_nodes = 1;
+    f.node_id = id;
+    f.node_off = off;
+    f.node_feat = feat.data();
+    return f;
+}
+
+static int run(const std::string& dir) {
+    int W = 0, H = 0, nfeat = 0;
+    float mbf = 0, mb = 0, ex = 0, ey = 0, F12[9];
+    {
+        FILE* f = std::fopen((dir + "/params.txt").c_str(), "r");
+        if (!f) return 2;
+        int got = std::fscanf(f, "%d %d %d %f %f %f %f", &W, &H, &nfeat, &mbf, &mb, &ex, &ey);
+        for (int i = 0; i < 9; ++i) got += std::fscanf(f, "%f", &F12[i]);
+        std::fclose(f);
+        if (got != 16) return 2;
+    }
+    std::vector<uint8_t> L, R;
+    if (!read_file(dir + "/left.raw", L) || !read_file(dir + "/right.raw", R) ||
+        L.size() != (size_t)W * H || R.size() != (size_t)W * H)
+        return 2;
+    std::printf("%s\n", orbx_version());
+
+    // Tracking.cc:136-139: one extractor per camera, same parameters
+    orbx_extractor_params p = {nfeat, 1.2f, 8, 20, 7, 1, 1, 0};
+    orbx_extractor *hl = nullptr, *hr = nullptr;
+    CHECK(orbx_extractor_create(&p, &hl));
+    CHECK(orbx_extractor_create(&p, &hr));
+    View vl, vr;
+    {   // Frame.cc:89-92
+        std::thread tl(extract, hl, L.data(), W, H, &vl);
+        std::thread tr(extract, hr, R.data(), W, H, &vr);
+        tl.join();
+        tr.join();
+    }
+    CHECK(vl.st);
+    CHECK(vr.st);
+    std::vector<float> uR((size_t)vl.n), depth((size_t)vl.n);
+    int nvalid = 0;
+    CHECK(orbx_stereo_match(hl, hr, mbf, mb, uR.data(), depth.data(), vl.n, &nvalid));
+
+    // matchers (LocalMapping / Tracking own their ORBmatcher objects)
+    const uint32_t node_id[1] = {0};
+    std::vector<int32_t> fl, fr;
+    const int32_t offl[2] = {0, vl.n}, offr[2] = {0, vr.n};
+    const orbx_featureset F = single_node(vl, fl, node_id, offl);
+    const orbx_featureset KF = single_node(vr, fr, node_id, offr);
+    orbx_matcher *mbow = nullptr, *mtri = nullptr;
+    const orbx_matcher_params pb = {0.75f, 1, 0}, pt = {0.6f, 0, 0};
+    CHECK(orbx_matcher_create(&pb, &mbow));
+    CHECK(orbx_matcher_create(&pt, &mtri));
+    std::vector<uint8_t> valid((size_t)vr.n, 1);
+    std::vector<int32_t> bow(1 + (size_t)vl.n);
+    CHECK(orbx_search_by_bow_kf_frame(mbow, &KF, valid.data(), &F, bow.data() + 1, bow.data()));
+    // scale tables of the extractor (mvLevelSigma2 / mvScaleFactors of KF2)
+    float scale[8], sigma2[8];
+    CHECK(orbx_extractor_tables(hr, scale, nullptr, sigma2, nullptr, nullptr));
+    std::vector<uint8_t> has1((size_t)vl.n, 0), has2((size_t)vr.n, 0);
+    std::vector<int32_t> tri(1 + 2 * (size_t)vl.n);
+    CHECK(orbx_search_for_triangulation(mtri, &F, has1.data(), &KF, has2.data(), F12, ex, ey,
+                                        sigma2, scale, 8, 0, tri.data() + 1, vl.n, tri.data()));
+
+    const int nl = vl.n, nr = vr.n;
+    bool ok = write_file(dir + "/n.bin", &nl, 4) && write_file(dir + "/nr.bin", &nr, 4) &&
+              write_file(dir + "/nvalid.bin", &nvalid, 4) &&
+              write_file(dir + "/kps_left.bin", vl.kps.data(), vl.kps.size() * 28) &&
+              write_file(dir + "/desc_left.bin", vl.desc.data(), vl.desc.size()) &&
+              write_file(dir + "/kps_right.bin", vr.kps.data(), vr.kps.size() * 28) &&
+              write_file(dir + "/desc_right.bin", vr.desc.data(), vr.desc.size()) &&
+              write_file(dir + "/uRight.bin", uR.data(), uR.size() * 4) &&
+              write_file(dir + "/depth.bin", depth.data(), depth.size() * 4) &&
+              write_file(dir + "/bow.bin", bow.data(), bow.size() * 4) &&
+              write_file(dir + "/tri.bin", tri.data(), (1 + 2 * (size_t)tri[0]) * 4);
+    orbx_matcher_destroy(mbow);
+    orbx_matcher_destroy(mtri);
+    orbx_extractor_destroy(hl);
+    orbx_extractor_destroy(hr);
+    std::printf("boundary_test: %d / %d keypoints, %d stereo, %d bow, %d triangulation\n", nl, nr,
+                nvalid, bow[0], tri[0]);
+    return ok ? 0 : 3;
+}
+
+// Per-stereo-frame latency of the drop-in path as ORB-SLAM2's Tracking thread sees it
+// (bench.py --workload dropin): per frame, Frame::Frame's two std::threads run ExtractORB on
+// the left and right images (Frame.cc:89-92), then ComputeStereoMatches (:102); host images
+// in, host keypoints / descriptors / uRight / depth out.  DIR holds P pairs
+// (pair_<i>_left.raw, pair_<i>_right.raw) and params.txt ("W H nfeatures mbf mb P"); frame f
+// uses pair f % P.  Prints one JSON line with every frame's latency after `warmup` frames,
+// timed with steady_clock like Examples/Stereo/stereo_kitti.cc:80-98.
+static int bench(const std::string& dir, int nframes, int warmup) {
+    int W = 0, H = 0, nfeat = 0, P = 0;
+    float mbf = 0, mb = 0;
+    {
+        FILE* f = std::fopen((dir + "/params.txt").c_str(), "r");
+        if (!f) return 2;
+        const int got = std::fscanf(f, "%d %d %d %f %f %d", &W, &H, &nfeat, &mbf, &mb, &P);
+        std::fclose(f);
+        if (got != 6 || P < 1) return 2;
+    }
+    std::vector<std::vector<uint8_t>> Ls((size_t)P), Rs((size_t)P);
+    for (int i = 0; i < P; ++i) {
+        const std::string b = dir + "/pair_" + std::to_string(i);
+        if (!read_file(b + "_left.raw", Ls[(size_t)i]) || !read_file(b + "_right.raw", Rs[(size_t)i]) ||
+            Ls[(size_t)i].size() != (size_t)W * H || Rs[(size_t)i].size() != (size_t)W * H)
+            return 2;
+    }
+    orbx_extractor_params p = {nfeat, 1.2f, 8, 20, 7, 1, 1, 0};
+    orbx_extractor *hl = nullptr, *hr = nullptr;
+    CHECK(orbx_extractor_create(&p, &hl));
+    CHECK(orbx_extractor_create(&p, &hr));
+    std::vector<double> ms;
+    std::vector<float> uR(4096), depth(4096);
+    long long kp_sum = 0, nv_sum = 0;
+    for (int f = 0; f < warmup + nframes; ++f) {
+        const int i = f % P;
+        View vl, vr;
+        const auto t0 = std::chrono::steady_clock::now();
+        std::thread tl(extract, hl, Ls[(size_t)i].data(), W, H, &vl);
+        std::thread tr(extract, hr, Rs[(size_t)i].data(), W, H, &vr);
+        tl.join();
+        tr.join();
+        CHECK(vl.st);
+        CHECK(vr.st);
+        int nvalid = 0;
+        if ((int)uR.size() < vl.n) { uR.resize((size_t)vl.n); depth.resize((size_t)vl.n); }
+        CHECK(orbx_stereo_match(hl, hr, mbf, mb, uR.data(), depth.data(), vl.n, &nvalid));
+        const auto t1 = std::chrono::steady_clock::now();
+        if (f >= warmup) {
+            ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            kp_sum += vl.n;
+            nv_sum += nvalid;
+        }
+    }
+    orbx_extractor_destroy(hl);
+    orbx_extractor_destroy(hr);
+    std::printf("{\"frames\": %d, \"warmup\": %d, \"mean_keypoints_left\": %.3f, "
+                "\"mean_stereo_matches\": %.3f, \"latency_ms\": [",
+                nframes, warmup, (double)kp_sum / std::max(nframes, 1),
+                (double)nv_sum / std::max(nframes, 1));
+    for (size_t k = 0; k < ms.size(); ++k) std::printf("%s%.4f", k ? ", " : "", ms[k]);
+    std::printf("]}\n");
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 2 && std::string(argv[1]) == "layout") return layout();
+    if (argc >= 3 && std::string(argv[1]) == "run") return run(argv[2]);
+    if (argc >= 5 && std::string(argv[1]) == "bench")
+        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
+    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP\n", argv[0]);
+    return 2;
+}

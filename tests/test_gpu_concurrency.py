@@ -1,0 +1,120 @@
+"""The host-image path under the reference's threading (src/System.cc:91-101, Frame.cc:89-92):
+per stereo frame two threads extract the left and right images on their own ORBextractor
+handles while a third thread (LocalMapping / LoopClosing) runs matcher calls on its own
+ORBmatcher, and a fourth runs batched device extractions on a torch stream.  Every result
+must be bit-identical to the same calls made one at a time."""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import assert_bytes_equal, assert_f32_bits_equal, assert_kps_equal
+from my_orb_slam2_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+MBF, FX = 386.1448, 718.856
+
+
+def test_concurrent_dropin_threads(orbx_lib, gpu):
+    import torch
+    import my_orb_slam2_amd as m
+    from my_orb_slam2_amd import ORBmatcher
+    mb = float(np.float32(MBF) / np.float32(FX))
+    frames = [synth.stereo_pair(700 + i, 1241, 376) for i in range(6)]
+    cases = [synth.feature_pair(710 + i, n1=1200, n2=1200) for i in range(4)]
+    tri = [synth.keyframe_pair(720 + i, n1=1500, n2=1500) for i in range(3)]
+    s, s2, _ = synth.scale_tables()
+    batch = torch.from_numpy(np.stack([synth.frame(730 + i, 640, 480) for i in range(8)])).to(gpu)
+
+    def frame_serial(gl, gr, L, R):
+        kl, dl = gl(L)
+        kr, dr = gr(R)
+        u, z, nv = m.compute_stereo_matches(gl, gr, MBF, mb)
+        return kl, dl, kr, dr, u, z, nv
+
+    def match_serial(mt, mt2):
+        out = []
+        for f1, f2, _ in cases:
+            out.append(mt.SearchByBoW(f1, np.ones(f1.n, bool), f2))
+        for k1, k2, F, epi, _ in tri:
+            out.append(mt2.SearchForTriangulation(k1, np.zeros(k1.n, bool), k2, np.zeros(k2.n, bool),
+                                                  F, epi, s2, s, False))
+        return out
+
+    def batch_serial(ext, st):
+        ext.extract_batch_device(batch, st)
+        return ext.batch_fetch()
+
+    gl, gr = m.ORBextractor(2000, 1.2, 8, 20, 7), m.ORBextractor(2000, 1.2, 8, 20, 7)
+    mt, mt2 = ORBmatcher(0.75, True), ORBmatcher(0.6, False)
+    bext = m.ORBextractor(1000, 1.2, 8, 20, 7, max_batch=8)
+    stream = torch.cuda.Stream(gpu)
+    ref_frames = [frame_serial(gl, gr, L, R) for L, R in frames]
+    ref_match = match_serial(mt, mt2)
+    ref_batch = batch_serial(bext, stream.cuda_stream)
+    torch.cuda.synchronize()
+
+    errors, got_match, got_batch = [], [], []
+    stop = threading.Event()
+
+    def mapping_thread():
+        try:
+            while not stop.is_set():
+                got_match.append(match_serial(mt, mt2))
+        except Exception as e:   # pragma: no cover - reported below
+            errors.append(e)
+
+    def batch_thread():
+        try:
+            while not stop.is_set():
+                got_batch.append(batch_serial(bext, stream.cuda_stream))
+        except Exception as e:   # pragma: no cover
+            errors.append(e)
+
+    side = [threading.Thread(target=mapping_thread), threading.Thread(target=batch_thread)]
+    for t in side:
+        t.start()
+    got_frames = []
+    try:
+        for rnd in range(3):
+            for L, R in frames:
+                res = {}
+
+                def ext(h, img, key):
+                    try:
+                        res[key] = h(img)
+                    except Exception as e:   # pragma: no cover
+                        errors.append(e)
+                tl = threading.Thread(target=ext, args=(gl, L, "l"))
+                tr = threading.Thread(target=ext, args=(gr, R, "r"))
+                tl.start()
+                tr.start()
+                tl.join()
+                tr.join()
+                u, z, nv = m.compute_stereo_matches(gl, gr, MBF, mb)
+                got_frames.append((*res["l"], *res["r"], u, z, nv))
+    finally:
+        stop.set()
+        for t in side:
+            t.join()
+    assert not errors, errors
+    assert len(got_match) >= 1 and len(got_batch) >= 1
+    for i, g in enumerate(got_frames):
+        r = ref_frames[i % len(frames)]
+        assert_kps_equal(g[0], r[0], f"frame {i} left")
+        assert_bytes_equal(g[1], r[1], f"frame {i} left desc")
+        assert_kps_equal(g[2], r[2], f"frame {i} right")
+        assert_bytes_equal(g[3], r[3], f"frame {i} right desc")
+        assert_f32_bits_equal(g[4], r[4], f"frame {i} uRight")
+        assert_f32_bits_equal(g[5], r[5], f"frame {i} depth")
+        assert g[6] == r[6]
+    for rnd in got_match:
+        for (n_g, m_g), (n_r, m_r) in zip(rnd, ref_match):
+            assert n_g == n_r
+            np.testing.assert_array_equal(m_g, m_r)
+    for nkp, kps, desc in got_batch:
+        assert np.array_equal(nkp, ref_batch[0])
+        for j in range(len(nkp)):
+            assert_kps_equal(kps[j, :nkp[j]], ref_batch[1][j, :nkp[j]], f"batch image {j}")
+            assert_bytes_equal(desc[j, :nkp[j]], ref_batch[2][j, :nkp[j]], f"batch image {j}")

@@ -233,8 +233,9 @@ def test_large_batch_equals_single_images(oracle_mod, orbx_lib, gpu):
 
 
 def test_stereo_split_equals_unsplit(orbx_lib, gpu):
-    """k_stereo splits a pair's left keypoints over two workgroups (median in k_stereo_cut)
-    when a call has at most 128 pairs, and keeps one workgroup per pair above that: 136 pairs
+    """k_stereo splits a pair's left keypoints over up to four workgroups (median in
+    k_stereo_cut) when a call has at most 128 pairs (8 pairs: 4 workgroups each), and keeps one
+    workgroup per pair above that: 136 pairs
     in one call (one workgroup per pair) give bit for bit the uRight / depth / counts of the
     same pairs in calls of 8 (split; those are checked against the oracle elsewhere)."""
     import torch
