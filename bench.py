@@ -73,7 +73,7 @@ def parse():
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
     ap.add_argument("--workload", default="stereo",
-                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin"],
+                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb"],
                     help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
                          "extract + SearchByProjection vs the local map); reloc = configs[3] "
                          "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
@@ -208,6 +208,8 @@ def main():
         return main_euroc(args)
     if args.workload == "dropin":
         return main_dropin(args)
+    if args.workload == "kfdb":
+        return main_kfdb(args)
     if args.workload != "stereo":
         return main_match(args)
     import torch
@@ -612,6 +614,73 @@ def main_dropin(args):
            "mean_stereo_matches": res["mean_stereo_matches"], "cpu_baseline": cpu}
     if cpu:
         out["speedup_vs_cpu_median"] = cpu["median_ms"] / lat["median_ms"]
+    emit(json.dumps(out))
+
+
+# ---- keyframe database candidate detection --------------------------------
+
+def main_kfdb(args):
+    """KeyFrameDatabase::DetectRelocalizationCandidates (KeyFrameDatabase.cc:220-337), the step
+    before configs[3]'s SearchByBoW loop (Tracking.cc:1447-1461), on a --kfs keyframe database
+    resident in HBM (synthetic BowVectors of ~300 words, 10 covisibles per keyframe).  One step
+    = one query frame: upload of its BowVector, the database scan, the selection, the
+    candidate list back on the host."""
+    from my_orb_slam2_amd import KeyFrameDatabase, synth
+    n = args.kfs
+    bows, cov, _ = synth.kfdb_scene(21, n_kf=n, revisit=n // 20)
+    db = KeyFrameDatabase(10)
+    for b in bows:
+        db.add(b)
+    for s, nb in enumerate(cov):
+        db.set_covisibles(s, nb)
+    rng = np.random.default_rng(5)
+    queries = [synth.kfdb_query(100 + q, bows[int(rng.integers(0, n))],
+                                keep=0.8 if q % 2 == 0 else 0.35) for q in range(64)]
+    for q in range(args.warmup):
+        db.DetectRelocalizationCandidates(queries[q % len(queries)])
+    scan, sel, ncand, wall = [], [], [], []
+    for q in range(args.steps):
+        t0 = time.perf_counter()
+        c = db.DetectRelocalizationCandidates(queries[q % len(queries)])
+        wall.append(1000.0 * (time.perf_counter() - t0))
+        a, b = db.last_timing()
+        scan.append(a)
+        sel.append(b)
+        ncand.append(len(c))
+    entries = sum(len(b[0]) for b in bows)
+    scan_ms = float(np.mean(scan))
+    scan_bytes = entries * 12 + n * 13          # words + weights, offsets / alive / outputs
+    cpu = None
+    if args.cpu_seconds > 0:
+        from oracle.kfdb import OracleKeyFrameDatabase
+        o = OracleKeyFrameDatabase(10)
+        for b in bows:
+            o.add(b)
+        for s, nb in enumerate(cov):
+            o.set_covisibles(s, nb)
+        ms, t_end = [], time.perf_counter() + min(args.cpu_seconds, 10.0)
+        while time.perf_counter() < t_end or len(ms) < 5:
+            t0 = time.perf_counter()
+            o.DetectRelocalizationCandidates(queries[len(ms) % len(queries)])
+            ms.append(1000.0 * (time.perf_counter() - t0))
+        cpu = {"value": 1000.0 / float(np.mean(ms)), "unit": "queries/sec", "cores": 1,
+               "kind": "port", "sample": f"{len(ms)} queries of the restated KeyFrameDatabase "
+               f"(inverted file, oracle/orb_kfdb_oracle.cpp) on {n} keyframes",
+               **latency_stats(ms)}
+    out = {"metric": f"DetectRelocalizationCandidates queries/sec, {n}-keyframe database",
+           "value": 1000.0 / float(np.mean(wall)), "unit": "queries/sec", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": float(np.mean(wall)),
+           "higher_is_better": True, "scaling": "none", "vs_baseline": None,
+           "dtype": "f64 (DBoW2 weights)", "data": "synthetic",
+           "config": {"workload": "kfdb_relocalisation_candidates", "keyframes": n,
+                      "bow_entries": entries, "covisibles": 10},
+           "latency": latency_stats(wall), "mean_candidates": float(np.mean(ncand)),
+           "kernel_ms": {"k_kfdb_scan": scan_ms, "k_kfdb_select": float(np.mean(sel))},
+           "roofline": {"kernel": "k_kfdb_scan", "bound": "hbm",
+                        "achieved": scan_bytes / (scan_ms / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": scan_bytes / (scan_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_launch": scan_bytes, "traffic": None},
+           "cpu_baseline": cpu}
     emit(json.dumps(out))
 
 

@@ -6,6 +6,7 @@ Host-side mirror of the reference's operator interface for this path:
 * ``compute_stereo_matches`` — Frame::ComputeStereoMatches (src/Frame.cc:496-686)
 * ``ORBmatcher`` — ORB_SLAM2::ORBmatcher descriptor matching (include/ORBmatcher.h)
 * ``Vocabulary`` — ORBVocabulary / DBoW2 transform (Frame::ComputeBoW, src/Frame.cc:420-427)
+* ``KeyFrameDatabase`` — ORB_SLAM2::KeyFrameDatabase candidate detection (src/KeyFrameDatabase.cc)
 
 Everything routes through liborbx.so (include/orbx.h).  There is no CPU fallback.
 """
@@ -15,6 +16,7 @@ from ._lib import KEYPOINT_DTYPE, OrbxError, load
 from .extractor import ORBextractor, compute_stereo_matches, StereoBatch
 from .matcher import ORBmatcher, descriptor_distance
 from .vocabulary import Vocabulary, bow_score_l1
+from .kfdb import KeyFrameDatabase
 
 __all__ = ["ORBextractor", "ORBmatcher", "compute_stereo_matches", "descriptor_distance",
-           "StereoBatch", "Vocabulary", "bow_score_l1", "KEYPOINT_DTYPE", "OrbxError", "load"]
+           "StereoBatch", "Vocabulary", "bow_score_l1", "KeyFrameDatabase", "KEYPOINT_DTYPE", "OrbxError", "load"]

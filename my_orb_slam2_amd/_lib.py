@@ -104,6 +104,18 @@ SIGNATURES = {
     "orbx_bow_score_l1": (ctypes.c_double, [_vp, _vp, _i, _vp, _vp, _i]),
     "orbx_bow_db_score": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _i]),
     "orbx_bow_db_score_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # include/orbx_kfdb.h
+    "orbx_kfdb_create": (_i, [_vp, ctypes.POINTER(_vp)]),
+    "orbx_kfdb_destroy": (_i, [_vp]),
+    "orbx_kfdb_add": (_i, [_vp, _vp, _vp, _i, ctypes.POINTER(_i)]),
+    "orbx_kfdb_erase": (_i, [_vp, _i]),
+    "orbx_kfdb_clear": (_i, [_vp]),
+    "orbx_kfdb_size": (_i, [_vp, ctypes.POINTER(_i)]),
+    "orbx_kfdb_set_covisibles": (_i, [_vp, _i, _vp, _i]),
+    "orbx_kfdb_detect_relocalization": (_i, [_vp, _vp, _vp, _i, _vp, _i, ctypes.POINTER(_i)]),
+    "orbx_kfdb_detect_loop": (_i, [_vp, _vp, _vp, _i, _vp, _i, _f, _vp, _i, ctypes.POINTER(_i)]),
+    "orbx_kfdb_last_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double)]),
     # include/orbx_frame.h
     "orbx_undistort_keypoints": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i]),
     "orbx_undistort_keypoints_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp]),

@@ -350,3 +350,53 @@ def write_vocabulary(path, k: int = 10, L: int = 3, seed: int = 0, scoring: int 
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
     return nid
+
+
+# ---- keyframe database scenes (KeyFrameDatabase, src/KeyFrameDatabase.cc) --------------------
+
+def _l1(values):
+    v = np.asarray(values, np.float64)
+    return v / v.sum() if len(v) else v
+
+
+def kfdb_scene(seed: int, n_kf: int = 2000, vocab: int = 100000, words: int = 300,
+               place: int = 600, window: int = 6, revisit: int = 0):
+    """A synthetic keyframe trajectory for the keyframe database: keyframe t draws 75 % of its
+    BowVector words from the word pool of its place (places drift along the trajectory, so
+    neighbouring keyframes share many words) and 25 % at random; weights are L1-normalised like
+    DBoW2's TF-IDF BowVectors.  With `revisit` > 0 the last `revisit` keyframes come back to the
+    places of the first ones (loop-closure candidates far away in time).  The covisibility
+    lists (KeyFrame::mvpOrderedConnectedKeyFrames) are the keyframes within `window` of t,
+    ordered by shared-word count descending (ties by index descending, the reference's
+    push_front of an ascending (weight, pointer) sort).  Returns (bows, covisibles, places)."""
+    rng = np.random.default_rng(seed)
+    n_places = max(2, n_kf // 4 + 2)
+    pools = [rng.choice(vocab, place, replace=False) for _ in range(n_places)]
+    place_of = np.minimum(np.arange(n_kf) // 4, n_places - 1)
+    if revisit:
+        place_of[n_kf - revisit:] = place_of[:revisit]
+    bows = []
+    for t in range(n_kf):
+        p = place_of[t]
+        own = rng.choice(pools[p], int(words * 0.75), replace=False)
+        nxt = rng.choice(pools[min(p + 1, n_places - 1)], words // 10, replace=False)
+        rnd = rng.choice(vocab, words - len(own) - len(nxt), replace=False)
+        w = np.unique(np.concatenate([own, nxt, rnd])).astype(np.uint32)
+        bows.append((w, _l1(rng.random(len(w)) + 0.05)))
+    sets = [set(b[0].tolist()) for b in bows]
+    cov = []
+    for t in range(n_kf):
+        cands = [u for u in range(max(0, t - window), min(n_kf, t + window + 1)) if u != t]
+        wts = [(len(sets[t] & sets[u]), u) for u in cands]
+        wts.sort()
+        cov.append([u for _, u in reversed(wts)])
+    return bows, cov, place_of
+
+
+def kfdb_query(seed: int, bow, keep: float = 0.7, extra: int = 80, vocab: int = 100000):
+    """A frame seen near a keyframe: `keep` of its words plus `extra` random words, weights
+    re-drawn and L1-normalised."""
+    rng = np.random.default_rng(seed)
+    w = bow[0][rng.random(len(bow[0])) < keep]
+    w = np.unique(np.concatenate([w, rng.choice(vocab, extra, replace=False)])).astype(np.uint32)
+    return w, _l1(rng.random(len(w)) + 0.05)

@@ -25,6 +25,7 @@
 
 #include "orbx.h"
 #include "orbx_frame.h"
+#include "orbx_kfdb.h"
 #include "orbx_match.h"
 #include "orbx_vocab.h"
 
@@ -93,6 +94,7 @@ static int layout() {
            FIELD(orbx_proj_query, ur); FIELD(orbx_proj_query, radius);
            FIELD(orbx_proj_query, min_level); FIELD(orbx_proj_query, max_level);
            FIELD(orbx_proj_query, pred_level); FIELD(orbx_proj_query, angle));
+    STRUCT(orbx_kfdb_params, FIELD(orbx_kfdb_params, covisibles); FIELD(orbx_kfdb_params, device));
     std::printf("}\n");
     return 0;
 }

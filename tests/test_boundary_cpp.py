@@ -39,6 +39,7 @@ def _dtype_layout(dt):
 def test_struct_layouts_match_python_mirrors(boundary_bin):
     from my_orb_slam2_amd._lib import KEYPOINT_DTYPE, BatchView, ExtractorParams
     from my_orb_slam2_amd.features import PROJ_QUERY_DTYPE, FeatureSetC
+    from my_orb_slam2_amd.kfdb import KfdbParams
     from my_orb_slam2_amd.matcher import KfDbC, MatcherParams
     import oracle
     from oracle import matcher as om
@@ -53,6 +54,7 @@ def test_struct_layouts_match_python_mirrors(boundary_bin):
         "orbx_matcher_params": [_ctypes_layout(MatcherParams)],
         "orbx_kf_db": [_ctypes_layout(KfDbC)],
         "orbx_proj_query": [_dtype_layout(PROJ_QUERY_DTYPE)],
+        "orbx_kfdb_params": [_ctypes_layout(KfdbParams)],
     }
     sizes = {"orbx_keypoint": [KEYPOINT_DTYPE.itemsize, oracle.KEYPOINT_DTYPE.itemsize],
              "orbx_extractor_params": [ctypes.sizeof(ExtractorParams)],
@@ -60,7 +62,8 @@ def test_struct_layouts_match_python_mirrors(boundary_bin):
              "orbx_featureset": [ctypes.sizeof(FeatureSetC), ctypes.sizeof(om._FeatC)],
              "orbx_matcher_params": [ctypes.sizeof(MatcherParams)],
              "orbx_kf_db": [ctypes.sizeof(KfDbC)],
-             "orbx_proj_query": [PROJ_QUERY_DTYPE.itemsize]}
+             "orbx_proj_query": [PROJ_QUERY_DTYPE.itemsize],
+             "orbx_kfdb_params": [ctypes.sizeof(KfdbParams)]}
     for name, lays in mirrors.items():
         assert name in c, name
         for lay in lays:

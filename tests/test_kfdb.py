@@ -1,0 +1,285 @@
+"""KeyFrameDatabase candidate detection (src/KeyFrameDatabase.cc:76-208, 220-337).
+
+CPU: the C++ restatement (oracle/orb_kfdb_oracle.cpp) against an independent pure-Python
+restatement below (inverted file, keyframe state, float32 arithmetic of the reference), over
+query sequences that exercise the persistent state (mRelocScore of neighbours that share a
+word but miss the 0.8 filter is the previous query's value), erase and clear.
+GPU: the HBM-resident database (my_orb_slam2_amd.kfdb, csrc/orbx_kfdb.hip) against the C++
+restatement: identical candidate lists, in order, over the same sequences, at 2000 and at
+10000 keyframes.
+"""
+import numpy as np
+import pytest
+
+from my_orb_slam2_amd import synth
+
+F32 = np.float32
+
+
+class PyKeyFrameDatabase:
+    """Pure-Python restatement (test-only), statement by statement with the reference."""
+
+    def __init__(self, covisibles=10):
+        self.K = covisibles
+        self.kfs = []            # dicts: words, values, ordered, state fields
+        self.inv = {}            # word -> list of slots in add order
+        self.qid = 1
+
+    def add(self, bow):
+        w, v = bow
+        s = len(self.kfs)
+        self.kfs.append(dict(w=[int(x) for x in w], v=[float(x) for x in v], ordered=[],
+                             lq=0, lw=0, ls=F32(0), rq=0, rw=0, rs=F32(0)))
+        for x in w:
+            self.inv.setdefault(int(x), []).append(s)
+        return s
+
+    def erase(self, s):
+        for x in self.kfs[s]["w"]:
+            lst = self.inv[x]
+            if s in lst:
+                lst.remove(s)
+
+    def clear(self):
+        self.kfs, self.inv = [], {}
+
+    def set_covisibles(self, s, nb):
+        self.kfs[s]["ordered"] = [int(x) for x in nb]
+
+    @staticmethod
+    def _score(qw, qv, k):
+        # L1Scoring::score (ScoringObject.cpp:23-67): merged walk in ascending word order
+        pos = {w: i for i, w in enumerate(k["w"])}
+        acc = 0.0
+        for w, vi in zip(qw, qv):
+            j = pos.get(int(w))
+            if j is not None:
+                wi = k["v"][j]
+                acc += abs(vi - wi) - abs(vi) - abs(wi)
+        return F32(-acc / 2.0)
+
+    def DetectRelocalizationCandidates(self, bow):
+        qw, qv = [int(x) for x in bow[0]], [float(x) for x in bow[1]]
+        qid, self.qid = self.qid, self.qid + 1
+        sharing = []
+        for w in qw:
+            for s in self.inv.get(w, []):
+                k = self.kfs[s]
+                if k["rq"] != qid:
+                    k["rw"] = 0
+                    k["rq"] = qid
+                    sharing.append(s)
+                k["rw"] += 1
+        if not sharing:
+            return []
+        mx = max(self.kfs[s]["rw"] for s in sharing)
+        minc = int(F32(mx) * F32(0.8))
+        scored = []
+        for s in sharing:
+            k = self.kfs[s]
+            if k["rw"] > minc:
+                k["rs"] = self._score(qw, qv, k)
+                scored.append((k["rs"], s))
+        if not scored:
+            return []
+        accl, best_acc = [], F32(0)
+        for sc, s in scored:
+            best, acc, bk = sc, sc, s
+            for n in self.kfs[s]["ordered"][:self.K]:
+                k2 = self.kfs[n]
+                if k2["rq"] != qid:
+                    continue
+                acc = F32(acc + k2["rs"])
+                if k2["rs"] > best:
+                    bk, best = n, k2["rs"]
+            accl.append((acc, bk))
+            if acc > best_acc:
+                best_acc = acc
+        thr = F32(F32(0.75) * best_acc)
+        out, seen = [], set()
+        for acc, bk in accl:
+            if acc > thr and bk not in seen:
+                out.append(bk)
+                seen.add(bk)
+        return out
+
+    def DetectLoopCandidates(self, bow, connected, min_score):
+        qw, qv = [int(x) for x in bow[0]], [float(x) for x in bow[1]]
+        conn = set(int(x) for x in connected)
+        min_score = F32(min_score)
+        qid, self.qid = self.qid, self.qid + 1
+        sharing = []
+        for w in qw:
+            for s in self.inv.get(w, []):
+                k = self.kfs[s]
+                if k["lq"] != qid:
+                    k["lw"] = 0
+                    if s not in conn:
+                        k["lq"] = qid
+                        sharing.append(s)
+                k["lw"] += 1
+        if not sharing:
+            return []
+        mx = max(self.kfs[s]["lw"] for s in sharing)
+        minc = int(F32(mx) * F32(0.8))
+        scored = []
+        for s in sharing:
+            k = self.kfs[s]
+            if k["lw"] > minc:
+                k["ls"] = self._score(qw, qv, k)
+                if k["ls"] >= min_score:
+                    scored.append((k["ls"], s))
+        if not scored:
+            return []
+        accl, best_acc = [], min_score
+        for sc, s in scored:
+            best, acc, bk = sc, sc, s
+            for n in self.kfs[s]["ordered"][:self.K]:
+                k2 = self.kfs[n]
+                if k2["lq"] == qid and k2["lw"] > minc:
+                    acc = F32(acc + k2["ls"])
+                    if k2["ls"] > best:
+                        bk, best = n, k2["ls"]
+            accl.append((acc, bk))
+            if acc > best_acc:
+                best_acc = acc
+        thr = F32(F32(0.75) * best_acc)
+        out, seen = [], set()
+        for acc, bk in accl:
+            if acc > thr and bk not in seen:
+                out.append(bk)
+                seen.add(bk)
+        return out
+
+
+def _build(dbs, bows, cov):
+    for b in bows:
+        slots = [d.add(b) for d in dbs]
+        assert len(set(slots)) == 1
+    for s, nb in enumerate(cov):
+        for d in dbs:
+            d.set_covisibles(s, nb)
+
+
+def _session(dbs, seed, bows, cov, n_reloc=12, n_loop=8, erase=(), check=None):
+    """A query sequence run identically on every database; `check` compares the results."""
+    rng = np.random.default_rng(seed)
+    n = len(bows)
+    for s in erase:
+        for d in dbs:
+            d.erase(s)
+    results = []
+    for q in range(n_reloc):
+        t = int(rng.integers(0, n))
+        # alternate near-duplicate and weak queries: the weak ones leave many sharing
+        # neighbours below the 0.8 filter, which then read the previous query's mRelocScore
+        bow = synth.kfdb_query(seed * 100 + q, bows[t], keep=0.8 if q % 2 == 0 else 0.35)
+        res = [list(d.DetectRelocalizationCandidates(bow)) for d in dbs]
+        results.append(("reloc", t, res))
+    for q in range(n_loop):
+        t = int(rng.integers(0, n))
+        conn = list(cov[t]) + [t]
+        ms = float(rng.uniform(0.0, 0.02))
+        res = [list(d.DetectLoopCandidates(bows[t], conn, ms)) for d in dbs]
+        results.append(("loop", t, res))
+    if check:
+        for kind, t, res in results:
+            for r in res[1:]:
+                assert r == res[0], f"{kind} query at keyframe {t}: {r} vs {res[0]}"
+    return results
+
+
+def test_oracle_matches_python_restatement(oracle_mod):
+    from oracle.kfdb import OracleKeyFrameDatabase
+    bows, cov, _ = synth.kfdb_scene(1, n_kf=300, vocab=20000, words=120, place=240, revisit=40)
+    py, cc = PyKeyFrameDatabase(), OracleKeyFrameDatabase()
+    _build([py, cc], bows, cov)
+    res = _session([py, cc], 3, bows, cov, n_reloc=16, n_loop=10, check=True)
+    assert sum(len(r[2][0]) for r in res) > 20
+    # erased keyframes leave the inverted file; the covisibility lists may still name them
+    _session([py, cc], 4, bows, cov, n_reloc=8, n_loop=6, erase=range(0, 300, 7), check=True)
+    for d in (py, cc):
+        d.clear()
+    assert py.DetectRelocalizationCandidates(bows[0]) == [] and \
+        list(cc.DetectRelocalizationCandidates(bows[0])) == []
+
+
+def test_state_carries_between_reloc_queries(oracle_mod):
+    """A neighbour that shares a word with the frame but misses the 0.8 filter adds its
+    mRelocScore from the previous query (KeyFrameDatabase.cc:300-303): the same second query
+    gives different candidates after different first queries."""
+    from oracle.kfdb import OracleKeyFrameDatabase
+    bows, cov, _ = synth.kfdb_scene(2, n_kf=120, vocab=8000, words=100, place=200)
+    outs = []
+    for first in (90, 48):   # far from keyframe 50 / one of its covisible neighbours
+        py, cc = PyKeyFrameDatabase(), OracleKeyFrameDatabase()
+        _build([py, cc], bows, cov)
+        for d in (py, cc):
+            d.DetectRelocalizationCandidates(synth.kfdb_query(5, bows[first], keep=0.9))
+        q = synth.kfdb_query(6, bows[50], keep=0.3, extra=300, vocab=8000)
+        a, b = py.DetectRelocalizationCandidates(q), list(cc.DetectRelocalizationCandidates(q))
+        assert a == b
+        outs.append(a)
+    assert outs[0] == [50] and outs[1] == [48], outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_kf,words", [(2000, 300), (10000, 250)])
+def test_gpu_kfdb_parity(oracle_mod, orbx_lib, gpu, n_kf, words):
+    from oracle.kfdb import OracleKeyFrameDatabase
+    from my_orb_slam2_amd import KeyFrameDatabase
+    bows, cov, _ = synth.kfdb_scene(7, n_kf=n_kf, words=words, revisit=n_kf // 20)
+    g, o = KeyFrameDatabase(10), OracleKeyFrameDatabase(10)
+    _build([g, o], bows, cov)
+    res = _session([o, g], 11, bows, cov, n_reloc=20, n_loop=12, check=True)
+    assert sum(len(r[2][0]) for r in res) > 20
+    # erase a tenth of the keyframes, update some covisibility lists, query again
+    rng = np.random.default_rng(1)
+    for s in rng.choice(n_kf, 40, replace=False):
+        nb = rng.permutation(cov[s])[:7]
+        for d in (g, o):
+            d.set_covisibles(int(s), nb)
+    _session([o, g], 12, bows, cov, n_reloc=12, n_loop=8, erase=range(3, n_kf, 10), check=True)
+    # keyframes added after queries (the database grows on the device)
+    more, cov2, _ = synth.kfdb_scene(8, n_kf=300, words=words)
+    for b in more:
+        assert g.add(b) == o.add(b)
+    _session([o, g], 13, bows + more, cov, n_reloc=6, n_loop=4, check=True)
+    scan_ms, sel_ms = g.last_timing()
+    assert scan_ms > 0 and sel_ms > 0
+
+
+@pytest.mark.gpu
+def test_gpu_kfdb_edges(oracle_mod, orbx_lib, gpu):
+    from my_orb_slam2_amd import KeyFrameDatabase
+    from oracle.kfdb import OracleKeyFrameDatabase
+    g, o = KeyFrameDatabase(10), OracleKeyFrameDatabase(10)
+    empty = (np.zeros(0, np.uint32), np.zeros(0))
+    assert len(g.DetectRelocalizationCandidates(empty)) == 0
+    bows, cov, _ = synth.kfdb_scene(9, n_kf=50, vocab=5000, words=60, place=100)
+    _build([g, o], bows, cov)
+    assert len(g.DetectRelocalizationCandidates(empty)) == 0
+    # a query sharing no word
+    far = (np.arange(900000, 900050, dtype=np.uint32), np.full(50, 0.02))
+    assert len(g.DetectRelocalizationCandidates(far)) == 0
+    # every keyframe connected: no loop candidate
+    assert len(g.DetectLoopCandidates(bows[3], list(range(50)), 0.0)) == 0
+    # min_score above every score
+    assert len(g.DetectLoopCandidates(bows[3], [], 2.0)) == 0
+    # identical BowVectors (score ties) and duplicate best keyframes
+    for _ in range(3):
+        g.add(bows[7])
+        o.add(bows[7])
+    for s in range(50, 53):
+        for d in (g, o):
+            d.set_covisibles(s, [7, 50, 51, 52])
+    for q in range(4):
+        b = synth.kfdb_query(q, bows[7], keep=0.9)
+        assert list(g.DetectRelocalizationCandidates(b)) == list(o.DetectRelocalizationCandidates(b))
+    g.clear()
+    o.clear()
+    assert len(g) == 0
+    s0 = g.add(bows[0])
+    assert s0 == 0 and o.add(bows[0]) == 0
+    assert list(g.DetectRelocalizationCandidates(bows[0])) == list(
+        o.DetectRelocalizationCandidates(bows[0])) == [0]
