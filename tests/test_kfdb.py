@@ -244,7 +244,7 @@ def test_gpu_kfdb_parity(oracle_mod, orbx_lib, gpu, n_kf, words):
     more, cov2, _ = synth.kfdb_scene(8, n_kf=300, words=words)
     for b in more:
         assert g.add(b) == o.add(b)
-    _session([o, g], 13, bows + more, cov, n_reloc=6, n_loop=4, check=True)
+    _session([o, g], 13, bows + more, cov + [[] for _ in more], n_reloc=6, n_loop=4, check=True)
     scan_ms, sel_ms = g.last_timing()
     assert scan_ms > 0 and sel_ms > 0
 
