@@ -36,13 +36,14 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r02_pmc_fetch_b512.csv", "r02_pmc_write_b512.csv"))
+                       ("r03_pmc_fetch_b512.csv", "r03_pmc_write_b512.csv"))
 
 
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
                              ("r02_pmc_fetch_euroc.csv", "r02_pmc_write_euroc.csv"))
 # SQ_INSTS_VALU passes (the VALU issue entry beside the HBM roofline)
-DEFAULT_INSTS = os.path.join(HERE, "profiles", "r02_pmc_insts_b512.csv")
+DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
+                         ("r03_pmc_insts_b512.csv", "r03_pmc_busy_b512.csv"))
 DEFAULT_INSTS_EUROC = os.path.join(HERE, "profiles", "r02_pmc_insts_euroc.csv")
 # VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
 # 2 cycles per SIMD for the full-rate class (add / logic / shifts / f32 mul-add), per 4 cycles
@@ -69,6 +70,11 @@ def parse():
                     help="stereo: time the PCIe-inclusive path (H2D of both views from pinned host "
                          "memory, extraction + stereo, D2H of keypoints, descriptors, uRight and "
                          "depth) instead of HBM-resident inputs")
+    ap.add_argument("--input", default="resident", choices=["resident", "tensor"],
+                    help="stereo: where the step's images sit in HBM: 'resident' = in the "
+                         "pyramid's level-0 slots (orbx_batch_input_view; the H2D copy of a "
+                         "frame lands there, so no device copy of the input is made), 'tensor' "
+                         "= a caller [B, H, W] tensor copied into level 0 by the first kernel")
     ap.add_argument("--inflight", type=int, default=1,
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
@@ -243,8 +249,20 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NI - 1)]
     sts = [s_.cuda_stream for s_ in streams]
 
-    def run_step(i):
-        sbs[i % NI](Ls, Rs, MBF, mb, stream=sts[i % NI])
+    resident = args.input == "resident" and not args.host_io
+    if resident:
+        # each handle's level-0 slots hold the step's images (written once, before timing)
+        for h in sbs:
+            Lv, Rv = h.input_views(W, H)
+            Lv.copy_(Ls)
+            Rv.copy_(Rs)
+        torch.cuda.synchronize(dev)
+
+        def run_step(i):
+            sbs[i % NI].run_resident(MBF, mb, stream=sts[i % NI])
+    else:
+        def run_step(i):
+            sbs[i % NI](Ls, Rs, MBF, mb, stream=sts[i % NI])
 
     io = None
     if args.host_io:
@@ -335,6 +353,13 @@ def main():
                 # every extraction / stereo kernel against the HBM roof (north_star: FAST and
                 # the matcher included), same definitions as the headline object
                 "per_kernel": per_kernel_hbm(prof, geo, args.traffic_csv, args.steps)}
+        # the pyramid's two kinds of launch apart: level 0 (blur of the input) and levels
+        # 1-7 (resize + blur)
+        if "k_level0" in prof and prof["k_level0"][1] and "k_level" in prof:
+            t_all, n_all = prof["k_level"]
+            t0l, n0l = prof["k_level0"]
+            prof_l17 = {"k_level1_7": (t_all - t0l, n_all - n0l)}
+            roof["per_kernel"].update(per_kernel_hbm(prof_l17, geo, args.traffic_csv, args.steps))
         # the integer kernels are bound by VALU issue, not HBM: the same launches against
         # the issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
         for k, e in [(dom, roof)] + list(roof["per_kernel"].items()):
@@ -395,15 +420,20 @@ def per_kernel_hbm(prof, geo, traffic_csv, steps):
 
 
 def kernel_bytes(ext, n, B):
-    """Algorithmic HBM bytes per launch of each kernel.  One launch
-    covers the n images (k_level: one level of them); B stereo pairs for k_stereo."""
+    """Algorithmic HBM bytes per launch of each kernel.  One
+    launch covers the n images (k_level: one level of them); B stereo pairs for k_stereo."""
     v = ext.batch_view()
     L = 8
     area = [v.level_w[l] * v.level_h[l] for l in range(L)]
     kc = v.kp_cap
     return {
-        # per level: read level l-1 (level 0: the input), write level l and its blur
-        "k_level": n * (sum(area[:-1]) + area[0] + 2 * sum(area)) / L,
+        # §8(d): the input is read once and never copied; level l >= 1 reads level l-1 and
+        # writes itself and its blur, level 0 reads the input and writes its blur (a device
+        # copy of the input, made only when the caller's images are not in the level-0 slots,
+        # is not algorithmic work): (sum_{l<L-1} A_l + 2 sum A) per step, averaged per launch
+        "k_level": n * (sum(area[:-1]) + 2 * sum(area)) / L,
+        "k_level0": n * 2 * area[0],
+        "k_level1_7": n * (sum(area[:-1]) + 2 * sum(area[1:])) / (L - 1),
         # every level byte read once
         "k_fast": n * sum(area),
         # candidates in (<= 4 B each, bounded by 2 x kp slots here) and survivors out
@@ -415,32 +445,52 @@ def kernel_bytes(ext, n, B):
     }
 
 
-def valu_from_csv(paths, kernel):
-    """SQ_INSTS_VALU (wave instructions) per launch of `kernel`, averaged over its dispatches
-    in rocprofv3 --pmc CSVs, or None."""
+# bench names of kernel groups -> the kernel-name pattern of their dispatches in rocprofv3 CSVs
+CSV_NAME = {"k_level0": "k_level_strip<4>", "k_level1_7": "k_level_strip<3>"}
+
+
+def counter_from_csv(paths, kernel, counter):
+    """Counter value per dispatch of `kernel` (summed over a dispatch's rows), averaged over
+    its dispatches in rocprofv3 --pmc CSVs, or None."""
     import csv
     import glob
+    pat = CSV_NAME.get(kernel, kernel)
     tot, ids = 0.0, set()
     for p in (paths or "").split(","):
         for path in (sorted(glob.glob(p.strip())) if p.strip() else []):
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == "SQ_INSTS_VALU":
+                    if pat in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                         tot += float(row["Counter_Value"])
                         ids.add((path, row.get("Dispatch_Id")))
     return tot / len(ids) if ids else None
 
 
+def valu_from_csv(paths, kernel):
+    return counter_from_csv(paths, kernel, "SQ_INSTS_VALU")
+
+
 def valu_entry(paths, kernel, avg_s):
-    """A launch's VALU issue rate against the chip's 2-cycle and 4-cycle class peaks."""
+    """A launch against the VALU issue roof, two ways:
+    * busy_frac: the fraction of the SIMDs' cycles spent issuing VALU instructions,
+      SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves; one VALU issue at a time per SIMD)
+      x 4 / (1024 SIMDs x the launch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) from the same PMC
+      pass: mix-aware (a 4-cycle instruction counts 4 cycles) and at most 1;
+    * the issue rate in wave instructions/s (SQ_INSTS_VALU over the HIP-event launch time)."""
     v = valu_from_csv(paths, kernel)
-    if not v or avg_s <= 0:
+    act = counter_from_csv(paths, kernel, "SQ_ACTIVE_INST_VALU")
+    grbm = counter_from_csv(paths, kernel, "GRBM_GUI_ACTIVE")
+    if not v and not act:
         return None
-    rate = v / avg_s
-    return {"bound": "valu", "wave_instr_per_launch": v, "achieved": rate / 1e12,
-            "unit": "T wave-instr/s", "peak_2cycle": VALU_PEAK_2CYC / 1e12,
-            "peak_4cycle": VALU_PEAK_4CYC / 1e12, "frac_2cycle": rate / VALU_PEAK_2CYC,
-            "frac_4cycle": rate / VALU_PEAK_4CYC}
+    out = {"bound": "valu"}
+    if act and grbm:
+        cycles = grbm / 8.0
+        out.update({"busy_frac": 4.0 * act / (1024.0 * cycles), "sq_active_inst_valu": act,
+                    "cycles": cycles})
+    if v and avg_s > 0:
+        out.update({"wave_instr_per_launch": v, "issue_rate": v / avg_s / 1e12,
+                    "unit": "T wave-instr/s"})
+    return out
 
 
 def traffic_from_csv(paths, kernel):
@@ -453,11 +503,12 @@ def traffic_from_csv(paths, kernel):
     files = []
     for p in (paths or "").split(","):
         files += sorted(glob.glob(p.strip())) if p.strip() else []
+    pat = CSV_NAME.get(kernel, kernel)
     per = {}
     for path in files:
         with open(path) as f:
             for row in csv.DictReader(f):
-                if kernel not in row.get("Kernel_Name", ""):
+                if pat not in row.get("Kernel_Name", ""):
                     continue
                 name = row.get("Counter_Name")
                 if name in ("FETCH_SIZE", "WRITE_SIZE"):

@@ -99,6 +99,22 @@ orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, 
                                       int width, int height, size_t stride,
                                       size_t batch_stride, void* stream);
 
+/* ---- resident inputs: level 0 of the pyramid is the input buffer ----------------------
+ * The extractor's pyramid level 0 (mvImagePyramid[0]) of image i lives at
+ * *d_level0 + i * *image_stride, rows *pitch bytes apart (64-byte aligned, pitch >= width + 4).
+ * A caller that writes its images there (an H2D copy straight from the camera buffer, or a
+ * kernel) runs the extraction on them without the device-side copy of the input the other
+ * batched entry points make: orbx_extract_batch_resident / orbx_stereo_frames_resident
+ * (left views in images [0, B), right views in [B, 2B)).  Prepares the workspace for `batch`
+ * images of width x height; the view stays valid until a call with another size or a larger
+ * batch.  orbx_extract uses the same path for its host image. */
+orbx_status orbx_batch_input_view(orbx_extractor* h, int width, int height, int batch,
+                                  uint8_t** d_level0, size_t* pitch, size_t* image_stride);
+orbx_status orbx_extract_batch_resident(orbx_extractor* h, int batch, void* stream);
+orbx_status orbx_stereo_frames_resident(orbx_extractor* h, int batch, float mbf, float mb,
+                                        float* d_uRight, float* d_depth, int32_t* d_nvalid,
+                                        void* stream);
+
 typedef struct {
     int batch;              /* images in the last call                        */
     int kp_cap;             /* keypoint slots per image                       */
@@ -150,8 +166,11 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, const uint8_t* d_left,
 int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 /* ---- per-kernel timing (HIP events around each launch, on the launch stream) ------------ */
+/* ORBX_K_LEVEL: every pyramid launch; ORBX_K_LEVEL0: the level-0 launch alone (a part of
+ * ORBX_K_LEVEL, reported separately: it blurs the input, the others also resize). */
 typedef enum {
-    ORBX_K_LEVEL = 0, ORBX_K_FAST, ORBX_K_OCTREE, ORBX_K_ORIENT_DESC, ORBX_K_STEREO, ORBX_K_COUNT
+    ORBX_K_LEVEL = 0, ORBX_K_FAST, ORBX_K_OCTREE, ORBX_K_ORIENT_DESC, ORBX_K_STEREO,
+    ORBX_K_LEVEL0, ORBX_K_COUNT
 } orbx_kernel_id;
 orbx_status orbx_profile_enable(orbx_extractor* h, int on);
 /* Waits for the recorded launches, returns per-kernel total ms and launch counts since the

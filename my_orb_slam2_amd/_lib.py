@@ -19,7 +19,7 @@ ORBX_LIB_ENV = "ORBX_LIB"
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
-KERNELS = ["k_level", "k_fast", "k_octree", "k_orient_desc", "k_stereo"]
+KERNELS = ["k_level", "k_fast", "k_octree", "k_orient_desc", "k_stereo", "k_level0"]
 MATCH_KERNELS = ["k_bow", "k_triangulate", "k_proj_search", "k_proj_resolve", "k_distinctive"]
 
 STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
@@ -59,6 +59,10 @@ SIGNATURES = {
     "orbx_blur_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orbx_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp]),
     "orbx_batch_view_get": (_i, [_vp, ctypes.POINTER(BatchView)]),
+    "orbx_batch_input_view": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_vp), ctypes.POINTER(_sz),
+                                   ctypes.POINTER(_sz)]),
+    "orbx_extract_batch_resident": (_i, [_vp, _i, _vp]),
+    "orbx_stereo_frames_resident": (_i, [_vp, _i, _f, _f, _vp, _vp, _vp, _vp]),
     "orbx_batch_fetch": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "orbx_stereo_match": (_i, [_vp, _vp, _f, _f, _vp, _vp, _i, ctypes.POINTER(_i)]),
     "orbx_stereo_match_batch_device": (_i, [_vp, _vp, _f, _f, _vp, _vp, _vp, _vp]),

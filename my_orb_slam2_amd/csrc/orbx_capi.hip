@@ -73,7 +73,7 @@ struct orbx_extractor {
     int ncap = 0, kcap = 0, ncap1 = 0, kcap1 = 0;
     size_t octree_lds = 0, octree_lds1 = 0, stereo_lds = 0, level_lds = 0;
     int cap_batch = 0;
-    DevBuf d_geom, d_cells, d_rtab, d_ltab, d_in, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
+    DevBuf d_geom, d_cells, d_rtab, d_ltab, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv, d_sscr;
     long long kscratch_per_image = 0;
     KernelTimer timer;
@@ -728,17 +728,24 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
                   h->d_kscr.ensure(B * h->kscratch_per_image) &&
                   h->d_kps.ensure(B * G.kp_cap * sizeof(orbx_keypoint)) &&
-                  h->d_desc.ensure(B * G.kp_cap * 32) && h->d_nkp.ensure(B * 4) &&
-                  h->d_in.ensure((size_t)W * H);
+                  h->d_desc.ensure(B * G.kp_cap * 32) && h->d_nkp.ensure(B * 4);
         if (!ok) return ORBX_ERR_DEVICE;
         h->cap_batch = batch;
     }
     return ORBX_OK;
 }
 
+// d_imgs == nullptr: level 0 of every image is already in the pyramid (in place).
 orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
                         int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
     ExtractLaunch a;
+    a.in_place = d_imgs == nullptr;
+    if (a.in_place) {
+        d_imgs = h->d_pyr.as<uint8_t>();
+        d_imgs2 = nullptr;
+        stride = (size_t)h->hg.lv[0].pitch;
+        batch_stride = (size_t)h->hg.pyr_bytes;
+    }
     a.hg = &h->hg;
     a.dg = h->d_geom.as<Geometry>();
     a.cells = h->d_cells.as<CellDesc>();
@@ -848,7 +855,7 @@ const char* orbx_last_error(void) { return g_err; }
 
 const char* orbx_kernel_name(int id) {
     static const char* names[K_COUNT] = {"k_level", "k_fast", "k_octree", "k_orient_desc",
-                                         "k_stereo"};
+                                         "k_stereo", "k_level0"};
     return (id >= 0 && id < K_COUNT) ? names[id] : "";
 }
 
@@ -930,7 +937,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->h_in) (void)hipHostFree(h->h_in);
     if (h->h_out) (void)hipHostFree(h->h_out);
-    DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_in, &h->d_pyr, &h->d_blur,
+    DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
     for (DevBuf* b : bufs) b->release();
@@ -981,10 +988,15 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
         for (int y = 0; y < height; ++y)
             std::memcpy(h->h_in + (size_t)y * width, img + (size_t)y * stride, width);
     }
+    // the DMA writes the image straight into pyramid level 0 (mvImagePyramid[0]): the
+    // extraction then only blurs it (no device-side copy of the input)
+    const LevelGeom& L0 = h->hg.lv[0];
     if (!order_after_last(h, st) ||
-        !HIPOK(hipMemcpyAsync(h->d_in.p, h->h_in, img_bytes, hipMemcpyHostToDevice, st)))
+        !HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off, (size_t)L0.pitch, h->h_in,
+                                (size_t)width, (size_t)width, (size_t)height,
+                                hipMemcpyHostToDevice, st)))
         return ORBX_ERR_DEVICE;
-    s = run_extract(h, h->d_in.as<uint8_t>(), nullptr, 1, 1, width, img_bytes, st);
+    s = run_extract(h, nullptr, nullptr, 1, 1, 0, 0, st);
     if (s != ORBX_OK) return s;
     if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
         !HIPOK(hipMemcpyAsync(h->h_out + o_kps, h->d_kps.p, KC * sizeof(orbx_keypoint),
@@ -1052,6 +1064,41 @@ orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, 
     orbx_status s = ensure_workspace(h, width, height, batch);
     if (s != ORBX_OK) return s;
     return run_extract(h, d_imgs, nullptr, batch, batch, stride, batch_stride, pick_stream(h, stream));
+}
+
+orbx_status orbx_batch_input_view(orbx_extractor* h, int width, int height, int batch,
+                                  uint8_t** d_level0, size_t* pitch, size_t* image_stride) {
+    if (!h || width <= 0 || height <= 0 || batch < 1 || !d_level0) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, batch);
+    if (s != ORBX_OK) return s;
+    *d_level0 = h->d_pyr.as<uint8_t>() + h->hg.lv[0].off;
+    if (pitch) *pitch = (size_t)h->hg.lv[0].pitch;
+    if (image_stride) *image_stride = (size_t)h->hg.pyr_bytes;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extract_batch_resident(orbx_extractor* h, int batch, void* stream) {
+    if (!h || batch < 1) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->have_geom) return ORBX_ERR_STATE;
+    if (batch > h->cap_batch) return ORBX_ERR_INVALID;
+    if (!HIPOK(hipSetDevice(h->device))) return ORBX_ERR_DEVICE;
+    return run_extract(h, nullptr, nullptr, batch, batch, 0, 0, pick_stream(h, stream));
+}
+
+orbx_status orbx_stereo_frames_resident(orbx_extractor* h, int batch, float mbf, float mb,
+                                        float* d_uRight, float* d_depth, int32_t* d_nvalid,
+                                        void* stream) {
+    if (!h || batch < 1 || !d_uRight || !d_depth) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->have_geom) return ORBX_ERR_STATE;
+    if (2 * batch > h->cap_batch) return ORBX_ERR_INVALID;
+    if (!HIPOK(hipSetDevice(h->device))) return ORBX_ERR_DEVICE;
+    hipStream_t st = pick_stream(h, stream);
+    orbx_status s = run_extract(h, nullptr, nullptr, 2 * batch, 2 * batch, 0, 0, st);
+    if (s != ORBX_OK) return s;
+    return run_stereo(h, h, batch, 0, batch, mbf, mb, d_uRight, d_depth, d_nvalid, st);
 }
 
 orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {

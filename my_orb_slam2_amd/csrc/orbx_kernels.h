@@ -10,7 +10,8 @@
 
 namespace orbx {
 
-enum KernelId { K_LEVEL = 0, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_COUNT };
+// K_LEVEL0 times the level-0 launch alone (it is also part of K_LEVEL, all levels)
+enum KernelId { K_LEVEL = 0, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_LEVEL0, K_COUNT };
 
 // Optional per-kernel HIP-event timing (orbx_profile_*): events bracket each launch on the
 // stream it is launched on; durations are read back by collect().
@@ -51,6 +52,13 @@ struct KernelTimer {
         return last ? last : start(st);
     }
     hipEvent_t last = nullptr;
+    // the last recorded interval counted a second time under `id` (a sub-total)
+    void alias(int id) {
+        if (!on || pending.empty()) return;
+        Rec r = pending.back();
+        r.id = id;
+        pending.push_back(r);
+    }
     void collect() {
         for (auto& r : pending) {
             float t = 0.f;
@@ -101,6 +109,8 @@ struct ExtractLaunch {
     // k_level_strip output rows per strip of each level for this call's batch (a kernel
     // argument: a batch-size change needs no device-side table update)
     int sth[ORBX_MAX_LEVELS];
+    // 1: level 0 of every image is already in the pyramid (d_imgs unused)
+    int in_place;
 };
 
 struct StereoLaunch {

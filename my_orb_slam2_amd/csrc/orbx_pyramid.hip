@@ -784,7 +784,11 @@ __device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, K..
 #define STRIP_WPE3 5
 #endif
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? STRIP_WPE0 : STRIP_WPE3))) void k_level_strip(const Geometry* __restrict__ g,
+// MODE 0: level 0 from the caller's images (copied into the pyramid as it is blurred);
+// MODE 4: level 0 already in the pyramid (written there by the H2D copy or the caller, see
+// orbx_batch_input_view): blurred only, the level itself is not stored again;
+// MODE 3: an INTER_LINEAR level from the level above.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE != 3 ? STRIP_WPE0 : STRIP_WPE3))) void k_level_strip(const Geometry* __restrict__ g,
                                                      const uint8_t* __restrict__ ltab,
                                                      const uint8_t* __restrict__ in0,
                                                      const uint8_t* __restrict__ in1, int split,
@@ -792,7 +796,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
                                                      uint8_t* __restrict__ pyr,
                                                      uint8_t* __restrict__ blur, int level,
                                                      int sth) {
-    static_assert(MODE == 0 || MODE == 3, "strip kernel: level 0 or INTER_LINEAR levels");
+    static_assert(MODE == 0 || MODE == 3 || MODE == 4, "strip kernel: level 0 or INTER_LINEAR levels");
+    constexpr bool L0 = MODE != 3;         // level 0: an 8-bit image in, no resize
     int bx, b;
     xcd_block(bx, b);
     const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -820,9 +825,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // Addresses are a wave-uniform row base (SGPRs) + a lane offset that is constant over the
     // walk, so loads and stores take the saddr forms and a step spends no VALU on 64-bit
     // address arithmetic.
-    const uint8_t* src;   // mode 0: the image (a row's loads start 4 bytes before the row)
+    const uint8_t* src;   // level 0: the image (a row's loads start 4 bytes before the row)
     size_t spitch;
-    if (MODE == 0) {
+    if (MODE == 4) {
+        src = pyr + (size_t)b * g->pyr_bytes + L.off;
+        spitch = (size_t)pitch;
+    } else if (MODE == 0) {
         src = b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride;
         spitch = stride;
     } else {
@@ -861,8 +869,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     // load slots (a ring of NS; step i consumes slot i mod NS, then refills it with row i+PF
     // ... PF <= NS): mode 0 two dwords of the input row + the perm selector for the row's
     // alignment, mode 3 three dwords of each of the two source rows + the row's betas
-    constexpr int NS = MODE == 0 ? STRIP_NS0 : STRIP_NS3;
-    constexpr int PF = MODE == 0 ? STRIP_PF0 : STRIP_PF;
+    constexpr int NS = L0 ? STRIP_NS0 : STRIP_NS3;
+    constexpr int PF = L0 ? STRIP_PF0 : STRIP_PF;
     static_assert(PF <= NS && (NS == 1 || NS == 2 || NS == 3 || NS == 7), "slot ring");
     uint32_t A[NS][3], C[NS][3], RB[NS];
     // mode 3: the source rows' byte offsets of each slot, and the last step's horizontal sums
@@ -873,7 +881,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     auto issue = [&](int slot, int i) {
         const int ic = min(i, n - 1);
         const uint4 ri = row_info(ic);
-        if (MODE == 0) {
+        if (L0) {
             // offsets relative to row - 4 (unsigned); the pointers formed are the load
             // addresses themselves: the aligned dwords holding the group's bytes, which start
             // before the tensor only when its first row does not start on a dword
@@ -905,7 +913,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
     };
     // this lane's group of level l from load slot `slot`
     auto level_group = [&](int slot, auto simd_c) -> uint32_t {
-        if (MODE == 0) return __builtin_amdgcn_perm(A[slot][1], A[slot][0], A[slot][2]);
+        if (L0) return __builtin_amdgcn_perm(A[slot][1], A[slot][0], A[slot][2]);
         constexpr bool SIMD = decltype(simd_c)::value;
         const uint32_t rb = RB[slot];
         const int b0 = (int)(int16_t)(rb & 0xFFFF), b1 = (int)(int16_t)(rb >> 16);
@@ -994,7 +1002,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
 #endif
         const uint32_t v = level_group(k % NS, rsimd_c);
         issue((k + PF) % NS, i + PF);
-        store_row(STRIP_LEV, Y0 + i - 3, ALL || (i >= 3 && i < vh + 3), v);
+        if constexpr (MODE != 4) store_row(STRIP_LEV, Y0 + i - 3, ALL || (i >= 3 && i < vh + 3), v);
         // row sums: the groups left and right of this lane's
         const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);  // wave_shr:1 (bound_ctrl: lane 0 reads 0)
         const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);  // wave_shl:1
@@ -1061,7 +1069,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
 #if STRIP_PRO_STORES
             // the same memory-op sequence as a block's last steps (two stores after each
             // issue), so the loop header sees one pending-load state from both edges
-            store_row(STRIP_LEV, 0, false, 0u);
+            if constexpr (MODE != 4) store_row(STRIP_LEV, 0, false, 0u);
             store_row(STRIP_BLR, 0, false, 0u);
 #endif
         }
@@ -1082,7 +1090,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
         for (; i0 < n; i0 += U) block(i0, std::false_type{});
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
-    if ((MODE == 0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
+    if ((L0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
     else walk(std::false_type{}, std::false_type{});
 }
 
@@ -1121,16 +1129,23 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
         const int mode = level_mode(L, l);
         if (L.strip) {
             const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;
-            hipLaunchKernelGGL(mode == 0 ? k_level_strip<0> : k_level_strip<3>,
+            hipLaunchKernelGGL(mode == 3 ? k_level_strip<3> : (a.in_place ? k_level_strip<4> : k_level_strip<0>),
                                dim3((L.snw * sns + 3) / 4, a.batch), dim3(256), 0, st, a.dg,
                                a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
                                a.pyr, a.blur, l, sth);
+        } else if (l == 0 && a.in_place) {
+            // the tiled level-0 kernel reading the pyramid's own level 0 (its level stores
+            // write back the bytes already there)
+            hipLaunchKernelGGL(level_kernel(0), dim3(L.ntx * L.nty, a.batch), dim3(256),
+                               a.level_lds, st, a.dg, a.ltab, a.pyr + L.off, a.pyr + L.off, a.batch,
+                               (size_t)L.pitch, (size_t)G.pyr_bytes, a.pyr, a.blur, l);
         } else {
             hipLaunchKernelGGL(level_kernel(mode), dim3(L.ntx * L.nty, a.batch), dim3(256),
                                a.level_lds, st, a.dg, a.ltab, a.d_imgs, a.d_imgs2, a.split,
                                a.stride, a.batch_stride, a.pyr, a.blur, l);
         }
         T.stop(K_LEVEL, e, st);
+        if (l == 0) T.alias(K_LEVEL0);
     }
     return hipGetLastError();
 }

@@ -13,6 +13,16 @@ import numpy as np
 from ._lib import BatchView, ExtractorParams, KERNELS, KEYPOINT_DTYPE, check, load, ptr
 
 
+class _DeviceArray:
+    """A device uint8 array by address (__cuda_array_interface__, which torch.as_tensor wraps
+    without copying)."""
+
+    def __init__(self, ptr_value: int, shape, strides):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "|u1",
+                                         "data": (int(ptr_value), False),
+                                         "strides": tuple(strides), "version": 2}
+
+
 class ORBextractor:
     """ORB_SLAM2::ORBextractor on the GPU.
 
@@ -163,6 +173,25 @@ class ORBextractor:
                                                             ptr(kps), ptr(desc)))
         return nkp, kps, desc
 
+    def input_views(self, width: int, height: int, batch: int):
+        """The pyramid's level-0 slots of `batch` images as a [batch, height, width] uint8
+        torch tensor on the device (a view, no copy; include/orbx.h orbx_batch_input_view):
+        images written there are extracted by ``extract_batch_resident`` without the input
+        copy.  Valid until a call with another size or a larger batch."""
+        import torch
+        p, pitch, istride = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_size_t()
+        check("orbx_batch_input_view", self._L.orbx_batch_input_view(
+            self._h, width, height, batch, ctypes.byref(p), ctypes.byref(pitch),
+            ctypes.byref(istride)))
+        return torch.as_tensor(_DeviceArray(p.value, (batch, height, width),
+                                            (istride.value, pitch.value, 1)),
+                               device=torch.device("cuda", self.params.device))
+
+    def extract_batch_resident(self, batch: int, stream=None):
+        """Extract the `batch` images already in the level-0 slots (``input_views``)."""
+        check("orbx_extract_batch_resident", self._L.orbx_extract_batch_resident(
+            self._h, batch, ptr(stream)))
+
     def launch_info(self, batch: int):
         """(strip rows per level, stereo workgroups per pair) of a batched call of `batch`
         images at the prepared size (include/orbx.h orbx_extractor_launch_info)."""
@@ -235,6 +264,36 @@ class StereoBatch:
             self.ext._h, ptr(left_imgs), ptr(right_imgs), B, W, H, stride, bstride, mbf, mb,
             ptr(self.uR), ptr(self.depth), ptr(self.nvalid), ctypes.c_void_p(st)))
         self._last_b = B
+        return self.uR, self.depth, self.nvalid
+
+    def input_views(self, width: int, height: int):
+        """(left, right) [B, H, W] device views of the pyramid's level-0 slots: pairs written
+        there run through ``run_resident`` without the device copy of the input images."""
+        v = self.ext.input_views(width, height, 2 * self.batch)
+        self._prepare_outputs(width, height)
+        return v[:self.batch], v[self.batch:]
+
+    def _prepare_outputs(self, W, H):
+        import torch
+        B = self.batch
+        if self._alloc_key is None or self._alloc_key[:3] != (B, W, H):
+            kc = self.ext.prepare(W, H, 2 * B)
+            if self._alloc_key is None or self._alloc_key[0] != B or self._alloc_key[3] != kc:
+                self.uR = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+                self.depth = torch.empty((B, kc), dtype=torch.float32, device=self.device)
+                self.nvalid = torch.empty((B,), dtype=torch.int32, device=self.device)
+            self._alloc_key = (B, W, H, kc)
+
+    def run_resident(self, mbf: float, mb: float, stream=None):
+        """The stereo front-end over the B pairs in ``input_views`` (orbx_stereo_frames_resident)."""
+        import torch
+        if self._alloc_key is None:
+            raise RuntimeError("run_resident before input_views")
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        check("orbx_stereo_frames_resident", self.ext._L.orbx_stereo_frames_resident(
+            self.ext._h, self.batch, mbf, mb, ptr(self.uR), ptr(self.depth), ptr(self.nvalid),
+            ctypes.c_void_p(st)))
+        self._last_b = self.batch
         return self.uR, self.depth, self.nvalid
 
     def fetch(self, side: str = "left"):

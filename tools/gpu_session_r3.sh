@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-3 measurement session on the GPU box: GPU tests, the headline's kernel trace and PMC
+# passes, then every bench line (headline with its measured traffic, EuRoC, relocalisation,
+# triangulation, drop-in latency, keyframe database).  usage: tools/gpu_session_r3.sh TAG
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "GPU TESTS FAILED"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+bash tools/prof_counters.sh $OUT/prof || { echo "PROFILING FAILED"; exit 1; }
+F=$(ls $OUT/prof/pmc3/*counter_collection.csv | head -1)
+W=$(ls $OUT/prof/pmc4/*counter_collection.csv | head -1)
+I=$(ls $OUT/prof/pmc1/*counter_collection.csv | head -1)
+V=$(ls $OUT/prof/pmc5/*counter_collection.csv | head -1)
+timeout -k 10 600 python bench.py --traffic-csv "$F,$W" --insts-csv "$I,$V" > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+bash tools/prof_counters.sh $OUT/prof_euroc --workload euroc || { echo "EUROC PROFILING FAILED"; exit 1; }
+FE=$(ls $OUT/prof_euroc/pmc3/*counter_collection.csv | head -1)
+WE=$(ls $OUT/prof_euroc/pmc4/*counter_collection.csv | head -1)
+IE=$(ls $OUT/prof_euroc/pmc1/*counter_collection.csv | head -1)
+VE=$(ls $OUT/prof_euroc/pmc5/*counter_collection.csv | head -1)
+timeout -k 10 600 python bench.py --workload euroc --traffic-csv "$FE,$WE" --insts-csv "$IE,$VE" > $OUT/euroc.json 2> $OUT/euroc.err || { echo "EUROC BENCH FAILED"; tail -20 $OUT/euroc.err; exit 1; }
+timeout -k 10 600 python bench.py --workload reloc --steps 10 --warmup 2 > $OUT/reloc.json 2> $OUT/reloc.err || { echo "RELOC BENCH FAILED"; tail -20 $OUT/reloc.err; exit 1; }
+timeout -k 10 600 python bench.py --workload triangulation --steps 20 --warmup 3 > $OUT/tri.json 2> $OUT/tri.err || { echo "TRI BENCH FAILED"; tail -20 $OUT/tri.err; exit 1; }
+timeout -k 10 600 python bench.py --workload dropin --frames 300 > $OUT/dropin.json 2> $OUT/dropin.err || { echo "DROPIN BENCH FAILED"; tail -20 $OUT/dropin.err; exit 1; }
+timeout -k 10 600 python bench.py --workload kfdb --steps 200 --warmup 10 > $OUT/kfdb.json 2> $OUT/kfdb.err || { echo "KFDB BENCH FAILED"; tail -20 $OUT/kfdb.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_reloc -o run --output-format csv -- python3 bench.py --workload reloc --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_reloc.log 2>&1 || { echo "RELOC TRACE FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_tri -o run --output-format csv -- python3 bench.py --workload triangulation --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_tri.log 2>&1 || { echo "TRI TRACE FAILED"; exit 1; }
+echo session done
