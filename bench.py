@@ -37,14 +37,13 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
                        ("r03_pmc_fetch_b512.csv", "r03_pmc_write_b512.csv"))
-
-
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                             ("r02_pmc_fetch_euroc.csv", "r02_pmc_write_euroc.csv"))
-# SQ_INSTS_VALU passes (the VALU issue entry beside the HBM roofline)
+                             ("r03_pmc_fetch_euroc.csv", "r03_pmc_write_euroc.csv"))
+# SQ_INSTS_VALU and SQ_ACTIVE_INST_VALU passes (the VALU issue entry beside the HBM roofline)
 DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
                          ("r03_pmc_insts_b512.csv", "r03_pmc_busy_b512.csv"))
-DEFAULT_INSTS_EUROC = os.path.join(HERE, "profiles", "r02_pmc_insts_euroc.csv")
+DEFAULT_INSTS_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
+                               ("r03_pmc_insts_euroc.csv", "r03_pmc_busy_euroc.csv"))
 # VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
 # 2 cycles per SIMD for the full-rate class (add / logic / shifts / f32 mul-add), per 4 cycles
 # for the rest (v_dot*, v_perm, v_pk_*, v_bcnt, 32-bit min / max, conversions), measured by
@@ -470,12 +469,57 @@ def valu_from_csv(paths, kernel):
     return counter_from_csv(paths, kernel, "SQ_INSTS_VALU")
 
 
+ISA_MIX = os.path.join(HERE, "profiles", "r03_isa_mix.json")
+
+
+def _mangled_key(demangled: str) -> str:
+    """'void orbx::k_level_strip<3>(...)' -> 'k_level_stripILi3E' (the form of the kernel's
+    symbol in tools/isa_mix.py's table); 'void orbx::k_fast(...)' -> '6k_fastE'."""
+    import re
+    m = re.search(r"(k_\w+)(<(-?\d+)>)?\(", demangled)
+    if not m:
+        return ""
+    name, targ = m.group(1), m.group(3)
+    return f"{name}ILi{targ}E" if targ is not None else f"{len(name)}{name}E"
+
+
+def mix_cycles_from_csv(paths, kernel, mix_path=ISA_MIX):
+    """Mean issue cycles per VALU instruction of a kernel group: each dispatch's SQ_INSTS_VALU
+    weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r03_isa_mix.json)."""
+    import csv
+    import glob
+    try:
+        mix = json.load(open(mix_path))
+    except OSError:
+        return None
+    pat = CSV_NAME.get(kernel, kernel)
+    num = den = 0.0
+    for p in (paths or "").split(","):
+        for path in (sorted(glob.glob(p.strip())) if p.strip() else []):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    name = row.get("Kernel_Name", "")
+                    if pat not in name or row.get("Counter_Name") != "SQ_INSTS_VALU":
+                        continue
+                    key = _mangled_key(name)
+                    costs = [v["mean_cycles"] for k, v in mix.items() if key and key in k
+                             and v.get("mean_cycles")]
+                    if not costs:
+                        continue
+                    num += float(row["Counter_Value"]) * costs[0]
+                    den += float(row["Counter_Value"])
+    return num / den if den else None
+
+
 def valu_entry(paths, kernel, avg_s):
-    """A launch against the VALU issue roof, two ways:
-    * busy_frac: the fraction of the SIMDs' cycles spent issuing VALU instructions,
-      SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves; one VALU issue at a time per SIMD)
-      x 4 / (1024 SIMDs x the launch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) from the same PMC
-      pass: mix-aware (a 4-cycle instruction counts 4 cycles) and at most 1;
+    """A launch against the VALU issue roof:
+    * busy_frac (mix-aware, <= 1 at the nominal clock): SQ_INSTS_VALU x the kernel's mean
+      issue cycles per VALU instruction (its opcode mix priced at the measured gfx950 rates,
+      tools/isa_mix.py) over the SIMDs' cycles of the launch (1024 SIMDs x the HIP-event launch
+      time x 2.4 GHz; the clock drops under load, so this is a lower bound);
+    * valubusy_4cycle: rocprof's VALUBusy (SQ_ACTIVE_INST_VALU, 4 cycles per instruction
+      whatever its rate, over GRBM_GUI_ACTIVE / 8 cycles: overstates full-rate-rich kernels,
+      may exceed 1, and the GRBM cycles of launches under ~0.3 ms read high), for reference;
     * the issue rate in wave instructions/s (SQ_INSTS_VALU over the HIP-event launch time)."""
     v = valu_from_csv(paths, kernel)
     act = counter_from_csv(paths, kernel, "SQ_ACTIVE_INST_VALU")
@@ -483,10 +527,13 @@ def valu_entry(paths, kernel, avg_s):
     if not v and not act:
         return None
     out = {"bound": "valu"}
-    if act and grbm:
-        cycles = grbm / 8.0
-        out.update({"busy_frac": 4.0 * act / (1024.0 * cycles), "sq_active_inst_valu": act,
+    cyc = mix_cycles_from_csv(paths, kernel)
+    if v and cyc and avg_s > 0:
+        cycles = avg_s * 2.4e9
+        out.update({"busy_frac": v * cyc / (1024.0 * cycles), "mean_issue_cycles": cyc,
                     "cycles": cycles})
+    if act and grbm:
+        out["valubusy_4cycle"] = 4.0 * act / (1024.0 * grbm / 8.0)
     if v and avg_s > 0:
         out.update({"wave_instr_per_launch": v, "issue_rate": v / avg_s / 1e12,
                     "unit": "T wave-instr/s"})

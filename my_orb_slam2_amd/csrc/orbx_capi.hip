@@ -974,27 +974,23 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     orbx_status s = ensure_workspace(h, width, height, 1);
     if (s != ORBX_OK) return s;
     hipStream_t st = h->stream;
-    // The image goes through the handle's pinned staging (a true async DMA, no pageable
-    // bounce), and every output comes back in one pinned block: one host wait per call.
-    const size_t img_bytes = (size_t)width * height;
+    // The image goes through the handle's pinned staging, laid out with the pyramid's row
+    // pitch, and one linear DMA writes it straight into pyramid level 0 (mvImagePyramid[0]):
+    // the extraction then only blurs it (no device-side copy of the input; a pitched 2-D
+    // host copy would run row by row).  Every output comes back in one pinned block: one
+    // host wait per call.
+    const LevelGeom& L0 = h->hg.lv[0];
+    const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)height;
     const size_t KC = (size_t)h->hg.kp_cap;
     const size_t o_kps = 256, o_desc = o_kps + KC * sizeof(orbx_keypoint);
     if (!ensure_pinned(h->h_in, h->h_in_n, img_bytes) ||
         !ensure_pinned(h->h_out, h->h_out_n, o_desc + KC * 32))
         return ORBX_ERR_DEVICE;
-    if (stride == (size_t)width) {
-        std::memcpy(h->h_in, img, img_bytes);
-    } else {
-        for (int y = 0; y < height; ++y)
-            std::memcpy(h->h_in + (size_t)y * width, img + (size_t)y * stride, width);
-    }
-    // the DMA writes the image straight into pyramid level 0 (mvImagePyramid[0]): the
-    // extraction then only blurs it (no device-side copy of the input)
-    const LevelGeom& L0 = h->hg.lv[0];
+    for (int y = 0; y < height; ++y)
+        std::memcpy(h->h_in + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
     if (!order_after_last(h, st) ||
-        !HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off, (size_t)L0.pitch, h->h_in,
-                                (size_t)width, (size_t)width, (size_t)height,
-                                hipMemcpyHostToDevice, st)))
+        !HIPOK(hipMemcpyAsync(h->d_pyr.as<uint8_t>() + L0.off, h->h_in, img_bytes,
+                              hipMemcpyHostToDevice, st)))
         return ORBX_ERR_DEVICE;
     s = run_extract(h, nullptr, nullptr, 1, 1, 0, 0, st);
     if (s != ORBX_OK) return s;

@@ -1,7 +1,9 @@
 """Parity at the benchmarked geometries: every workload bench.py times, at exactly the size and
 launch geometry it times, built by bench.py's own input builders.
 
-* C2 (the headline, configs[1]): 512 KITTI stereo pairs per call.  At 1024 images every
+* C2 (the headline, configs[1]): 512 KITTI stereo pairs per call, resident in the pyramid's
+  level-0 slots as bench.py times them (the copying tensor path is covered by
+  test_gpu_extract.py and test_resident_equals_tensor_path below).  At 1024 images every
   pyramid level walks 64-row strips and k_stereo runs one workgroup per pair (asserted through
   orbx_extractor_launch_info); a single image runs 8-row strips and split stereo.  Every slot
   must equal its single-image run, and 16 slots must equal the CPU restatement bit for bit
@@ -31,7 +33,11 @@ def test_c2_stereo_b512(oracle_mod, orbx_lib, gpu):
     Ls, Rs = torch.from_numpy(Lh).to(gpu), torch.from_numpy(Rh).to(gpu)
     mb = float(np.float32(bench.MBF) / np.float32(bench.FX))
     sb = m.StereoBatch(B, bench.NFEAT, 1.2, 8, 20, 7)
-    uR, dep, nv = sb(Ls, Rs, bench.MBF, mb)
+    # the timed path: the pairs sit in the pyramid's level-0 slots (bench.py --input resident)
+    Lv, Rv = sb.input_views(bench.W, bench.H)
+    Lv.copy_(Ls)
+    Rv.copy_(Rs)
+    uR, dep, nv = sb.run_resident(bench.MBF, mb)
     torch.cuda.synchronize()
     rows, split = sb.ext.launch_info(2 * B)
     assert (rows == 64).all() and split == 1, (rows, split)   # the timed geometry
@@ -197,3 +203,32 @@ def test_c5_triangulation_512(oracle_mod, orbx_lib, gpu):
         assert cnt[j] == n_o, f"job {j}"
         np.testing.assert_array_equal(np.stack([idx1, seg[idx1]], 1), p_o, f"job {j}")
     assert cnt.min() > 0
+
+
+def test_resident_equals_tensor_path(orbx_lib, gpu):
+    """The level-0-in-place path (orbx_stereo_frames_resident) and the copying path
+    (orbx_stereo_frames_device, strided caller tensor) give the same bits at 96 pairs."""
+    import torch
+    import my_orb_slam2_amd as m
+    B = 96
+    Lh, Rh, _, _ = bench.stereo_inputs(3, B, 8)
+    Ls, Rs = torch.from_numpy(Lh).to(gpu), torch.from_numpy(Rh).to(gpu)
+    mb = float(np.float32(bench.MBF) / np.float32(bench.FX))
+    a, b = m.StereoBatch(B, bench.NFEAT), m.StereoBatch(B, bench.NFEAT)
+    ua, da, na = (t.clone() for t in a(Ls, Rs, bench.MBF, mb))
+    Lv, Rv = b.input_views(bench.W, bench.H)
+    Lv.copy_(Ls)
+    Rv.copy_(Rs)
+    ub, db, nb = b.run_resident(bench.MBF, mb)
+    torch.cuda.synchronize()
+    assert torch.equal(na, nb) and torch.equal(ua.view(torch.int32), ub.view(torch.int32))
+    assert torch.equal(da.view(torch.int32), db.view(torch.int32))
+    for side in ("left", "right"):
+        ka, kb = a.fetch(side), b.fetch(side)
+        assert np.array_equal(ka[0], kb[0])
+        for i in range(B):
+            n = ka[0][i]
+            assert_kps_equal(kb[1][i, :n], ka[1][i, :n], f"{side} {i}")
+            assert_bytes_equal(kb[2][i, :n], ka[2][i, :n], f"{side} {i} desc")
+        # the level-0 slots hold the inputs untouched by the extraction
+    assert torch.equal(Lv, Ls) and torch.equal(Rv, Rs)

@@ -1,23 +1,26 @@
 #!/bin/bash
-# Copy one GPU session's summaries (tools/gpu_session.sh TAG) into profiles/.
-# usage: [ROUND=r02] tools/collect_profiles.sh TAG
+# Copy one GPU session's summaries (tools/gpu_session_r3.sh TAG) into profiles/.
+# usage: [ROUND=r03] tools/collect_profiles.sh TAG
 set -e
 V=gpurun_out/$1
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 cp $V/bench.json profiles/${R}_$1_bench.json
 cp $V/prof/trace/run_kernel_stats.csv profiles/${R}_$1_kernel_stats_b512.csv
 cp $V/prof/pmc3/run_counter_collection.csv profiles/${R}_pmc_fetch_b512.csv
 cp $V/prof/pmc4/run_counter_collection.csv profiles/${R}_pmc_write_b512.csv
 cp $V/prof/pmc1/run_counter_collection.csv profiles/${R}_pmc_insts_b512.csv
 cp $V/prof/pmc2/run_counter_collection.csv profiles/${R}_pmc_waits_b512.csv
+cp $V/prof/pmc5/run_counter_collection.csv profiles/${R}_pmc_busy_b512.csv
 cp $V/euroc.json profiles/${R}_c3_euroc_bench.json
 cp $V/reloc.json profiles/${R}_c4_reloc_bench.json
 cp $V/tri.json profiles/${R}_c5_triangulation_bench.json
+[ -f $V/dropin.json ] && cp $V/dropin.json profiles/${R}_dropin_bench.json
+[ -f $V/kfdb.json ] && cp $V/kfdb.json profiles/${R}_kfdb_bench.json
 cp $V/prof_euroc/trace/run_kernel_stats.csv profiles/${R}_euroc_kernel_stats_b256.csv
 cp $V/prof_euroc/pmc3/run_counter_collection.csv profiles/${R}_pmc_fetch_euroc.csv
 cp $V/prof_euroc/pmc4/run_counter_collection.csv profiles/${R}_pmc_write_euroc.csv
 cp $V/prof_euroc/pmc1/run_counter_collection.csv profiles/${R}_pmc_insts_euroc.csv
+cp $V/prof_euroc/pmc5/run_counter_collection.csv profiles/${R}_pmc_busy_euroc.csv
 [ -f $V/prof_reloc/run_kernel_stats.csv ] && cp $V/prof_reloc/run_kernel_stats.csv profiles/${R}_c4_reloc_kernel_stats.csv
 [ -f $V/prof_tri/run_kernel_stats.csv ] && cp $V/prof_tri/run_kernel_stats.csv profiles/${R}_c5_triangulation_kernel_stats.csv
-ls $V/prof_reloc $V/prof_tri 2>/dev/null | head
 echo copied
