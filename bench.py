@@ -483,13 +483,13 @@ def _mangled_key(demangled: str) -> str:
     return f"{name}ILi{targ}E" if targ is not None else f"{len(name)}{name}E"
 
 
-def mix_cycles_from_csv(paths, kernel, mix_path=ISA_MIX):
+def mix_cycles_from_csv(paths, kernel, mix_path=None):
     """Mean issue cycles per VALU instruction of a kernel group: each dispatch's SQ_INSTS_VALU
     weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r03_isa_mix.json)."""
     import csv
     import glob
     try:
-        mix = json.load(open(mix_path))
+        mix = json.load(open(mix_path or ISA_MIX))
     except OSError:
         return None
     pat = CSV_NAME.get(kernel, kernel)

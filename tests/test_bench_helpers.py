@@ -101,20 +101,32 @@ def test_gpus_flag_must_match_world_size():
 
 
 def test_valu_entry_from_pmc(tmp_path):
-    """The roofline's VALU issue entry: SQ_INSTS_VALU averaged over a kernel's dispatches,
-    per launch duration, against the 2- and 4-cycle issue peaks of 1024 SIMDs at 2.4 GHz."""
+    """The roofline's VALU issue entry: SQ_INSTS_VALU averaged over a kernel's dispatches; the
+    mix-aware busy fraction prices them at the kernel's mean issue cycles (tools/isa_mix.py)
+    over 1024 SIMDs x the launch time at 2.4 GHz; rocprof's VALUBusy (4 cycles per
+    instruction, over GRBM_GUI_ACTIVE / 8) rides along."""
     b = _bench()
     f = tmp_path / "insts.csv"
     f.write_text('"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
-                 '1,"orbx::k_level_strip<0>(x)","SQ_INSTS_VALU",100\n'
-                 '2,"orbx::k_level_strip<3>(x)","SQ_INSTS_VALU",300\n'
+                 '1,"void orbx::k_level_strip<4>(x)","SQ_INSTS_VALU",100\n'
+                 '2,"void orbx::k_level_strip<3>(x)","SQ_INSTS_VALU",300\n'
                  '3,"orbx::k_fast(x)","SQ_INSTS_VALU",999\n'
-                 '3,"orbx::k_fast(x)","SQ_INSTS_SALU",5\n')
+                 '3,"orbx::k_fast(x)","SQ_INSTS_SALU",5\n'
+                 '3,"orbx::k_fast(x)","SQ_ACTIVE_INST_VALU",1000\n'
+                 '3,"orbx::k_fast(x)","GRBM_GUI_ACTIVE",8000\n')
+    mix = tmp_path / "mix.json"
+    mix.write_text(json.dumps({"_ZN4orbx6k_fastEPKNS_8G": {"mean_cycles": 3.0},
+                               "_ZN4orbx13k_level_stripILi3EEEvPK": {"mean_cycles": 3.5},
+                               "_ZN4orbx13k_level_stripILi4EEEvPK": {"mean_cycles": 2.5}}))
     assert b.valu_from_csv(str(f), "k_level") == pytest.approx(200.0)
+    assert b.mix_cycles_from_csv(str(f), "k_level", str(mix)) == pytest.approx(
+        (100 * 2.5 + 300 * 3.5) / 400)
+    b.ISA_MIX = str(mix)
     e = b.valu_entry(str(f), "k_fast", 1e-6)
+    b.ISA_MIX = os.path.join(ROOT, "profiles", "r03_isa_mix.json")
     assert e["wave_instr_per_launch"] == pytest.approx(999.0)
-    assert e["frac_4cycle"] == pytest.approx(999.0 / 1e-6 / (1024 * 2.4e9 / 4))
-    assert e["frac_2cycle"] == pytest.approx(e["frac_4cycle"] / 2)
+    assert e["busy_frac"] == pytest.approx(999.0 * 3.0 / (1024 * 1e-6 * 2.4e9))
+    assert e["valubusy_4cycle"] == pytest.approx(4.0 * 1000 / (1024 * 1000))
     assert b.valu_entry(str(f), "k_stereo", 1e-6) is None
 
 
@@ -127,4 +139,5 @@ def test_headline_valu_entry_matches_committed_pmc():
         pytest.skip("headline line predates the VALU entry")
     v = b.valu_from_csv(b.DEFAULT_INSTS, roof["kernel"])
     assert roof["valu"]["wave_instr_per_launch"] == pytest.approx(v)
-    assert roof["valu"]["achieved"] == pytest.approx(v / (roof["avg_launch_ms"] / 1000.0) / 1e12)
+    assert roof["valu"]["issue_rate"] == pytest.approx(v / (roof["avg_launch_ms"] / 1000.0) / 1e12)
+    assert 0 < roof["valu"]["busy_frac"] <= 1.0

@@ -1,11 +1,12 @@
 #!/bin/bash
 # Copy one GPU session's summaries (tools/gpu_session_r3.sh TAG) into profiles/.
-# usage: [ROUND=r03] tools/collect_profiles.sh TAG
+# usage: [ROUND=r03] tools/collect_profiles.sh SESSION_TAG [PROFILE_TAG]
 set -e
 V=gpurun_out/$1
+T=${2:-$1}
 R=${ROUND:-r03}
-cp $V/bench.json profiles/${R}_$1_bench.json
-cp $V/prof/trace/run_kernel_stats.csv profiles/${R}_$1_kernel_stats_b512.csv
+cp $V/bench.json profiles/${R}_${T}_bench.json
+cp $V/prof/trace/run_kernel_stats.csv profiles/${R}_${T}_kernel_stats_b512.csv
 cp $V/prof/pmc3/run_counter_collection.csv profiles/${R}_pmc_fetch_b512.csv
 cp $V/prof/pmc4/run_counter_collection.csv profiles/${R}_pmc_write_b512.csv
 cp $V/prof/pmc1/run_counter_collection.csv profiles/${R}_pmc_insts_b512.csv
