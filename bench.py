@@ -78,7 +78,7 @@ def parse():
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
     ap.add_argument("--workload", default="stereo",
-                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb"],
+                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb", "tum"],
                     help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
                          "extract + SearchByProjection vs the local map); reloc = configs[3] "
                          "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
@@ -215,6 +215,8 @@ def main():
         return main_dropin(args)
     if args.workload == "kfdb":
         return main_kfdb(args)
+    if args.workload == "tum":
+        return main_tum(args)
     if args.workload != "stereo":
         return main_match(args)
     import torch
@@ -715,6 +717,88 @@ def main_dropin(args):
     emit(json.dumps(out))
 
 
+# ---- configs[0]: one TUM frame, extraction + ComputeBoW + SearchByBoW vs one keyframe --------
+
+TUM_W, TUM_H, TUM_NFEAT = 640, 480, 1000          # Examples/RGB-D/TUM1.yaml:42
+
+
+def main_tum(args):
+    """configs[0] ("Single 640x480 TUM RGB-D frame, 1000 features, ORBextractor + SearchByBoW
+    vs one keyframe"), as Tracking::TrackReferenceKeyFrame runs it (Tracking.cc:805-847): per
+    frame ExtractORB, Frame::ComputeBoW (DBoW2 transform) and ORBmatcher(0.7, true)
+    .SearchByBoW(reference keyframe, frame), on the drop-in host path one frame at a time (the
+    C++ loop of tests/native/boundary_test.cpp `tum`).  The vocabulary is synthetic (ORBvoc.txt
+    is absent): k = 10, L = 5 with levelsup 3, so FeatureVector buckets sit at level 2 of the
+    tree as with ORBvoc's L = 6, levelsup 4.  Beside it the CPU restatement of the same frame
+    work on one core (the reference runs it on the Tracking thread)."""
+    import subprocess
+    import tempfile
+    from my_orb_slam2_amd import synth
+    P = max(1, min(args.distinct, 16))
+    pairs = [synth.stereo_pair(3000 + i, TUM_W, TUM_H) for i in range(P)]
+    warm = max(20, args.warmup)
+    binp = os.path.join(ROOT, "tests", "native", "boundary_test")
+    levelsup = 3
+    with tempfile.TemporaryDirectory() as d:
+        voc = os.path.join(d, "voc.txt")
+        synth.write_vocabulary(voc, k=10, L=5, seed=11)
+        for i, (L, R) in enumerate(pairs):
+            L.tofile(os.path.join(d, f"pair_{i}_left.raw"))
+            R.tofile(os.path.join(d, f"pair_{i}_right.raw"))
+        with open(os.path.join(d, "params.txt"), "w") as f:
+            f.write(f"{TUM_W} {TUM_H} {TUM_NFEAT} {P} {levelsup} {voc}\n")
+        r = subprocess.run([binp, "tum", d, str(args.frames), str(warm)], capture_output=True,
+                           text=True, timeout=600)
+        if r.returncode != 0:
+            sys.exit(f"bench.py: {binp} tum failed ({r.returncode}): {r.stderr[-2000:]}")
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        cpu = None
+        if args.cpu_seconds > 0:
+            import oracle
+            from oracle import matcher as om
+            from my_orb_slam2_amd.features import FeatureSet, FeatureVector
+            ov = om.OracleVocabulary(voc)
+            rng = np.random.default_rng(0)
+            kfs = []
+            for L, _ in pairs:
+                k, dsc = oracle.OracleExtractor(TUM_NFEAT, 1.2, 8, 20, 7)(L)
+                fv = FeatureVector(*ov.transform(dsc, levelsup)[3])
+                kfs.append((FeatureSet(k, dsc, None, fv, None), rng.random(len(k)) < 0.85))
+            ox = oracle.OracleExtractor(TUM_NFEAT, 1.2, 8, 20, 7)
+            ms, t_end, f = [], time.perf_counter() + min(args.cpu_seconds, 10.0), 0
+            while time.perf_counter() < t_end or len(ms) < 20:
+                i = f % P
+                t0 = time.perf_counter()
+                k, dsc = ox(pairs[i][1])
+                fv = FeatureVector(*ov.transform(dsc, levelsup)[3])
+                om.search_by_bow_kf_frame(kfs[i][0], kfs[i][1], FeatureSet(k, dsc, None, fv, None),
+                                          0.7, True)
+                t1 = time.perf_counter()
+                f += 1
+                if f > warm // 4:
+                    ms.append(1000.0 * (t1 - t0))
+            cpu = {"value": 1000.0 / float(np.mean(ms)), "unit": "frames/sec", "cores": 1,
+                   "kind": "port", "sample": f"{len(ms)} TUM-size synthetic frames: extraction + "
+                   "DBoW2 transform + SearchByBoW(KF, F) restatement, one thread",
+                   **latency_stats(ms)}
+    lat = latency_stats(res["latency_ms"])
+    out = {"metric": "configs[0] per-frame latency: TUM 640x480 extract + ComputeBoW + "
+                     "SearchByBoW vs one keyframe (drop-in host path)",
+           "value": 1000.0 / lat["mean_ms"], "unit": "frames/sec", "n_gpus": 1,
+           "steps": args.frames, "warmup": warm, "ms_per_step": lat["mean_ms"],
+           "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic",
+           "config": {"workload": "tum_extract_bow_searchbybow", "width": TUM_W,
+                      "height": TUM_H, "nfeatures": TUM_NFEAT, "nnratio": 0.7,
+                      "check_orientation": True, "vocabulary": "synthetic k=10 L=5",
+                      "levelsup": levelsup, "distinct_frames": P},
+           "latency": lat, "mean_keypoints": res["mean_keypoints"],
+           "mean_bow_matches": res["mean_bow_matches"], "cpu_baseline": cpu}
+    if cpu:
+        out["speedup_vs_cpu_median"] = cpu["median_ms"] / lat["median_ms"]
+    emit(json.dumps(out))
+
+
 # ---- keyframe database candidate detection (SURVEY §8f row 4) --------------------------------
 
 def main_kfdb(args):
@@ -1013,7 +1097,7 @@ def main_match(args):
     import torch.distributed as dist
     from my_orb_slam2_amd import ORBmatcher
     from my_orb_slam2_amd.distributed import (all_gather_counts, broadcast_query,
-                                              gather_candidate_matches, gather_rows, shard_range)
+                                              gather_candidate_blocks, gather_rows, shard_range)
     from my_orb_slam2_amd.features import FeatureSetC
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1057,8 +1141,9 @@ def main_match(args):
             m.search_by_bow_kf_frame_batch_device(db, fc, out, cnt, st)
             if dist_on:
                 allc = all_gather_counts(cnt[:k1 - k0], args.kfs, world)
-                # the candidates' match lists travel to every rank (Tracking.cc:1503-1528)
-                gather_candidate_matches(out, allc, args.kfs, world)
+                # the candidates' match lists travel to every rank (Tracking.cc:1503-1528), built
+                # and exchanged on the device: no host round trip inside the step
+                gather_candidate_blocks(out, cnt[:k1 - k0], k0, world)
                 return allc
             return cnt[:k1 - k0]
         units, unit_name = 1, "query frames/sec"

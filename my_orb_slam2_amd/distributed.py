@@ -33,18 +33,72 @@ def broadcast_query(tensors, src: int = 0):
     return tensors
 
 
+# ---- pure merge functions: what every rank does with the all-gathered shard buffers ----------
+# (factored out of the collectives so that a one-device test can run the shards in turn and
+# merge them with exactly this code, tests/test_gpu_sharding.py)
+
+def pad_shard(local, n_total: int, world: int):
+    """A rank's shard rows in the fixed-size buffer every rank all-gathers (the largest shard
+    of shard_range; the tail of a smaller shard is zero)."""
+    import torch
+    cap = max(e - b for b, e in (shard_range(n_total, r, world) for r in range(world)))
+    buf = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    buf[:local.shape[0]] = local
+    return buf
+
+
+def merge_shards(parts, n_total: int, world: int):
+    """The per-rank padded buffers (all_gather's output, rank order) as one [n_total, ...]
+    tensor in global unit order."""
+    import torch
+    sizes = [shard_range(n_total, r, world) for r in range(world)]
+    return torch.cat([parts[r][:e - b] for r, (b, e) in enumerate(sizes)])
+
+
+def candidate_block(local_matches, local_counts, k0: int, cap: int = 64, min_matches: int = 15):
+    """This rank's relocalisation candidates (keyframes with >= min_matches, Tracking.cc:1487)
+    as a fixed [cap, 1 + F] int32 block built on the device without a host round trip: row i =
+    (global keyframe id, its match list) for the i-th candidate in keyframe order, kf id -1
+    past the last one.  cap bounds the candidates per rank (a relocalisation keeps a handful)."""
+    import torch
+    dev = local_matches.device
+    n, F = local_matches.shape
+    mask = local_counts[:n] >= min_matches
+    order = torch.argsort((~mask).to(torch.int8), stable=True)[:cap]   # candidates first
+    k = min(cap, n)
+    block = torch.full((cap, 1 + F), -1, dtype=torch.int32, device=dev)
+    if k:
+        ids = torch.where(mask[order[:k]], order[:k].to(torch.int32) + k0,
+                          torch.full((k,), -1, dtype=torch.int32, device=dev))
+        block[:k, 0] = ids
+        block[:k, 1:] = torch.where((ids >= 0)[:, None], local_matches[order[:k]].to(torch.int32),
+                                    torch.full((k, F), -1, dtype=torch.int32, device=dev))
+    return block
+
+
+def merge_candidate_blocks(parts):
+    """[(kf_id, matches[F]), ...] in keyframe order from the all-gathered candidate blocks."""
+    out = []
+    for blk in parts:
+        b = blk.cpu().numpy() if hasattr(blk, "cpu") else np.asarray(blk)
+        for row in b:
+            if row[0] >= 0:
+                out.append((int(row[0]), row[1:]))
+    out.sort(key=lambda t: t[0])
+    return out
+
+
+# ---- collectives ------------------------------------------------------------------------------
+
 def all_gather_counts(local, n_total: int, world: int):
     """All-gather per-unit counts of every rank's shard into one [n_total] tensor in global
     unit order (shards are the contiguous blocks of shard_range)."""
     import torch
     import torch.distributed as dist
-    sizes = [shard_range(n_total, r, world) for r in range(world)]
-    cap = max(e - b for b, e in sizes)
-    buf = torch.zeros(cap, dtype=local.dtype, device=local.device)
-    buf[:local.numel()] = local
+    buf = pad_shard(local, n_total, world)
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
-    return torch.cat([parts[r][:e - b] for r, (b, e) in enumerate(sizes)])
+    return merge_shards(parts, n_total, world)
 
 
 def relocalisation_candidates(counts, min_matches: int = 15) -> np.ndarray:
@@ -58,43 +112,33 @@ def gather_rows(local, n_total: int, world: int):
     contiguous blocks of shard_range) into one [n_total, ...] tensor in global order."""
     import torch
     import torch.distributed as dist
-    sizes = [shard_range(n_total, r, world) for r in range(world)]
-    cap = max(e - b for b, e in sizes)
-    buf = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    buf[:local.shape[0]] = local
+    buf = pad_shard(local, n_total, world)
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
-    return torch.cat([parts[r][:e - b] for r, (b, e) in enumerate(sizes)])
+    return merge_shards(parts, n_total, world)
+
+
+def gather_candidate_blocks(local_matches, local_counts, k0: int, world: int, cap: int = 64,
+                            min_matches: int = 15):
+    """All-gather every rank's candidate block (candidate_block): a [world, cap, 1 + F] device
+    tensor, built and exchanged with no host synchronisation (so it can sit inside a timed
+    step); merge_candidate_blocks decodes it afterwards."""
+    import torch
+    import torch.distributed as dist
+    blk = candidate_block(local_matches, local_counts, k0, cap, min_matches)
+    parts = [torch.empty_like(blk) for _ in range(world)]
+    dist.all_gather(parts, blk)
+    return parts
 
 
 def gather_candidate_matches(local_matches, counts, n_total: int, world: int,
-                             min_matches: int = 15):
-    """The match lists of the relocalisation candidates (keyframes with >= min_matches, from
-    the all-gathered counts) collected from the ranks that own them.  local_matches is this
-    rank's [n_local, F] SearchByBoW output (keyframe-local feature index per frame feature, or
-    -1).  Every rank receives [(kf_id, matches[F]), ...] in keyframe order; only the
-    candidates travel (a [cap, 1 + F] int32 block per rank, cap = the largest per-rank
-    candidate count)."""
-    import torch
+                             min_matches: int = 15, cap: int = 64):
+    """The match lists of the relocalisation candidates collected from the ranks that own
+    them: [(kf_id, matches[F]), ...] in keyframe order on every rank.  `counts` is this
+    rank's shard counts or the all-gathered [n_total] counts."""
     import torch.distributed as dist
     rank = dist.get_rank()
-    c = counts.cpu().numpy() if hasattr(counts, "cpu") else np.asarray(counts)
-    sizes = [shard_range(n_total, r, world) for r in range(world)]
-    per_rank = [np.nonzero(c[b:e] >= min_matches)[0] + b for b, e in sizes]
-    cap = max(1, max(len(p) for p in per_rank))
-    F = local_matches.shape[1]
-    buf = torch.full((cap, 1 + F), -1, dtype=torch.int32, device=local_matches.device)
-    mine = per_rank[rank]
-    if len(mine):
-        b0 = sizes[rank][0]
-        idx = torch.as_tensor(mine - b0, dtype=torch.long, device=local_matches.device)
-        buf[:len(mine), 0] = torch.as_tensor(mine, dtype=torch.int32, device=buf.device)
-        buf[:len(mine), 1:] = local_matches.index_select(0, idx).to(torch.int32)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf)
-    out = []
-    for r in range(world):
-        for i in range(len(per_rank[r])):
-            row = parts[r][i]
-            out.append((int(row[0].item()), row[1:]))
-    return out
+    b, e = shard_range(n_total, rank, world)
+    local_counts = counts[b:e] if counts.shape[0] == n_total else counts
+    parts = gather_candidate_blocks(local_matches, local_counts, b, world, cap, min_matches)
+    return merge_candidate_blocks(parts)

@@ -307,11 +307,123 @@ static int bench(const std::string& dir, int nframes, int warmup) {
     return 0;
 }
 
+// configs[0] as Tracking::TrackReferenceKeyFrame runs it on one frame (Tracking.cc:805-847):
+// ExtractORB of the frame (Frame.cc:204), Frame::ComputeBoW (Frame.cc:420-427, DBoW2 transform
+// with levelsup), then ORBmatcher(0.7, true).SearchByBoW(reference keyframe, frame)
+// (ORBmatcher.cc:182-319), timed per frame.  DIR: pair_<i>_left.raw (the reference keyframes'
+// images, extracted and transformed once, untimed) and pair_<i>_right.raw (the frames), and
+// params.txt ("W H nfeatures P levelsup vocabulary_path").  Frame f is matched against
+// keyframe f % P; 85 % of a keyframe's features carry a MapPoint (seeded mask).
+struct BowFrame {
+    View v;
+    std::vector<uint32_t> bow_w, fv_node;
+    std::vector<double> bow_v;
+    std::vector<int32_t> fv_off, fv_feat;
+    orbx_featureset fs;
+};
+
+static orbx_status make_bow_frame(orbx_extractor* h, orbx_vocabulary* voc, int levelsup,
+                                  const uint8_t* img, int W, int H, BowFrame* f) {
+    extract(h, img, W, H, &f->v);
+    if (f->v.st != ORBX_OK) return f->v.st;
+    const int n = f->v.n;
+    f->bow_w.resize((size_t)n + 1);
+    f->bow_v.resize((size_t)n + 1);
+    f->fv_node.resize((size_t)n + 1);
+    f->fv_off.resize((size_t)n + 2);
+    f->fv_feat.resize((size_t)n + 1);
+    int32_t nb = 0, nf = 0;
+    const orbx_status s = orbx_vocabulary_transform(voc, f->v.desc.data(), n, levelsup, nullptr,
+                                                    nullptr, f->bow_w.data(), f->bow_v.data(), &nb,
+                                                    f->fv_node.data(), f->fv_off.data(),
+                                                    f->fv_feat.data(), &nf);
+    std::memset(&f->fs, 0, sizeof(f->fs));
+    f->fs.n = n;
+    f->fs.keys = f->v.kps.data();
+    f->fs.desc = f->v.desc.data();
+    f->fs.n_nodes = nf;
+    f->fs.node_id = f->fv_node.data();
+    f->fs.node_off = f->fv_off.data();
+    f->fs.node_feat = f->fv_feat.data();
+    return s;
+}
+
+static int tum(const std::string& dir, int nframes, int warmup) {
+    int W = 0, H = 0, nfeat = 0, P = 0, levelsup = 4;
+    char vpath[4096] = {0};
+    {
+        FILE* f = std::fopen((dir + "/params.txt").c_str(), "r");
+        if (!f) return 2;
+        const int got = std::fscanf(f, "%d %d %d %d %d %4095s", &W, &H, &nfeat, &P, &levelsup, vpath);
+        std::fclose(f);
+        if (got != 6 || P < 1) return 2;
+    }
+    std::vector<std::vector<uint8_t>> Ls((size_t)P), Rs((size_t)P);
+    for (int i = 0; i < P; ++i) {
+        const std::string b = dir + "/pair_" + std::to_string(i);
+        if (!read_file(b + "_left.raw", Ls[(size_t)i]) || !read_file(b + "_right.raw", Rs[(size_t)i]))
+            return 2;
+    }
+    orbx_vocabulary* voc = nullptr;
+    CHECK(orbx_vocabulary_load_text(vpath, 0, &voc));
+    orbx_extractor_params p = {nfeat, 1.2f, 8, 20, 7, 1, 1, 0};
+    orbx_extractor *hk = nullptr, *hf = nullptr;
+    CHECK(orbx_extractor_create(&p, &hk));
+    CHECK(orbx_extractor_create(&p, &hf));
+    orbx_matcher* m = nullptr;
+    const orbx_matcher_params mp = {0.7f, 1, 0};   // Tracking.cc:812
+    CHECK(orbx_matcher_create(&mp, &m));
+    std::vector<BowFrame> kfs((size_t)P);
+    std::vector<std::vector<uint8_t>> valid((size_t)P);
+    uint32_t rng = 12345u;
+    for (int i = 0; i < P; ++i) {
+        CHECK(make_bow_frame(hk, voc, levelsup, Ls[(size_t)i].data(), W, H, &kfs[(size_t)i]));
+        valid[(size_t)i].resize((size_t)kfs[(size_t)i].v.n);
+        for (auto& b : valid[(size_t)i]) {
+            rng = rng * 1664525u + 1013904223u;
+            b = (rng >> 8) % 100 < 85;
+        }
+    }
+    std::vector<double> ms;
+    long long matches = 0, kps = 0;
+    std::vector<int32_t> out;
+    for (int f = 0; f < warmup + nframes; ++f) {
+        const int i = f % P;
+        BowFrame fr;
+        const auto t0 = std::chrono::steady_clock::now();
+        CHECK(make_bow_frame(hf, voc, levelsup, Rs[(size_t)i].data(), W, H, &fr));
+        out.resize((size_t)std::max(fr.v.n, 1));
+        int32_t nm = 0;
+        CHECK(orbx_search_by_bow_kf_frame(m, &kfs[(size_t)i].fs, valid[(size_t)i].data(), &fr.fs,
+                                          out.data(), &nm));
+        const auto t1 = std::chrono::steady_clock::now();
+        if (f >= warmup) {
+            ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            matches += nm;
+            kps += fr.v.n;
+        }
+    }
+    orbx_matcher_destroy(m);
+    orbx_extractor_destroy(hk);
+    orbx_extractor_destroy(hf);
+    orbx_vocabulary_destroy(voc);
+    std::printf("{\"frames\": %d, \"warmup\": %d, \"mean_keypoints\": %.3f, "
+                "\"mean_bow_matches\": %.3f, \"latency_ms\": [",
+                nframes, warmup, (double)kps / std::max(nframes, 1),
+                (double)matches / std::max(nframes, 1));
+    for (size_t k = 0; k < ms.size(); ++k) std::printf("%s%.4f", k ? ", " : "", ms[k]);
+    std::printf("]}\n");
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "layout") return layout();
     if (argc >= 3 && std::string(argv[1]) == "run") return run(argv[2]);
     if (argc >= 5 && std::string(argv[1]) == "bench")
         return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
-    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP\n", argv[0]);
+    if (argc >= 5 && std::string(argv[1]) == "tum")
+        return tum(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
+    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP | tum DIR NFRAMES WARMUP\n",
+                 argv[0]);
     return 2;
 }

@@ -43,7 +43,7 @@ def _worker(rank, world, port, n_total, q):
         everything = gather_rows(rows, n_total, world)
         cand = gather_candidate_matches(rows, allc, n_total, world)
         q.put((rank, desc.sum().item(), allc.numpy().tolist(), everything.numpy().tolist(),
-               [(k, m.numpy().tolist()) for k, m in cand]))
+               [(k, np.asarray(m).tolist()) for k, m in cand]))
     finally:
         dist.destroy_process_group()
 
