@@ -714,7 +714,7 @@ def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20):
                      f"L/R extraction on 2 threads + ComputeStereoMatches (Frame.cc:89-102), "
                      f"{el:.1f} s",
            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-           "build": "g++ -O3 -march=x86-64-v3 -ffp-contract=off (oracle/Makefile)"}
+           "build": f"g++ -O3 -march={oracle.ISA} -ffp-contract=off (oracle/Makefile)"}
     out.update(latency_stats(ms))
     return out
 

@@ -1097,7 +1097,14 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                                                 long long kscratch_per_image, int NCAP, int KCAP,
                                                 int level_base) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if OCT_MERGED && OCT_LEVEL_MAJOR
+    // one launch for all levels, the (long) level-0 lists dispatched first
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int level = lin / gridDim.y, b = lin - level * gridDim.y, tid = threadIdx.x;
+    (void)level_base;
+#else
     const int level = level_base + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+#endif
     const LevelGeom& L = g->lv[level];
     OSTAMP(0);
     // carve LDS

@@ -55,11 +55,14 @@ struct LevelGeom {
 #ifndef OD_NK
 #define OD_NK 8               // keypoints per wave in k_orient_desc (<= 64)
 #endif
-// k_octree: one launch over all levels (OCT_MERGED) under one LDS budget per workgroup; a
-// level whose candidates exceed the budget's kcap keeps them in global scratch
+// k_octree: one launch over all levels (OCT_MERGED) under one LDS budget per workgroup, the
+// blocks in level-major order so the long level-0 lists start first and the shorter lists of
+// levels 1.. fill the CUs behind them; a level whose candidates exceed the budget's kcap keeps
+// them in global scratch.  B = 512, two runs each (profiles/r03_ab_octree_merged.txt): merged
+// level-major at 40 KB 0.322-0.323 ms, two launches (level 0, then levels 1..) at 40 KB
+// 0.335-0.339, merged in (image, level) order 0.536-0.542, merged level-major at 52 KB 0.358-0.361
 #ifndef OCT_MERGED
-#define OCT_MERGED 0   // measured slower (0.50 vs 0.46 ms at B = 512): the level-0 lists need
-                       // their large LDS footprint
+#define OCT_MERGED 1
 #endif
 #ifndef OCT_LDS0_KB
 #define OCT_LDS0_KB 40  // level 0 launch (OCT_MERGED = 0): four workgroups per CU, all 1024 images in
@@ -68,8 +71,11 @@ struct LevelGeom {
 #ifndef OCT_LDS1_KB
 #define OCT_LDS1_KB 40  // levels 1.. launch (OCT_MERGED = 0): four workgroups per CU
 #endif
+#ifndef OCT_LEVEL_MAJOR
+#define OCT_LEVEL_MAJOR 1   // OCT_MERGED: blocks in level-major order (level 0's lists first)
+#endif
 #ifndef OCT_LDS_KB
-#define OCT_LDS_KB 52
+#define OCT_LDS_KB 40       // OCT_MERGED: four workgroups per CU
 #endif
 #define LT_W 128              // output tile width  (32 groups of 4)
 #ifndef LT_H

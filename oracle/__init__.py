@@ -19,7 +19,23 @@ import subprocess
 import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = HERE / "_build" / "liborb_oracle.so"
+LIB_V3 = HERE / "_build" / "liborb_oracle.so"
+LIB_V4 = HERE / "_build" / "liborb_oracle_v4.so"
+AVX512 = ("avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl")
+
+
+def host_has_v4() -> bool:
+    """x86-64-v4 (AVX-512 F/BW/CD/DQ/VL) on this host's CPU."""
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+    except (OSError, StopIteration):
+        return False
+    return all(f in flags for f in AVX512)
+
+
+# the build a -march=native compile would come closest to on this host
+LIB_PATH = LIB_V4 if LIB_V4.exists() and host_has_v4() else LIB_V3
+ISA = "x86-64-v4" if LIB_PATH == LIB_V4 else "x86-64-v3"
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -30,7 +46,8 @@ _lib = None
 def build(force: bool = False) -> pathlib.Path:
     """Compile the restatement with its Makefile (g++; no GPU needed)."""
     srcs = list(HERE.glob("*.cpp")) + list(HERE.glob("*.h"))
-    stale = not LIB_PATH.exists() or any(p.stat().st_mtime > LIB_PATH.stat().st_mtime for p in srcs)
+    stale = any(not p.exists() for p in (LIB_V3, LIB_V4)) or \
+        any(p.stat().st_mtime > min(LIB_V3.stat().st_mtime, LIB_V4.stat().st_mtime) for p in srcs)
     if force or stale:
         subprocess.run(["make", "-s", "-B" if force else "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
