@@ -761,6 +761,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_HMASK
 #define STRIP_HMASK 1   // mode 3, SSE2 waves: horizontal sums masked once per source row
 #endif
+// One workgroup per strip row (its snw <= 8 waves side by side) with an s_barrier every
+// STRIP_SYNC* blocks of 7 steps (0: 4-wave workgroups, no barrier): the waves of a strip row
+// then store each row within a few steps of each other, so the 128-byte lines split between
+// two waves' 120-pixel runs are merged in L2 before they are written back (without it one
+// write-back per part: level 0 wrote 1.24x its bytes, levels 1-7 1.10x).
+#ifndef STRIP_SYNC0
+#define STRIP_SYNC0 0  // level 0
+#endif
+#ifndef STRIP_SYNC3
+#define STRIP_SYNC3 2  // INTER_LINEAR levels
+#endif
 #ifndef STRIP_PEEL
 #define STRIP_PEEL 1   // interior blocks of a walk without store predicates
 #endif
@@ -788,14 +799,14 @@ template <int MODE>
 // MODE 4: level 0 already in the pyramid (written there by the H2D copy or the caller, see
 // orbx_batch_input_view): blurred only, the level itself is not stored again;
 // MODE 3: an INTER_LINEAR level from the level above.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE != 3 ? STRIP_WPE0 : STRIP_WPE3))) void k_level_strip(const Geometry* __restrict__ g,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ? STRIP_WPE0 : STRIP_WPE3))) void k_level_strip(const Geometry* __restrict__ g,
                                                      const uint8_t* __restrict__ ltab,
                                                      const uint8_t* __restrict__ in0,
                                                      const uint8_t* __restrict__ in1, int split,
                                                      size_t stride, size_t bstride,
                                                      uint8_t* __restrict__ pyr,
                                                      uint8_t* __restrict__ blur, int level,
-                                                     int sth) {
+                                                     int sth, int sync) {
     static_assert(MODE == 0 || MODE == 3 || MODE == 4, "strip kernel: level 0 or INTER_LINEAR levels");
     constexpr bool L0 = MODE != 3;         // level 0: an 8-bit image in, no resize
     int bx, b;
@@ -804,7 +815,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
     const LevelGeom& L = g->lv[level];
     // wave of this image; readfirstlane makes it (and the strip row, the row counters and the
     // row addresses derived from it) scalar for the compiler, not per-lane VALU work
-    const int wv = bx * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wv = bx * (int)(blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int sns = (L.h + sth - 1) / sth;        // strip rows of this call's height
     if (wv >= L.snw * sns) return;                // whole waves only
     const int swx = wv % L.snw, sy = wv / L.snw;
@@ -1075,7 +1086,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
         }
         // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
         // store nothing)
+        // sync > 0 only when a workgroup is one strip row (every wave takes the same steps)
+        int nblk = 0;
         auto block = [&](int i0, auto all_c) {
+            if (sync > 0) {
+                if (nblk % sync == 0) __builtin_amdgcn_s_barrier();
+                ++nblk;
+            }
             unroll_seq([&](auto k_c) { step(k_c, i0 + decltype(k_c)::value, rsimd_c, bsimd_c, all_c); },
                        std::make_integer_sequence<int, U>{});
         };
@@ -1129,10 +1146,12 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
         const int mode = level_mode(L, l);
         if (L.strip) {
             const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;
+            const int sync = L.snw <= 8 ? (mode == 3 ? STRIP_SYNC3 : STRIP_SYNC0) : 0;
             hipLaunchKernelGGL(mode == 3 ? k_level_strip<3> : (a.in_place ? k_level_strip<4> : k_level_strip<0>),
-                               dim3((L.snw * sns + 3) / 4, a.batch), dim3(256), 0, st, a.dg,
+                               sync > 0 ? dim3(sns, a.batch) : dim3((L.snw * sns + 3) / 4, a.batch),
+                               dim3(sync > 0 ? 64 * L.snw : 256), 0, st, a.dg,
                                a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
-                               a.pyr, a.blur, l, sth);
+                               a.pyr, a.blur, l, sth, sync);
         } else if (l == 0 && a.in_place) {
             // the tiled level-0 kernel reading the pyramid's own level 0 (its level stores
             // write back the bytes already there)
