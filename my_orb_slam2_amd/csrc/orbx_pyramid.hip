@@ -772,6 +772,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_SYNC3
 #define STRIP_SYNC3 2  // INTER_LINEAR levels
 #endif
+#ifndef STRIP_SYNC_LEVELS
+#define STRIP_SYNC_LEVELS 0xFFFF  // bit l: level l may take strip-row workgroups
+#endif
 #ifndef STRIP_PEEL
 #define STRIP_PEEL 1   // interior blocks of a walk without store predicates
 #endif
@@ -1146,7 +1149,7 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
         const int mode = level_mode(L, l);
         if (L.strip) {
             const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;
-            const int sync = L.snw <= 8 ? (mode == 3 ? STRIP_SYNC3 : STRIP_SYNC0) : 0;
+            const int sync = L.snw <= 8 && ((STRIP_SYNC_LEVELS >> l) & 1) ? (mode == 3 ? STRIP_SYNC3 : STRIP_SYNC0) : 0;
             hipLaunchKernelGGL(mode == 3 ? k_level_strip<3> : (a.in_place ? k_level_strip<4> : k_level_strip<0>),
                                sync > 0 ? dim3(sns, a.batch) : dim3((L.snw * sns + 3) / 4, a.batch),
                                dim3(sync > 0 ? 64 * L.snw : 256), 0, st, a.dg,
