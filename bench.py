@@ -81,15 +81,20 @@ def parse():
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
     ap.add_argument("--workload", default="stereo",
-                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb", "tum"],
+                    choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb", "tum",
+                             "bf"],
                     help="stereo = the BASELINE metric (configs[1]); euroc = configs[2] (mono "
                          "extract + SearchByProjection vs the local map); reloc = configs[3] "
                          "(1 frame vs 10k keyframes, DB sharded); triangulation = configs[4] "
                          "(512 SearchForTriangulation jobs, sharded); dropin = the host-image "
-                         "drop-in path one stereo frame at a time (per-frame latency)")
+                         "drop-in path one stereo frame at a time (per-frame latency); bf = "
+                         "configs[3] as a pure brute-force top-2 (1000 query descriptors vs "
+                         "--db-rows database rows, rows sharded, RCCL all-gather + merge)")
     ap.add_argument("--frames", type=int, default=300,
                     help="dropin: timed stereo frames (after --warmup frames, at least 20)")
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
+    ap.add_argument("--db-rows", type=int, default=10_000_000,
+                    help="bf: database descriptors (10k keyframes x 1000, SURVEY §8(d) C4)")
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
     ap.add_argument("--queries", type=int, default=2000,
                     help="euroc: projected local-map MapPoints per frame")
@@ -220,6 +225,8 @@ def main():
         return main_kfdb(args)
     if args.workload == "tum":
         return main_tum(args)
+    if args.workload == "bf":
+        return main_bf(args)
     if args.workload != "stereo":
         return main_match(args)
     import torch
@@ -1358,6 +1365,154 @@ def main_match(args):
                     "data": "synthetic", "config": cfg, **extra, "roofline": roof,
                     "cpu_baseline": cpu}
         emit(json.dumps(out_line))
+    if dist_on:
+        dist.destroy_process_group()
+
+
+def bf_rows(r0: int, r1: int) -> np.ndarray:
+    """Database rows [r0, r1) of the bf workload: 32 bytes per row from a counter hash
+    (splitmix64 of 4 * row + k), so any row, and any shard, is computed independently of the
+    others and of the world size (uniform random bits)."""
+    x = (np.arange(r0, r1, dtype=np.uint64)[:, None] * np.uint64(4) +
+         np.arange(4, dtype=np.uint64)[None, :])
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return np.ascontiguousarray(x).view(np.uint8).reshape(r1 - r0, 32)
+
+
+def bf_query(ndb: int, nq: int = 1000, seed: int = 7):
+    """The bf workload's query frame: nq random descriptors, 30 % of them replaced by database
+    rows with 0-40 bits flipped.  Returns (q, planted query ids, their rows)."""
+    rng = np.random.default_rng(seed)
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    ids = rng.choice(nq, int(0.3 * nq), replace=False)
+    rows = rng.integers(0, ndb, len(ids))
+    for i, r in zip(ids, rows):
+        q[i] = bf_rows(int(r), int(r) + 1)[0]
+        for b in rng.choice(256, int(rng.integers(0, 41)), replace=False):
+            q[i, b // 8] ^= np.uint8(1 << (b % 8))
+    return q, ids, rows
+
+
+def main_bf(args):
+    """configs[3] as a pure brute-force top-2: one query frame (1000 descriptors) against the
+    whole descriptor database (default 10^7 rows = 10k keyframes x 1000), the rows sharded
+    across ranks.  Step: RCCL broadcast of the query (32 KB), every rank's top-2 over
+    its shard (orbx_hamming_bf_top2_device, global row numbers), RCCL all-gather of the
+    12-byte per-query results and the merge in rank order (distributed.gather_top2)."""
+    import torch
+    import torch.distributed as dist
+
+    from my_orb_slam2_amd import ORBmatcher
+    from my_orb_slam2_amd.distributed import broadcast_query, gather_top2, shard_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist_on = world > 1 or (os.environ.get("ORBX_FORCE_DIST") == "1" and "RANK" in os.environ)
+    if dist_on:
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ndb = args.db_rows
+    if ndb < world:
+        sys.exit(f"bench.py: {ndb} database rows < world size {world}")
+    r0, r1 = shard_range(ndb, rank, world)
+    ddb = torch.empty((r1 - r0, 32), dtype=torch.uint8, device=dev)
+    blk = 1 << 20
+    for b0 in range(r0, r1, blk):                  # the shard, built block by block
+        b1 = min(b0 + blk, r1)
+        ddb[b0 - r0:b1 - r0] = torch.from_numpy(bf_rows(b0, b1)).to(dev)
+    qh, ids, rows = bf_query(ndb)
+    nq = len(qh)
+    dq = torch.from_numpy(qh).to(dev)
+    m = ORBmatcher(0.75, True, device=local)
+    out = [torch.empty(nq, dtype=torch.int32, device=dev) for _ in range(3)]
+
+    def step():
+        if dist_on:
+            broadcast_query([dq])
+        m.hamming_bf_top2_device(dq, nq, ddb, r1 - r0, *out, idx_base=r0, stream=st)
+        if dist_on:
+            return gather_top2(*out, world)
+        return out
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize(dev)
+    m.profile(not args.no_kernel_timing)
+    m.collect_profile()
+    if dist_on:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize(dev)
+    if dist_on:
+        dist.barrier(device_ids=[local])
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = m.collect_profile() if not args.no_kernel_timing else {}
+    bi, bd, sd = (t.cpu().numpy() for t in res)
+    roof = None
+    if prof and prof.get("k_bf", (0, 0))[1]:
+        tot_ms, launches = prof["k_bf"]
+        avg_s = tot_ms / 1000.0 / launches
+        dist_n = float(nq) * (r1 - r0)
+        ops = 16.0 * dist_n                           # 8 XOR + 8 BCNT per 256-bit distance
+        dps = dist_n / avg_s
+        db_bytes = 32.0 * (r1 - r0) + 32.0 * nq + 12.0 * nq
+        roof = {"kernel": "k_bf_top2 + k_bf_merge", "bound": "valu", "achieved": ops / avg_s / 1e12,
+                "peak": VALU_PEAK_TOPS, "unit": "Tops/s (int32 lane-ops)",
+                "frac": ops / avg_s / 1e12 / VALU_PEAK_TOPS, "traffic": None,
+                "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_s * 1000.0,
+                "distances_per_s": dps, "issue_peak_distances_per_s": DIST_ISSUE_PEAK,
+                "issue_frac": dps / DIST_ISSUE_PEAK,
+                "hbm": {"achieved": db_bytes / avg_s / 1e9, "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                        "frac": db_bytes / avg_s / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_launch": db_bytes}}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        try:
+            from oracle import matcher as om
+            n_s, spent = 2000, 0.0
+            while spent < min(args.cpu_seconds, 20.0) / 4 and n_s < ndb:
+                t1 = time.perf_counter()
+                om.bf_top2(qh, bf_rows(0, n_s))
+                spent = time.perf_counter() - t1
+                if spent < min(args.cpu_seconds, 20.0) / 4:
+                    n_s = min(ndb, n_s * 4)
+            per_frame = spent * ndb / n_s
+            cpu = {"value": 1.0 / per_frame, "unit": "query frames/sec", "cores": 1,
+                   "kind": "port",
+                   "sample": f"the 1000-descriptor query frame against {n_s} of the {ndb} rows "
+                             f"({spent:.1f} s, oracle_bf_top2: ORBmatcher's best / second loop), "
+                             f"scaled to the whole database"}
+        except Exception:
+            cpu = None
+    if rank == 0:
+        found = int((bi[ids] == rows).sum())
+        line = {"metric": "brute-force top-2 query frames/sec, 1000 descriptors vs "
+                          f"{ndb} database descriptors", "value": args.steps / elapsed,
+                "unit": "query frames/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "u8 (256-bit Hamming)", "data": "synthetic",
+                "config": {"workload": "relocalisation_pure_bf_top2", "db_rows": ndb,
+                           "query_descriptors": nq, "planted_queries": int(len(ids)),
+                           "parallelism": f"row shards x{world}, RCCL broadcast + all-gather "
+                                          "of per-query top-2, merge in rank order"},
+                "planted_found": found, "mean_best_dist": float(bd.mean()),
+                "roofline": roof, "cpu_baseline": cpu}
+        emit(json.dumps(line))
     if dist_on:
         dist.destroy_process_group()
 

@@ -238,6 +238,27 @@ orbx_status orbx_search_by_projection_batch_device(
     const int32_t* d_q_off, int32_t nq, const float* inv_sigma2, int32_t nlevels,
     int32_t orb_dist, int32_t* d_match, int32_t* d_nmatches, void* stream);
 
+/* Brute-force Hamming top-2 of nq query descriptors (q: nq x 32) against ndb database rows
+ * (db: ndb x 32) — SURVEY §8(b) orbx_hamming_bf_top2 / §8(e) C4.  The semantics are the best /
+ * second loop of the ORBmatcher searches (src/ORBmatcher.cc:232-256) run over every row in
+ * order: bestDist1 = bestDist2 = 256 initially, `dist < bestDist1` moves the best to the
+ * second, else `dist < bestDist2` updates the second.  best_idx[i] = the first row at the least
+ * distance (-1 if no row is below 256), best_dist[i] that distance (256 if none),
+ * second_dist[i] the second least distance (equal to best_dist[i] on a tie, 256 if none).
+ * Host pointers; the database is copied to the device for the call (keep a large database
+ * resident and use the _device form instead). */
+orbx_status orbx_hamming_bf_top2(orbx_matcher* m, const uint8_t* q, int32_t nq,
+                                 const uint8_t* db, int64_t ndb, int32_t* best_idx,
+                                 int32_t* best_dist, int32_t* second_dist);
+/* The same on device arrays, on the caller's stream; best_idx is offset by idx_base (a shard
+ * of a larger database reports global row numbers, so per-shard results merge in shard order
+ * with distributed.merge_top2).  ndb < 2^31 - idx_base.  The partial results live in the
+ * matcher's scratch: calls on one matcher must share `stream` or be serialised. */
+orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int32_t nq,
+                                        const uint8_t* d_db, int64_t ndb, int64_t idx_base,
+                                        int32_t* d_best_idx, int32_t* d_best_dist,
+                                        int32_t* d_second_dist, void* stream);
+
 /* Waits for `stream` and returns ORBX_ERR_CAPACITY if a batched call on this matcher met a
  * keyframe above max_feat since the last sync (the flag is then cleared). */
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream);
@@ -261,7 +282,7 @@ orbx_status orbx_compute_distinctive_descriptors_device(orbx_matcher* m, const u
 /* ---- per-kernel timing for the matcher handle ------------------------------------------ */
 typedef enum {
     ORBX_MK_BOW = 0, ORBX_MK_TRIANGULATE, ORBX_MK_PROJ_SEARCH, ORBX_MK_PROJ_RESOLVE,
-    ORBX_MK_DISTINCTIVE, ORBX_MK_COUNT
+    ORBX_MK_DISTINCTIVE, ORBX_MK_BF, ORBX_MK_COUNT
 } orbx_match_kernel_id;
 orbx_status orbx_matcher_profile_enable(orbx_matcher* m, int on);
 orbx_status orbx_matcher_profile_collect(orbx_matcher* m, double* total_ms, int64_t* launches);

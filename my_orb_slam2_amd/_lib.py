@@ -20,7 +20,8 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
 KERNELS = ["k_level", "k_fast", "k_octree", "k_orient_desc", "k_stereo", "k_level0"]
-MATCH_KERNELS = ["k_bow", "k_triangulate", "k_proj_search", "k_proj_resolve", "k_distinctive"]
+MATCH_KERNELS = ["k_bow", "k_triangulate", "k_proj_search", "k_proj_resolve", "k_distinctive",
+                 "k_bf"]
 
 STATUS = {0: "ORBX_OK", -1: "ORBX_ERR_INVALID", -2: "ORBX_ERR_DEVICE", -3: "ORBX_ERR_CAPACITY",
           -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_STATE"}
@@ -95,6 +96,9 @@ SIGNATURES = {
     "orbx_matcher_sync": (_i, [_vp, _vp]),
     "orbx_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp]),
     "orbx_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
+    "orbx_hamming_bf_top2": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, _vp, _vp, _vp]),
+    "orbx_hamming_bf_top2_device": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, ctypes.c_int64,
+                                         _vp, _vp, _vp, _vp]),
     "orbx_matcher_profile_enable": (_i, [_vp, _i]),
     "orbx_matcher_profile_collect": (_i, [_vp, _vp, _vp]),
     "orbx_match_kernel_name": (ctypes.c_char_p, [_i]),

@@ -23,7 +23,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "liborbx.so"
 SOURCES = ["orbx_pyramid.hip", "orbx_extract.hip", "orbx_stereo.hip", "orbx_match.hip",
            "orbx_capi.hip", "orbx_match_capi.hip", "orbx_vocab.hip", "orbx_frame.hip",
-           "orbx_kfdb.hip"]
+           "orbx_kfdb.hip", "orbx_bf.hip"]
 HEADERS = ["orbx_internal.h", "orbx_device.h", "orbx_math.h", "orbx_kernels.h", "orbx_host.h",
            "orbx_match_kernels.h", "orbx_pattern.inc", "../../include/orbx.h",
            "../../include/orbx_match.h", "../../include/orbx_vocab.h", "../../include/orbx_frame.h",

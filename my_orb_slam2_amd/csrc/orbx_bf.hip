@@ -1,0 +1,218 @@
+// orbx_bf.hip — brute-force Hamming top-2 over a descriptor database (SURVEY §8(b)
+// orbx_hamming_bf_top2; §8(e) C4 "per-rank top-2, then an all-gather and a merge").
+//
+// Semantics: the best / second-best loop every ORBmatcher search runs over its candidates
+// (src/ORBmatcher.cc:232-256: bestDist1 = bestDist2 = 256, `dist < bestDist1` moves the best
+// to second, else `dist < bestDist2`), with the candidates = every database row in order.
+// For query i: best = the FIRST row at the least distance below 256 (-1 if none), second =
+// the second least distance of the multiset {256, 256} ∪ {distances} (so it equals the best
+// on a tie).  A distance of 256 (every bit differs) never becomes the best, as in the loop.
+//
+//   k_bf_top2   lane = query (its 8 dwords in VGPRs), a workgroup = 4 waves = 256 queries
+//               against one chunk of database rows read by scalar loads (wave-uniform rows,
+//               XOR operands straight from SGPRs).  Per row and lane: 8 v_xor + 8 v_bcnt
+//               (accumulating) + key = dist << 23 | row-in-chunk, then the top-2 update as one
+//               v_min_u32 + one v_med3_u32 on keys (the key order is (distance, row), i.e.
+//               the first row wins a tie).  Partial top-2 per (chunk, query) to global.
+//   k_bf_merge  folds the chunks' partials in chunk order (= row order): best = the earlier
+//               chunk's on equal distance, second = the second least of the two pairs' union
+//               (8 threads per query over contiguous chunk ranges, then those 8 in order).
+// Issue bound: 8 x 2.3 + 8 x 4.4 + 3 x 4.2 ≈ 66 cycles per 64 distances per SIMD, i.e.
+// ≈2.4·10^12 distances/s over 1024 SIMDs at 2.4 GHz (profiles/r01_valu_issue_rates.txt).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "orbx_device.h"
+#include "orbx_kernels.h"
+#include "orbx_match_kernels.h"
+
+namespace orbx {
+
+namespace {
+
+#ifndef BF_PIPE
+#define BF_PIPE 1      // k_bf_top2: ping-pong row groups (0: 8-row groups, one wait each)
+#endif
+
+constexpr uint32_t BF_NONE = 256u << 23;       // (distance 256, row 0): the loop's initial value
+constexpr int BF_ROW_BITS = 23;                 // rows per chunk < 2^23
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+static_assert(BF_ROW_BITS == 23, "the key's shift is written out in k_bf_top2");
+
+__global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q, int nq,
+                                                  const uint32_t* __restrict__ db, long long ndb,
+                                                  int chunk, int nqpad, uint2* __restrict__ part) {
+    int bx, c;
+    xcd_block(bx, c);                  // the query blocks of one chunk share an XCD's L2
+    const int qi = bx * 256 + (int)threadIdx.x;
+    const int qc = min(qi, nq - 1);
+    uint32_t a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = q[(size_t)qc * 8 + k];
+    const long long r0 = (long long)c * chunk;
+    const int n = (int)min((long long)chunk, ndb - r0);
+    const uint32_t* __restrict__ p = db + r0 * 8;
+    uint32_t b1 = BF_NONE, b2 = BF_NONE;
+    // per row: 8 v_xor (SGPR operands) + 8 accumulating v_bcnt + one v_lshl_or for the key
+    // (written out: the compiler otherwise splits the popcount chain into trees of v_add3 and
+    // builds the key with two 4-cycle ops) + v_med3 / v_min for the top-2
+    auto row = [&](const uint32_t* r, int e) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d = bcnt_acc(a[k] ^ r[k], d);
+        uint32_t key;
+        asm("v_lshl_or_b32 %0, %1, 23, %2" : "=v"(key) : "v"(d), "s"(e));
+        b2 = med3_u32(b1, b2, key);
+        b1 = min(b1, key);
+    };
+    // groups of BF_G rows in two register sets (ping-pong, no copies): the scalar loads
+    // (s_load_dwordx8 per row) of one set are in flight while the other set is computed, so
+    // the wait for them (scalar loads retire out of order: lgkmcnt(0)) comes a group later
+    constexpr int BF_G = 4;
+    int e = 0;
+    auto load = [&](uint32_t (&g)[BF_G][8], int e0) {
+#pragma unroll
+        for (int j = 0; j < BF_G; ++j)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[j][k] = p[(size_t)(e0 + j) * 8 + k];
+    };
+    auto group = [&](const uint32_t (&g)[BF_G][8], int e0) {
+#pragma unroll
+        for (int j = 0; j < BF_G; ++j) row(g[j], e0 + j);
+    };
+#if BF_PIPE == 0
+    // plain groups of 8 rows: all 8 rows' loads, one wait, then the 8 rows
+    for (; e + 8 <= n; e += 8) {
+        uint32_t A[BF_G][8], B[BF_G][8];
+        load(A, e);
+        load(B, e + BF_G);
+        group(A, e);
+        group(B, e + BF_G);
+    }
+#else
+    if (n >= 2 * BF_G) {
+        uint32_t A[BF_G][8], B[BF_G][8];
+        load(A, 0);
+        for (; e + 4 * BF_G <= n; e += 2 * BF_G) {
+            load(B, e + BF_G);
+            group(A, e);
+            load(A, e + 2 * BF_G);
+            group(B, e + BF_G);
+        }
+        load(B, e + BF_G);
+        group(A, e);
+        group(B, e + BF_G);
+        e += 2 * BF_G;
+    }
+#endif
+    for (; e < n; ++e) row(p + (size_t)e * 8, e);
+    if (qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1, b2);
+}
+
+// 32 queries per workgroup, 8 threads per query: thread slice s folds the contiguous chunk
+// range [s*L, (s+1)*L) in order, then slice 0 folds the 8 slice results in order (the fold is
+// associative: (earlier, later) -> best of the earlier on a tie).
+__global__ __launch_bounds__(256) void k_bf_merge(const uint2* __restrict__ part, int nq,
+                                                   int nqpad, int nchunks, int chunk,
+                                                   long long idx_base, int32_t* __restrict__ best_idx,
+                                                   int32_t* __restrict__ best_dist,
+                                                   int32_t* __restrict__ second_dist) {
+    __shared__ uint32_t sd1[8][32], sd2[8][32];
+    __shared__ long long srow[8][32];
+    const int ql = (int)threadIdx.x & 31, sl = (int)threadIdx.x >> 5;
+    const int qi = blockIdx.x * 32 + ql;
+    const int L = (nchunks + 7) / 8;
+    const int c0 = sl * L, c1 = min(nchunks, c0 + L);
+    uint32_t d1 = 256, d2 = 256;
+    long long row = -1;
+    if (qi < nq) {
+        // eight partials loaded together, then folded in order (branch-free)
+        for (int cb = c0; cb < c1; cb += 8) {
+            uint2 k[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) k[j] = part[(size_t)min(cb + j, c1 - 1) * nqpad + qi];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (cb + j >= c1) k[j] = make_uint2(BF_NONE, BF_NONE);   // past the range
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t e1 = k[j].x >> BF_ROW_BITS, e2 = k[j].y >> BF_ROW_BITS;
+                // second = second least of {d1, d2} ∪ {e1, e2} (both pairs sorted)
+                d2 = min(max(d1, e1), min(d2, e2));
+                const bool take = e1 < d1;     // strict: the earlier chunk keeps a tie
+                d1 = take ? e1 : d1;
+                row = take ? (long long)(cb + j) * chunk + (k[j].x & ((1u << BF_ROW_BITS) - 1)) : row;
+            }
+        }
+    }
+    sd1[sl][ql] = d1;
+    sd2[sl][ql] = d2;
+    srow[sl][ql] = row;
+    __syncthreads();
+    if (sl != 0 || qi >= nq) return;
+    for (int t = 1; t < 8; ++t) {
+        const uint32_t e1 = sd1[t][ql], e2 = sd2[t][ql];
+        d2 = min(max(d1, e1), min(d2, e2));
+        if (e1 < d1) {
+            d1 = e1;
+            row = srow[t][ql];
+        }
+    }
+    best_idx[qi] = row < 0 ? -1 : (int32_t)(idx_base + row);
+    best_dist[qi] = (int32_t)d1;
+    second_dist[qi] = (int32_t)d2;
+}
+
+}  // namespace
+
+// Rows per chunk: enough chunks that the (query block, chunk) grid gives every CU several
+// workgroups, rounded so the grid fills the 8 XCDs evenly.
+int bf_chunk_rows(long long ndb, int nq, int ncu) {
+    const int qb = (nq + 255) / 256;
+    long long target = (long long)std::max(ncu, 1) * 8 / qb;          // chunks wanted
+    if (target < 8) target = 8;
+    long long rows = (ndb + target - 1) / target;
+    rows = ((rows + 63) / 64) * 64;
+    if (rows < 256) rows = 256;
+    if (rows > (1ll << BF_ROW_BITS) - 64) rows = (1ll << BF_ROW_BITS) - 64;
+    return (int)rows;
+}
+
+size_t bf_partial_bytes(long long ndb, int nq, int chunk) {
+    const long long nchunks = (ndb + chunk - 1) / chunk;
+    const int nqpad = ((nq + 255) / 256) * 256;
+    return (size_t)nchunks * (size_t)nqpad * sizeof(uint2);
+}
+
+hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer) {
+    if (a.nq <= 0) return hipSuccess;
+    const int nqpad = ((a.nq + 255) / 256) * 256;
+    const long long nchunks = a.ndb > 0 ? (a.ndb + a.chunk - 1) / a.chunk : 0;
+    if (nchunks > INT32_MAX / 2) return hipErrorInvalidValue;
+    hipEvent_t e = timer ? timer->start(st) : nullptr;
+    if (nchunks > 0)
+        hipLaunchKernelGGL(k_bf_top2, dim3(nqpad / 256, (unsigned)nchunks), dim3(256), 0, st,
+                           (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db, a.ndb, a.chunk,
+                           nqpad, (uint2*)a.part);
+    hipLaunchKernelGGL(k_bf_merge, dim3((a.nq + 31) / 32), dim3(256), 0, st, (const uint2*)a.part,
+                       a.nq, nqpad, (int)nchunks, a.chunk, a.idx_base, a.best_idx, a.best_dist,
+                       a.second_dist);
+    if (timer) timer->stop(ORBX_MK_BF, e, st);
+    return hipGetLastError();
+}
+
+}  // namespace orbx

@@ -20,10 +20,13 @@
 
 using namespace orbx;
 
+static_assert((int)ORBX_MK_COUNT <= (int)orbx::K_COUNT, "the matcher timer shares KernelTimer's slots");
+
 struct orbx_matcher {
     orbx_matcher_params prm;
     hipStream_t stream = nullptr;
-    DevBuf d_in, d_out, d_aux, d_proj;
+    int ncu = 256;                     // compute units of the device (BF chunk sizing)
+    DevBuf d_in, d_out, d_aux, d_proj, d_bf;
     int* d_err = nullptr;
     std::vector<uint8_t> staging;
     KernelTimer timer;
@@ -343,6 +346,9 @@ orbx_status orbx_matcher_create(const orbx_matcher_params* params, orbx_matcher*
         orbx_matcher_destroy(m);
         return ORBX_ERR_DEVICE;
     }
+    hipDeviceProp_t prop;
+    if (HIPOK(hipGetDeviceProperties(&prop, p.device)) && prop.multiProcessorCount > 0)
+        m->ncu = prop.multiProcessorCount;
     *out = m;
     return ORBX_OK;
 }
@@ -355,6 +361,7 @@ orbx_status orbx_matcher_destroy(orbx_matcher* m) {
     m->d_out.release();
     m->d_aux.release();
     m->d_proj.release();
+    m->d_bf.release();
     if (m->d_err) (void)hipFree(m->d_err);
     m->timer.destroy();
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -742,6 +749,70 @@ orbx_status orbx_compute_distinctive_descriptors_device(orbx_matcher* m, const u
         return ORBX_ERR_DEVICE;
     m->timer.stop(ORBX_MK_DISTINCTIVE, e, st);
     return ORBX_OK;
+}
+
+namespace {
+orbx_status bf_run(orbx_matcher* m, const uint8_t* d_q, int nq, const uint8_t* d_db,
+                   long long ndb, long long idx_base, int32_t* bi, int32_t* bd, int32_t* sd,
+                   hipStream_t st) {
+    BfLaunch a{};
+    a.q = d_q;
+    a.nq = nq;
+    a.db = d_db;
+    a.ndb = ndb;
+    a.idx_base = idx_base;
+    a.chunk = bf_chunk_rows(ndb, nq, m->ncu);
+    if (!m->d_bf.ensure(bf_partial_bytes(ndb, nq, a.chunk))) return ORBX_ERR_DEVICE;
+    a.part = m->d_bf.p;
+    a.best_idx = bi;
+    a.best_dist = bd;
+    a.second_dist = sd;
+    return HIPOK(launch_bf_top2(a, st, &m->timer)) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+}  // namespace
+
+orbx_status orbx_hamming_bf_top2(orbx_matcher* m, const uint8_t* q, int32_t nq,
+                                 const uint8_t* db, int64_t ndb, int32_t* best_idx,
+                                 int32_t* best_dist, int32_t* second_dist) {
+    if (!m || nq < 0 || ndb < 0 || ndb >= INT32_MAX) return ORBX_ERR_INVALID;
+    if (nq == 0) return ORBX_OK;
+    if (!q || !best_idx || !best_dist || !second_dist || (ndb > 0 && !db)) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    const size_t qb = 32 * (size_t)nq, dbb = 32 * (size_t)ndb, ob = 4 * (size_t)nq;
+    if (!m->d_in.ensure(align256(qb) + std::max<size_t>(dbb, 32)) || !m->d_out.ensure(3 * align256(ob)))
+        return ORBX_ERR_DEVICE;
+    uint8_t* din = m->d_in.as<uint8_t>();
+    uint8_t* dout = m->d_out.as<uint8_t>();
+    if (!HIPOK(hipMemcpyAsync(din, q, qb, hipMemcpyHostToDevice, m->stream)) ||
+        (dbb && !HIPOK(hipMemcpyAsync(din + align256(qb), db, dbb, hipMemcpyHostToDevice, m->stream))))
+        return ORBX_ERR_DEVICE;
+    int32_t* bi = (int32_t*)dout;
+    int32_t* bd = (int32_t*)(dout + align256(ob));
+    int32_t* sd = (int32_t*)(dout + 2 * align256(ob));
+    orbx_status s = bf_run(m, din, nq, din + align256(qb), ndb, 0, bi, bd, sd, m->stream);
+    if (s != ORBX_OK) return s;
+    if (!HIPOK(hipMemcpyAsync(best_idx, bi, ob, hipMemcpyDeviceToHost, m->stream)) ||
+        !HIPOK(hipMemcpyAsync(best_dist, bd, ob, hipMemcpyDeviceToHost, m->stream)) ||
+        !HIPOK(hipMemcpyAsync(second_dist, sd, ob, hipMemcpyDeviceToHost, m->stream)) ||
+        !HIPOK(hipStreamSynchronize(m->stream)))
+        return ORBX_ERR_DEVICE;
+    return ORBX_OK;
+}
+
+orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int32_t nq,
+                                        const uint8_t* d_db, int64_t ndb, int64_t idx_base,
+                                        int32_t* d_best_idx, int32_t* d_best_dist,
+                                        int32_t* d_second_dist, void* stream) {
+    if (!m || nq < 0 || ndb < 0 || idx_base < 0 || ndb + idx_base >= INT32_MAX)
+        return ORBX_ERR_INVALID;
+    if (nq == 0) return ORBX_OK;
+    if (!d_q || !d_best_idx || !d_best_dist || !d_second_dist || (ndb > 0 && !d_db))
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    return bf_run(m, d_q, nq, d_db, ndb, idx_base, d_best_idx, d_best_dist, d_second_dist,
+                  (hipStream_t)stream);
 }
 
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream) {

@@ -85,6 +85,24 @@ struct KernelTimer;
 hipError_t launch_proj(const ProjLaunch& a, hipStream_t st, KernelTimer* timer);
 size_t proj_resolve_lds_bytes(int mode, int n_target, int nq);
 hipError_t prepare_match_kernels();
+// Brute-force Hamming top-2 (orbx_bf.hip): q nq x 32, db ndb x 32 (device); part = scratch of
+// bf_partial_bytes(ndb, nq, chunk) bytes.
+struct BfLaunch {
+    const uint8_t* q;
+    int nq;
+    const uint8_t* db;
+    long long ndb;
+    long long idx_base;
+    int chunk;
+    void* part;
+    int32_t* best_idx;
+    int32_t* best_dist;
+    int32_t* second_dist;
+};
+int bf_chunk_rows(long long ndb, int nq, int ncu);
+size_t bf_partial_bytes(long long ndb, int nq, int chunk);
+struct KernelTimer;
+hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer);
 hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, int32_t* best,
                               int* err, hipStream_t st);
 size_t distinctive_lds_bytes();

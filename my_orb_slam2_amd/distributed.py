@@ -11,7 +11,9 @@ an exchange step:
   Tracking::Relocalization keeps (Tracking.cc:1479-1500); the match lists of those
   candidates are then gathered (only they go on to PnP, :1503-1528);
 * batched SearchForTriangulation (C5): keyframe-pair jobs are sharded; counts and the per-job
-  match arrays are all-gathered.
+  match arrays are all-gathered;
+* brute-force top-2 against a descriptor database (C4, pure BF): the database is sharded by
+  row, every rank's top-2 of every query is all-gathered and folded in rank order.
 """
 from __future__ import annotations
 
@@ -89,6 +91,34 @@ def merge_candidate_blocks(parts):
 
 
 # ---- collectives ------------------------------------------------------------------------------
+
+def merge_top2(parts):
+    """Fold per-shard brute-force top-2 results (best_idx, best_dist, second_dist), given in
+    shard order = database row order, into the whole database's: the best is the earlier
+    shard's on equal distance (the reference loop's strict `<`, src/ORBmatcher.cc:247), the
+    second is the second least distance of the union of the two sorted pairs.  Same
+    arithmetic as k_bf_merge (orbx_bf.hip) over its chunks; tensors or numpy arrays."""
+    bi, b1, b2 = parts[0]
+    lib = np if isinstance(b1, np.ndarray) else __import__("torch")
+    for ei, e1, e2 in parts[1:]:
+        b2 = lib.minimum(lib.maximum(b1, e1), lib.minimum(b2, e2))
+        take = e1 < b1
+        bi = lib.where(take, ei, bi)
+        b1 = lib.where(take, e1, b1)
+    return bi, b1, b2
+
+
+def gather_top2(best_idx, best_dist, second_dist, world: int):
+    """All-gather every rank's top-2 over its database shard (global row numbers, see
+    orbx_hamming_bf_top2_device's idx_base) and fold them in rank order: 12 bytes per query
+    and rank cross the links (pure BF)."""
+    import torch
+    import torch.distributed as dist
+    loc = torch.stack([best_idx, best_dist, second_dist])
+    parts = [torch.empty_like(loc) for _ in range(world)]
+    dist.all_gather(parts, loc)
+    return merge_top2([(p[0], p[1], p[2]) for p in parts])
+
 
 def all_gather_counts(local, n_total: int, world: int):
     """All-gather per-unit counts of every rank's shard into one [n_total] tensor in global

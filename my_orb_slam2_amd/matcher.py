@@ -215,6 +215,32 @@ class ORBmatcher:
                                                               ptr(best)))
         return best[:len(o) - 1]
 
+    def hamming_bf_top2(self, q, db):
+        """Brute-force Hamming top-2 of every query row against every database row, with the
+        best / second loop of the ORBmatcher searches (src/ORBmatcher.cc:232-256): returns
+        (best_idx, best_dist, second_dist), best_idx -1 where no row is below distance 256."""
+        qa = np.ascontiguousarray(q, np.uint8).reshape(-1, 32)
+        da = np.ascontiguousarray(db, np.uint8).reshape(-1, 32)
+        n = len(qa)
+        bi = np.full(max(n, 1), -1, np.int32)
+        bd = np.full(max(n, 1), 256, np.int32)
+        sd = np.full(max(n, 1), 256, np.int32)
+        check("orbx_hamming_bf_top2",
+              self._lib.orbx_hamming_bf_top2(self._h, ptr(qa), n, ptr(da), len(da), ptr(bi),
+                                             ptr(bd), ptr(sd)))
+        return bi[:n], bd[:n], sd[:n]
+
+    def hamming_bf_top2_device(self, d_q, nq, d_db, ndb, d_best_idx, d_best_dist, d_second_dist,
+                               idx_base=0, stream=0):
+        """The same on device arrays (e.g. torch tensors) on `stream`; best_idx is offset by
+        idx_base, so a shard of a larger database reports global rows (distributed.merge_top2
+        folds the shards' results in shard order)."""
+        check("orbx_hamming_bf_top2_device",
+              self._lib.orbx_hamming_bf_top2_device(self._h, ptr(d_q), int(nq), ptr(d_db),
+                                                    int(ndb), int(idx_base), ptr(d_best_idx),
+                                                    ptr(d_best_dist), ptr(d_second_dist),
+                                                    ctypes.c_void_p(stream)))
+
     # ---- batched device path ---------------------------------------------------------------
     def search_by_bow_kf_frame_batch_device(self, db: KfDbC, frame_c, d_match, d_nmatches,
                                             stream=0):

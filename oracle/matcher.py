@@ -165,6 +165,22 @@ def distinctive_descriptors(desc, off):
     return out[:len(o) - 1]
 
 
+def bf_top2(q, db, r0=0, r1=None):
+    """Brute-force Hamming top-2 restated (ORBmatcher's best / second loop over every row of
+    db[r0:r1]); returns (best_idx, best_dist, second_dist) with global row numbers."""
+    qa = np.ascontiguousarray(q, np.uint8).reshape(-1, 32)
+    da = np.ascontiguousarray(db, np.uint8).reshape(-1, 32)
+    r1 = len(da) if r1 is None else r1
+    n = len(qa)
+    bi = np.zeros(max(n, 1), np.int32)
+    bd = np.zeros(max(n, 1), np.int32)
+    sd = np.zeros(max(n, 1), np.int32)
+    L = lib()
+    L.oracle_bf_top2.argtypes = [_vp, _i, _vp, ctypes.c_longlong, ctypes.c_longlong, _vp, _vp, _vp]
+    L.oracle_bf_top2(_a(qa), n, _a(da), r0, r1, _a(bi), _a(bd), _a(sd))
+    return bi[:n], bd[:n], sd[:n]
+
+
 class OracleVocabulary:
     """The DBoW2 restatement (oracle/orb_vocab_oracle.cpp)."""
 

@@ -568,4 +568,28 @@ void oracle_distinctive_descriptors(const uint8_t* desc, const int32_t* off, int
         best[p] = BestIdx;
     }
 }
+
+// Brute-force Hamming top-2 (SURVEY §8(b) orbx_hamming_bf_top2): the best / second loop of
+// SearchByBoW (src/ORBmatcher.cc:232-256) with every database row as a candidate, in order.
+// Rows [r0, r1) only, so a caller can time or check a slice of a large database.
+void oracle_bf_top2(const uint8_t* q, int nq, const uint8_t* db, long long r0, long long r1,
+                    int32_t* best_idx, int32_t* best_dist, int32_t* second_dist) {
+    for (int i = 0; i < nq; ++i) {
+        int bestDist1 = 256, bestDist2 = 256;
+        long long bestIdx = -1;
+        for (long long r = r0; r < r1; ++r) {
+            const int dist = dd(q + 32 * (size_t)i, db + 32 * (size_t)r);
+            if (dist < bestDist1) {
+                bestDist2 = bestDist1;
+                bestDist1 = dist;
+                bestIdx = r;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        best_idx[i] = (int32_t)bestIdx;
+        best_dist[i] = bestDist1;
+        second_dist[i] = bestDist2;
+    }
+}
 }  // extern "C"

@@ -18,6 +18,7 @@ cp $V/tri.json profiles/${R}_c5_triangulation_bench.json
 [ -f $V/dropin.json ] && cp $V/dropin.json profiles/${R}_dropin_bench.json
 [ -f $V/kfdb.json ] && cp $V/kfdb.json profiles/${R}_kfdb_bench.json
 [ -f $V/tum.json ] && cp $V/tum.json profiles/${R}_c1_tum_bench.json
+[ -f $V/bf.json ] && cp $V/bf.json profiles/${R}_c4_bf_bench.json
 [ -f $V/hostio.json ] && cp $V/hostio.json profiles/${R}_hostio_graphs.json
 cp $V/prof_euroc/trace/run_kernel_stats.csv profiles/${R}_euroc_kernel_stats_b256.csv
 cp $V/prof_euroc/pmc3/run_counter_collection.csv profiles/${R}_pmc_fetch_euroc.csv

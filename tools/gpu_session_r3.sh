@@ -26,6 +26,7 @@ timeout -k 10 600 python bench.py --workload reloc --steps 10 --warmup 2 > $OUT/
 timeout -k 10 600 python bench.py --workload triangulation --steps 20 --warmup 3 > $OUT/tri.json 2> $OUT/tri.err || { echo "TRI BENCH FAILED"; tail -20 $OUT/tri.err; exit 1; }
 timeout -k 10 600 python bench.py --workload dropin --frames 300 > $OUT/dropin.json 2> $OUT/dropin.err || { echo "DROPIN BENCH FAILED"; tail -20 $OUT/dropin.err; exit 1; }
 timeout -k 10 600 python bench.py --workload kfdb --steps 200 --warmup 10 > $OUT/kfdb.json 2> $OUT/kfdb.err || { echo "KFDB BENCH FAILED"; tail -20 $OUT/kfdb.err; exit 1; }
+timeout -k 10 600 python bench.py --workload bf --steps 20 --warmup 3 > $OUT/bf.json 2> $OUT/bf.err || { echo "BF BENCH FAILED"; tail -20 $OUT/bf.err; exit 1; }
 timeout -k 10 600 python bench.py --workload tum --frames 300 > $OUT/tum.json 2> $OUT/tum.err || { echo "TUM BENCH FAILED"; tail -20 $OUT/tum.err; exit 1; }
 timeout -k 10 300 python bench.py --host-io --steps 20 --warmup 4 --cpu-seconds 0 > $OUT/hostio.json 2> $OUT/hostio.err || { echo "HOSTIO BENCH FAILED"; tail -20 $OUT/hostio.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_reloc -o run --output-format csv -- python3 bench.py --workload reloc --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_reloc.log 2>&1 || { echo "RELOC TRACE FAILED"; exit 1; }
