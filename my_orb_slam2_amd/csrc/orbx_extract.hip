@@ -1193,6 +1193,22 @@ static_assert(OD_RAW_DW == 9 && OD_BLR_DW == 10, "k_orient_desc row divisions ar
 #define OD_RL ((OD_RAW_N + 31) / 32)               // 9 dword loads per lane per raw patch
 #define OD_BL ((OD_BLR_N + 31) / 32)               // 12 per blurred patch
 static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
+#ifndef OD_X4
+#define OD_X4 1        // patches staged by 16-byte loads, three lanes per 48-byte LDS row: the
+                       // dword form kept the texture addresser 85 % busy (TA_BUSY_avr)
+#endif
+#if OD_X4
+#define OD_RP 48                                   // LDS bytes per patch row (both patches)
+#define OD_RAW_RP OD_RP
+#define OD_BLR_RP OD_RP
+#define OD_RL4 3                                   // 16-byte loads per lane: raw, 31 rows x 3 <= 96
+#define OD_BL4 4                                   // blurred, 37 rows x 3 = 111 <= 128
+#define OD_PATCH_DW (37 * OD_RP / 4)               // 444 dwords per half-wave
+#else
+#define OD_RAW_RP (OD_RAW_DW * 4)
+#define OD_BLR_RP (OD_BLR_DW * 4)
+#define OD_PATCH_DW OD_BLR_N
+#endif
 
 // Sums over each half-wave (lanes 0-31 / 32-63) as two scalars.
 __device__ __forceinline__ void half_sums_dpp(int v, int& lo, int& hi) {
@@ -1213,7 +1229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const uint8_t* __restrict__ blur, const int* __restrict__ ocnt,
     const uint32_t* __restrict__ okp, float* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkp) {
-    __shared__ uint32_t patch[4][2][OD_BLR_N];
+    __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][OD_PATCH_DW];
     int blk, b;
     xcd_block(blk, b);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1237,6 +1253,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     // every keypoint word of the wave in one load: lane k holds keypoint k
     const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
 
+    const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
+    const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
+#if OD_X4
+    // per-lane offsets of the 16-byte chunks relative to the patch bases: chunk t = l32 + 32 j
+    // is row t / 3, bytes 16 (t % 3) .. +16 of it; in LDS it lands at 16 t (rows 48 bytes apart)
+    uint32_t sor4[OD_RL4], sob4[OD_BL4];
+#pragma unroll
+    for (int k = 0; k < OD_RL4; ++k) {
+        const int t = min(l32 + 32 * k, 31 * 3 - 1), row = t / 3;
+        sor4[k] = __umul24(row, pitch) + 16 * (t - 3 * row);
+    }
+#pragma unroll
+    for (int k = 0; k < OD_BL4; ++k) {
+        const int t = min(l32 + 32 * k, 37 * 3 - 1), row = t / 3;
+        sob4[k] = __umul24(row, pitch) + 16 * (t - 3 * row);
+    }
+#else
     // per-lane patch offsets relative to the patch bases
     uint32_t sor[OD_RL], sob[OD_BL];
 #pragma unroll
@@ -1251,8 +1284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         const int row = (int)(__umul24((uint32_t)t, 6554u) >> 16);   // t / 10 for t < 1000
         sob[k] = __umul24(row, pitch) + 4 * (t - row * OD_BLR_DW);
     }
-    const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
-    const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
+#endif
     // keypoint of this half-wave in pair p: k = 2p + half (clamped: a lone last keypoint is
     // computed by both halves, the upper half's results are not used)
     auto kp_word = [&](int p) {
@@ -1263,6 +1295,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     };
     uint32_t* P = patch[wid][half];
     const int npair = (nk + 1) >> 1;
+    // buffer loads: one 32-bit offset add per load instead of a 64-bit address
+    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc((void*)blr_l, 0, 0x7FFFFFFF, 0x00020000);
+#if OD_X4
+    // a chunk reads up to 14 bytes past the patch row: the row's padding or the next row of
+    // the same buffer (patch rows end at least one row before the level's last)
+    const __amdgpu_buffer_rsrc_t rraw = __builtin_amdgcn_make_buffer_rsrc((void*)pyr_l, 0, 0x7FFFFFFF, 0x00020000);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v[OD_BL4];
+    auto issue_raw = [&](int p) {
+        const uint32_t c = kp_word(p);
+        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
+        const uint32_t vo = __umul24((uint32_t)(y - 15), (uint32_t)pitch) + (uint32_t)((x - 15) & ~3);
+#pragma unroll
+        for (int j = 0; j < OD_RL4; ++j)
+            v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rraw, vo + sor4[j], 0, 0));
+    };
+    auto issue_blr = [&](int p) {
+        const uint32_t c = kp_word(p);
+        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
+        const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
+#pragma unroll
+        for (int j = 0; j < OD_BL4; ++j)
+            v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rblr, vo + sob4[j], 0, 0));
+    };
+#else
     uint32_t v[OD_BL];
     auto issue_raw = [&](int p) {
         const uint32_t c = kp_word(p);
@@ -1271,8 +1328,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_RL; ++j) v[j] = *(const uint32_t*)(pr + sor[j]);
     };
-    // buffer loads: one 32-bit offset add per dword instead of a 64-bit address
-    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc((void*)blr_l, 0, 0x7FFFFFFF, 0x00020000);
     auto issue_blr = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
@@ -1280,6 +1335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_BL; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rblr, vo + sob[j], 0, 0);
     };
+#endif
 
     // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
     //      u = l32 - 15 of its half's keypoint, rows v = 1..15; umax decreases with v, so the
@@ -1288,7 +1344,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const int uw = l32 < 31 ? u : 0;
     int vend = 1;
     for (int vv = 1; vv < 16; ++vv) vend += (l32 < 31 && au <= g->umax[vv]) ? 1 : 0;
-    const uint8_t* raw = (const uint8_t*)P;   // [31][36]
+    const uint8_t* raw = (const uint8_t*)P;   // [31][OD_RAW_RP]
     int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
     issue_raw(0);
 #if OD_DIAG == 2   // diagnostic builds only: no moment phase (angle from zero moments)
@@ -1297,21 +1353,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     for (int p = 0; p < npair; ++p) {
 #endif
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
+#if OD_X4
+#pragma unroll
+        for (int j = 0; j < OD_RL4; ++j) {
+            const int t = l32 + 32 * j;
+            if (t < 31 * 3) ((u32x4*)P)[t] = v[j];
+        }
+#else
 #pragma unroll
         for (int j = 0; j < OD_RL; ++j) {
             const int t = l32 + 32 * j;
             if (t < OD_RAW_N) P[t] = v[j];
         }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_raw(p + 1);   // next pair's patches in flight
         else issue_blr(0);                     // phase 3's first patches in flight
-        const uint8_t* center = raw + 15 * (OD_RAW_DW * 4) + (x - ((x - 15) & ~3));
+        const uint8_t* center = raw + 15 * OD_RAW_RP + (x - ((x - 15) & ~3));
         // fixed trip count (all 30 reads in flight at once); rows v >= vend contribute 0.  The
         // reads stay inside the staged patch for every lane (lane 31: u = 16, weight 0).
         int m10 = __mul24(uw, (int)center[u]), m01 = 0;
 #pragma unroll
         for (int vv = 1; vv < 16; ++vv) {
-            const int vp = center[u + vv * (OD_RAW_DW * 4)], vm = center[u - vv * (OD_RAW_DW * 4)];
+            const int vp = center[u + vv * OD_RAW_RP], vm = center[u - vv * OD_RAW_RP];
             const bool on = vv < vend;
             m10 += __mul24(uw, on ? vp + vm : 0);
             m01 += __mul24(vv, on ? vp - vm : 0);
@@ -1357,7 +1421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         px2[w] = (float)c_pattern[4 * q + 2];
         py2[w] = (float)c_pattern[4 * q + 3];
     }
-    const uint8_t* blr = (const uint8_t*)P;   // [37][40]
+    const uint8_t* blr = (const uint8_t*)P;   // [37][OD_BLR_RP]
 #if OD_DIAG == 1   // diagnostic builds only (tools/variants.py): no descriptor phase
     if (npair > 0) return;
 #endif
@@ -1367,14 +1431,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         const float ca0 = readlane_f(ca_l, k0), ca1 = readlane_f(ca_l, k1);
         const float sb0 = readlane_f(sb_l, k0), sb1 = readlane_f(sb_l, k1);
         const float ca = half ? ca1 : ca0, sb = half ? sb1 : sb0;
+#if OD_X4
+#pragma unroll
+        for (int j = 0; j < OD_BL4; ++j) {
+            const int t = l32 + 32 * j;
+            if (t < 37 * 3) ((u32x4*)P)[t] = v[j];
+        }
+#else
 #pragma unroll
         for (int j = 0; j < OD_BL; ++j) {
             const int t = l32 + 32 * j;
             if (t < OD_BLR_N) P[t] = v[j];
         }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_blr(p + 1);
-        const uint8_t* bc = blr + 18 * (OD_BLR_DW * 4) + (x - ((x - 18) & ~3));
+        const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~3));
         // cvRound (:118-120) by the round-to-nearest-even of a float add: for |v| < 2^22,
         // v + 1.5*2^23 holds rint(v) in its low mantissa bits, so its bit pattern is
         // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
@@ -1383,11 +1455,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         // (the constant is folded into a wrapping u32 offset from the patch start, not into
         // the pointer: a pointer that far outside the LDS object is undefined behaviour, which
         // the compiler may turn into a constant descriptor)
-        const uint32_t bko = (uint32_t)(bc - blr) - (0x400000u * (OD_BLR_DW * 4) + 0x4B400000u);
+        const uint32_t bko = (uint32_t)(bc - blr) - (0x400000u * OD_BLR_RP + 0x4B400000u);
         auto sample = [&](float ra, float rb, float cA, float cB) {
             const uint32_t ro = __builtin_bit_cast(uint32_t, (ra + rb) + MAGIC);
             const uint32_t co = __builtin_bit_cast(uint32_t, (cA - cB) + MAGIC);
-            return (int)blr[__umul24(ro, OD_BLR_DW * 4) + co + bko];
+            return (int)blr[__umul24(ro, OD_BLR_RP) + co + bko];
         };
         uint32_t words[8];
 #pragma unroll
