@@ -12,6 +12,7 @@ cp $V/prof/pmc4/run_counter_collection.csv profiles/${R}_pmc_write_b512.csv
 cp $V/prof/pmc1/run_counter_collection.csv profiles/${R}_pmc_insts_b512.csv
 cp $V/prof/pmc2/run_counter_collection.csv profiles/${R}_pmc_waits_b512.csv
 cp $V/prof/pmc5/run_counter_collection.csv profiles/${R}_pmc_busy_b512.csv
+[ -f $V/prof/pmc6/run_counter_collection.csv ] && cp $V/prof/pmc6/run_counter_collection.csv profiles/${R}_pmc_ta_b512.csv
 cp $V/euroc.json profiles/${R}_c3_euroc_bench.json
 cp $V/reloc.json profiles/${R}_c4_reloc_bench.json
 cp $V/tri.json profiles/${R}_c5_triangulation_bench.json

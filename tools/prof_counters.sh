@@ -3,7 +3,8 @@
 # usage: tools/prof_counters.sh OUTDIR [bench args...]
 # One counter group per pass (rocprofv3 does not split passes; see MI355X_MICROARCH.md
 # §rocprofv3 PMC slots): pmc1 instruction counts, pmc2 wait/busy cycles, pmc3 FETCH_SIZE,
-# pmc4 WRITE_SIZE, pmc5 VALU issue cycles (SQ_ACTIVE_INST_VALU) with the launch's cycles.
+# pmc4 WRITE_SIZE, pmc5 VALU issue cycles (SQ_ACTIVE_INST_VALU) with the launch's cycles,
+# pmc6 the texture addresser's busy cycles (TA_BUSY_avr: per-XCD cycles the TA was busy).
 set -e
 OUT=$1; shift
 export TMPDIR=/tmp
@@ -14,4 +15,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_W
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc3 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-kernel-timing "$@" > $OUT/pmc3.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d $OUT/pmc4 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-kernel-timing "$@" > $OUT/pmc4.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/pmc5 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-kernel-timing "$@" > $OUT/pmc5.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE -d $OUT/pmc6 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-kernel-timing "$@" > $OUT/pmc6.log 2>&1
 echo done
