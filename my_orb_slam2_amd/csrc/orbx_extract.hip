@@ -1198,16 +1198,48 @@ static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
                        // dword form kept the texture addresser 85 % busy (TA_BUSY_avr)
 #endif
 #if OD_X4
-#define OD_RP 48                                   // LDS bytes per patch row (both patches)
-#define OD_RAW_RP OD_RP
-#define OD_BLR_RP OD_RP
-#define OD_RL4 3                                   // 16-byte loads per lane: raw, 31 rows x 3 <= 96
-#define OD_BL4 4                                   // blurred, 37 rows x 3 = 111 <= 128
-#define OD_PATCH_DW (37 * OD_RP / 4)               // 444 dwords per half-wave
+#ifndef OD_RAW_W
+#define OD_RAW_W 12    // bytes per lane chunk of a raw-patch row (12 or 16; 3 chunks per row)
+#endif
+#ifndef OD_BLR_W
+#define OD_BLR_W 16    // ... of a blurred-patch row (8: 5 chunks per row, 16: 3)
+#endif
+static_assert((OD_RAW_W == 12 || OD_RAW_W == 16) && (OD_BLR_W == 8 || OD_BLR_W == 16), "chunk widths");
+#define OD_RAW_CH 3                                // chunks per raw row (36 / 48 bytes >= 34)
+#define OD_BLR_CH (OD_BLR_W == 8 ? 5 : 3)          // chunks per blurred row (40 / 48 >= 40)
+#define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per patch row
+#define OD_BLR_RP (OD_BLR_CH * OD_BLR_W)
+#define OD_RL4 ((31 * OD_RAW_CH + 31) / 32)        // loads per lane per raw patch (3)
+#define OD_BL4 ((37 * OD_BLR_CH + 31) / 32)        // ... per blurred patch (4 or 6)
+#define OD_PATCH_B (37 * OD_BLR_RP > 31 * OD_RAW_RP ? 37 * OD_BLR_RP : 31 * OD_RAW_RP)
+#define OD_PATCH_DW ((OD_PATCH_B + 15) / 16 * 4)   // dwords per half-wave, 16-byte multiple
 #else
 #define OD_RAW_RP (OD_RAW_DW * 4)
 #define OD_BLR_RP (OD_BLR_DW * 4)
 #define OD_PATCH_DW OD_BLR_N
+#endif
+
+#if OD_X4
+// Patch staging chunks of W bytes: buffer load and the store of chunk t at byte W t of the
+// half-wave's LDS patch (rows are OD_*_CH chunks apart, so chunk t = row * CH + c).
+template <int W> struct od_chunk;
+template <> struct od_chunk<8> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
+template <> struct od_chunk<12> { typedef uint32_t type __attribute__((ext_vector_type(3))); };
+template <> struct od_chunk<16> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+template <int W>
+__device__ __forceinline__ typename od_chunk<W>::type od_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef typename od_chunk<W>::type T;
+    if constexpr (W == 8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    else if constexpr (W == 12) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0));
+    else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <int W>
+__device__ __forceinline__ void od_store(uint32_t* P, int t, typename od_chunk<W>::type v) {
+    uint32_t* d = P + (W / 4) * t;
+    if constexpr (W == 8) { typedef uint32_t T2 __attribute__((ext_vector_type(2))); *(T2*)d = v; }
+    else if constexpr (W == 12) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
+    else { typedef uint32_t T4 __attribute__((ext_vector_type(4))); *(T4*)d = v; }
+}
 #endif
 
 // Sums over each half-wave (lanes 0-31 / 32-63) as two scalars.
@@ -1261,13 +1293,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     uint32_t sor4[OD_RL4], sob4[OD_BL4];
 #pragma unroll
     for (int k = 0; k < OD_RL4; ++k) {
-        const int t = min(l32 + 32 * k, 31 * 3 - 1), row = t / 3;
-        sor4[k] = __umul24(row, pitch) + 16 * (t - 3 * row);
+        const int t = min(l32 + 32 * k, 31 * OD_RAW_CH - 1), row = t / OD_RAW_CH;
+        sor4[k] = __umul24(row, pitch) + OD_RAW_W * (t - OD_RAW_CH * row);
     }
 #pragma unroll
     for (int k = 0; k < OD_BL4; ++k) {
-        const int t = min(l32 + 32 * k, 37 * 3 - 1), row = t / 3;
-        sob4[k] = __umul24(row, pitch) + 16 * (t - 3 * row);
+        const int t = min(l32 + 32 * k, 37 * OD_BLR_CH - 1), row = t / OD_BLR_CH;
+        sob4[k] = __umul24(row, pitch) + OD_BLR_W * (t - OD_BLR_CH * row);
     }
 #else
     // per-lane patch offsets relative to the patch bases
@@ -1301,23 +1333,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     // a chunk reads up to 14 bytes past the patch row: the row's padding or the next row of
     // the same buffer (patch rows end at least one row before the level's last)
     const __amdgpu_buffer_rsrc_t rraw = __builtin_amdgcn_make_buffer_rsrc((void*)pyr_l, 0, 0x7FFFFFFF, 0x00020000);
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 v[OD_BL4];
+    typedef od_chunk<OD_RAW_W>::type raw_t;
+    typedef od_chunk<OD_BLR_W>::type blr_t;
+    raw_t vr[OD_RL4];
+    blr_t v[OD_BL4];
     auto issue_raw = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint32_t vo = __umul24((uint32_t)(y - 15), (uint32_t)pitch) + (uint32_t)((x - 15) & ~3);
 #pragma unroll
-        for (int j = 0; j < OD_RL4; ++j)
-            v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rraw, vo + sor4[j], 0, 0));
+        for (int j = 0; j < OD_RL4; ++j) vr[j] = od_load<OD_RAW_W>(rraw, vo + sor4[j]);
     };
     auto issue_blr = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
 #pragma unroll
-        for (int j = 0; j < OD_BL4; ++j)
-            v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rblr, vo + sob4[j], 0, 0));
+        for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo + sob4[j]);
     };
 #else
     uint32_t v[OD_BL];
@@ -1357,7 +1389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_RL4; ++j) {
             const int t = l32 + 32 * j;
-            if (t < 31 * 3) ((u32x4*)P)[t] = v[j];
+            if (t < 31 * OD_RAW_CH) od_store<OD_RAW_W>(P, t, vr[j]);
         }
 #else
 #pragma unroll
@@ -1435,7 +1467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) {
             const int t = l32 + 32 * j;
-            if (t < 37 * 3) ((u32x4*)P)[t] = v[j];
+            if (t < 37 * OD_BLR_CH) od_store<OD_BLR_W>(P, t, v[j]);
         }
 #else
 #pragma unroll
