@@ -313,14 +313,31 @@ static int bench(const std::string& dir, int nframes, int warmup) {
 // (ORBmatcher.cc:182-319), timed per frame.  DIR: pair_<i>_left.raw (the reference keyframes'
 // images, extracted and transformed once, untimed) and pair_<i>_right.raw (the frames), and
 // params.txt ("W H nfeatures P levelsup vocabulary_path").  Frame f is matched against
-// keyframe f % P; 85 % of a keyframe's features carry a MapPoint (seeded mask).
+// keyframe f % P; 85 % of a keyframe's features carry a MapPoint (seeded mask).  With DUMPDIR
+// the first P frames' keyframe / frame features, BoW / FeatureVectors and matches are written
+// there for the parity test (tests/test_boundary_cpp.py).
 struct BowFrame {
     View v;
     std::vector<uint32_t> bow_w, fv_node;
     std::vector<double> bow_v;
     std::vector<int32_t> fv_off, fv_feat;
+    int32_t nb = 0;
     orbx_featureset fs;
 };
+
+// one BowFrame's extraction and transform as raw arrays: PREFIX_kps.bin (28-byte keypoints),
+// _desc.bin, _bow_w.bin / _bow_v.bin (nb entries), _fv_node.bin, _fv_off.bin (nodes + 1),
+// _fv_feat.bin
+static bool dump_bow_frame(const std::string& prefix, const BowFrame& f) {
+    const size_t nf = (size_t)f.fs.n_nodes;
+    return write_file(prefix + "_kps.bin", f.v.kps.data(), (size_t)f.v.n * 28) &&
+           write_file(prefix + "_desc.bin", f.v.desc.data(), (size_t)f.v.n * 32) &&
+           write_file(prefix + "_bow_w.bin", f.bow_w.data(), (size_t)f.nb * 4) &&
+           write_file(prefix + "_bow_v.bin", f.bow_v.data(), (size_t)f.nb * 8) &&
+           write_file(prefix + "_fv_node.bin", f.fv_node.data(), nf * 4) &&
+           write_file(prefix + "_fv_off.bin", f.fv_off.data(), (nf + 1) * 4) &&
+           write_file(prefix + "_fv_feat.bin", f.fv_feat.data(), (size_t)f.fv_off[nf] * 4);
+}
 
 static orbx_status make_bow_frame(orbx_extractor* h, orbx_vocabulary* voc, int levelsup,
                                   const uint8_t* img, int W, int H, BowFrame* f) {
@@ -337,6 +354,7 @@ static orbx_status make_bow_frame(orbx_extractor* h, orbx_vocabulary* voc, int l
                                                     nullptr, f->bow_w.data(), f->bow_v.data(), &nb,
                                                     f->fv_node.data(), f->fv_off.data(),
                                                     f->fv_feat.data(), &nf);
+    f->nb = nb;
     std::memset(&f->fs, 0, sizeof(f->fs));
     f->fs.n = n;
     f->fs.keys = f->v.kps.data();
@@ -348,7 +366,7 @@ static orbx_status make_bow_frame(orbx_extractor* h, orbx_vocabulary* voc, int l
     return s;
 }
 
-static int tum(const std::string& dir, int nframes, int warmup) {
+static int tum(const std::string& dir, int nframes, int warmup, const std::string& dump) {
     int W = 0, H = 0, nfeat = 0, P = 0, levelsup = 4;
     char vpath[4096] = {0};
     {
@@ -402,6 +420,16 @@ static int tum(const std::string& dir, int nframes, int warmup) {
             matches += nm;
             kps += fr.v.n;
         }
+        // parity dump (outside the timed interval): the first pass over the P pairs
+        if (!dump.empty() && f < P) {
+            const std::string b = dump + "/frame_" + std::to_string(i);
+            const std::string k = dump + "/kf_" + std::to_string(i);
+            if (!dump_bow_frame(b, fr) || !dump_bow_frame(k, kfs[(size_t)i]) ||
+                !write_file(k + "_valid.bin", valid[(size_t)i].data(), valid[(size_t)i].size()) ||
+                !write_file(b + "_nm.bin", &nm, 4) ||
+                !write_file(b + "_matches.bin", out.data(), (size_t)fr.v.n * 4))
+                return 3;
+        }
     }
     orbx_matcher_destroy(m);
     orbx_extractor_destroy(hk);
@@ -422,8 +450,8 @@ int main(int argc, char** argv) {
     if (argc >= 5 && std::string(argv[1]) == "bench")
         return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
     if (argc >= 5 && std::string(argv[1]) == "tum")
-        return tum(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
-    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP | tum DIR NFRAMES WARMUP\n",
+        return tum(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc >= 6 ? argv[5] : "");
+    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP | tum DIR NFRAMES WARMUP [DUMPDIR]\n",
                  argv[0]);
     return 2;
 }

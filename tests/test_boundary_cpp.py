@@ -125,3 +125,63 @@ def test_cpp_dropin_sequence(boundary_bin, oracle_mod, gpu, tmp_path, seed):
                                            np.array([ex, ey], np.float32), s2, s, False, False)
     assert tri[0] == t_o and t_o > 0
     np.testing.assert_array_equal(tri[1:].reshape(-1, 2), p_o)
+
+
+@pytest.mark.gpu
+def test_cpp_tum_mode_parity(boundary_bin, oracle_mod, gpu, tmp_path):
+    """bench.py --workload tum's own loop (boundary_test `tum`, configs[0]: extraction,
+    ComputeBoW with the synthetic k=10 L=5 vocabulary at levelsup 3, ORBmatcher(0.7, true)
+    .SearchByBoW(KF, F)) at its bench geometry (640x480, 1000 features, the same seeds): the
+    dumped keyframe / frame features, BoW / FeatureVectors and matches equal the restatement's
+    on the same images."""
+    import bench
+    import oracle
+    from oracle import matcher as om
+    from my_orb_slam2_amd import synth
+    from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
+    from my_orb_slam2_amd.features import FeatureSet, FeatureVector
+    P, levelsup = 3, 3
+    W, H, nfeat = bench.TUM_W, bench.TUM_H, bench.TUM_NFEAT
+    pairs = [synth.stereo_pair(3000 + i, W, H) for i in range(P)]
+    voc = tmp_path / "voc.txt"
+    synth.write_vocabulary(str(voc), k=10, L=5, seed=11)
+    for i, (L, R) in enumerate(pairs):
+        L.tofile(tmp_path / f"pair_{i}_left.raw")
+        R.tofile(tmp_path / f"pair_{i}_right.raw")
+    (tmp_path / "params.txt").write_text(f"{W} {H} {nfeat} {P} {levelsup} {voc}\n")
+    dump = tmp_path / "dump"
+    dump.mkdir()
+    r = subprocess.run([str(boundary_bin), "tum", str(tmp_path), "2", str(P), str(dump)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["mean_keypoints"] > 0.9 * nfeat and res["mean_bow_matches"] > 0
+    ov = om.OracleVocabulary(str(voc))
+    ox = oracle.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+
+    def check(prefix, img):
+        rd = lambda s, dt: np.fromfile(dump / f"{prefix}_{s}.bin", dt)
+        k = rd("kps", KEYPOINT_DTYPE)
+        d = rd("desc", np.uint8).reshape(-1, 32)
+        ko, do = ox(img)
+        np.testing.assert_array_equal(k.view(np.uint8), np.ascontiguousarray(ko).view(np.uint8))
+        np.testing.assert_array_equal(d, do)
+        _, _, (bw, bv), (fn, fo, ff) = ov.transform(do, levelsup)
+        np.testing.assert_array_equal(rd("bow_w", np.uint32), bw)
+        np.testing.assert_array_equal(rd("bow_v", np.float64), bv)
+        np.testing.assert_array_equal(rd("fv_node", np.uint32), fn)
+        np.testing.assert_array_equal(rd("fv_off", np.int32), fo)
+        np.testing.assert_array_equal(rd("fv_feat", np.int32), ff)
+        return FeatureSet(ko, do, None, FeatureVector(fn, fo, ff), None)
+
+    total = 0
+    for i, (L, R) in enumerate(pairs):
+        kf = check(f"kf_{i}", L)
+        fr = check(f"frame_{i}", R)
+        valid = np.fromfile(dump / f"kf_{i}_valid.bin", np.uint8).astype(bool)
+        assert len(valid) == len(kf.keys) and 0.75 < valid.mean() < 0.95
+        n_o, m_o = om.search_by_bow_kf_frame(kf, valid, fr, 0.7, True)
+        assert int(np.fromfile(dump / f"frame_{i}_nm.bin", np.int32)[0]) == n_o
+        np.testing.assert_array_equal(np.fromfile(dump / f"frame_{i}_matches.bin", np.int32), m_o)
+        total += n_o
+    assert total > 0

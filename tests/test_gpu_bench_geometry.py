@@ -12,6 +12,10 @@ launch geometry it times, built by bench.py's own input builders.
   frame, every slot against the restatement (ORBmatcher.cc:41-136).
 * C4 (configs[3]): the 10k-keyframe relocalisation database, 512 sampled keyframes (the 10
   planted true ones among them) against SearchByBoW(KF, F) restated (ORBmatcher.cc:182-319).
+* C4 pure brute force (bench.py --workload bf): one 1000-descriptor query frame against the
+  10^7-row database, whole and in 3 / 8 shards (global row numbers, merge in shard order);
+  every planted query finds its row, and 64 queries equal the restated loop over all 10^7
+  rows (ORBmatcher.cc:232-256).
 * C5 (configs[4]): all 512 SearchForTriangulation jobs against the restatement
   (ORBmatcher.cc:702-872).
 """
@@ -170,6 +174,43 @@ def test_c4_relocalisation_10k(oracle_mod, orbx_lib, gpu):
                                              flag[sl].cpu().numpy(), frame, 0.75, True)
         assert cnt_h[k] == n_o, f"keyframe {k}"
         np.testing.assert_array_equal(out[k].cpu().numpy(), m_o, f"keyframe {k}")
+
+
+def test_c4_bf_10m(orbx_lib, gpu):
+    import torch
+    from oracle import matcher as om
+    from my_orb_slam2_amd import ORBmatcher
+    from my_orb_slam2_amd.distributed import merge_top2, shard_range
+    ndb = 10_000_000
+    db = np.empty((ndb, 32), np.uint8)
+    for b0 in range(0, ndb, 1 << 20):
+        b1 = min(b0 + (1 << 20), ndb)
+        db[b0:b1] = bench.bf_rows(b0, b1)
+    q, ids, rows = bench.bf_query(ndb)
+    nq = len(q)
+    ddb, dq = torch.from_numpy(db).to(gpu), torch.from_numpy(q).to(gpu)
+    m = ORBmatcher(0.75, True)
+
+    def run(world):
+        parts = []
+        for r in range(world):
+            r0, r1 = shard_range(ndb, r, world)
+            out = [torch.full((nq,), -7, dtype=torch.int32, device=gpu) for _ in range(3)]
+            m.hamming_bf_top2_device(dq, nq, ddb[r0:], r1 - r0, *out, idx_base=r0)
+            parts.append(tuple(out))
+        torch.cuda.synchronize(gpu)
+        return [t.cpu().numpy() for t in merge_top2(parts)] if world > 1 else \
+            [t.cpu().numpy() for t in parts[0]]
+    bi, bd, sd = run(1)
+    np.testing.assert_array_equal(bi[ids], rows)          # every planted row found
+    assert bd[ids].max() <= 40 and (bd >= 0).all() and (sd >= bd).all()
+    for world in (3, 8):
+        for g, w in zip(run(world), (bi, bd, sd)):
+            np.testing.assert_array_equal(g, w)
+    sample = np.unique(np.concatenate([ids[:16], np.linspace(0, nq - 1, 48).astype(int)]))
+    want = om.bf_top2(q[sample], db)
+    for g, w in zip((bi[sample], bd[sample], sd[sample]), want):
+        np.testing.assert_array_equal(g, w)
 
 
 def test_c5_triangulation_512(oracle_mod, orbx_lib, gpu):
