@@ -54,6 +54,10 @@ struct orbx_extractor {
     hipEvent_t done = nullptr;
     hipStream_t done_stream = nullptr;
     bool have_done = false;
+    // side branch of launch_extract (level-0 FAST beside the level launches): a stream of its
+    // own, forked from and joined back into the call's stream by two events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -722,7 +726,11 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         const size_t B = (size_t)batch;
         // k_fast (FAST_PFU) reads up to 4 * FAST_PF2D rows past a cell's ROI
         const size_t pyr_slack = (size_t)4 * FAST_PF2D * G.lv[0].pitch + 256;
-        bool ok = h->d_pyr.ensure(B * G.pyr_bytes + pyr_slack) && h->d_blur.ensure(B * G.pyr_bytes) &&
+        // k_orient_desc reads whole 16-byte stripes (BLUR_STRIPE), up to one stripe past a
+        // level's last
+        const size_t blur_slack = (size_t)16 * (G.lv[0].h + 64);
+        bool ok = h->d_pyr.ensure(B * G.pyr_bytes + pyr_slack) &&
+                  h->d_blur.ensure(B * G.pyr_bytes + blur_slack) &&
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
                   h->d_cand.ensure(B * G.cand_words * 4) &&
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
@@ -776,6 +784,9 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.desc = h->d_desc.as<uint8_t>();
     a.nkp = h->d_nkp.as<int>();
     a.timer = &h->timer;
+    a.side = h->side;
+    a.ev_fork = h->ev_fork;
+    a.ev_join = h->ev_join;
     strip_heights(h, batch, a.sth);
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
@@ -903,6 +914,20 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return d;
 }
 
+#ifndef FAST_SIDE_PRIO
+#define FAST_SIDE_PRIO 0   // 1: the side stream at the lowest priority (the level chain first)
+#endif
+static hipError_t create_side_stream(hipStream_t* s) {
+#if FAST_SIDE_PRIO
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+#else
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+#endif
+}
+
 orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor** out) {
     if (!p || !out) return ORBX_ERR_INVALID;
     *out = nullptr;
@@ -920,7 +945,13 @@ orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor
     hipDeviceProp_t prop;
     if (!HIPOK(hipSetDevice(h->device)) || !HIPOK(hipGetDeviceProperties(&prop, h->device)) ||
         !HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) ||
-        !HIPOK(hipEventCreateWithFlags(&h->done, hipEventDisableTiming))) {
+        !HIPOK(hipEventCreateWithFlags(&h->done, hipEventDisableTiming)) ||
+        !HIPOK(create_side_stream(&h->side)) ||
+        !HIPOK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) ||
+        !HIPOK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming))) {
+        if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+        if (h->side) (void)hipStreamDestroy(h->side);
+        if (h->done) (void)hipEventDestroy(h->done);
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         return ORBX_ERR_DEVICE;
@@ -942,7 +973,11 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
+    if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->done) (void)hipEventDestroy(h->done);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return ORBX_OK;
@@ -1012,7 +1047,7 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
 }
 
 static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,
-                              uint8_t* out, int* width, int* height) {
+                              uint8_t* out, int* width, int* height, bool blurred = false) {
     if (!h || !h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
         index >= h->last_batch)
         return ORBX_ERR_INVALID;
@@ -1023,6 +1058,20 @@ static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, i
     std::lock_guard<std::mutex> lk(h->mu);
     (void)hipSetDevice(h->device);
     const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
+#if BLUR_STRIPE
+    if (blurred) {   // column stripes (blur_off): the whole level, re-laid row-major here
+        std::vector<uint8_t> tmp((size_t)lv.pitch * lv.h);
+        if (!order_after_last(h, h->stream) ||
+            !HIPOK(hipMemcpyAsync(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost, h->stream)) ||
+            !HIPOK(hipStreamSynchronize(h->stream)))
+            return ORBX_ERR_DEVICE;
+        for (int y = 0; y < lv.h; ++y)
+            for (int x = 0; x < lv.w; ++x) out[(size_t)y * lv.w + x] = tmp[blur_off(x, y, lv.pitch, lv.h)];
+        return ORBX_OK;
+    }
+#else
+    (void)blurred;
+#endif
     if (!order_after_last(h, h->stream) ||
         !HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
         !HIPOK(hipStreamSynchronize(h->stream)))
@@ -1039,7 +1088,7 @@ orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t*
 orbx_status orbx_blur_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,
                             int* height) {
     if (!h) return ORBX_ERR_INVALID;
-    return copy_level(h, h->d_blur, index, level, out, width, height);
+    return copy_level(h, h->d_blur, index, level, out, width, height, true);
 }
 
 orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int batch,

@@ -148,6 +148,12 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_PF
 #define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
+#ifndef FAST_SIDE
+#define FAST_SIDE 0      // level-0 FAST (2: + its octree) on a side stream beside the level launches
+#endif
+#ifndef FAST_SIDE_AT
+#define FAST_SIDE_AT 0   // ... forked before this level's launch
+#endif
 #ifndef FAST_XCD
 #define FAST_XCD 0   // XCD block order for k_fast: measured slower (1.445-1.456 vs 1.434-1.439 ms)
 #endif
@@ -349,7 +355,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                                               const CellDesc* __restrict__ cells,
                                               const uint8_t* __restrict__ pyr,
                                               int* __restrict__ ccnt,
-                                              uint32_t* __restrict__ cand) {
+                                              uint32_t* __restrict__ cand,
+                                              int c_begin, int c_end) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #if FAST_XCD
@@ -361,9 +368,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     const int bx = blockIdx.x, b = blockIdx.y;
 #endif
     // one wave owns FAST_NC consecutive cells; no block-level barriers: waves are independent
-    const int c_first = __builtin_amdgcn_readfirstlane((bx * 4 + wid) * FAST_NC);
-    if (c_first >= g->n_cells) return;
-    const int ncw = min(FAST_NC, g->n_cells - c_first);
+    // cells [c_begin, c_end) of every image (a launch may cover a range of levels)
+    const int c_first = __builtin_amdgcn_readfirstlane(c_begin + (bx * 4 + wid) * FAST_NC);
+    if (c_first >= c_end) return;
+    const int ncw = min(FAST_NC, c_end - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
 #if FAST_W16
@@ -1100,8 +1108,8 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
 #if OCT_MERGED && OCT_LEVEL_MAJOR
     // one launch for all levels, the (long) level-0 lists dispatched first
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-    const int level = lin / gridDim.y, b = lin - level * gridDim.y, tid = threadIdx.x;
-    (void)level_base;
+    const int lrel = lin / gridDim.y, b = lin - lrel * gridDim.y, tid = threadIdx.x;
+    const int level = level_base + lrel;
 #else
     const int level = level_base + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
 #endif
@@ -1208,9 +1216,17 @@ static_assert((OD_RAW_W == 12 || OD_RAW_W == 16) && (OD_BLR_W == 8 || OD_BLR_W =
 #define OD_RAW_CH 3                                // chunks per raw row (36 / 48 bytes >= 34)
 #define OD_BLR_CH (OD_BLR_W == 8 ? 5 : 3)          // chunks per blurred row (40 / 48 >= 40)
 #define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per patch row
-#define OD_BLR_RP (OD_BLR_CH * OD_BLR_W)
 #define OD_RL4 ((31 * OD_RAW_CH + 31) / 32)        // loads per lane per raw patch (3)
-#define OD_BL4 ((37 * OD_BLR_CH + 31) / 32)        // ... per blurred patch (4 or 6)
+#if BLUR_STRIPE
+// blurred patch: 4 column stripes x 37 rows of 16 bytes (148 contiguous-per-stripe chunks),
+// restaged row-major in LDS (rows of 64 bytes: the 4 stripes side by side)
+#define OD_BLR_NCH 148
+#define OD_BLR_RP 64
+#else
+#define OD_BLR_NCH (37 * OD_BLR_CH)
+#define OD_BLR_RP (OD_BLR_CH * OD_BLR_W)
+#endif
+#define OD_BL4 ((OD_BLR_NCH + 31) / 32)            // loads per lane per blurred patch (4, 5 or 6)
 #define OD_PATCH_B (37 * OD_BLR_RP > 31 * OD_RAW_RP ? 37 * OD_BLR_RP : 31 * OD_RAW_RP)
 #define OD_PATCH_DW ((OD_PATCH_B + 15) / 16 * 4)   // dwords per half-wave, 16-byte multiple
 #else
@@ -1295,11 +1311,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     for (int k = 0; k < OD_RL4; ++k) {
         const int t = min(l32 + 32 * k, 31 * OD_RAW_CH - 1), row = t / OD_RAW_CH;
         sor4[k] = __umul24(row, pitch) + OD_RAW_W * (t - OD_RAW_CH * row);
+#if OD_DIAG == 6
+        sor4[k] = OD_RAW_W * t;
+#endif
     }
+#if BLUR_STRIPE
+    // chunk t: stripe t / 37, row t % 37; LDS 16-byte slot row * 4 + stripe
+    static_assert(OD_BLR_W == 16, "stripe chunks are 16 bytes");
+    const uint32_t sh16 = 16u * (uint32_t)L.h;   // bytes per stripe of this level
+    uint32_t sdst[OD_BL4];
+#endif
 #pragma unroll
     for (int k = 0; k < OD_BL4; ++k) {
+#if BLUR_STRIPE
+        const int t = min(l32 + 32 * k, OD_BLR_NCH - 1), st = t / 37, row = t - 37 * st;
+        sob4[k] = (uint32_t)st * sh16 + 16u * (uint32_t)row;
+        sdst[k] = (uint32_t)(row * 4 + st);
+#else
         const int t = min(l32 + 32 * k, 37 * OD_BLR_CH - 1), row = t / OD_BLR_CH;
         sob4[k] = __umul24(row, pitch) + OD_BLR_W * (t - OD_BLR_CH * row);
+#endif
+#if OD_DIAG == 5 || OD_DIAG == 6   // timing diagnostics only (wrong descriptors): contiguous chunks
+        sob4[k] = OD_BLR_W * t;
+#endif
     }
 #else
     // per-lane patch offsets relative to the patch bases
@@ -1347,7 +1381,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     auto issue_blr = [&](int p) {
         const uint32_t c = kp_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
+#if BLUR_STRIPE
+        const uint32_t vo = (uint32_t)((x - 18) >> 4) * sh16 + 16u * (uint32_t)(y - 18);
+#else
         const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
+#endif
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo + sob4[j]);
     };
@@ -1467,7 +1505,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) {
             const int t = l32 + 32 * j;
+#if BLUR_STRIPE
+            if (t < OD_BLR_NCH) od_store<OD_BLR_W>(P, (int)sdst[j], v[j]);
+#else
             if (t < 37 * OD_BLR_CH) od_store<OD_BLR_W>(P, t, v[j]);
+#endif
         }
 #else
 #pragma unroll
@@ -1478,7 +1520,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_blr(p + 1);
+#if BLUR_STRIPE
+        const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~15));
+#else
         const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~3));
+#endif
         // cvRound (:118-120) by the round-to-nearest-even of a float add: for |v| < 2^22,
         // v + 1.5*2^23 holds rint(v) in its low mantissa bits, so its bit pattern is
         // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
@@ -1521,20 +1567,17 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const Geometry& G = *a.hg;
     KernelTimer dummy;
     KernelTimer& T = a.timer ? *a.timer : dummy;
-    hipError_t err = launch_levels(a, st);
-    if (err != hipSuccess) return err;
-    hipEvent_t e = T.start_after(st);
-    hipLaunchKernelGGL(k_fast, dim3((G.n_cells + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch), dim3(256),
-                       fast_lds_bytes(G), st,
-                       a.dg, a.cells, a.pyr, a.ccnt, a.cand);
-    T.stop(K_FAST, e, st);
-    e = T.start_after(st);
+    const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
+    auto fast = [&](int c0, int c1, hipStream_t s) {
+        if (c1 <= c0) return;
+        hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch), dim3(256),
+                           fast_lds_bytes(G), s, a.dg, a.cells, a.pyr, a.ccnt, a.cand, c0, c1);
+    };
     // threads per list: OCT_NT, or OCT_NT_SMALL while the batch's lists fit one round on the
     // CUs (each list is a serial chain of rounds with a few barriers each)
-    const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
-    auto oct = [&](dim3 grid, size_t lds, int ncap, int kcap, int level_base) {
+    auto oct = [&](dim3 grid, size_t lds, int ncap, int kcap, int level_base, hipStream_t s) {
 #define ORBX_OCT_LAUNCH(T)                                                                   \
-        hipLaunchKernelGGL(k_octree<T>, grid, dim3(T), lds, st, a.dg, a.cells, a.ccnt, a.cand, \
+        hipLaunchKernelGGL(k_octree<T>, grid, dim3(T), lds, s, a.dg, a.cells, a.ccnt, a.cand, \
                            a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
         if (nt == 64) ORBX_OCT_LAUNCH(64);
         else if (nt == 128) ORBX_OCT_LAUNCH(128);
@@ -1542,14 +1585,62 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         else ORBX_OCT_LAUNCH(256);
 #undef ORBX_OCT_LAUNCH
     };
+    // Level-0 side branch: FAST on level 0 reads only the input slot, so it need not wait for
+    // the pyramid.  With a side stream it runs beside the level launches from level
+    // FAST_SIDE_AT on (fork / join by events), filling the SIMDs the latency-bound small
+    // levels leave idle; FAST_SIDE 2 also runs the level-0 octree there.
+    const int c_l1 = G.nlevels > 1 ? G.lv[1].cell_begin : G.n_cells;
+    const bool side = FAST_SIDE && a.side && a.ev_fork && a.ev_join && G.nlevels > 1;
+    const int fork_at = a.in_place ? FAST_SIDE_AT : (FAST_SIDE_AT < 1 ? 1 : FAST_SIDE_AT);
+    hipError_t err = hipSuccess;
+    if (side) {
+        err = launch_levels(a, st, 0, fork_at);
+        if (err != hipSuccess) return err;
+        if ((err = hipEventRecord(a.ev_fork, st)) != hipSuccess) return err;
+        if ((err = hipStreamWaitEvent(a.side, a.ev_fork, 0)) != hipSuccess) return err;
+        hipEvent_t e = T.start(a.side);
+        fast(0, c_l1, a.side);
+        T.stop(K_FAST, e, a.side);
+        if (FAST_SIDE >= 2) {
+            e = T.start(a.side);
+            oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
+            T.stop(K_OCTREE, e, a.side);
+        }
+        T.last = nullptr;   // the next interval on `st` starts with its own marker
+        if ((err = hipEventRecord(a.ev_join, a.side)) != hipSuccess) return err;
+        err = launch_levels(a, st, fork_at, G.nlevels);
+        if (err != hipSuccess) return err;
+        hipEvent_t e2 = T.start(st);
+        fast(c_l1, G.n_cells, st);
+        T.stop(K_FAST, e2, st);
+        if (FAST_SIDE >= 2) {
+            e2 = T.start_after(st);
+            oct(dim3(G.nlevels - 1, a.batch), a.octree_lds, a.ncap, a.kcap, 1, st);
+            T.stop(K_OCTREE, e2, st);
+        }
+        if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
+        T.last = nullptr;
+        if (FAST_SIDE < 2) {
+            e2 = T.start(st);
+            oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
+            T.stop(K_OCTREE, e2, st);
+        }
+    } else {
+        err = launch_levels(a, st, 0, G.nlevels);
+        if (err != hipSuccess) return err;
+        hipEvent_t e = T.start_after(st);
+        fast(0, G.n_cells, st);
+        T.stop(K_FAST, e, st);
+        e = T.start_after(st);
 #if OCT_MERGED
-    oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0);
+        oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
 #else
-    oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0);
-    if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1);
+        oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
+        if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1, st);
 #endif
-    T.stop(K_OCTREE, e, st);
-    e = T.start_after(st);
+        T.stop(K_OCTREE, e, st);
+    }
+    hipEvent_t e = T.start_after(st);
     hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,
                        a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp);
     T.stop(K_ORIENT, e, st);

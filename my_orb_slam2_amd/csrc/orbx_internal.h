@@ -11,6 +11,7 @@
 //   desc  [B][kp_cap][32]      u8
 //   nkp   [B]                  i32
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -77,6 +78,22 @@ struct LevelGeom {
 #ifndef OCT_LDS_KB
 #define OCT_LDS_KB 40       // OCT_MERGED: four workgroups per CU
 #endif
+// Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches).  BLUR_STRIPE:
+// each level is stored as 16-byte-wide column stripes of all its rows (byte (x, y) at
+// (x / 16) * 16 h + 16 y + x % 16, the same pitch * h bytes as row-major), so a 37-row
+// patch is 4 contiguous runs of 592 bytes instead of 37 rows on 37+ cache lines.
+#ifndef BLUR_STRIPE
+#define BLUR_STRIPE 0
+#endif
+__host__ __device__ inline uint32_t blur_off(int x, int y, int pitch, int h) {
+#if BLUR_STRIPE
+    (void)pitch;
+    return (uint32_t)(x >> 4) * (uint32_t)(16 * h) + 16u * (uint32_t)y + (uint32_t)(x & 15);
+#else
+    (void)h;
+    return (uint32_t)y * (uint32_t)pitch + (uint32_t)x;
+#endif
+}
 #define LT_W 128              // output tile width  (32 groups of 4)
 #ifndef LT_H
 #define LT_H 32               // output tile height

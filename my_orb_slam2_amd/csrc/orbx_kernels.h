@@ -111,6 +111,9 @@ struct ExtractLaunch {
     int sth[ORBX_MAX_LEVELS];
     // 1: level 0 of every image is already in the pyramid (d_imgs unused)
     int in_place;
+    // the handle's side stream and fork / join events (level-0 branch, launch_extract)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 struct StereoLaunch {
@@ -138,7 +141,7 @@ struct StereoLaunch {
 };
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
-hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st);
+hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, int l_end);
 size_t level_lds_bytes(int ltw, int lth, int win_cap);
 size_t fast_lds_bytes(const Geometry& g);
 size_t octree_lds_bytes(int ncap, int kcap);

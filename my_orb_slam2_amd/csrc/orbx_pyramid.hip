@@ -158,7 +158,7 @@ __device__ __forceinline__ void tile_out_rows(const uint32_t* lvl, uint16_t* row
 // symmetric rows' u16 sums and four v_dot2_u32_u16 accumulate (S < 2^24: exact).
 template <bool FULL>
 __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int vw, int vh,
-                                             uint8_t* dblur, int X0, int Y0, int pitch,
+                                             uint8_t* dblur, int X0, int Y0, int pitch, int bh,
                                              int bsimd_end, const BlurTaps& tp) {
     const int ng = FULL ? LT_GW : (vw + 3) >> 2;
     const int n5 = FULL ? LT_H * LT_GW : vh * LT_GW;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int 
             const uint32_t val = (S + (simd ? 32767u + ((S >> 16) & 1u) : 32768u)) >> 16;
             packed |= min(val, 255u) << (8 * j);
         }
-        uint8_t* d = dblur + __umul24(Y0 + r, pitch) + xg;
+        uint8_t* d = dblur + blur_off(xg, Y0 + r, pitch, bh);
         if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = packed;
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
@@ -267,7 +267,7 @@ __device__ __forceinline__ void tile_out_rows_f(const uint32_t* lvl, float* rows
 // tail takes (S + 32768) >> 16 from the exact integer.
 template <bool FULL>
 __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int vw, int vh,
-                                               uint8_t* dblur, int X0, int Y0, int pitch,
+                                               uint8_t* dblur, int X0, int Y0, int pitch, int bh,
                                                int bsimd_end, const BlurTaps& tp) {
     const int ng = FULL ? LT_GW : (vw + 3) >> 2;
     const int n5 = FULL ? LT_H * LT_GW : vh * LT_GW;
@@ -312,7 +312,7 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
                 packed |= min(val, 255u) << (8 * j);
             }
         }
-        uint8_t* d = dblur + __umul24(Y0 + r, pitch) + xg;
+        uint8_t* d = dblur + blur_off(xg, Y0 + r, pitch, bh);
         if (FULL || 4 * gq + 4 <= vw) *(uint32_t*)d = packed;
         else
             for (int j = 0; 4 * gq + j < vw; ++j) d[j] = (uint8_t)(packed >> (8 * j));
@@ -705,15 +705,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     __syncthreads();
     STAMP(4);
     if (LEVEL_DIAG & 4) {} else
-    if (full) tile_columns_f<true>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
-    else tile_columns_f<false>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+    if (full) tile_columns_f<true>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
+    else tile_columns_f<false>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
 #else
     if (full) tile_out_rows<true>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     else tile_out_rows<false>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     __syncthreads();
     STAMP(4);
-    if (full) tile_columns<true>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
-    else tile_columns<false>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.bsimd_end, tp);
+    if (full) tile_columns<true>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
+    else tile_columns<false>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
 #endif
     STAMP(5);
 }
@@ -996,12 +996,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
     auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, int r, bool ok, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, STRIP_ST_POLICY);
     };
+#if BLUR_STRIPE
+    // the blurred rows go to the column-stripe layout (blur_off): a lane's 4-pixel group sits
+    // in one 16-byte stripe, rows 16 bytes apart
+    const uint32_t blane_off = (out_lane && !(STRIP_DIAG & 1)) ? blur_off(x, 0, pitch, H) : 0x80000000u;
+    auto store_blr = [&](int r, bool ok, uint32_t v) {
+        __builtin_amdgcn_raw_buffer_store_b32(v, rblr, ok ? blane_off : 0x80000000u, ok ? r * 16 : 0, STRIP_ST_POLICY);
+    };
+#else
+    auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(rblr, r, ok, v); };
+#endif
 #else
     const uint32_t pad_off = (uint32_t)(pitch - 4);
     const uint32_t lane_off = out_lane ? (uint32_t)x : pad_off;
     auto store_row = [&](uint8_t* base, int r, bool ok, uint32_t v) {
         *(uint32_t*)(base + (size_t)(ok ? r : 0) * pitch + (ok ? lane_off : pad_off)) = v;
     };
+    static_assert(!BLUR_STRIPE, "BLUR_STRIPE needs the buffer-store strip walk");
+    auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(blr0, r, ok, v); };
 #endif
     // step i (k = i mod U: the load slot k mod NS, the row-sum register k mod 7)
     // ALL: every step of this block stores both rows (no per-step store predicates)
@@ -1072,7 +1084,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
                     packed |= min(val, 255u) << (8 * j);
                 }
             }
-            store_row(STRIP_BLR, Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
+            store_blr(Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
         }
     };
     constexpr int U = NS == 7 ? 7 : 7 * NS;   // steps per block: a multiple of NS and of 7
@@ -1084,7 +1096,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
             // the same memory-op sequence as a block's last steps (two stores after each
             // issue), so the loop header sees one pending-load state from both edges
             if constexpr (MODE != 4) store_row(STRIP_LEV, 0, false, 0u);
-            store_row(STRIP_BLR, 0, false, 0u);
+            store_blr(0, false, 0u);
 #endif
         }
         // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
@@ -1139,13 +1151,14 @@ static LevelKernel level_kernel(int mode) {
     }
 }
 
-hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st) {
+// levels [l_begin, l_end) (launch_extract may fork a side branch in between)
+hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, int l_end) {
     const Geometry& G = *a.hg;
     KernelTimer dummy;
     KernelTimer& T = a.timer ? *a.timer : dummy;
-    for (int l = 0; l < G.nlevels; ++l) {
+    for (int l = l_begin; l < l_end && l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
-        hipEvent_t e = l == 0 ? T.start(st) : T.start_after(st);
+        hipEvent_t e = l == l_begin ? T.start(st) : T.start_after(st);
         const int mode = level_mode(L, l);
         if (L.strip) {
             const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;

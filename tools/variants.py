@@ -30,7 +30,9 @@ def build(specs):
         flags = [d for d in defs.split(",") if d]
         lib = b.PKG / f"liborbx_{name}.so"
         srcs = [str(b.CSRC / s) for s in b.SOURCES]
-        cmd = [b.hipcc()] + b.FLAGS + flags + srcs + ["-o", str(lib)]
+        # the tree's source hash too, so the test fixture accepts a variant (ORBX_LIB=...)
+        cmd = ([b.hipcc()] + b.FLAGS + flags + [f'-DORBX_SRC_HASH="{b.source_hash()}"'] + srcs +
+               ["-o", str(lib)])
         procs.append((name, subprocess.Popen(cmd)))
         out[name] = {"lib": str(lib.relative_to(ROOT)), "flags": flags}
     for name, p in procs:
