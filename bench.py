@@ -77,6 +77,13 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true",
                     help="--host-io: launch the compute sequence eagerly instead of replaying "
                          "a captured HIP graph")
+    ap.add_argument("--overlap", default=None,
+                    help="stereo: MODE[,FORK_LEVEL,LEVELS] side branch of each extraction "
+                         "(orbx_extractor_set_overlap; 0 = every kernel in sequence; default: the "
+                         "library's)")
+    ap.add_argument("--serial-steps", type=int, default=20,
+                    help="stereo: steps of the one-stream comparison pass after the timed region "
+                         "(0: none)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
                          "and stream i %% inflight)")
@@ -260,6 +267,12 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NI - 1)]
     sts = [s_.cuda_stream for s_ in streams]
 
+    if args.overlap is not None:
+        ov = [int(v) for v in args.overlap.split(",")]
+        for h in sbs:
+            h.ext.set_overlap(*ov)
+    overlap = sbs[0].ext.overlap()
+
     resident = args.input == "resident" and not args.host_io
     if resident:
         # each handle's level-0 slots hold the step's images (written once, before timing)
@@ -320,6 +333,38 @@ def main():
     nv = sb.nvalid.cpu().numpy()
     nkp, _, _ = sb.fetch("left")
 
+    # The same step with every kernel in sequence on one stream (outside the timed region): the
+    # overlap's gain measured in this run, and each kernel's launch time on its own (in the
+    # timed, overlapped run the side branch shares the device with the pyramid launches, so
+    # their HIP-event spans include that sharing)
+    serial = None
+    if overlap[0] > 0 and args.serial_steps > 0 and io is None and NI == 1:
+        for h in sbs:
+            h.ext.set_overlap(0)
+            if not args.no_kernel_timing:
+                h.collect_profile()
+        for i in range(3):
+            run_step(i)
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        for i in range(args.serial_steps):
+            run_step(i)
+        torch.cuda.synchronize(dev)
+        t_ser = time.perf_counter() - ts
+        serial = {"steps": args.serial_steps, "ms_per_step": 1000.0 * t_ser / args.serial_steps,
+                  "value": B * args.serial_steps / t_ser}
+        if not args.no_kernel_timing:
+            sprof = {}
+            for h in sbs:
+                for k, (ms, n) in h.collect_profile().items():
+                    t0_, n0_ = sprof.get(k, (0.0, 0))
+                    sprof[k] = (t0_ + ms, n0_ + n)
+            serial["kernel_ms_per_step"] = {k: round(v[0] / args.serial_steps, 4)
+                                            for k, v in sprof.items()}
+            serial["prof"] = sprof
+        for h in sbs:
+            h.ext.set_overlap(*overlap)
+
     total_pairs = B * args.steps * world
     fps = total_pairs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -327,7 +372,9 @@ def main():
     # roofline of the dominant kernel
     roof = None
     if prof:
-        dom = max(prof, key=lambda k: prof[k][0])
+        # the pyramid (the largest kernel of the one-stream step; with the side branch the
+        # other kernels' spans overlap it and each other, so the largest span is no guide)
+        dom = "k_level" if "k_level" in prof else max(prof, key=lambda k: prof[k][0])
         tot_ms, launches = prof[dom]
         avg_s = tot_ms / 1000.0 / max(launches, 1)
         geo = kernel_bytes(sb.ext, 2 * B, B)
@@ -355,6 +402,17 @@ def main():
         # the issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
         for k, e in [(dom, roof)] + list(roof["per_kernel"].items()):
             e["valu"] = valu_entry(args.insts_csv, k, e["avg_launch_ms"] / 1000.0)
+        roof["overlap"] = {"mode": overlap[0], "fork_level": overlap[1], "levels": overlap[2]}
+        if serial and "prof" in serial:
+            st_ms, st_n = serial["prof"][dom]
+            s_avg = st_ms / 1000.0 / max(st_n, 1)
+            s_ach = (alg / s_avg / 1e9) if (alg and s_avg > 0) else None
+            roof["serial_pass"] = {"avg_launch_ms": s_avg * 1000.0, "achieved": s_ach,
+                                   "frac": (s_ach / HBM_PEAK_GBS) if s_ach else None,
+                                   "kernel_ms_per_step": serial["kernel_ms_per_step"]}
+    if serial:
+        serial.pop("prof", None)
+        serial.pop("kernel_ms_per_step", None)
 
     cpu = cpu_tp = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -373,7 +431,8 @@ def main():
                           "parallelism": f"dp{world}"},
                "mean_keypoints_left": float(nkp.mean()),
                "mean_stereo_matches": float(nv.mean()),
-               "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp}
+               "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp,
+               "one_stream": serial}
         if io is not None:
             out["metric"] = METRIC + " (PCIe-inclusive: host images in, host keypoints out)"
             out["config"]["host_io"] = io

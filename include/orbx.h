@@ -165,6 +165,17 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, const uint8_t* d_left,
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1715-1731) on host memory. */
 int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
+/* ---- overlap inside one extraction (no reference counterpart: scheduling only) ----------
+ * The pyramid is a chain of launches (level l is resized from level l-1, ORBextractor.cc:
+ * 1129-1154) whose small levels leave most of the device idle.  The first `levels` levels'
+ * FAST (mode 1), + DistributeOctTree (2), + IC_Angle / rBRIEF (3) then run on the handle's
+ * second stream, forked by an event before level `fork_level`'s launch and joined back before
+ * the other levels' orientation; mode 0 runs every kernel in sequence on the call's stream.
+ * Outputs are identical in every mode.  mode < 0 restores the built-in default. */
+orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_level, int levels);
+orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* fork_level,
+                                       int* levels);
+
 /* ---- per-kernel timing (HIP events around each launch, on the launch stream) ------------ */
 /* ORBX_K_LEVEL: every pyramid launch; ORBX_K_LEVEL0: the level-0 launch alone (a part of
  * ORBX_K_LEVEL, reported separately: it blurs the input, the others also resize). */

@@ -73,6 +73,9 @@ SIGNATURES = {
     "orbx_version": (ctypes.c_char_p, []),
     "orbx_last_error": (ctypes.c_char_p, []),
     "orbx_device_count": (_i, [ctypes.POINTER(_i)]),
+    "orbx_extractor_set_overlap": (_i, [_vp, _i, _i, _i]),
+    "orbx_extractor_get_overlap": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                        ctypes.POINTER(_i)]),
     "orbx_profile_enable": (_i, [_vp, _i]),
     "orbx_profile_collect": (_i, [_vp, _vp, _vp]),
     "orbx_kernel_name": (ctypes.c_char_p, [_i]),

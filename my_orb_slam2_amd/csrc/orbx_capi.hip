@@ -58,6 +58,7 @@ struct orbx_extractor {
     // own, forked from and joined back into the call's stream by two events
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int side_mode = FAST_SIDE, side_at = FAST_SIDE_AT, side_lv = FAST_SIDE_LV;
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -787,6 +788,9 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.side = h->side;
     a.ev_fork = h->ev_fork;
     a.ev_join = h->ev_join;
+    a.side_mode = h->side_mode;
+    a.side_at = h->side_at;
+    a.side_lv = h->side_lv;
     strip_heights(h, batch, a.sth);
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
@@ -868,6 +872,30 @@ const char* orbx_kernel_name(int id) {
     static const char* names[K_COUNT] = {"k_level", "k_fast", "k_octree", "k_orient_desc",
                                          "k_stereo", "k_level0"};
     return (id >= 0 && id < K_COUNT) ? names[id] : "";
+}
+
+orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_level, int levels) {
+    if (!h || mode > 3 || (mode > 0 && (fork_level < 0 || levels < 1))) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (mode < 0) {
+        h->side_mode = FAST_SIDE;
+        h->side_at = FAST_SIDE_AT;
+        h->side_lv = FAST_SIDE_LV;
+    } else {
+        h->side_mode = mode;
+        h->side_at = fork_level;
+        h->side_lv = levels;
+    }
+    return ORBX_OK;
+}
+
+orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* fork_level,
+                                       int* levels) {
+    if (!h) return ORBX_ERR_INVALID;
+    if (mode) *mode = h->side_mode;
+    if (fork_level) *fork_level = h->side_at;
+    if (levels) *levels = h->side_lv;
+    return ORBX_OK;
 }
 
 orbx_status orbx_profile_enable(orbx_extractor* h, int on) {

@@ -148,12 +148,6 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_PF
 #define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
-#ifndef FAST_SIDE
-#define FAST_SIDE 0      // level-0 FAST (2: + its octree) on a side stream beside the level launches
-#endif
-#ifndef FAST_SIDE_AT
-#define FAST_SIDE_AT 0   // ... forked before this level's launch
-#endif
 #ifndef FAST_XCD
 #define FAST_XCD 0   // XCD block order for k_fast: measured slower (1.445-1.456 vs 1.434-1.439 ms)
 #endif
@@ -1276,17 +1270,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const Geometry* __restrict__ g, const uint8_t* __restrict__ pyr,
     const uint8_t* __restrict__ blur, const int* __restrict__ ocnt,
     const uint32_t* __restrict__ okp, float* __restrict__ kps, uint8_t* __restrict__ desc,
-    int* __restrict__ nkp) {
+    int* __restrict__ nkp, int blk_base, int nkp_blk) {
     __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][OD_PATCH_DW];
     int blk, b;
     xcd_block(blk, b);
+    blk += blk_base;   // a launch may cover a range of the blocks (launch_extract's side branch)
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int half = lane >> 5, l32 = lane & 31;
     int level = 0;
     while (level + 1 < g->nlevels && blk >= g->orient_block_begin[level + 1]) ++level;
     const int i0 = ((blk - g->orient_block_begin[level]) * 4 + wid) * OD_NK;
     const int* oc = ocnt + b * g->nlevels;
-    if (level == 0 && i0 == 0 && lane == 0) {
+    if (blk == nkp_blk && wid == 0 && lane == 0) {   // every level's count is final here
         int tot = 0;
         for (int l = 0; l < g->nlevels; ++l) tot += oc[l];
         nkp[b] = tot;
@@ -1585,13 +1580,19 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         else ORBX_OCT_LAUNCH(256);
 #undef ORBX_OCT_LAUNCH
     };
-    // Level-0 side branch: FAST on level 0 reads only the input slot, so it need not wait for
-    // the pyramid.  With a side stream it runs beside the level launches from level
-    // FAST_SIDE_AT on (fork / join by events), filling the SIMDs the latency-bound small
-    // levels leave idle; FAST_SIDE 2 also runs the level-0 octree there.
-    const int c_l1 = G.nlevels > 1 ? G.lv[1].cell_begin : G.n_cells;
-    const bool side = FAST_SIDE && a.side && a.ev_fork && a.ev_join && G.nlevels > 1;
-    const int fork_at = a.in_place ? FAST_SIDE_AT : (FAST_SIDE_AT < 1 ? 1 : FAST_SIDE_AT);
+    // Side branch: the first FAST_SIDE_LV levels' FAST (FAST_SIDE 2: + their octree, 3: + their
+    // orientation / descriptors) run on the handle's side stream, forked (event) before level
+    // FAST_SIDE_AT's launch and joined back before the main stream's orientation launch, so
+    // they fill the SIMDs the latency-bound small levels leave idle.  Level 0's FAST reads only
+    // the input slot; every other part needs its level (and its blur) launched before the fork.
+    const int nside = a.side_lv < G.nlevels - 1 ? a.side_lv : G.nlevels - 1;
+    const int mode = a.side_mode;
+    const bool side = mode > 0 && a.side && a.ev_fork && a.ev_join && nside >= 1;
+    const int c_l1 = side ? G.lv[nside].cell_begin : G.n_cells;
+    const bool side_od = side && mode >= 3 && G.orient_block_begin[nside] < G.orient_blocks;
+    const int min_fork = (nside == 1 && a.in_place && !side_od) ? 0 : nside;
+    const int fork_at = a.side_at < min_fork ? min_fork : a.side_at;
+    const int ob0 = side_od ? G.orient_block_begin[nside] : 0;   // first block of the main launch
     hipError_t err = hipSuccess;
     if (side) {
         err = launch_levels(a, st, 0, fork_at);
@@ -1601,10 +1602,16 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         hipEvent_t e = T.start(a.side);
         fast(0, c_l1, a.side);
         T.stop(K_FAST, e, a.side);
-        if (FAST_SIDE >= 2) {
+        if (mode >= 2) {
             e = T.start(a.side);
-            oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
+            oct(dim3(nside, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
             T.stop(K_OCTREE, e, a.side);
+        }
+        if (side_od) {
+            e = T.start(a.side);
+            hipLaunchKernelGGL(k_orient_desc, dim3(ob0, a.batch), dim3(256), 0, a.side, a.dg, a.pyr,
+                               a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp, 0, -1);
+            T.stop(K_ORIENT, e, a.side);
         }
         T.last = nullptr;   // the next interval on `st` starts with its own marker
         if ((err = hipEventRecord(a.ev_join, a.side)) != hipSuccess) return err;
@@ -1613,14 +1620,14 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         hipEvent_t e2 = T.start(st);
         fast(c_l1, G.n_cells, st);
         T.stop(K_FAST, e2, st);
-        if (FAST_SIDE >= 2) {
+        if (mode >= 2) {
             e2 = T.start_after(st);
-            oct(dim3(G.nlevels - 1, a.batch), a.octree_lds, a.ncap, a.kcap, 1, st);
+            oct(dim3(G.nlevels - nside, a.batch), a.octree_lds, a.ncap, a.kcap, nside, st);
             T.stop(K_OCTREE, e2, st);
         }
         if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
         T.last = nullptr;
-        if (FAST_SIDE < 2) {
+        if (mode < 2) {
             e2 = T.start(st);
             oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
             T.stop(K_OCTREE, e2, st);
@@ -1641,8 +1648,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         T.stop(K_OCTREE, e, st);
     }
     hipEvent_t e = T.start_after(st);
-    hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks, a.batch), dim3(256), 0, st, a.dg,
-                       a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp);
+    hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks - ob0, a.batch), dim3(256), 0, st, a.dg,
+                       a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp, ob0, ob0);
     T.stop(K_ORIENT, e, st);
     return hipGetLastError();
 }

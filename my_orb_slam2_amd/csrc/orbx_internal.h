@@ -78,6 +78,20 @@ struct LevelGeom {
 #ifndef OCT_LDS_KB
 #define OCT_LDS_KB 40       // OCT_MERGED: four workgroups per CU
 #endif
+// Default side branch of an extraction (orbx_extractor_set_overlap): the first FAST_SIDE_LV
+// levels' FAST (FAST_SIDE 1), + octree (2), + orientation / descriptors (3) on the handle's
+// second stream, forked before level FAST_SIDE_AT's launch; 0 = every kernel on one stream.
+// B = 512 (profiles/r03_ab_side_*.txt): one stream 4.66-4.68 ms per step; mode 3 forked at
+// level 3, 4.47 ms
+#ifndef FAST_SIDE
+#define FAST_SIDE 3
+#endif
+#ifndef FAST_SIDE_AT
+#define FAST_SIDE_AT 3
+#endif
+#ifndef FAST_SIDE_LV
+#define FAST_SIDE_LV 1
+#endif
 // Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches).  BLUR_STRIPE:
 // each level is stored as 16-byte-wide column stripes of all its rows (byte (x, y) at
 // (x / 16) * 16 h + 16 y + x % 16, the same pitch * h bytes as row-major), so a 37-row

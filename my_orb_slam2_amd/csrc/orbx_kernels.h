@@ -114,6 +114,9 @@ struct ExtractLaunch {
     // the handle's side stream and fork / join events (level-0 branch, launch_extract)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // side branch: 0 off, 1 FAST, 2 + octree, 3 + orientation / descriptors of levels
+    // [0, side_lv), forked before level side_at's launch
+    int side_mode = 0, side_at = 0, side_lv = 1;
 };
 
 struct StereoLaunch {

@@ -150,6 +150,20 @@ class ORBextractor:
         check("orbx_extract_batch_device", self._L.orbx_extract_batch_device(
             self._h, ptr(images), B, W, H, stride, bstride, ptr(stream)))
 
+    def set_overlap(self, mode: int, fork_level: int = 3, levels: int = 1):
+        """Side branch of the extraction (orbx_extractor_set_overlap): mode 0 = every kernel
+        in sequence, 1-3 = the first `levels` levels' FAST (+ octree, + orientation) beside
+        the pyramid chain, forked before level `fork_level`; mode < 0 = the built-in default."""
+        check("orbx_extractor_set_overlap",
+              self._L.orbx_extractor_set_overlap(self._h, mode, fork_level, levels))
+
+    def overlap(self):
+        """(mode, fork_level, levels) of the side branch."""
+        m, f, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check("orbx_extractor_get_overlap", self._L.orbx_extractor_get_overlap(
+            self._h, ctypes.byref(m), ctypes.byref(f), ctypes.byref(l)))
+        return m.value, f.value, l.value
+
     def profile(self, on: bool = True):
         """Bracket every kernel launch with HIP events (on its launch stream)."""
         check("orbx_profile_enable", self._L.orbx_profile_enable(self._h, 1 if on else 0))

@@ -292,3 +292,47 @@ def test_stereo_batch_shape_and_size_changes(orbx_lib, gpu):
             u1, _, n1 = m.compute_stereo_matches(gl, gr, KITTI_MBF, mb)
             assert_f32_bits_equal(uRh[i, :nkp[i]], u1, f"{w}x{h} B={B} pair {i} uRight")
             assert nvh[i] == n1
+
+
+@pytest.mark.parametrize("nlevels", [8, 3])
+def test_overlap_modes_identical(orbx_lib, gpu, nlevels):
+    """The side branch (orbx_extractor_set_overlap: the first levels' FAST / octree /
+    orientation on a second stream, forked inside the pyramid chain) changes only the
+    schedule: every mode, fork level and level count gives the one-stream outputs bit for bit
+    (keypoints, descriptors, uRight, depth, counts) on 24 stereo pairs, including fork points
+    past the last level and side branches wider than the pyramid."""
+    import torch
+    import my_orb_slam2_amd as m
+    B = 24
+    base = [synth.stereo_pair(600 + i) for i in range(6)]
+    pairs = [tuple(np.roll(base[i % 6][v], 31 * (i // 6), axis=0) for v in (0, 1)) for i in range(B)]
+    Ls = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    sb = m.StereoBatch(B, 2000, 1.2, nlevels, 20, 7)
+
+    def run(cfg):
+        sb.ext.set_overlap(*cfg)
+        outs = [t.cpu().numpy().copy() for t in sb(Ls, Rs, KITTI_MBF, mb)]
+        torch.cuda.synchronize()
+        return outs, sb.fetch("left"), sb.fetch("right")
+
+    ref = run((0, 0, 1))
+    assert ref[0][2].sum() > 0
+    for cfg in [(-1, 0, 0), (1, 0, 1), (2, 1, 1), (3, 1, 1), (3, 3, 1), (3, 3, 2), (3, 4, 3),
+                (3, 9, 1), (3, 2, 12)]:
+        got = run(cfg)
+        (u0, d0, n0), l0, r0 = ref
+        (u1, d1, n1), l1, r1 = got
+        assert np.array_equal(n0, n1), f"{cfg}: valid counts"
+        for side, a, b in (("left", l0, l1), ("right", r0, r1)):
+            assert np.array_equal(a[0], b[0]), f"{cfg}: {side} keypoint counts"
+            for i in range(B):
+                n = a[0][i]
+                assert_kps_equal(b[1][i, :n], a[1][i, :n], f"{cfg} {side} pair {i}")
+                assert_bytes_equal(b[2][i, :n], a[2][i, :n], f"{cfg} {side} pair {i} desc")
+        for i in range(B):
+            n = l0[0][i]
+            assert_f32_bits_equal(u1[i, :n], u0[i, :n], f"{cfg} pair {i} uRight")
+            assert_f32_bits_equal(d1[i, :n], d0[i, :n], f"{cfg} pair {i} depth")
+    sb.ext.set_overlap(-1)
