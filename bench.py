@@ -282,11 +282,14 @@ def main():
             Rv.copy_(Rs)
         torch.cuda.synchronize(dev)
 
-        def run_step(i):
-            sbs[i % NI].run_resident(MBF, mb, stream=sts[i % NI])
+        def run_on(h, st):
+            h.run_resident(MBF, mb, stream=st)
     else:
-        def run_step(i):
-            sbs[i % NI](Ls, Rs, MBF, mb, stream=sts[i % NI])
+        def run_on(h, st):
+            h(Ls, Rs, MBF, mb, stream=st)
+
+    def run_step(i):
+        run_on(sbs[i % NI], sts[i % NI])
 
     io = None
     if args.host_io:
@@ -333,22 +336,22 @@ def main():
     nv = sb.nvalid.cpu().numpy()
     nkp, _, _ = sb.fetch("left")
 
-    # The same step with every kernel in sequence on one stream (outside the timed region): the
-    # overlap's gain measured in this run, and each kernel's launch time on its own (in the
-    # timed, overlapped run the side branch shares the device with the pyramid launches, so
-    # their HIP-event spans include that sharing)
+    # The same step with every kernel in sequence on one stream and one batch in flight
+    # (outside the timed region): the overlap's gain measured in this run, and each kernel's
+    # launch time on its own (in the timed run the side branch and the other batch in flight
+    # share the device with every launch, so the HIP-event spans include that sharing)
     serial = None
-    if overlap[0] > 0 and args.serial_steps > 0 and io is None and NI == 1:
+    if (overlap[0] > 0 or NI > 1) and args.serial_steps > 0 and io is None:
         for h in sbs:
             h.ext.set_overlap(0)
             if not args.no_kernel_timing:
                 h.collect_profile()
         for i in range(3):
-            run_step(i)
+            run_on(sbs[0], sts[0])
         torch.cuda.synchronize(dev)
         ts = time.perf_counter()
         for i in range(args.serial_steps):
-            run_step(i)
+            run_on(sbs[0], sts[0])
         torch.cuda.synchronize(dev)
         t_ser = time.perf_counter() - ts
         serial = {"steps": args.serial_steps, "ms_per_step": 1000.0 * t_ser / args.serial_steps,
@@ -458,6 +461,11 @@ def host_io_pipeline(torch, orbx, dev, local, B, Lh, Rh, mb, graphs=True):
     hip.hipMemcpyAsync.argtypes = [vp, vp, sz, ctypes.c_int, vp]
     hip.hipMemcpy2DAsync.argtypes = [vp, sz, vp, sz, sz, sz, ctypes.c_int, vp]
     hs = [orbx.StereoBatch(B, NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(2)]
+    # one stream per handle: the link is the bound here, and the side branches' two extra
+    # streams would share the device's 4 hardware queues with the copy streams (88 % of the
+    # PCIe bound with them, 98-103 % without)
+    for h in hs:
+        h.ext.set_overlap(0)
     base, pitch, istride = [], None, None
     for h in hs:
         h.input_views(W, H)          # prepares the workspace and the output tensors
