@@ -84,9 +84,9 @@ def parse():
     ap.add_argument("--serial-steps", type=int, default=20,
                     help="stereo: steps of the one-stream comparison pass after the timed region "
                          "(0: none)")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="stereo: batches in flight on separate HIP streams (step i uses handle "
-                         "and stream i %% inflight)")
+                         "and stream i %% inflight; 1: one batch at a time)")
     ap.add_argument("--workload", default="stereo",
                     choices=["stereo", "euroc", "reloc", "triangulation", "dropin", "kfdb", "tum",
                              "bf"],
@@ -390,17 +390,24 @@ def main():
                 "algorithmic_bytes_per_launch": alg,
                 "requested_bytes_per_launch": geo.get(dom), "avg_launch_ms": avg_s * 1000.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4)
-                                       for k, v in prof.items()},
-                # every extraction / stereo kernel against the HBM roof (north_star: FAST and
-                # the matcher included), same definitions as the headline object
-                "per_kernel": per_kernel_hbm(prof, geo, args.traffic_csv, args.steps)}
+                                       for k, v in prof.items()}}
+        # every extraction / stereo kernel against the HBM roof (north_star: FAST and the
+        # matcher included), same definitions as the headline object.  With a side branch or
+        # several batches in flight the timed run's spans overlap each other, so these come
+        # from the one-stream pass (one launch per kernel per step, as in the PMC passes,
+        # tools/prof_counters.sh) when the run has one
+        kprof, ksteps = prof, args.steps
+        if serial and "prof" in serial:
+            kprof, ksteps = serial["prof"], serial["steps"]
+            roof["per_kernel_source"] = "one-stream pass (one_stream)"
+        roof["per_kernel"] = per_kernel_hbm(kprof, geo, args.traffic_csv, ksteps)
         # the pyramid's two kinds of launch apart: level 0 (blur of the input) and levels
         # 1-7 (resize + blur)
-        if "k_level0" in prof and prof["k_level0"][1] and "k_level" in prof:
-            t_all, n_all = prof["k_level"]
-            t0l, n0l = prof["k_level0"]
+        if "k_level0" in kprof and kprof["k_level0"][1] and "k_level" in kprof:
+            t_all, n_all = kprof["k_level"]
+            t0l, n0l = kprof["k_level0"]
             prof_l17 = {"k_level1_7": (t_all - t0l, n_all - n0l)}
-            roof["per_kernel"].update(per_kernel_hbm(prof_l17, geo, args.traffic_csv, args.steps))
+            roof["per_kernel"].update(per_kernel_hbm(prof_l17, geo, args.traffic_csv, ksteps))
         # the integer kernels are bound by VALU issue, not HBM: the same launches against
         # the issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
         for k, e in [(dom, roof)] + list(roof["per_kernel"].items()):
@@ -1059,6 +1066,8 @@ def main_euroc(args):
     frames, idx = euroc_frames(rank, B, P)
     d_imgs = torch.from_numpy(np.stack([frames[i] for i in idx])).to(dev)
     mt = MonoTrackBatch(B, EUROC_W, EUROC_H, K4, distc, EUROC_NFEAT, device=local)
+    if args.overlap is not None:
+        mt.ext.set_overlap(*[int(v) for v in args.overlap.split(",")])
 
     # inputs: the local map projected into each frame (built from the frame's own features)
     mt.frames(d_imgs, st)
@@ -1111,7 +1120,8 @@ def main_euroc(args):
     counts = cnt.cpu().numpy()
     roof = None
     if prof:
-        dom = max(prof, key=lambda k: prof[k][0])
+        # the pyramid (with the side branch the other kernels' spans overlap it)
+        dom = "k_level" if "k_level" in prof else max(prof, key=lambda k: prof[k][0])
         tot_ms, launches = prof[dom]
         avg_s = tot_ms / 1000.0 / max(launches, 1)
         geo = kernel_bytes(mt.ext, B, 0)

@@ -6,6 +6,7 @@ V=gpurun_out/$1
 T=${2:-$1}
 R=${ROUND:-r03}
 cp $V/bench.json profiles/${R}_${T}_bench.json
+[ -f $V/bench_inflight1.json ] && cp $V/bench_inflight1.json profiles/${R}_${T}_bench_inflight1.json
 cp $V/prof/trace/run_kernel_stats.csv profiles/${R}_${T}_kernel_stats_b512.csv
 cp $V/prof/pmc3/run_counter_collection.csv profiles/${R}_pmc_fetch_b512.csv
 cp $V/prof/pmc4/run_counter_collection.csv profiles/${R}_pmc_write_b512.csv

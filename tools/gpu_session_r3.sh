@@ -16,6 +16,7 @@ I=$(ls $OUT/prof/pmc1/*counter_collection.csv | head -1)
 V=$(ls $OUT/prof/pmc5/*counter_collection.csv | head -1)
 timeout -k 10 600 python bench.py --traffic-csv "$F,$W" --insts-csv "$I,$V" > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
+timeout -k 10 600 python bench.py --inflight 1 --cpu-seconds 0 --traffic-csv "$F,$W" --insts-csv "$I,$V" > $OUT/bench_inflight1.json 2> $OUT/bench_inflight1.err || { echo "BENCH INFLIGHT1 FAILED"; tail -20 $OUT/bench_inflight1.err; exit 1; }
 bash tools/prof_counters.sh $OUT/prof_euroc --workload euroc || { echo "EUROC PROFILING FAILED"; exit 1; }
 FE=$(ls $OUT/prof_euroc/pmc3/*counter_collection.csv | head -1)
 WE=$(ls $OUT/prof_euroc/pmc4/*counter_collection.csv | head -1)
