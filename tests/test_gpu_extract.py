@@ -336,3 +336,52 @@ def test_overlap_modes_identical(orbx_lib, gpu, nlevels):
             assert_f32_bits_equal(u1[i, :n], u0[i, :n], f"{cfg} pair {i} uRight")
             assert_f32_bits_equal(d1[i, :n], d0[i, :n], f"{cfg} pair {i} depth")
     sb.ext.set_overlap(-1)
+
+
+def test_overlap_branch_in_a_hip_graph(orbx_lib, gpu):
+    """A stereo call with the side branch (mode 3: the fork / join events between the caller's
+    stream and the handle's second stream) captured into a HIP graph and replayed gives the
+    eager one-stream outputs bit for bit (the pipelined host-io path replays such graphs)."""
+    import torch
+    import my_orb_slam2_amd as m
+    B, W, H = 8, 1241, 376
+    pairs = [synth.stereo_pair(700 + i) for i in range(B)]
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    sb = m.StereoBatch(B, 2000)
+    Lv, Rv = sb.input_views(W, H)
+    Lv.copy_(torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu))
+    Rv.copy_(torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu))
+    s = torch.cuda.Stream(gpu)
+    sb.ext.set_overlap(0)
+    with torch.cuda.stream(s):
+        ref = [t.cpu().numpy().copy() for t in sb.run_resident(KITTI_MBF, mb, stream=s.cuda_stream)]
+    s.synchronize()
+    ref_l, ref_r = sb.fetch("left"), sb.fetch("right")
+    sb.ext.set_overlap(3, 3, 1)
+    with torch.cuda.stream(s):   # eager run first (workspace and batch view ready)
+        sb.run_resident(KITTI_MBF, mb, stream=s.cuda_stream)
+    s.synchronize()
+    for t in (sb.uR, sb.depth, sb.nvalid):
+        t.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sb.run_resident(KITTI_MBF, mb, stream=s.cuda_stream)
+    for _ in range(2):
+        with torch.cuda.stream(s):
+            g.replay()
+    s.synchronize()
+    got = [t.cpu().numpy() for t in (sb.uR, sb.depth, sb.nvalid)]
+    got_l, got_r = sb.fetch("left"), sb.fetch("right")
+    assert np.array_equal(got[2], ref[2]) and ref[2].sum() > 0
+    for a, b_, side in ((ref_l, got_l, "left"), (ref_r, got_r, "right")):
+        assert np.array_equal(a[0], b_[0]), side
+        for i in range(B):
+            n = a[0][i]
+            assert_kps_equal(b_[1][i, :n], a[1][i, :n], f"graph {side} {i}")
+            assert_bytes_equal(b_[2][i, :n], a[2][i, :n], f"graph {side} {i} desc")
+    for i in range(B):
+        n = ref_l[0][i]
+        assert_f32_bits_equal(got[0][i, :n], ref[0][i, :n], f"graph uRight {i}")
+        assert_f32_bits_equal(got[1][i, :n], ref[1][i, :n], f"graph depth {i}")
+    sb.ext.set_overlap(-1)
