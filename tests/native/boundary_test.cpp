@@ -225,6 +225,25 @@ static int run(const std::string& dir) {
     CHECK(orbx_search_for_triangulation(mtri, &F, has1.data(), &KF, has2.data(), F12, ex, ey,
                                         sigma2, scale, 8, 0, tri.data() + 1, vl.n, tri.data()));
 
+    // the schedule inside an extraction (orbx_extractor_set_overlap) does not change results:
+    // the left view again with every kernel on the caller's stream
+    {
+        orbx_extractor* h1 = nullptr;
+        CHECK(orbx_extractor_create(&p, &h1));
+        CHECK(orbx_extractor_set_overlap(h1, 0, 0, 1));
+        int mode = -1, fork_level = -1, levels = -1;
+        CHECK(orbx_extractor_get_overlap(h1, &mode, &fork_level, &levels));
+        View v1;
+        extract(h1, L.data(), W, H, &v1);
+        CHECK(v1.st);
+        orbx_extractor_destroy(h1);
+        if (mode != 0 || v1.n != vl.n || v1.desc != vl.desc ||
+            std::memcmp(v1.kps.data(), vl.kps.data(), (size_t)vl.n * sizeof(orbx_keypoint)) != 0) {
+            std::printf("boundary_test: the one-stream extraction differs\n");
+            return 4;
+        }
+    }
+
     const int nl = vl.n, nr = vr.n;
     bool ok = write_file(dir + "/n.bin", &nl, 4) && write_file(dir + "/nr.bin", &nr, 4) &&
               write_file(dir + "/nvalid.bin", &nvalid, 4) &&
