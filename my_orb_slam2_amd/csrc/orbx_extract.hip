@@ -1565,20 +1565,27 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
     auto fast = [&](int c0, int c1, hipStream_t s) {
         if (c1 <= c0) return;
-        hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch), dim3(256),
-                           fast_lds_bytes(G), s, a.dg, a.cells, a.pyr, a.ccnt, a.cand, c0, c1);
+        ORBX_TIMED_LAUNCH(T, K_FAST, k_fast, dim3((c1 - c0 + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch),
+                          dim3(256), fast_lds_bytes(G), s, a.dg, a.cells, (const uint8_t*)a.pyr,
+                          a.ccnt, a.cand, c0, c1);
     };
     // threads per list: OCT_NT, or OCT_NT_SMALL while the batch's lists fit one round on the
     // CUs (each list is a serial chain of rounds with a few barriers each)
     auto oct = [&](dim3 grid, size_t lds, int ncap, int kcap, int level_base, hipStream_t s) {
-#define ORBX_OCT_LAUNCH(T)                                                                   \
-        hipLaunchKernelGGL(k_octree<T>, grid, dim3(T), lds, s, a.dg, a.cells, a.ccnt, a.cand, \
-                           a.ocnt, a.okp, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
+#define ORBX_OCT_LAUNCH(N)                                                                   \
+        ORBX_TIMED_LAUNCH(T, K_OCTREE, k_octree<N>, grid, dim3(N), lds, s, a.dg, a.cells,     \
+                          (const int*)a.ccnt, (const uint32_t*)a.cand, a.ocnt, a.okp,         \
+                          a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
         if (nt == 64) ORBX_OCT_LAUNCH(64);
         else if (nt == 128) ORBX_OCT_LAUNCH(128);
         else if (nt == 512) ORBX_OCT_LAUNCH(512);
         else ORBX_OCT_LAUNCH(256);
 #undef ORBX_OCT_LAUNCH
+    };
+    auto orient = [&](int blk0, int nblk, int nkp_blk, hipStream_t s) {
+        ORBX_TIMED_LAUNCH(T, K_ORIENT, k_orient_desc, dim3(nblk, a.batch), dim3(256), 0, s, a.dg,
+                          (const uint8_t*)a.pyr, (const uint8_t*)a.blur, (const int*)a.ocnt,
+                          (const uint32_t*)a.okp, a.kps, a.desc, a.nkp, blk0, nkp_blk);
     };
     // Side branch: the first FAST_SIDE_LV levels' FAST (FAST_SIDE 2: + their octree, 3: + their
     // orientation / descriptors) run on the handle's side stream, forked (event) before level
@@ -1599,58 +1606,28 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         if (err != hipSuccess) return err;
         if ((err = hipEventRecord(a.ev_fork, st)) != hipSuccess) return err;
         if ((err = hipStreamWaitEvent(a.side, a.ev_fork, 0)) != hipSuccess) return err;
-        hipEvent_t e = T.start(a.side);
         fast(0, c_l1, a.side);
-        T.stop(K_FAST, e, a.side);
-        if (mode >= 2) {
-            e = T.start(a.side);
-            oct(dim3(nside, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
-            T.stop(K_OCTREE, e, a.side);
-        }
-        if (side_od) {
-            e = T.start(a.side);
-            hipLaunchKernelGGL(k_orient_desc, dim3(ob0, a.batch), dim3(256), 0, a.side, a.dg, a.pyr,
-                               a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp, 0, -1);
-            T.stop(K_ORIENT, e, a.side);
-        }
-        T.last = nullptr;   // the next interval on `st` starts with its own marker
+        if (mode >= 2) oct(dim3(nside, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
+        if (side_od) orient(0, ob0, -1, a.side);
         if ((err = hipEventRecord(a.ev_join, a.side)) != hipSuccess) return err;
         err = launch_levels(a, st, fork_at, G.nlevels);
         if (err != hipSuccess) return err;
-        hipEvent_t e2 = T.start(st);
         fast(c_l1, G.n_cells, st);
-        T.stop(K_FAST, e2, st);
-        if (mode >= 2) {
-            e2 = T.start_after(st);
-            oct(dim3(G.nlevels - nside, a.batch), a.octree_lds, a.ncap, a.kcap, nside, st);
-            T.stop(K_OCTREE, e2, st);
-        }
+        if (mode >= 2) oct(dim3(G.nlevels - nside, a.batch), a.octree_lds, a.ncap, a.kcap, nside, st);
         if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
-        T.last = nullptr;
-        if (mode < 2) {
-            e2 = T.start(st);
-            oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
-            T.stop(K_OCTREE, e2, st);
-        }
+        if (mode < 2) oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
     } else {
         err = launch_levels(a, st, 0, G.nlevels);
         if (err != hipSuccess) return err;
-        hipEvent_t e = T.start_after(st);
         fast(0, G.n_cells, st);
-        T.stop(K_FAST, e, st);
-        e = T.start_after(st);
 #if OCT_MERGED
         oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
 #else
         oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
         if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1, st);
 #endif
-        T.stop(K_OCTREE, e, st);
     }
-    hipEvent_t e = T.start_after(st);
-    hipLaunchKernelGGL(k_orient_desc, dim3(G.orient_blocks - ob0, a.batch), dim3(256), 0, st, a.dg,
-                       a.pyr, a.blur, a.ocnt, a.okp, a.kps, a.desc, a.nkp, ob0, ob0);
-    T.stop(K_ORIENT, e, st);
+    orient(ob0, G.orient_blocks - ob0, ob0, st);
     return hipGetLastError();
 }
 

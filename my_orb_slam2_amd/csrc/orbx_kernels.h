@@ -1,6 +1,7 @@
 // orbx_kernels.h — host-side launch descriptors of the gfx950 kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -77,6 +78,24 @@ struct KernelTimer {
         used = 0;
     }
 };
+
+// A kernel launch timed by its own dispatch (hipExtLaunchKernel sets the two events from the
+// kernel's start and end, as rocprofv3's kernel trace sees them): with a side branch or another
+// batch in flight a kernel may wait for the device after its stream reaches it, and a stream-
+// ordered event pair would charge it that wait.  The interval is recorded under ID; untimed
+// launches (timing off) are plain launches.
+#define ORBX_TIMED_LAUNCH(T, ID, KERNEL, GRID, BLOCK, SHM, ST, ...)                            \
+    do {                                                                                      \
+        hipEvent_t a_ = (T).on ? (T).get() : nullptr;                                         \
+        hipEvent_t z_ = (T).on ? (T).get() : nullptr;                                         \
+        if (a_ && z_) {                                                                       \
+            hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, (uint32_t)(SHM), ST, a_, z_, 0u,       \
+                                  __VA_ARGS__);                                               \
+            (T).pending.push_back(KernelTimer::Rec{ID, a_, z_});                              \
+        } else {                                                                              \
+            hipLaunchKernelGGL(KERNEL, GRID, BLOCK, SHM, ST, __VA_ARGS__);                    \
+        }                                                                                     \
+    } while (0)
 
 struct ExtractLaunch {
     const Geometry* hg;        // host copy of the geometry

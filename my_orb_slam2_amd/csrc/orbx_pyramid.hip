@@ -1158,28 +1158,28 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, in
     KernelTimer& T = a.timer ? *a.timer : dummy;
     for (int l = l_begin; l < l_end && l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
-        hipEvent_t e = l == l_begin ? T.start(st) : T.start_after(st);
         const int mode = level_mode(L, l);
         if (L.strip) {
             const int sth = a.sth[l], sns = (L.h + sth - 1) / sth;
             const int sync = L.snw <= 8 && ((STRIP_SYNC_LEVELS >> l) & 1) ? (mode == 3 ? STRIP_SYNC3 : STRIP_SYNC0) : 0;
-            hipLaunchKernelGGL(mode == 3 ? k_level_strip<3> : (a.in_place ? k_level_strip<4> : k_level_strip<0>),
-                               sync > 0 ? dim3(sns, a.batch) : dim3((L.snw * sns + 3) / 4, a.batch),
-                               dim3(sync > 0 ? 64 * L.snw : 256), 0, st, a.dg,
-                               a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
-                               a.pyr, a.blur, l, sth, sync);
+            ORBX_TIMED_LAUNCH(T, K_LEVEL,
+                              mode == 3 ? k_level_strip<3> : (a.in_place ? k_level_strip<4> : k_level_strip<0>),
+                              sync > 0 ? dim3(sns, a.batch) : dim3((L.snw * sns + 3) / 4, a.batch),
+                              dim3(sync > 0 ? 64 * L.snw : 256), 0, st, a.dg,
+                              a.ltab, a.d_imgs, a.d_imgs2, a.split, a.stride, a.batch_stride,
+                              a.pyr, a.blur, l, sth, sync);
         } else if (l == 0 && a.in_place) {
             // the tiled level-0 kernel reading the pyramid's own level 0 (its level stores
             // write back the bytes already there)
-            hipLaunchKernelGGL(level_kernel(0), dim3(L.ntx * L.nty, a.batch), dim3(256),
-                               a.level_lds, st, a.dg, a.ltab, a.pyr + L.off, a.pyr + L.off, a.batch,
-                               (size_t)L.pitch, (size_t)G.pyr_bytes, a.pyr, a.blur, l);
+            ORBX_TIMED_LAUNCH(T, K_LEVEL, level_kernel(0), dim3(L.ntx * L.nty, a.batch), dim3(256),
+                              a.level_lds, st, a.dg, a.ltab, (const uint8_t*)(a.pyr + L.off),
+                              (const uint8_t*)(a.pyr + L.off), a.batch, (size_t)L.pitch,
+                              (size_t)G.pyr_bytes, a.pyr, a.blur, l);
         } else {
-            hipLaunchKernelGGL(level_kernel(mode), dim3(L.ntx * L.nty, a.batch), dim3(256),
-                               a.level_lds, st, a.dg, a.ltab, a.d_imgs, a.d_imgs2, a.split,
-                               a.stride, a.batch_stride, a.pyr, a.blur, l);
+            ORBX_TIMED_LAUNCH(T, K_LEVEL, level_kernel(mode), dim3(L.ntx * L.nty, a.batch), dim3(256),
+                              a.level_lds, st, a.dg, a.ltab, a.d_imgs, a.d_imgs2, a.split,
+                              a.stride, a.batch_stride, a.pyr, a.blur, l);
         }
-        T.stop(K_LEVEL, e, st);
         if (l == 0) T.alias(K_LEVEL0);
     }
     return hipGetLastError();

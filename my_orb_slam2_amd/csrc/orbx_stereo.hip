@@ -437,15 +437,21 @@ int stereo_split(int batch) {
 }
 
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {
-    hipEvent_t e = a.timer ? a.timer->start(st) : nullptr;
+    // timed by the kernels' own dispatches (ORBX_TIMED_LAUNCH): from k_stereo's start to the
+    // end of the last kernel (k_stereo_cut on the split path)
+    KernelTimer* T = a.timer && a.timer->on ? a.timer : nullptr;
+    hipEvent_t e0 = T ? T->get() : nullptr, e1 = T ? T->get() : nullptr;
+    if (!e0 || !e1) e0 = e1 = nullptr;
     const int ns = stereo_split(a.batch);
-    hipLaunchKernelGGL(k_stereo, dim3(a.batch * ns), dim3(ST_THREADS), a.lds, st, a.dg, a.kpsL,
-                       a.descL, a.nkpL, a.pyrL, a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb,
-                       a.uR, a.depth, a.nvalid, ns, a.scnt, a.ssad, a.sidx);
+    hipExtLaunchKernelGGL(k_stereo, dim3(a.batch * ns), dim3(ST_THREADS), (uint32_t)a.lds, st, e0,
+                          ns > 1 ? nullptr : e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
+                          a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb, a.uR, a.depth, a.nvalid,
+                          ns, a.scnt, a.ssad, a.sidx);
     if (ns > 1)
-        hipLaunchKernelGGL(k_stereo_cut, dim3(a.batch), dim3(ST_THREADS), 0, st, a.dg, a.uR,
-                           a.depth, a.nvalid, a.scnt, a.ssad, a.sidx);
-    if (a.timer) a.timer->stop(K_STEREO, e, st);
+        hipExtLaunchKernelGGL(k_stereo_cut, dim3(a.batch), dim3(ST_THREADS), 0u, st, nullptr, e1, 0u,
+                              a.dg, a.uR, a.depth, a.nvalid, a.scnt, (const int*)a.ssad,
+                              (const int16_t*)a.sidx);
+    if (e0 && e1) T->pending.push_back(KernelTimer::Rec{K_STEREO, e0, e1});
     return hipGetLastError();
 }
 
