@@ -92,9 +92,11 @@ orbx_status orbx_blur_level(orbx_extractor* h, int index, int level, uint8_t* ou
 /* ---- batched, device-resident API (throughput path) -------------------------------------
  * d_imgs: `batch` images in device memory, image i at d_imgs + i*batch_stride, rows
  * `stride` bytes apart.  Results stay in the handle's workspace; orbx_batch_view exposes
- * them as device pointers.  `stream` is the hipStream_t every kernel of the call is
- * launched on (0 = the null stream).  Calls that consume another call's results (stereo
- * after both extractions) must be on the same stream or ordered by the caller. */
+ * them as device pointers.  `stream` is the hipStream_t the call is ordered on (0 = the null
+ * stream): its kernels run there, except the extraction's side branch, which is forked from
+ * and joined back into it by events (orbx_extractor_set_overlap).  Calls that consume another
+ * call's results (stereo after both extractions) must be on the same stream or ordered by
+ * the caller. */
 orbx_status orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int batch,
                                       int width, int height, size_t stride,
                                       size_t batch_stride, void* stream);
@@ -176,7 +178,7 @@ orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_lev
 orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* fork_level,
                                        int* levels);
 
-/* ---- per-kernel timing (HIP events around each launch, on the launch stream) ------------ */
+/* ---- per-kernel timing (HIP events set by each kernel's own dispatch, hipExtLaunchKernel) - */
 /* ORBX_K_LEVEL: every pyramid launch; ORBX_K_LEVEL0: the level-0 launch alone (a part of
  * ORBX_K_LEVEL, reported separately: it blurs the input, the others also resize). */
 typedef enum {

@@ -14,8 +14,9 @@ namespace orbx {
 // K_LEVEL0 times the level-0 launch alone (it is also part of K_LEVEL, all levels)
 enum KernelId { K_LEVEL = 0, K_FAST, K_OCTREE, K_ORIENT, K_STEREO, K_LEVEL0, K_COUNT };
 
-// Optional per-kernel HIP-event timing (orbx_profile_*): events bracket each launch on the
-// stream it is launched on; durations are read back by collect().
+// Optional per-kernel HIP-event timing (orbx_profile_*): the extraction and stereo kernels
+// get their events from their own dispatch (ORBX_TIMED_LAUNCH); durations are read back by
+// collect().
 struct KernelTimer {
     bool on = false;
     std::vector<hipEvent_t> pool;
