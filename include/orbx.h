@@ -170,9 +170,10 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
 /* ---- overlap inside one extraction (no reference counterpart: scheduling only) ----------
  * The pyramid is a chain of launches (level l is resized from level l-1, ORBextractor.cc:
  * 1129-1154) whose small levels leave most of the device idle.  The first `levels` levels'
- * FAST (mode 1), + DistributeOctTree (2), + IC_Angle / rBRIEF (3) then run on the handle's
- * second stream, forked by an event before level `fork_level`'s launch and joined back before
- * the other levels' orientation; mode 0 runs every kernel in sequence on the call's stream.
+ * FAST (mode 1), + DistributeOctTree (2), + IC_Angle / rBRIEF (3), + level 0's blur (4,
+ * images in place only) then run on the handle's second stream, forked by an event before
+ * level `fork_level`'s launch and joined back before the other levels' orientation; mode 0
+ * runs every kernel in sequence on the call's stream.
  * Outputs are identical in every mode.  mode < 0 restores the built-in default. */
 orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_level, int levels);
 orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* fork_level,

@@ -875,7 +875,7 @@ const char* orbx_kernel_name(int id) {
 }
 
 orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_level, int levels) {
-    if (!h || mode > 3 || (mode > 0 && (fork_level < 0 || levels < 1))) return ORBX_ERR_INVALID;
+    if (!h || mode > 4 || (mode > 0 && (fork_level < 0 || levels < 1))) return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(h->mu);
     if (mode < 0) {
         h->side_mode = FAST_SIDE;

@@ -1600,17 +1600,24 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const int min_fork = (nside == 1 && a.in_place && !side_od) ? 0 : nside;
     const int fork_at = a.side_at < min_fork ? min_fork : a.side_at;
     const int ob0 = side_od ? G.orient_block_begin[nside] : 0;   // first block of the main launch
+    // mode 4: level 0's own launch (the blur of the input slot, which only the level-0
+    // descriptors read) moves to the side branch too, so the main chain starts with level 1
+    // (resized from the input slot itself); needs the images in place
+    const bool side_l0 = side_od && mode >= 4 && a.in_place;
+    const int main0 = side_l0 ? 1 : 0;
+    const int fork_main = fork_at > main0 ? fork_at : main0;
     hipError_t err = hipSuccess;
     if (side) {
-        err = launch_levels(a, st, 0, fork_at);
+        err = launch_levels(a, st, main0, fork_main);
         if (err != hipSuccess) return err;
         if ((err = hipEventRecord(a.ev_fork, st)) != hipSuccess) return err;
         if ((err = hipStreamWaitEvent(a.side, a.ev_fork, 0)) != hipSuccess) return err;
+        if (side_l0 && (err = launch_levels(a, a.side, 0, 1)) != hipSuccess) return err;
         fast(0, c_l1, a.side);
         if (mode >= 2) oct(dim3(nside, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
         if (side_od) orient(0, ob0, -1, a.side);
         if ((err = hipEventRecord(a.ev_join, a.side)) != hipSuccess) return err;
-        err = launch_levels(a, st, fork_at, G.nlevels);
+        err = launch_levels(a, st, fork_main, G.nlevels);
         if (err != hipSuccess) return err;
         fast(c_l1, G.n_cells, st);
         if (mode >= 2) oct(dim3(G.nlevels - nside, a.batch), a.octree_lds, a.ncap, a.kcap, nside, st);

@@ -294,8 +294,8 @@ def test_stereo_batch_shape_and_size_changes(orbx_lib, gpu):
             assert nvh[i] == n1
 
 
-@pytest.mark.parametrize("nlevels", [8, 3])
-def test_overlap_modes_identical(orbx_lib, gpu, nlevels):
+@pytest.mark.parametrize("nlevels,resident", [(8, False), (3, False), (8, True)])
+def test_overlap_modes_identical(orbx_lib, gpu, nlevels, resident):
     """The side branch (orbx_extractor_set_overlap: the first levels' FAST / octree /
     orientation on a second stream, forked inside the pyramid chain) changes only the
     schedule: every mode, fork level and level count gives the one-stream outputs bit for bit
@@ -310,17 +310,22 @@ def test_overlap_modes_identical(orbx_lib, gpu, nlevels):
     Rs = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
     mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
     sb = m.StereoBatch(B, 2000, 1.2, nlevels, 20, 7)
+    if resident:   # images in the level-0 slots: mode 4 moves level 0's launch to the branch
+        Lv, Rv = sb.input_views(Ls.shape[2], Ls.shape[1])
+        Lv.copy_(Ls)
+        Rv.copy_(Rs)
 
     def run(cfg):
         sb.ext.set_overlap(*cfg)
-        outs = [t.cpu().numpy().copy() for t in sb(Ls, Rs, KITTI_MBF, mb)]
+        res = sb.run_resident(KITTI_MBF, mb) if resident else sb(Ls, Rs, KITTI_MBF, mb)
+        outs = [t.cpu().numpy().copy() for t in res]
         torch.cuda.synchronize()
         return outs, sb.fetch("left"), sb.fetch("right")
 
     ref = run((0, 0, 1))
     assert ref[0][2].sum() > 0
     for cfg in [(-1, 0, 0), (1, 0, 1), (2, 1, 1), (3, 1, 1), (3, 3, 1), (3, 3, 2), (3, 4, 3),
-                (3, 9, 1), (3, 2, 12)]:
+                (3, 9, 1), (3, 2, 12), (4, 0, 1), (4, 1, 1), (4, 3, 1), (4, 2, 2)]:
         got = run(cfg)
         (u0, d0, n0), l0, r0 = ref
         (u1, d1, n1), l1, r1 = got
