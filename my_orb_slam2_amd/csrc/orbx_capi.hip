@@ -727,9 +727,9 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         const size_t B = (size_t)batch;
         // k_fast (FAST_PFU) reads up to 4 * FAST_PF2D rows past a cell's ROI
         const size_t pyr_slack = (size_t)4 * FAST_PF2D * G.lv[0].pitch + 256;
-        // k_orient_desc reads whole 16-byte stripes (BLUR_STRIPE), up to one stripe past a
+        // BLUR_STRIPE: k_orient_desc reads whole 16-byte stripes, up to one stripe past a
         // level's last
-        const size_t blur_slack = (size_t)16 * (G.lv[0].h + 64);
+        const size_t blur_slack = BLUR_STRIPE ? (size_t)16 * (G.lv[0].h + 64) : 0;
         bool ok = h->d_pyr.ensure(B * G.pyr_bytes + pyr_slack) &&
                   h->d_blur.ensure(B * G.pyr_bytes + blur_slack) &&
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
