@@ -59,10 +59,6 @@ struct orbx_extractor {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_mode = FAST_SIDE, side_at = FAST_SIDE_AT, side_lv = FAST_SIDE_LV;
-    // orbx_extract's whole sequence (H2D, kernels, D2H) as one HIP graph, rebuilt when its key
-    // (image size, overlap setting, every buffer address it names) changes
-    hipGraphExec_t g1 = nullptr;
-    std::vector<const void*> g1key;
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -748,10 +744,9 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     return ORBX_OK;
 }
 
-// The launch descriptor of one batched extraction (d_imgs == nullptr: level 0 of every image
-// is already in the pyramid, in place).
-static ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
-                                    int split, int batch, size_t stride, size_t batch_stride) {
+// d_imgs == nullptr: level 0 of every image is already in the pyramid (in place).
+orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
+                        int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
     ExtractLaunch a;
     a.in_place = d_imgs == nullptr;
     if (a.in_place) {
@@ -797,12 +792,6 @@ static ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, co
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
     strip_heights(h, batch, a.sth);
-    return a;
-}
-
-orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
-                        int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
-    ExtractLaunch a = extract_launch(h, d_imgs, d_imgs2, split, batch, stride, batch_stride);
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
@@ -1012,7 +1001,6 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
-    if (h->g1) (void)hipGraphExecDestroy(h->g1);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->done) (void)hipEventDestroy(h->done);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
@@ -1036,55 +1024,6 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
     return ORBX_OK;
 }
 
-#ifndef ORBX_EXTRACT_GRAPH
-#define ORBX_EXTRACT_GRAPH 1   // orbx_extract replays its launch sequence from a HIP graph
-#endif
-
-// orbx_extract's device work for the image staged in h_in: one linear DMA into pyramid level 0,
-// the extraction, and every output back to h_out in one pinned block.
-static bool enqueue_extract1(orbx_extractor* h, hipStream_t st, size_t img_bytes, size_t o_kps,
-                             size_t o_desc, size_t KC) {
-    const LevelGeom& L0 = h->hg.lv[0];
-    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 1, 1, 0, 0);
-    return HIPOK(hipMemcpyAsync(h->d_pyr.as<uint8_t>() + L0.off, h->h_in, img_bytes,
-                                hipMemcpyHostToDevice, st)) &&
-           HIPOK(launch_extract(a, st)) &&
-           HIPOK(hipMemcpyAsync(h->h_out, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) &&
-           HIPOK(hipMemcpyAsync(h->h_out + o_kps, h->d_kps.p, KC * sizeof(orbx_keypoint),
-                                hipMemcpyDeviceToHost, st)) &&
-           HIPOK(hipMemcpyAsync(h->h_out + o_desc, h->d_desc.p, KC * 32, hipMemcpyDeviceToHost, st));
-}
-
-// The graph of enqueue_extract1 for the handle's current state, captured on st when missing
-// or stale (a single frame per call is launch-bound: one graph launch replaces ~15 enqueues).
-static bool extract1_graph(orbx_extractor* h, hipStream_t st, int width, int height,
-                           size_t img_bytes, size_t o_kps, size_t o_desc, size_t KC) {
-    const DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr, &h->d_blur,
-                            &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
-                            &h->d_desc, &h->d_nkp};
-    std::vector<const void*> key = {(const void*)(intptr_t)width, (const void*)(intptr_t)height,
-                                    (const void*)(intptr_t)h->side_mode,
-                                    (const void*)(intptr_t)h->side_at,
-                                    (const void*)(intptr_t)h->side_lv, h->h_in, h->h_out};
-    for (const DevBuf* b : bufs) key.push_back(b->p);
-    if (h->g1 && key == h->g1key) return true;
-    if (h->g1) {
-        (void)hipGraphExecDestroy(h->g1);
-        h->g1 = nullptr;
-    }
-    hipGraph_t g = nullptr;
-    if (!HIPOK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal))) return false;
-    const bool ok = enqueue_extract1(h, st, img_bytes, o_kps, o_desc, KC);
-    const bool ended = HIPOK(hipStreamEndCapture(st, &g));
-    hipGraphExec_t ex = nullptr;
-    const bool inst = ok && ended && g && HIPOK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    if (g) (void)hipGraphDestroy(g);
-    if (!inst) return false;
-    h->g1 = ex;
-    h->g1key = key;
-    return true;
-}
-
 orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
                          size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
                          int* n_out) {
@@ -1102,7 +1041,7 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     // pitch, and one linear DMA writes it straight into pyramid level 0 (mvImagePyramid[0]):
     // the extraction then only blurs it (no device-side copy of the input; a pitched 2-D
     // host copy would run row by row).  Every output comes back in one pinned block: one
-    // host wait per call.  Without per-kernel timing the sequence is replayed from a graph.
+    // host wait per call.
     const LevelGeom& L0 = h->hg.lv[0];
     const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)height;
     const size_t KC = (size_t)h->hg.kp_cap;
@@ -1112,14 +1051,18 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
         return ORBX_ERR_DEVICE;
     for (int y = 0; y < height; ++y)
         std::memcpy(h->h_in + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
-    if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
-    const bool graph = ORBX_EXTRACT_GRAPH && !h->timer.on &&
-                       extract1_graph(h, st, width, height, img_bytes, o_kps, o_desc, KC);
-    if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue_extract1(h, st, img_bytes, o_kps, o_desc, KC)) ||
+    if (!order_after_last(h, st) ||
+        !HIPOK(hipMemcpyAsync(h->d_pyr.as<uint8_t>() + L0.off, h->h_in, img_bytes,
+                              hipMemcpyHostToDevice, st)))
+        return ORBX_ERR_DEVICE;
+    s = run_extract(h, nullptr, nullptr, 1, 1, 0, 0, st);
+    if (s != ORBX_OK) return s;
+    if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(h->h_out + o_kps, h->d_kps.p, KC * sizeof(orbx_keypoint),
+                              hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(h->h_out + o_desc, h->d_desc.p, KC * 32, hipMemcpyDeviceToHost, st)) ||
         !mark_done(h, st) || !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
-    h->last_batch = 1;
-    h->last_valid = true;
     int n = 0;
     std::memcpy(&n, h->h_out, 4);
     *n_out = n;
