@@ -390,3 +390,28 @@ def test_overlap_branch_in_a_hip_graph(orbx_lib, gpu):
         assert_f32_bits_equal(got[0][i, :n], ref[0][i, :n], f"graph uRight {i}")
         assert_f32_bits_equal(got[1][i, :n], ref[1][i, :n], f"graph depth {i}")
     sb.ext.set_overlap(-1)
+
+
+def test_overlap_setting_api(orbx_lib, gpu):
+    """orbx_extractor_set_overlap / get_overlap: the built-in default (mode 3, fork before
+    level 3, one level), explicit settings read back, mode < 0 restores the default, and
+    out-of-range arguments are rejected with ORBX_ERR_INVALID without changing the setting."""
+    import ctypes
+    import my_orb_slam2_amd as m
+    from my_orb_slam2_amd._lib import OrbxError
+    e = m.ORBextractor(1000, 1.2, 8, 20, 7)
+    assert e.overlap() == (3, 3, 1)
+    e.set_overlap(0, 0, 1)
+    assert e.overlap() == (0, 0, 1)
+    e.set_overlap(2, 4, 2)
+    assert e.overlap() == (2, 4, 2)
+    L = orbx_lib
+    for bad in [(5, 3, 1), (3, -1, 1), (3, 3, 0)]:
+        assert L.orbx_extractor_set_overlap(e._h, *bad) == -1, bad
+        assert e.overlap() == (2, 4, 2)
+    assert L.orbx_extractor_set_overlap(None, 0, 0, 1) == -1
+    assert L.orbx_extractor_get_overlap(None, None, None, None) == -1
+    e.set_overlap(-1)
+    assert e.overlap() == (3, 3, 1)
+    with pytest.raises(OrbxError):
+        e.set_overlap(7)
