@@ -396,7 +396,6 @@ def test_overlap_setting_api(orbx_lib, gpu):
     """orbx_extractor_set_overlap / get_overlap: the built-in default (mode 3, fork before
     level 3, one level), explicit settings read back, mode < 0 restores the default, and
     out-of-range arguments are rejected with ORBX_ERR_INVALID without changing the setting."""
-    import ctypes
     import my_orb_slam2_amd as m
     from my_orb_slam2_amd._lib import OrbxError
     e = m.ORBextractor(1000, 1.2, 8, 20, 7)
