@@ -4,8 +4,8 @@
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 --no-kernel-timing --serial-steps 0 > $O/trace.log 2>&1 || { echo TRACE FAILED; tail $O/trace.log; exit 1; }
-timeout -k 10 300 python bench.py --steps 20 --warmup 2 --cpu-seconds 0 --serial-steps 0 > $O/bench20.json 2> $O/bench20.err || { echo BENCH FAILED; tail $O/bench20.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --no-kernel-timing --serial-steps 0 > $O/trace.log 2>&1 || { echo TRACE FAILED; tail $O/trace.log; exit 1; }
+timeout -k 10 300 python bench.py --cpu-seconds 0 --serial-steps 0 > $O/bench20.json 2> $O/bench20.err || { echo BENCH FAILED; tail $O/bench20.err; exit 1; }
 python - <<PY
 import csv, json
 rows = list(csv.DictReader(open("$O/trace/run_kernel_stats.csv")))
