@@ -262,34 +262,10 @@ def main():
 
     mb = float(np.float32(MBF) / np.float32(FX))
     NI = max(1, args.inflight)
-    sbs = [orbx.StereoBatch(B, NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(NI)]
-    sb = sbs[0]
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NI - 1)]
-    sts = [s_.cuda_stream for s_ in streams]
-
-    if args.overlap is not None:
-        ov = [int(v) for v in args.overlap.split(",")]
-        for h in sbs:
-            h.ext.set_overlap(*ov)
-    overlap = sbs[0].ext.overlap()
-
     resident = args.input == "resident" and not args.host_io
-    if resident:
-        # each handle's level-0 slots hold the step's images (written once, before timing)
-        for h in sbs:
-            Lv, Rv = h.input_views(W, H)
-            Lv.copy_(Ls)
-            Rv.copy_(Rs)
-        torch.cuda.synchronize(dev)
-
-        def run_on(h, st):
-            h.run_resident(MBF, mb, stream=st)
-    else:
-        def run_on(h, st):
-            h(Ls, Rs, MBF, mb, stream=st)
-
-    def run_step(i):
-        run_on(sbs[i % NI], sts[i % NI])
+    sbs, sts, run_on, run_step, overlap = headline_handles(
+        torch, orbx, dev, local, B, Ls, Rs, NI, args.overlap, resident, mb)
+    sb = sbs[0]
 
     io = None
     if args.host_io:
@@ -335,13 +311,16 @@ def main():
     # sanity on the produced work (outside the timed region)
     nv = sb.nvalid.cpu().numpy()
     nkp, _, _ = sb.fetch("left")
+    # every in-flight handle's outputs of its last timed step, per slot (outside the timed
+    # region), for the comparison with the one-stream pass below
+    dig_inflight = [stereo_digests(h) for h in sbs] if io is None else None
 
     # The same step with every kernel in sequence on one stream and one batch in flight
     # (outside the timed region): the overlap's gain measured in this run, and each kernel's
     # launch time on its own (in the timed run the side branch and the other batch in flight
     # share the device with every launch, so the HIP-event spans include that sharing)
-    serial = None
-    if (overlap[0] > 0 or NI > 1) and args.serial_steps > 0 and io is None:
+    serial = dig_serial = None
+    if args.serial_steps > 0 and io is None:
         for h in sbs:
             h.ext.set_overlap(0)
         for i in range(3):
@@ -357,6 +336,7 @@ def main():
         t_ser = time.perf_counter() - ts
         serial = {"steps": args.serial_steps, "ms_per_step": 1000.0 * t_ser / args.serial_steps,
                   "value": B * args.serial_steps / t_ser}
+        dig_serial = stereo_digests(sbs[0])
         if not args.no_kernel_timing:
             sprof = {}
             for h in sbs:
@@ -369,66 +349,32 @@ def main():
         for h in sbs:
             h.ext.set_overlap(*overlap)
 
+    verify = verification(dig_inflight, dig_serial, B)
+
     total_pairs = B * args.steps * world
     fps = total_pairs / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # roofline of the dominant kernel
+    # roofline of the dominant kernel: the largest kernel group of the one-stream pass (the
+    # run's own measurement of each kernel alone), its launches timed in the timed region
     roof = None
     if prof:
-        # the pyramid (the largest kernel of the one-stream step; with the side branch the
-        # other kernels' spans overlap it and each other, so the largest span is no guide)
-        dom = "k_level" if "k_level" in prof else max(prof, key=lambda k: prof[k][0])
-        tot_ms, launches = prof[dom]
-        avg_s = tot_ms / 1000.0 / max(launches, 1)
-        geo = kernel_bytes(sb.ext, 2 * B, B)
-        traffic = traffic_from_csv(args.traffic_csv, dom)
-        alg = counted_bytes(geo.get(dom), traffic)
-        achieved = (alg / avg_s / 1e9) if (alg and avg_s > 0) else None
-        roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": alg,
-                "requested_bytes_per_launch": geo.get(dom), "avg_launch_ms": avg_s * 1000.0,
-                "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4)
-                                       for k, v in prof.items()}}
-        # every extraction / stereo kernel against the HBM roof (north_star: FAST and the
-        # matcher included), same definitions as the headline object.  With a side branch or
-        # several batches in flight the timed run's spans overlap each other, so these come
-        # from the one-stream pass (one launch per kernel per step, as in the PMC passes,
-        # tools/prof_counters.sh) when the run has one
-        kprof, ksteps = prof, args.steps
-        if serial and "prof" in serial:
-            kprof, ksteps = serial["prof"], serial["steps"]
-            roof["per_kernel_source"] = "one-stream pass (one_stream)"
-        roof["per_kernel"] = per_kernel_hbm(kprof, geo, args.traffic_csv, ksteps)
-        # the pyramid's two kinds of launch apart: level 0 (blur of the input) and levels
-        # 1-7 (resize + blur)
-        if "k_level0" in kprof and kprof["k_level0"][1] and "k_level" in kprof:
-            t_all, n_all = kprof["k_level"]
-            t0l, n0l = kprof["k_level0"]
-            prof_l17 = {"k_level1_7": (t_all - t0l, n_all - n0l)}
-            roof["per_kernel"].update(per_kernel_hbm(prof_l17, geo, args.traffic_csv, ksteps))
-        # the integer kernels are bound by VALU issue, not HBM: the same launches against
-        # the issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
-        for k, e in [(dom, roof)] + list(roof["per_kernel"].items()):
-            e["valu"] = valu_entry(args.insts_csv, k, e["avg_launch_ms"] / 1000.0)
+        sprof = serial.get("prof") if serial else None
+        roof = headline_roofline(prof, args.steps, sprof, args.serial_steps, sb.ext, B,
+                                 args.traffic_csv, args.insts_csv)
         roof["overlap"] = {"mode": overlap[0], "fork_level": overlap[1], "levels": overlap[2]}
-        if serial and "prof" in serial:
-            st_ms, st_n = serial["prof"][dom]
-            s_avg = st_ms / 1000.0 / max(st_n, 1)
-            s_ach = (alg / s_avg / 1e9) if (alg and s_avg > 0) else None
-            roof["serial_pass"] = {"avg_launch_ms": s_avg * 1000.0, "achieved": s_ach,
-                                   "frac": (s_ach / HBM_PEAK_GBS) if s_ach else None,
-                                   "kernel_ms_per_step": serial["kernel_ms_per_step"]}
     if serial:
         serial.pop("prof", None)
         serial.pop("kernel_ms_per_step", None)
 
-    cpu = cpu_tp = None
+    cpu = cpu_tp = cpu_tp16 = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(pairs, mb, args.cpu_seconds)
+        ref = dig_serial or (dig_inflight[0] if dig_inflight else None)
+        cpu = cpu_baseline(pairs, mb, args.cpu_seconds,
+                           gpu_digests=ref[:min(P, 8)] if ref else None)
+        # SURVEY §8(d) mode (ii) on every host CPU, and on the box's CPU share per GPU (16)
         cpu_tp = cpu_baseline_throughput(pairs, mb, min(args.cpu_seconds, 6.0))
+        cpu_tp16 = cpu_baseline_throughput(pairs, mb, min(args.cpu_seconds, 6.0), workers=16)
 
     if rank == 0:
         out = {"metric": METRIC, "value": fps, "unit": "frames/sec", "n_gpus": world,
@@ -442,8 +388,9 @@ def main():
                           "parallelism": f"dp{world}"},
                "mean_keypoints_left": float(nkp.mean()),
                "mean_stereo_matches": float(nv.mean()),
+               "verified": verify["verified"] if verify else None, "verification": verify,
                "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp,
-               "one_stream": serial}
+               "cpu_baseline_throughput_16": cpu_tp16, "one_stream": serial}
         if io is not None:
             out["metric"] = METRIC + " (PCIe-inclusive: host images in, host keypoints out)"
             out["config"]["host_io"] = io
@@ -451,6 +398,80 @@ def main():
         emit(json.dumps(out))
     if dist_on:
         dist.destroy_process_group()
+
+
+def headline_handles(torch, orbx, dev, local, B, Ls, Rs, NI, overlap_arg, resident, mb):
+    """The timed configuration of the headline: NI StereoBatch handles of B pairs, step i on
+    handle i % NI and stream i % NI (stream 0 = the current stream), every extraction with the
+    side branch `overlap_arg` ("MODE,FORK,LEVELS"; None = the library's default); with
+    `resident` the B pairs sit in each handle's level-0 slots (written once, here), else they
+    are copied in from the Ls / Rs tensors by the first kernel.  tests/test_gpu_bench_geometry.py
+    runs exactly this.  Returns (handles, raw streams, run_on(handle, stream), run_step(i),
+    overlap tuple)."""
+    sbs = [orbx.StereoBatch(B, NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(NI)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NI - 1)]
+    sts = [s_.cuda_stream for s_ in streams]
+    if overlap_arg is not None:
+        ov = [int(v) for v in str(overlap_arg).split(",")]
+        for h in sbs:
+            h.ext.set_overlap(*ov)
+    overlap = sbs[0].ext.overlap()
+    if resident:
+        for h in sbs:
+            Lv, Rv = h.input_views(W, H)
+            Lv.copy_(Ls)
+            Rv.copy_(Rs)
+        torch.cuda.synchronize(dev)
+
+        def run_on(h, st):
+            h.run_resident(MBF, mb, stream=st)
+    else:
+        def run_on(h, st):
+            h(Ls, Rs, MBF, mb, stream=st)
+
+    def run_step(i):
+        run_on(sbs[i % NI], sts[i % NI])
+    return sbs, sts, run_on, run_step, overlap
+
+
+def slot_digest(kl, dl, kr, dr, u, z, nv) -> str:
+    """SHA-256 of one stereo frame's outputs: left / right keypoints (cv::KeyPoint records) and
+    descriptors, uRight and depth of the left keypoints, and the valid-match count."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in (kl, dl, kr, dr, u, z):
+        a = np.zeros(0, np.uint8) if a is None else np.ascontiguousarray(a)
+        h.update(int(a.shape[0]).to_bytes(8, "little"))
+        h.update(a.tobytes())
+    h.update(int(nv).to_bytes(8, "little", signed=True))
+    return h.hexdigest()
+
+
+def stereo_digests(sb) -> list:
+    """slot_digest of every pair of a StereoBatch's last call (host copies of its outputs)."""
+    nkl, kl, dl = sb.fetch("left")
+    nkr, kr, dr = sb.fetch("right")
+    B = len(nkl)
+    u = sb.uR[:B].cpu().numpy()
+    z = sb.depth[:B].cpu().numpy()
+    nv = sb.nvalid[:B].cpu().numpy()
+    return [slot_digest(kl[i, :nkl[i]], dl[i, :nkl[i]], kr[i, :nkr[i]], dr[i, :nkr[i]],
+                        u[i, :nkl[i]], z[i, :nkl[i]], nv[i]) for i in range(B)]
+
+
+def verification(dig_inflight, dig_serial, B):
+    """`verified`: every in-flight handle's last timed step equals the one-stream pass of the
+    same pairs, slot by slot (or, without that pass, the in-flight handles equal each other)."""
+    if not dig_inflight:
+        return None
+    import hashlib
+    ref = dig_serial if dig_serial is not None else dig_inflight[0]
+    bad = [(k, i) for k, d in enumerate(dig_inflight) for i in range(B) if d[i] != ref[i]]
+    return {"verified": not bad, "slots": B, "handles": len(dig_inflight),
+            "against": "one-stream pass (overlap 0, one batch in flight)" if dig_serial is not None
+                       else "the first in-flight handle",
+            "mismatched_slots": len(bad), "first_mismatches": bad[:8],
+            "digest": hashlib.sha256("".join(ref).encode()).hexdigest()[:16]}
 
 
 def host_io_pipeline(torch, orbx, dev, local, B, Lh, Rh, mb, graphs=True):
@@ -560,6 +581,99 @@ def host_io_pipeline(torch, orbx, dev, local, B, Lh, Rh, mb, graphs=True):
     return run_step, io, hs[0]
 
 
+# kernel groups of the stereo step: the pyramid's two kinds of launch apart (level 0 blurs the
+# input slot, levels 1-7 resize + blur), then the other kernels
+HEADLINE_GROUPS = ("k_level0", "k_level1_7", "k_fast", "k_octree", "k_orient_desc", "k_stereo")
+# launches per step of each group in the one-stream step (overlap 0, one batch in flight): the
+# launch count of the PMC passes (tools/prof_counters.sh), whose per-dispatch averages scale by it
+ONE_STREAM_LAUNCHES = {"k_level": 8, "k_level0": 1, "k_level1_7": 7, "k_fast": 1, "k_octree": 1,
+                       "k_orient_desc": 1, "k_stereo": 1}
+
+
+def split_level(prof):
+    """{group: (total_ms, launches)} with k_level split into k_level0 and k_level1_7 (the
+    library times level 0's launches under both k_level and k_level0)."""
+    out = {k: v for k, v in prof.items() if v[1]}
+    if "k_level" in out:
+        t_all, n_all = out["k_level"]
+        t0, n0 = out.get("k_level0", (0.0, 0))
+        if n_all - n0 > 0:
+            out["k_level1_7"] = (t_all - t0, n_all - n0)
+    return out
+
+
+def step_bytes(ext, n, B):
+    """Algorithmic HBM bytes per STEP of each kernel group (kernel_bytes per one-stream launch x
+    the one-stream launches per step)."""
+    return {k: v * ONE_STREAM_LAUNCHES.get(k, 1) for k, v in kernel_bytes(ext, n, B).items()}
+
+
+def traffic_per_step(paths, kernel):
+    """PMC HBM bytes per step of a kernel group: the per-dispatch average of the one-stream PMC
+    passes x that pass's launches per step."""
+    t = traffic_from_csv(paths, kernel)
+    return t * ONE_STREAM_LAUNCHES.get(kernel, 1) if t else t
+
+
+def roofline_entry(name, tot_ms, launches, steps, alg_step, traffic_step):
+    """One kernel group against the HBM roof: algorithmic bytes per launch (the step's bytes
+    over its launches per step; capped by the measured traffic, counted_bytes) / the mean
+    HIP-event launch duration."""
+    per_step = launches / max(steps, 1)
+    req = alg_step / per_step if alg_step else None
+    traffic = traffic_step / per_step if traffic_step else None
+    alg = counted_bytes(req, traffic)
+    avg_s = tot_ms / 1000.0 / max(launches, 1)
+    ach = (alg / avg_s / 1e9) if (alg and avg_s > 0) else None
+    return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": traffic,
+            "algorithmic_bytes_per_launch": alg, "requested_bytes_per_launch": req,
+            "avg_launch_ms": avg_s * 1000.0, "launches_per_step": per_step,
+            "ms_per_step": tot_ms / max(steps, 1)}
+
+
+def pick_dominant(gprof, steps):
+    """The kernel group with the most time per step (one stream: kernels do not overlap)."""
+    cand = {k: v for k, v in gprof.items() if k in HEADLINE_GROUPS}
+    return max(cand, key=lambda k: cand[k][0] / max(steps, 1)) if cand else None
+
+
+def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv):
+    """The headline `roofline` object.  `kernel` is the group that takes the most time in the
+    run's one-stream pass (`sprof` over `ssteps` steps; the timed profile when the run has no
+    such pass); `frac` is that group's algorithmic bytes per launch over its mean launch
+    duration in the timed region (hipExtLaunchKernel events from the kernel's own dispatch,
+    the quantity rocprofv3 --kernel-trace reports).  `serial_pass` is the same group timed in
+    the one-stream pass; `per_kernel` holds every group, from the one-stream pass."""
+    gt = split_level(prof)
+    gs = split_level(sprof) if sprof else None
+    dom = pick_dominant(gs if gs else gt, ssteps if gs else steps)
+    geo = step_bytes(ext, 2 * B, B)
+    if dom is None or dom not in gt:
+        return None
+    roof = roofline_entry(dom, *gt[dom], steps, geo.get(dom), traffic_per_step(traffic_csv, dom))
+    roof["selected_by"] = ("largest kernel group per step in the one-stream pass" if gs else
+                           "largest kernel group per step in the timed region")
+    roof["kernel_ms_per_step"] = {k: round(v[0] / max(steps, 1), 4) for k, v in gt.items()}
+    kp, ks = (gs, ssteps) if gs else (gt, steps)
+    roof["per_kernel_source"] = "one-stream pass (one_stream)" if gs else "timed region"
+    roof["per_kernel"] = {k: roofline_entry(k, *kp[k], ks, geo.get(k),
+                                            traffic_per_step(traffic_csv, k))
+                          for k in HEADLINE_GROUPS + ("k_level",) if k in kp}
+    roof["one_stream_ms_per_step"] = {k: round(v[0] / max(ks, 1), 4) for k, v in kp.items()}
+    # the integer kernels are bound by VALU issue, not HBM: the same launches against the
+    # issue rate (SQ_INSTS_VALU from a PMC pass of the same workload)
+    # (the PMC pass counts one-stream dispatches: scaled to this entry's launches per step)
+    for e in [roof] + list(roof["per_kernel"].values()):
+        e["valu"] = valu_entry(insts_csv, e["kernel"], e["avg_launch_ms"] / 1000.0,
+                               ONE_STREAM_LAUNCHES.get(e["kernel"], 1) / e["launches_per_step"])
+    if gs and dom in gs:
+        se = roof["per_kernel"][dom]
+        roof["serial_pass"] = {"avg_launch_ms": se["avg_launch_ms"], "achieved": se["achieved"],
+                               "frac": se["frac"], "launches_per_step": se["launches_per_step"]}
+    return roof
+
+
 def counted_bytes(requested, traffic):
     """Bytes a roofline entry credits to one launch: the kernel's requested (algorithmic)
     bytes, capped by the measured HBM traffic when a PMC pass holds it.  Requested bytes
@@ -569,23 +683,6 @@ def counted_bytes(requested, traffic):
     if not requested:
         return requested
     return min(requested, traffic) if traffic else requested
-
-
-def per_kernel_hbm(prof, geo, traffic_csv, steps):
-    out = {}
-    for k, (tot_ms, launches) in prof.items():
-        req = geo.get(k)
-        if not req or not launches or tot_ms <= 0:
-            continue
-        traffic = traffic_from_csv(traffic_csv, k)
-        alg = counted_bytes(req, traffic)
-        avg_s = tot_ms / 1000.0 / launches
-        ach = alg / avg_s / 1e9
-        out[k] = {"achieved": ach, "frac": ach / HBM_PEAK_GBS, "unit": "GB/s",
-                  "algorithmic_bytes_per_launch": alg, "requested_bytes_per_launch": req,
-                  "avg_launch_ms": avg_s * 1000.0,
-                  "launches_per_step": launches / max(steps, 1), "traffic": traffic}
-    return out
 
 
 def kernel_bytes(ext, n, B):
@@ -681,7 +778,7 @@ def mix_cycles_from_csv(paths, kernel, mix_path=None):
     return num / den if den else None
 
 
-def valu_entry(paths, kernel, avg_s):
+def valu_entry(paths, kernel, avg_s, scale=1.0):
     """A launch against the VALU issue roof:
     * busy_frac (mix-aware, <= 1 at the nominal clock): SQ_INSTS_VALU x the kernel's mean
       issue cycles per VALU instruction (its opcode mix priced at the measured gfx950 rates,
@@ -690,8 +787,12 @@ def valu_entry(paths, kernel, avg_s):
     * valubusy_4cycle: rocprof's VALUBusy (SQ_ACTIVE_INST_VALU, 4 cycles per instruction
       whatever its rate, over GRBM_GUI_ACTIVE / 8 cycles: overstates full-rate-rich kernels,
       may exceed 1, and the GRBM cycles of launches under ~0.3 ms read high), for reference;
-    * the issue rate in wave instructions/s (SQ_INSTS_VALU over the HIP-event launch time)."""
+    * the issue rate in wave instructions/s (SQ_INSTS_VALU over the HIP-event launch time).
+    `scale` converts the PMC pass's per-dispatch count to one launch of the entry (a kernel the
+    timed schedule launches twice per step where the one-stream pass launches it once: 1/2)."""
     v = valu_from_csv(paths, kernel)
+    if v:
+        v *= scale
     act = counter_from_csv(paths, kernel, "SQ_ACTIVE_INST_VALU")
     grbm = counter_from_csv(paths, kernel, "GRBM_GUI_ACTIVE")
     if not v and not act:
@@ -758,12 +859,14 @@ def latency_stats(ms) -> dict:
             "frames": len(v)}
 
 
-def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20):
+def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20, gpu_digests=None):
     """The CPU restatement timed on this host in the reference's own mode (src/Frame.cc:89-102:
     left and right extraction on two threads, then ComputeStereoMatches on one), per stereo
     frame: `warmup` untimed frames, then at least `min_frames` timed ones (more while the
     budget lasts); median and mean latency like stereo_kitti.cc:115-123, value = frames/s over
-    the timed frames."""
+    the timed frames.  The first warm-up frames are the base pairs, i.e. batch slots 0..P-1:
+    their outputs are checked against the GPU's (`gpu_digests`, bench.slot_digest of those
+    slots) before the timed frames start."""
     try:
         import oracle
     except Exception:
@@ -773,19 +876,25 @@ def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20):
     ms = []
     t_start = None
     f = 0
+    checked, agree = 0, 0
+    ncheck = min(len(gpu_digests or []), warmup, len(pairs))
     while True:
         Lp, Rp = pairs[f % len(pairs)]
         t0 = time.perf_counter()
         res = {}
         th = threading.Thread(target=lambda: res.__setitem__("r", orr(Rp)))
         th.start()
-        kl, _ = ol(Lp)
+        kl, dl = ol(Lp)
         th.join()
-        oracle.stereo_match(ol, orr, len(kl), MBF, mb)
+        u, z, nv = oracle.stereo_match(ol, orr, len(kl), MBF, mb)
         t1 = time.perf_counter()
+        if f < ncheck:      # a warm-up frame: outside the timed frames
+            kr, dr = res["r"]
+            checked += 1
+            agree += slot_digest(kl, dl, kr, dr, u, z, nv) == gpu_digests[f]
         f += 1
         if f == warmup:
-            t_start = t1
+            t_start = time.perf_counter()
         elif f > warmup:
             ms.append(1000.0 * (t1 - t0))
             if len(ms) >= min_frames and t1 - t_start >= budget_s:
@@ -797,44 +906,62 @@ def cpu_baseline(pairs, mb, budget_s, min_frames=200, warmup=20):
                      f"{el:.1f} s",
            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
            "build": f"g++ -O3 -march={oracle.ISA} -ffp-contract=off (oracle/Makefile)"}
+    if ncheck:
+        out["gpu_slots_checked"] = checked
+        out["gpu_slots_equal"] = agree
     out.update(latency_stats(ms))
     return out
 
 
-def cpu_baseline_throughput(pairs, mb, budget_s, workers=16):
+def cpu_baseline_throughput(pairs, mb, budget_s, workers=None):
     """SURVEY §8(d) mode (ii): one stereo-frame pipeline per core (extract L, extract R,
-    ComputeStereoMatches, each worker with its own extractors), `workers` threads (the GPU box's
-    CPU share per GPU; ctypes releases the GIL inside the restatement)."""
+    ComputeStereoMatches, each worker with its own extractors) on every host CPU by default
+    (`workers` = os.cpu_count(); ctypes releases the GIL inside the restatement).  Reports the
+    aggregate frames/s and the per-pair median / mean latency of the workers' frames."""
     try:
         import oracle
     except Exception:
         return None
-    counts = [0] * workers
+    workers = workers or os.cpu_count() or 1
+    lat = [[] for _ in range(workers)]
     stop = [False]
+    go = threading.Barrier(workers + 1)
 
     def work(w):
         ol = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
         orr = oracle.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
         i = w
+        go.wait()
         while not stop[0]:
             Lp, Rp = pairs[i % len(pairs)]
+            t0 = time.perf_counter()
             kl, _ = ol(Lp)
             orr(Rp)
             oracle.stereo_match(ol, orr, len(kl), MBF, mb)
-            counts[w] += 1
+            lat[w].append(1000.0 * (time.perf_counter() - t0))
             i += workers
     ths = [threading.Thread(target=work, args=(w,)) for w in range(workers)]
-    t0 = time.perf_counter()
     for t in ths:
         t.start()
+    go.wait()
+    t0 = time.perf_counter()
     time.sleep(budget_s)
     stop[0] = True
     for t in ths:
         t.join()
     el = time.perf_counter() - t0
-    return {"value": sum(counts) / el, "unit": "frames/sec", "cores": workers, "kind": "port",
-            "sample": f"{sum(counts)} KITTI-size synthetic stereo pairs on {workers} worker threads "
-                      f"(one pipeline per core, SURVEY §8d mode ii), {el:.1f} s"}
+    allms = [v for l_ in lat for v in l_]
+    out = {"value": len(allms) / el, "unit": "frames/sec", "cores": workers, "kind": "port",
+           "sample": f"{len(allms)} KITTI-size synthetic stereo pairs on {workers} worker threads "
+                     f"(one pipeline per core, every host CPU; SURVEY §8d mode ii), {el:.1f} s",
+           "host_cpus": os.cpu_count()}
+    try:
+        out["usable_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    if allms:
+        out.update(latency_stats(allms))
+    return out
 
 
 # ---- the drop-in host path, one stereo frame at a time ---------------------------------------

@@ -253,7 +253,8 @@ orbx_status orbx_hamming_bf_top2(orbx_matcher* m, const uint8_t* q, int32_t nq,
 /* The same on device arrays, on the caller's stream; best_idx is offset by idx_base (a shard
  * of a larger database reports global row numbers, so per-shard results merge in shard order
  * with distributed.merge_top2).  ndb < 2^31 - idx_base.  The partial results live in the
- * matcher's scratch: calls on one matcher must share `stream` or be serialised. */
+ * matcher's scratch: a call on another stream than the previous call's waits (on the device,
+ * by an event) until that call's kernels are done with it. */
 orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int32_t nq,
                                         const uint8_t* d_db, int64_t ndb, int64_t idx_base,
                                         int32_t* d_best_idx, int32_t* d_best_dist,

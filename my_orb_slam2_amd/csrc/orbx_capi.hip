@@ -85,7 +85,8 @@ struct orbx_extractor {
     // last extraction
     int last_batch = 0;
     bool last_valid = false;
-    std::mutex mu;
+    // guards every field above against concurrent calls on one handle (const queries too)
+    mutable std::mutex mu;
 };
 
 namespace {
@@ -892,6 +893,7 @@ orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_lev
 orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* fork_level,
                                        int* levels) {
     if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
     if (mode) *mode = h->side_mode;
     if (fork_level) *fork_level = h->side_at;
     if (levels) *levels = h->side_lv;
@@ -900,12 +902,14 @@ orbx_status orbx_extractor_get_overlap(const orbx_extractor* h, int* mode, int* 
 
 orbx_status orbx_profile_enable(orbx_extractor* h, int on) {
     if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
     h->timer.on = on != 0;
     return ORBX_OK;
 }
 
 orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* launches) {
     if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
     h->timer.collect();
     for (int k = 0; k < K_COUNT; ++k) {
         if (total_ms) total_ms[k] = h->timer.ms[k];
@@ -919,6 +923,7 @@ orbx_status orbx_profile_collect(orbx_extractor* h, double* total_ms, int64_t* l
 orbx_status orbx_extractor_launch_info(const orbx_extractor* h, int batch, int* strip_rows,
                                        int* stereo_split) {
     if (!h || batch < 1) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
     if (!h->have_geom) return ORBX_ERR_STATE;
     int sth[ORBX_MAX_LEVELS];
     strip_heights(h, batch, sth);
@@ -1076,14 +1081,15 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
 
 static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,
                               uint8_t* out, int* width, int* height, bool blurred = false) {
-    if (!h || !h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
+    if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
         index >= h->last_batch)
         return ORBX_ERR_INVALID;
     const LevelGeom& lv = h->hg.lv[level];
     if (width) *width = lv.w;
     if (height) *height = lv.h;
     if (!out) return ORBX_OK;
-    std::lock_guard<std::mutex> lk(h->mu);
     (void)hipSetDevice(h->device);
     const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
 #if BLUR_STRIPE
@@ -1175,7 +1181,11 @@ orbx_status orbx_stereo_frames_resident(orbx_extractor* h, int batch, float mbf,
 }
 
 orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {
-    if (!h || !v || !h->last_valid) return ORBX_ERR_STATE;
+    if (!h || !v) return ORBX_ERR_STATE;
+    // a snapshot under the handle's lock: an extraction running on another thread cannot
+    // change the batch size or reallocate the buffers halfway through the copy
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->last_valid) return ORBX_ERR_STATE;
     memset(v, 0, sizeof(*v));
     v->batch = h->last_batch;
     v->kp_cap = h->hg.kp_cap;
@@ -1195,9 +1205,9 @@ orbx_status orbx_batch_view_get(const orbx_extractor* h, orbx_batch_view* v) {
 
 orbx_status orbx_batch_fetch(orbx_extractor* h, int first, int count, int32_t* nkp,
                              orbx_keypoint* kps, uint8_t* desc) {
-    if (!h || !h->last_valid || first < 0 || count < 0 || first + count > h->last_batch)
-        return ORBX_ERR_INVALID;
+    if (!h || first < 0 || count < 0) return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->last_valid || first + count > h->last_batch) return ORBX_ERR_INVALID;
     (void)hipSetDevice(h->device);
     // after the handle's last launches (on whatever stream), on the handle's own stream
     hipStream_t st = h->stream;

@@ -1654,15 +1654,21 @@ size_t octree_lds_bytes(int ncap, int kcap) {
 namespace orbx {
 hipError_t prepare_stereo(size_t lds);
 hipError_t prepare_level(size_t lds);
-// Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).  The
-// attribute is process-wide and only ever raised (to the largest size any handle needs), under
-// a lock: handles on several host threads may prepare concurrently.
+// Dynamic LDS above 64 KiB needs the per-kernel opt-in (gfx950 has 160 KiB per CU).
+// hipFuncSetAttribute acts on the current device, so the sizes already set are kept per device
+// (the caller has made the handle's device current) and only ever raised (to the largest size
+// any handle on that device needs), under a lock: handles on several host threads may prepare
+// concurrently.
 hipError_t prepare_kernels(size_t octree_lds, size_t stereo_lds, size_t level_lds,
                            size_t fast_lds) {
     static std::mutex mu;
-    static size_t have[4] = {0, 0, 0, 0};
+    static size_t have_dev[ORBX_MAX_DEVICES][4] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= ORBX_MAX_DEVICES) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lk(mu);
-    hipError_t e = hipSuccess;
+    size_t* have = have_dev[dev];
     if (octree_lds > have[0]) {
         for (const void* k : {(const void*)k_octree<256>, (const void*)k_octree<64>,
                               (const void*)k_octree<128>, (const void*)k_octree<512>})

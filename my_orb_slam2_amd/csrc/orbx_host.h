@@ -4,6 +4,10 @@
 
 #include <cstddef>
 
+#ifndef ORBX_MAX_DEVICES
+#define ORBX_MAX_DEVICES 64  // per-device kernel attribute caches (prepare_kernels, kfdb)
+#endif
+
 namespace orbx {
 
 // Text of the first failing HIP call on this thread (orbx_last_error()).

@@ -18,6 +18,9 @@
 #define ORBX_MAX_LEVELS 16
 #define ORBX_EDGE 19
 #define ORBX_MIN_BORDER 16   // EDGE_THRESHOLD - 3, src/ORBextractor.cc:785
+#ifndef ORBX_MAX_DEVICES
+#define ORBX_MAX_DEVICES 64  // per-device kernel attribute caches (prepare_kernels, kfdb)
+#endif
 
 namespace orbx {
 

@@ -302,7 +302,7 @@ struct orbx_kfdb {
     orbx_kfdb_params prm;
     hipStream_t stream = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    std::mutex mu;
+    mutable std::mutex mu;   // const queries (orbx_kfdb_size) lock it too
     // host mirror of the resident database
     std::vector<uint32_t> words;
     std::vector<double> vals;
@@ -474,14 +474,19 @@ orbx_status orbx_kfdb_create(const orbx_kfdb_params* params, orbx_kfdb** out) {
               HIPOK(hipStreamCreateWithFlags(&db->stream, hipStreamNonBlocking));
     for (int i = 0; i < 3 && ok; ++i) ok = HIPOK(hipEventCreate(&db->ev[i]));
     if (ok) {
-        // the scan's LDS: query words + weights + 64 terms per wave
-        static std::once_flag once;
-        static hipError_t attr = hipSuccess;
-        std::call_once(once, [] {
-            attr = hipFuncSetAttribute((const void*)k_kfdb_scan,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds(QMAX));
-        });
-        ok = HIPOK(attr);
+        // the scan's LDS: query words + weights + 64 terms per wave.  The attribute belongs to
+        // the current device (set above), so it is set once per device, not once per process
+        static std::mutex amu;
+        static bool have[ORBX_MAX_DEVICES] = {};
+        std::lock_guard<std::mutex> lk(amu);
+        if (p.device >= ORBX_MAX_DEVICES) {
+            ok = false;
+        } else if (!have[p.device]) {
+            ok = HIPOK(hipFuncSetAttribute((const void*)k_kfdb_scan,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)scan_lds(QMAX)));
+            have[p.device] = ok;
+        }
     }
     if (!ok) {
         orbx_kfdb_destroy(db);
@@ -553,6 +558,7 @@ orbx_status orbx_kfdb_clear(orbx_kfdb* db) {
 
 orbx_status orbx_kfdb_size(const orbx_kfdb* db, int32_t* nslots) {
     if (!db || !nslots) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(db->mu);
     *nslots = (int32_t)db->alive.size();
     return ORBX_OK;
 }
@@ -563,10 +569,11 @@ orbx_status orbx_kfdb_set_covisibles(orbx_kfdb* db, int32_t slot, const int32_t*
     std::lock_guard<std::mutex> lk(db->mu);
     if (slot < 0 || (size_t)slot >= db->alive.size()) return ORBX_ERR_INVALID;
     const int K = db->prm.covisibles;
+    // checked before the row is written: an invalid call leaves the host and device rows alike
+    for (int j = 0; j < K && j < n; ++j)
+        if (neighbours[j] < 0) return ORBX_ERR_INVALID;
     int32_t* row = db->cov.data() + (size_t)slot * K;
     for (int j = 0; j < K; ++j) row[j] = j < n ? neighbours[j] : -1;
-    for (int j = 0; j < K && j < n; ++j)
-        if (row[j] < 0) return ORBX_ERR_INVALID;
     db->cov_lo = std::min(db->cov_lo, slot);
     db->cov_hi = std::max(db->cov_hi, slot);
     return ORBX_OK;
@@ -586,6 +593,7 @@ orbx_status orbx_kfdb_detect_loop(orbx_kfdb* db, const uint32_t* qwords, const d
 
 orbx_status orbx_kfdb_last_timing(const orbx_kfdb* db, double* scan_ms, double* select_ms) {
     if (!db) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(db->mu);
     if (scan_ms) *scan_ms = db->t_scan;
     if (select_ms) *select_ms = db->t_select;
     return ORBX_OK;

@@ -31,6 +31,11 @@ struct orbx_matcher {
     std::vector<uint8_t> staging;
     KernelTimer timer;
     std::mutex mu;
+    // recorded after the last brute-force launch (its partial-result scratch d_bf is shared by
+    // every call): a call on another stream waits for it before reusing the scratch
+    hipEvent_t bf_done = nullptr;
+    hipStream_t bf_stream = nullptr;
+    bool have_bf = false;
 };
 
 namespace {
@@ -342,6 +347,7 @@ orbx_status orbx_matcher_create(const orbx_matcher_params* params, orbx_matcher*
     if (!HIPOK(hipSetDevice(p.device)) ||
         !HIPOK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking)) ||
         !HIPOK(hipMalloc((void**)&m->d_err, 64)) || !HIPOK(hipMemset(m->d_err, 0, 64)) ||
+        !HIPOK(hipEventCreateWithFlags(&m->bf_done, hipEventDisableTiming)) ||
         !HIPOK(prepare_match_kernels())) {
         orbx_matcher_destroy(m);
         return ORBX_ERR_DEVICE;
@@ -357,6 +363,8 @@ orbx_status orbx_matcher_destroy(orbx_matcher* m) {
     if (!m) return ORBX_ERR_INVALID;
     (void)hipSetDevice(m->prm.device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->have_bf) (void)hipEventSynchronize(m->bf_done);
+    if (m->bf_done) (void)hipEventDestroy(m->bf_done);
     m->d_in.release();
     m->d_out.release();
     m->d_aux.release();
@@ -762,12 +770,23 @@ orbx_status bf_run(orbx_matcher* m, const uint8_t* d_q, int nq, const uint8_t* d
     a.ndb = ndb;
     a.idx_base = idx_base;
     a.chunk = bf_chunk_rows(ndb, nq, m->ncu);
-    if (!m->d_bf.ensure(bf_partial_bytes(ndb, nq, a.chunk))) return ORBX_ERR_DEVICE;
+    const size_t need = bf_partial_bytes(ndb, nq, a.chunk);
+    // growing frees the scratch an earlier launch (any stream) may still use
+    if (need > m->d_bf.n && m->have_bf && !HIPOK(hipEventSynchronize(m->bf_done)))
+        return ORBX_ERR_DEVICE;
+    if (!m->d_bf.ensure(need)) return ORBX_ERR_DEVICE;
+    // the previous launch on another stream must be done with the scratch
+    if (m->have_bf && m->bf_stream != st && !HIPOK(hipStreamWaitEvent(st, m->bf_done, 0)))
+        return ORBX_ERR_DEVICE;
     a.part = m->d_bf.p;
     a.best_idx = bi;
     a.best_dist = bd;
     a.second_dist = sd;
-    return HIPOK(launch_bf_top2(a, st, &m->timer)) ? ORBX_OK : ORBX_ERR_DEVICE;
+    if (!HIPOK(launch_bf_top2(a, st, &m->timer)) || !HIPOK(hipEventRecord(m->bf_done, st)))
+        return ORBX_ERR_DEVICE;
+    m->bf_stream = st;
+    m->have_bf = true;
+    return ORBX_OK;
 }
 }  // namespace
 

@@ -57,35 +57,59 @@ def merge_shards(parts, n_total: int, world: int):
     return torch.cat([parts[r][:e - b] for r, (b, e) in enumerate(sizes)])
 
 
+class CandidateOverflow(RuntimeError):
+    """A rank found more relocalisation candidates than its block holds; `needed` is the
+    largest per-rank count (a block capacity that holds every rank's candidates)."""
+
+    def __init__(self, needed: int, cap: int):
+        super().__init__(f"{needed} relocalisation candidates on one rank, block capacity {cap}")
+        self.needed = needed
+        self.cap = cap
+
+
 def candidate_block(local_matches, local_counts, k0: int, cap: int = 64, min_matches: int = 15):
     """This rank's relocalisation candidates (keyframes with >= min_matches, Tracking.cc:1487)
-    as a fixed [cap, 1 + F] int32 block built on the device without a host round trip: row i =
-    (global keyframe id, its match list) for the i-th candidate in keyframe order, kf id -1
-    past the last one.  cap bounds the candidates per rank (a relocalisation keeps a handful)."""
+    as a fixed [1 + cap, 1 + F] int32 block built on the device without a host round trip.
+    Row 0 is a header: (the rank's true candidate count, cap, -1, ...); row 1 + i = (global
+    keyframe id, its match list) for the i-th candidate in keyframe order, kf id -1 past the
+    last one.  The reference keeps every candidate, so a count above cap is not truncated
+    silently: merge_candidate_blocks raises CandidateOverflow from the header, and
+    gather_candidate_matches then gathers again with a block that holds them all."""
     import torch
     dev = local_matches.device
     n, F = local_matches.shape
     mask = local_counts[:n] >= min_matches
     order = torch.argsort((~mask).to(torch.int8), stable=True)[:cap]   # candidates first
     k = min(cap, n)
-    block = torch.full((cap, 1 + F), -1, dtype=torch.int32, device=dev)
+    block = torch.full((1 + cap, 1 + F), -1, dtype=torch.int32, device=dev)
+    block[0, 0] = mask.sum().to(torch.int32)
+    block[0, 1] = cap
     if k:
         ids = torch.where(mask[order[:k]], order[:k].to(torch.int32) + k0,
                           torch.full((k,), -1, dtype=torch.int32, device=dev))
-        block[:k, 0] = ids
-        block[:k, 1:] = torch.where((ids >= 0)[:, None], local_matches[order[:k]].to(torch.int32),
-                                    torch.full((k, F), -1, dtype=torch.int32, device=dev))
+        block[1:1 + k, 0] = ids
+        block[1:1 + k, 1:] = torch.where((ids >= 0)[:, None],
+                                         local_matches[order[:k]].to(torch.int32),
+                                         torch.full((k, F), -1, dtype=torch.int32, device=dev))
     return block
 
 
 def merge_candidate_blocks(parts):
-    """[(kf_id, matches[F]), ...] in keyframe order from the all-gathered candidate blocks."""
+    """[(kf_id, matches[F]), ...] in keyframe order from the all-gathered candidate blocks.
+    Raises CandidateOverflow if any rank's header counts more candidates than its block
+    holds."""
     out = []
+    needed, cap = 0, None
     for blk in parts:
         b = blk.cpu().numpy() if hasattr(blk, "cpu") else np.asarray(blk)
-        for row in b:
+        cnt, bcap = int(b[0, 0]), int(b[0, 1])
+        if cnt > bcap:
+            needed, cap = max(needed, cnt), bcap
+        for row in b[1:]:
             if row[0] >= 0:
                 out.append((int(row[0]), row[1:]))
+    if cap is not None:
+        raise CandidateOverflow(needed, cap)
     out.sort(key=lambda t: t[0])
     return out
 
@@ -150,8 +174,8 @@ def gather_rows(local, n_total: int, world: int):
 
 def gather_candidate_blocks(local_matches, local_counts, k0: int, world: int, cap: int = 64,
                             min_matches: int = 15):
-    """All-gather every rank's candidate block (candidate_block): a [world, cap, 1 + F] device
-    tensor, built and exchanged with no host synchronisation (so it can sit inside a timed
+    """All-gather every rank's candidate block (candidate_block): world [1 + cap, 1 + F] device
+    tensors, built and exchanged with no host synchronisation (so it can sit inside a timed
     step); merge_candidate_blocks decodes it afterwards."""
     import torch
     import torch.distributed as dist
@@ -165,10 +189,17 @@ def gather_candidate_matches(local_matches, counts, n_total: int, world: int,
                              min_matches: int = 15, cap: int = 64):
     """The match lists of the relocalisation candidates collected from the ranks that own
     them: [(kf_id, matches[F]), ...] in keyframe order on every rank.  `counts` is this
-    rank's shard counts or the all-gathered [n_total] counts."""
+    rank's shard counts or the all-gathered [n_total] counts.  Every rank reads the same
+    gathered headers, so on an overflow all ranks gather again together, with a block sized to
+    the largest rank's count: no candidate is dropped (Tracking.cc:1479-1500 keeps them all)."""
     import torch.distributed as dist
     rank = dist.get_rank()
     b, e = shard_range(n_total, rank, world)
     local_counts = counts[b:e] if counts.shape[0] == n_total else counts
     parts = gather_candidate_blocks(local_matches, local_counts, b, world, cap, min_matches)
-    return merge_candidate_blocks(parts)
+    try:
+        return merge_candidate_blocks(parts)
+    except CandidateOverflow as ov:
+        parts = gather_candidate_blocks(local_matches, local_counts, b, world, ov.needed,
+                                        min_matches)
+        return merge_candidate_blocks(parts)

@@ -15,6 +15,8 @@ import numpy as np
 
 from ._lib import check, load, ptr
 
+ORBX_ERR_CAPACITY = -3
+
 
 class KfdbParams(ctypes.Structure):
     _fields_ = [("covisibles", ctypes.c_int32), ("device", ctypes.c_int32)]
@@ -76,11 +78,20 @@ class KeyFrameDatabase:
             self._h, int(slot), ptr(nb), len(nb)))
 
     def _result(self, fn, name, *args):
+        """Runs a detector into a buffer sized from the database; if keyframes were added
+        concurrently and the list outgrew it (ORBX_ERR_CAPACITY, *ncand = the true count), runs
+        it again with room for that count."""
         cap = max(len(self), 1)
-        out = np.zeros(cap, np.int32)
-        n = ctypes.c_int32(0)
-        check(name, fn(*args, ptr(out), cap, ctypes.byref(n)))
-        return out[:n.value].copy()
+        for _ in range(4):
+            out = np.zeros(cap, np.int32)
+            n = ctypes.c_int32(0)
+            code = fn(*args, ptr(out), cap, ctypes.byref(n))
+            if code == ORBX_ERR_CAPACITY and n.value > cap:
+                cap = max(n.value, len(self), 1)
+                continue
+            check(name, code)
+            return out[:n.value].copy()
+        check(name, code)
 
     def DetectRelocalizationCandidates(self, bow) -> np.ndarray:
         """KeyFrameDatabase::DetectRelocalizationCandidates (:220-337): candidate slots."""

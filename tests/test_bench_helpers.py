@@ -29,25 +29,44 @@ def test_headline_traffic_matches_committed_pmc():
     b = _bench()
     line = json.load(open(_latest("r[0-9][0-9]_v*_bench.json")))
     roof = line["roofline"]
-    t = b.traffic_from_csv(b.DEFAULT_PMC, roof["kernel"])
+    if "launches_per_step" not in roof:
+        pytest.skip("headline line predates the per-step roofline (round 4)")
+    # the PMC passes count one-stream dispatches; the entry is per launch of the timed schedule
+    t = b.traffic_per_step(b.DEFAULT_PMC, roof["kernel"])
     assert t is not None and t > 0
-    assert t == pytest.approx(roof["traffic"], rel=1e-9)
+    assert t / roof["launches_per_step"] == pytest.approx(roof["traffic"], rel=1e-9)
     # the algorithmic bytes and the achieved rate are consistent with the launch time
     assert roof["achieved"] == pytest.approx(
         roof["algorithmic_bytes_per_launch"] / (roof["avg_launch_ms"] / 1000.0) / 1e9, rel=1e-9)
     assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-9)
 
 
-def test_per_kernel_entries():
+def test_roofline_entries_per_launch():
+    """Per-step algorithmic bytes and traffic divide by the launches per step of the run the
+    entry times: k_fast launched twice per step (the side branch) gets half a step's bytes per
+    launch."""
     b = _bench()
-    prof = {"k_level": (16.0, 160), "k_fast": (10.0, 20), "k_missing": (1.0, 0)}
-    geo = {"k_level": 3.0e8, "k_fast": 7.0e8}
-    out = b.per_kernel_hbm(prof, geo, b.DEFAULT_PMC, 20)
-    assert set(out) == {"k_level", "k_fast"}
-    assert out["k_level"]["launches_per_step"] == 8
-    assert out["k_level"]["avg_launch_ms"] == pytest.approx(0.1)
-    assert out["k_level"]["achieved"] == pytest.approx(3.0e8 / 1e-4 / 1e9)
-    assert out["k_fast"]["frac"] == pytest.approx(out["k_fast"]["achieved"] / b.HBM_PEAK_GBS)
+    e = b.roofline_entry("k_level", 16.0, 160, 20, 2.4e9, None)
+    assert e["launches_per_step"] == 8
+    assert e["avg_launch_ms"] == pytest.approx(0.1)
+    assert e["algorithmic_bytes_per_launch"] == pytest.approx(3.0e8)
+    assert e["achieved"] == pytest.approx(3.0e8 / 1e-4 / 1e9)
+    e = b.roofline_entry("k_fast", 10.0, 40, 20, 7.0e8, 1.4e9)
+    assert e["launches_per_step"] == 2
+    assert e["algorithmic_bytes_per_launch"] == pytest.approx(3.5e8)
+    assert e["traffic"] == pytest.approx(7.0e8)
+    assert e["frac"] == pytest.approx(e["achieved"] / b.HBM_PEAK_GBS)
+
+
+def test_headline_picks_largest_one_stream_group():
+    """roofline.kernel is the kernel group with the most one-stream time per step (VERDICT r3:
+    k_fast, not the hard-coded k_level); k_level splits into level 0 and levels 1-7."""
+    b = _bench()
+    sprof = {"k_level": (30.0, 160), "k_level0": (5.0, 20), "k_fast": (28.0, 20),
+             "k_octree": (6.0, 20), "k_orient_desc": (22.0, 20), "k_stereo": (5.0, 20)}
+    g = b.split_level(sprof)
+    assert g["k_level1_7"] == (25.0, 140)
+    assert b.pick_dominant(g, 20) == "k_fast"
 
 
 def test_traffic_needs_both_passes(tmp_path):
@@ -84,9 +103,8 @@ def test_counted_bytes_capped_by_traffic():
     assert b.counted_bytes(4.95e9, 3.07e9) == 3.07e9
     assert b.counted_bytes(6.1e8, 6.2e8) == 6.1e8
     assert b.counted_bytes(6.1e8, None) == 6.1e8
-    prof = {"k_orient_desc": (13.6, 10)}
-    out = b.per_kernel_hbm(prof, {"k_orient_desc": 1e12}, b.DEFAULT_PMC, 10)
-    e = out["k_orient_desc"]
+    e = b.roofline_entry("k_orient_desc", 13.6, 10, 10, 1e12,
+                         b.traffic_per_step(b.DEFAULT_PMC, "k_orient_desc"))
     assert e["algorithmic_bytes_per_launch"] == e["traffic"] < e["requested_bytes_per_launch"]
 
 
@@ -137,7 +155,10 @@ def test_headline_valu_entry_matches_committed_pmc():
     roof = json.load(open(_latest("r[0-9][0-9]_v*_bench.json")))["roofline"]
     if "valu" not in roof:
         pytest.skip("headline line predates the VALU entry")
-    v = b.valu_from_csv(b.DEFAULT_INSTS, roof["kernel"])
+    if "launches_per_step" not in roof:
+        pytest.skip("headline line predates the per-step roofline (round 4)")
+    v = b.valu_from_csv(b.DEFAULT_INSTS, roof["kernel"]) * \
+        b.ONE_STREAM_LAUNCHES.get(roof["kernel"], 1) / roof["launches_per_step"]
     assert roof["valu"]["wave_instr_per_launch"] == pytest.approx(v)
     assert roof["valu"]["issue_rate"] == pytest.approx(v / (roof["avg_launch_ms"] / 1000.0) / 1e12)
     assert 0 < roof["valu"]["busy_frac"] <= 1.0

@@ -8,9 +8,10 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from my_orb_slam2_amd.distributed import (all_gather_counts, broadcast_query,
-                                          gather_candidate_matches, gather_rows,
-                                          relocalisation_candidates, shard_range)
+from my_orb_slam2_amd.distributed import (CandidateOverflow, all_gather_counts, broadcast_query,
+                                          candidate_block, gather_candidate_matches, gather_rows,
+                                          merge_candidate_blocks, relocalisation_candidates,
+                                          shard_range)
 
 
 @pytest.mark.parametrize("n,world", [(10000, 8), (7, 3), (3, 4), (0, 2), (512, 8)])
@@ -42,8 +43,12 @@ def _worker(rank, world, port, n_total, q):
         rows = torch.where(feat < 4, (kf * 7 + feat) % 11, torch.full_like(kf * feat, -1))
         everything = gather_rows(rows, n_total, world)
         cand = gather_candidate_matches(rows, allc, n_total, world)
+        # a block of 1 candidate per rank overflows (each rank owns 4-5 candidates): both ranks
+        # read the headers and gather again with room for all of them
+        cand_small = gather_candidate_matches(rows, allc, n_total, world, cap=1)
         q.put((rank, desc.sum().item(), allc.numpy().tolist(), everything.numpy().tolist(),
-               [(k, np.asarray(m).tolist()) for k, m in cand]))
+               [(k, np.asarray(m).tolist()) for k, m in cand],
+               [(k, np.asarray(m).tolist()) for k, m in cand_small]))
     finally:
         dist.destroy_process_group()
 
@@ -64,10 +69,30 @@ def test_gloo_broadcast_and_gather():
     F = 6
     rows = [[(k * 7 + f) % 11 if f < 4 else -1 for f in range(F)] for k in range(n_total)]
     want_cand = [(k, rows[k]) for k in range(n_total) if k % 20 >= 15]
-    for rank, s, allc, everything, cand in res:
+    for rank, s, allc, everything, cand, cand_small in res:
         assert s == int(np.arange(160).sum())
         assert allc == expect
         assert everything == rows
         assert cand == want_cand
+        assert cand_small == want_cand
     cand = relocalisation_candidates(np.array(expect))
     np.testing.assert_array_equal(cand, [i for i in range(n_total) if i % 20 >= 15])
+
+
+def test_candidate_block_reports_overflow():
+    """A rank with more candidates than its block holds is reported, not truncated (ADVICE r3:
+    Tracking::Relocalization keeps every keyframe with >= 15 matches, Tracking.cc:1487)."""
+    n, F = 40, 3
+    counts = torch.tensor([20 if k % 3 == 0 else 3 for k in range(n)], dtype=torch.int32)
+    rows = torch.arange(n * F, dtype=torch.int32).reshape(n, F)
+    want = [k for k in range(n) if k % 3 == 0]            # 14 candidates
+    blk = candidate_block(rows, counts, 100, cap=len(want))
+    got = merge_candidate_blocks([blk])
+    assert [k for k, _ in got] == [100 + k for k in want]
+    for k, m in got:
+        np.testing.assert_array_equal(m, rows[k - 100].numpy())
+    with pytest.raises(CandidateOverflow) as ei:
+        merge_candidate_blocks([candidate_block(rows, counts, 100, cap=5), blk])
+    assert ei.value.needed == len(want) and ei.value.cap == 5
+    # no candidate at all: an empty list, header count 0
+    assert merge_candidate_blocks([candidate_block(rows, counts * 0, 0, cap=4)]) == []

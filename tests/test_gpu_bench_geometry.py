@@ -82,6 +82,45 @@ def test_c2_stereo_b512(oracle_mod, orbx_lib, gpu):
         assert nvh[i] == n_o
 
 
+def test_c2_timed_schedule_b512(oracle_mod, orbx_lib, gpu):
+    """The headline's exact timed configuration (bench.headline_handles, as bench.py builds
+    it): two StereoBatch handles of 512 pairs alternating steps on two torch streams, each
+    extraction with the side branch 3,3,1, six steps.  Every slot of both handles equals the
+    single-handle one-stream run (overlap 0) of the same pairs, and 16 slots equal the CPU
+    restatement (ORBextractor.cc:1065-1154, Frame.cc:496-686)."""
+    import torch
+    import my_orb_slam2_amd as m
+    B = 512
+    Lh, Rh, pairs, _ = bench.stereo_inputs(0, B, 32)
+    Ls, Rs = torch.from_numpy(Lh).to(gpu), torch.from_numpy(Rh).to(gpu)
+    mb = float(np.float32(bench.MBF) / np.float32(bench.FX))
+    sbs, sts, run_on, run_step, overlap = bench.headline_handles(
+        torch, m, gpu, 0, B, Ls, Rs, 2, "3,3,1", True, mb)
+    assert overlap == (3, 3, 1)
+    for i in range(6):
+        run_step(i)
+    torch.cuda.synchronize()
+    got = [bench.stereo_digests(h) for h in sbs]
+    # the reference schedule: one handle, every kernel in sequence on one stream
+    sbs[0].ext.set_overlap(0)
+    run_on(sbs[0], sts[0])
+    torch.cuda.synchronize()
+    ref = bench.stereo_digests(sbs[0])
+    for k in range(2):
+        bad = [i for i in range(B) if got[k][i] != ref[i]]
+        assert not bad, f"handle {k}: slots {bad[:8]} differ from the one-stream run"
+    v = bench.verification(got, ref, B)
+    assert v["verified"] and v["mismatched_slots"] == 0
+    for i in np.linspace(0, B - 1, 16).astype(int):
+        ol = oracle_mod.OracleExtractor(bench.NFEAT, 1.2, 8, 20, 7)
+        orr = oracle_mod.OracleExtractor(bench.NFEAT, 1.2, 8, 20, 7)
+        k_o, d_o = ol(Lh[i])
+        kr_o, dr_o = orr(Rh[i])
+        u_o, z_o, n_o = oracle_mod.stereo_match(ol, orr, len(k_o), bench.MBF, mb)
+        assert bench.slot_digest(k_o, d_o, kr_o, dr_o, u_o, z_o, n_o) == got[1][i], \
+            f"slot {i} differs from the oracle"
+
+
 def test_c3_euroc_b256(oracle_mod, orbx_lib, gpu):
     import torch
     from oracle import matcher as om

@@ -118,3 +118,53 @@ def test_concurrent_dropin_threads(orbx_lib, gpu):
         for j in range(len(nkp)):
             assert_kps_equal(kps[j, :nkp[j]], ref_batch[1][j, :nkp[j]], f"batch image {j}")
             assert_bytes_equal(desc[j, :nkp[j]], ref_batch[2][j, :nkp[j]], f"batch image {j}")
+
+
+def test_batch_fetch_races_extract(orbx_lib, gpu):
+    """orbx_batch_fetch / orbx_batch_view_get on one thread while another thread keeps
+    extracting batches on the same handle (on a torch stream): the handle's lock and done event
+    order them, so every fetch returns one whole extraction, batch A's or batch B's, never a mix
+    (include/orbx.h: calls on one handle may come from any thread)."""
+    import torch
+    import my_orb_slam2_amd as m
+    imgs = [torch.from_numpy(np.stack([synth.frame(760 + 10 * k + i, 640, 480) for i in range(6)]))
+            .to(gpu) for k in range(2)]
+    ext = m.ORBextractor(1000, 1.2, 8, 20, 7, max_batch=6)
+    stream = torch.cuda.Stream(gpu)
+    refs = []
+    for b in imgs:
+        ext.extract_batch_device(b, stream.cuda_stream)
+        refs.append(ext.batch_fetch())
+    assert not np.array_equal(refs[0][2], refs[1][2])
+    errors, fetched = [], []
+    stop = threading.Event()
+
+    def extractor_thread():
+        try:
+            i = 0
+            while not stop.is_set():
+                ext.extract_batch_device(imgs[i % 2], stream.cuda_stream)
+                i += 1
+        except Exception as e:   # pragma: no cover
+            errors.append(e)
+
+    t = threading.Thread(target=extractor_thread)
+    t.start()
+    try:
+        for _ in range(40):
+            v = ext.batch_view()
+            assert v.batch == 6 and v.kp_cap == refs[0][1].shape[1]
+            fetched.append(ext.batch_fetch())
+    finally:
+        stop.set()
+        t.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    seen = set()
+    for nkp, kps, desc in fetched:
+        which = [k for k, r in enumerate(refs) if np.array_equal(nkp, r[0]) and
+                 all(np.array_equal(desc[j, :nkp[j]], r[2][j, :nkp[j]]) and
+                     np.array_equal(kps[j, :nkp[j]].view(np.uint8), r[1][j, :nkp[j]].view(np.uint8))
+                     for j in range(len(nkp)))]
+        assert which, "a fetch mixed two extractions"
+        seen.add(which[0])
