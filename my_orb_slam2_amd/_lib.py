@@ -137,6 +137,8 @@ SIGNATURES = {
     "orbx_undistort_keypoints_batch_device": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i, _vp, _vp]),
     "orbx_cvt_color": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _i]),
     "orbx_cvt_color_device": (_i, [_vp, _i, _i, _sz, _i, _i, _vp, _sz, _vp]),
+    "orbx_is_in_frustum_batch_device": (_i, [_vp, _i, _vp, _vp, _i, _vp, _f, _f, _vp, _vp, _vp]),
+    "orbx_is_in_frustum": (_i, [_vp, _vp, _i, _vp, _f, _f, _vp, _vp, _i]),
 }
 
 _lib = None

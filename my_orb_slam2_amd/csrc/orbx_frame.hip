@@ -6,6 +6,8 @@
 //                  cell of every keypoint (PosInGrid, std::round half away from zero in
 //                  float), per-cell LDS counts, a block scan over the 3072 cells, an atomic
 //                  fill, then each cell sorted by feature index (the push_back order)
+//   k_frustum      one lane per (frame, local MapPoint): Frame::isInFrustum + PredictScale, the
+//                  SearchByProjection query of every MapPoint in view (SearchLocalPoints)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -15,6 +17,7 @@
 #include "../../include/orbx_frame.h"
 #include "orbx_device.h"
 #include "orbx_host.h"
+#include "orbx_math.h"
 
 using namespace orbx;
 
@@ -176,6 +179,93 @@ __global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ src, i
     }
     uint8_t* d = dst + (size_t)y * dstride + x0;
     for (int j = 0; j < nx; ++j) d[j] = (uint8_t)(out >> (8 * j));
+}
+
+// Frame::isInFrustum (src/Frame.cc:285-349) with MapPoint::PredictScale (MapPoint.cc:430-444)
+// and the query SearchByProjection(Frame&, vpMapPoints, th) forms from its outputs
+// (ORBmatcher.cc:55-80).  The float / double steps follow the reference's types (see
+// include/orbx_frame.h); the library is built with -ffp-contract=off, so every float op is
+// rounded on its own as on x86.
+__device__ __forceinline__ bool frustum_query(const orbx_frame_pose& F, const orbx_map_point& M,
+                                              float cos_lim, float th, orbx_proj_query& q) {
+    // Pc = mRcw*P + mtcw: cv::gemm(Rcw, P, 1, tcw, 1) small-matrix path (len 3, one column):
+    // t_r = a_r0*b0 + a_r1*b1 + a_r2*b2 in float, d_r = (float)(t_r*1.0 + c_r*1.0)
+    float Pc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float t = __fmul_rn(F.Rcw[3 * r], M.pos[0]);
+        t = __fadd_rn(t, __fmul_rn(F.Rcw[3 * r + 1], M.pos[1]));
+        t = __fadd_rn(t, __fmul_rn(F.Rcw[3 * r + 2], M.pos[2]));
+        Pc[r] = (float)((double)t + (double)F.tcw[r]);
+    }
+    if (Pc[2] < 0.0f) return false;                       // positive depth
+    const float invz = __fdiv_rn(1.0f, Pc[2]);
+    const float u = __fadd_rn(__fmul_rn(__fmul_rn(F.fx, Pc[0]), invz), F.cx);
+    const float v = __fadd_rn(__fmul_rn(__fmul_rn(F.fy, Pc[1]), invz), F.cy);
+    if (u < F.min_x || u > F.max_x) return false;
+    if (v < F.min_y || v > F.max_y) return false;
+    const float maxD = __fmul_rn(1.2f, M.max_dist), minD = __fmul_rn(0.8f, M.min_dist);
+    // PO = P - mOw; dist = cv::norm(PO): squares accumulated in double (normL2Sqr<float,
+    // double>), sqrt, stored in a float
+    const float PO[3] = {__fsub_rn(M.pos[0], F.Ow[0]), __fsub_rn(M.pos[1], F.Ow[1]),
+                         __fsub_rn(M.pos[2], F.Ow[2])};
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ss = __dadd_rn(ss, __dmul_rn((double)PO[k], (double)PO[k]));
+    const float dist = (float)__dsqrt_rn(ss);
+    if (dist < minD || dist > maxD) return false;
+    // viewCos = PO.dot(Pn) / dist: Mat::dot in double (dotProd_), / dist in double
+    double dot = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dot = __dadd_rn(dot, __dmul_rn((double)PO[k], (double)M.normal[k]));
+    const float viewCos = (float)__ddiv_rn(dot, (double)dist);
+    if (viewCos < cos_lim) return false;
+    // PredictScale: ceil(log(ratio) / mfLogScaleFactor) on floats (std::log / std::ceil)
+    const float ratio = __fdiv_rn(M.max_dist, dist);
+    const float qf = ceilf(__fdiv_rn(glibc_logf(ratio), F.log_scale_factor));
+    // (int) of a float as x86 cvttss2si: INT_MIN when out of range or NaN
+    int lvl = (qf >= -2147483648.0f && qf < 2147483648.0f) ? (int)qf : INT_MIN;
+    if (lvl < 0) lvl = 0;
+    else if (lvl >= F.nlevels) lvl = F.nlevels - 1;
+    // SearchByProjection: r = RadiusByViewingCos (viewCos > 0.998 in double), * th if th != 1
+    float r = (double)viewCos > 0.998 ? 2.5f : 4.0f;
+    if ((double)th != 1.0) r = __fmul_rn(r, th);
+    q.u = u;
+    q.v = v;
+    q.ur = __fsub_rn(u, __fmul_rn(F.mbf, invz));        // mTrackProjXR
+    q.radius = __fmul_rn(r, F.scale[lvl]);
+    q.min_level = lvl - 1;
+    q.max_level = lvl;
+    q.pred_level = lvl;
+    q.angle = 0.0f;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_frustum(const orbx_frame_pose* __restrict__ frames,
+                                                 const orbx_map_point* __restrict__ mps,
+                                                 const int32_t* __restrict__ mp_off,
+                                                 const uint8_t* __restrict__ skip, float cos_lim,
+                                                 float th, orbx_proj_query* __restrict__ q,
+                                                 int32_t* __restrict__ nvisible) {
+    const int f = blockIdx.y;
+    const int b = mp_off[f], e = mp_off[f + 1];
+    const int i = b + blockIdx.x * 256 + threadIdx.x;
+    bool vis = false;
+    if (i < e) {
+        orbx_proj_query out;
+        vis = (!skip || !skip[i]) && frustum_query(frames[f], mps[i], cos_lim, th, out);
+        if (!vis) {
+            out.u = out.v = out.ur = 0.0f;
+            out.radius = -1.0f;
+            out.min_level = out.max_level = out.pred_level = -1;
+            out.angle = 0.0f;
+        }
+        q[i] = out;
+    }
+    if (nvisible) {
+        const uint64_t m = __ballot(vis);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nvisible[f], (int)__popcll(m));
+    }
 }
 
 // Device staging of the host-array entry points: a pool of (device, non-blocking stream,
@@ -365,6 +455,67 @@ orbx_status orbx_undistort_keypoints_batch_device(const float* K4, const float* 
     hipLaunchKernelGGL(k_undistort_batch, dim3((kp_stride + 255) / 256, batch), dim3(256), 0,
                        (hipStream_t)stream, P, d_kps, kp_stride, d_n, d_kps_un, copy);
     return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_is_in_frustum_batch_device(const orbx_frame_pose* d_frames, int32_t nframes,
+                                            const orbx_map_point* d_mps,
+                                            const int32_t* d_mp_off, int32_t max_mps,
+                                            const uint8_t* d_skip, float viewing_cos_limit,
+                                            float th, orbx_proj_query* d_q,
+                                            int32_t* d_nvisible, void* stream) {
+    if (nframes < 0 || max_mps < 0 || nframes > 65535) return ORBX_ERR_INVALID;
+    if (nframes == 0) return ORBX_OK;
+    if (!d_frames || !d_mp_off || (max_mps > 0 && (!d_mps || !d_q))) return ORBX_ERR_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    if (d_nvisible && !HIPOK(hipMemsetAsync(d_nvisible, 0, 4 * (size_t)nframes, st)))
+        return ORBX_ERR_DEVICE;
+    if (max_mps == 0) return ORBX_OK;
+    hipLaunchKernelGGL(k_frustum, dim3((max_mps + 255) / 256, nframes), dim3(256), 0, st,
+                       d_frames, d_mps, d_mp_off, d_skip, viewing_cos_limit, th, d_q, d_nvisible);
+    return HIPOK(hipGetLastError()) ? ORBX_OK : ORBX_ERR_DEVICE;
+}
+
+orbx_status orbx_is_in_frustum(const orbx_frame_pose* frame, const orbx_map_point* mps,
+                               int32_t n, const uint8_t* skip, float viewing_cos_limit,
+                               float th, orbx_proj_query* q, int32_t* nvisible, int device) {
+    if (!frame || n < 0 || (n > 0 && (!mps || !q)) || frame->nlevels < 1 || frame->nlevels > 16)
+        return ORBX_ERR_INVALID;
+    if (n == 0) {
+        if (nvisible) *nvisible = 0;
+        return ORBX_OK;
+    }
+    if (!HIPOK(hipSetDevice(device))) return ORBX_ERR_DEVICE;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_f = 0, o_off = al(sizeof(orbx_frame_pose)), o_cnt = o_off + 256,
+                 o_mp = o_cnt + 256, o_sk = o_mp + al(sizeof(orbx_map_point) * (size_t)n),
+                 o_q = o_sk + al((size_t)n), end = o_q + sizeof(orbx_proj_query) * (size_t)n;
+    ScratchLease L(device);
+    if (!L.s || !L.s->buf.ensure(end)) return ORBX_ERR_DEVICE;
+    hipStream_t st = L.s->st;
+    uint8_t* d = L.s->buf.as<uint8_t>();
+    const int32_t off[2] = {0, n};
+    int32_t cnt = 0;
+    orbx_status s = ORBX_OK;
+    if (!HIPOK(hipMemcpyAsync(d + o_f, frame, sizeof(*frame), hipMemcpyHostToDevice, st)) ||
+        !HIPOK(hipMemcpyAsync(d + o_off, off, sizeof(off), hipMemcpyHostToDevice, st)) ||
+        !HIPOK(hipMemcpyAsync(d + o_mp, mps, sizeof(orbx_map_point) * (size_t)n,
+                              hipMemcpyHostToDevice, st)) ||
+        (skip && !HIPOK(hipMemcpyAsync(d + o_sk, skip, (size_t)n, hipMemcpyHostToDevice, st))))
+        s = ORBX_ERR_DEVICE;
+    if (s == ORBX_OK)
+        s = orbx_is_in_frustum_batch_device((const orbx_frame_pose*)(d + o_f), 1,
+                                            (const orbx_map_point*)(d + o_mp),
+                                            (const int32_t*)(d + o_off), n,
+                                            skip ? d + o_sk : nullptr, viewing_cos_limit, th,
+                                            (orbx_proj_query*)(d + o_q), (int32_t*)(d + o_cnt), st);
+    if (s == ORBX_OK &&
+        (!HIPOK(hipMemcpyAsync(q, d + o_q, sizeof(orbx_proj_query) * (size_t)n,
+                               hipMemcpyDeviceToHost, st)) ||
+         !HIPOK(hipMemcpyAsync(&cnt, d + o_cnt, 4, hipMemcpyDeviceToHost, st))))
+        s = ORBX_ERR_DEVICE;
+    if (!HIPOK(hipStreamSynchronize(st))) s = ORBX_ERR_DEVICE;
+    if (s == ORBX_OK && nvisible) *nvisible = cnt;
+    return s;
 }
 
 }  // extern "C"

@@ -178,4 +178,61 @@ ORBX_HD float cv_fast_atan2(float y, float x) {
     return a;
 }
 
+// logf: glibc 2.35 sysdeps/ieee754/flt-32 (e_logf.c, e_logf_data.c; LOGF_TABLE_BITS 4,
+// LOGF_POLY_ORDER 4): log(x) = log1p(z/c - 1) + log(c) + k ln2 in double, one rounding to
+// float.  MapPoint::PredictScale (src/MapPoint.cc:430-444) and Frame's mfLogScaleFactor
+// (src/Frame.cc:82) call std::log on floats (TemplatedVocabulary.h:36 puts `using namespace
+// std` in scope), i.e. logf.  This port equals the host glibc logf for every positive normal
+// float, both with the polynomial's a*b+c contracted into fma (the __logf_fma ifunc variant)
+// and without (tests/native/libm_port_check.cpp checks every one).
+struct LogfEntry { double invc, logc; };
+ORBX_HD LogfEntry logf_tab(int i) {
+    switch (i) {
+        case 0: return {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2};
+        case 1: return {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2};
+        case 2: return {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2};
+        case 3: return {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3};
+        case 4: return {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3};
+        case 5: return {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3};
+        case 6: return {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4};
+        case 7: return {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4};
+        case 8: return {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5};
+        case 9: return {0x1p+0, 0x0p+0};
+        case 10: return {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5};
+        case 11: return {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4};
+        case 12: return {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3};
+        case 13: return {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3};
+        case 14: return {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2};
+        default: return {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2};
+    }
+}
+
+ORBX_HD float glibc_logf(float x) {
+    uint32_t ix = f2u(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        // x < 0x1p-126, inf or nan
+        if (ix * 2 == 0) return -INFINITY;                 // log(+-0)
+        if (ix == 0x7f800000u) return x;                   // log(inf)
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return NAN;   // x < 0 or nan
+        ix = f2u(x * 0x1p23f);                             // subnormal: normalize
+        ix -= 23u << 23;
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> (23 - 4)) % 16);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    const LogfEntry e = logf_tab(i);
+    const double z = (double)u2f(iz);
+    const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+    const double Ln2 = 0x1.62e42fefa39efp-1;
+    const double r = z * e.invc - 1;
+    const double y0 = e.logc + (double)k * Ln2;
+    const double r2 = r * r;
+    double y = A1 * r + A2;
+    y = A0 * r2 + y;
+    y = y * r2 + (y0 + r);
+    return (float)y;
+}
+
 }  // namespace orbx

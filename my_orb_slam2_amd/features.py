@@ -244,3 +244,68 @@ def cvt_color_gray(img: np.ndarray, rgb: bool = False, device: int = 0) -> np.nd
     check("orbx_cvt_color", load().orbx_cvt_color(ptr(src), w, h, w * c, c, int(rgb), ptr(out),
                                                    w, device))
     return out
+
+
+# ---- Frame::isInFrustum + MapPoint::PredictScale (include/orbx_frame.h) ---------------------
+
+# orbx_map_point: GetWorldPos, mfMinDistance, GetNormal, mfMaxDistance (32 bytes)
+MAP_POINT_DTYPE = np.dtype([("pos", "<f4", 3), ("min_dist", "<f4"), ("normal", "<f4", 3),
+                            ("max_dist", "<f4")])
+# orbx_frame_pose: mRcw (row-major), mtcw, mOw, fx fy cx cy mbf, image bounds,
+# mfLogScaleFactor, mnScaleLevels, mvScaleFactors
+FRAME_POSE_DTYPE = np.dtype([("Rcw", "<f4", 9), ("tcw", "<f4", 3), ("Ow", "<f4", 3),
+                             ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                             ("mbf", "<f4"), ("min_x", "<f4"), ("max_x", "<f4"),
+                             ("min_y", "<f4"), ("max_y", "<f4"), ("log_scale_factor", "<f4"),
+                             ("nlevels", "<i4"), ("scale", "<f4", 16)])
+
+
+def frame_pose(Rcw, tcw, K4, bounds, scale_factors, mbf: float = 0.0,
+               scale_factor: float = 1.2) -> np.ndarray:
+    """One orbx_frame_pose record from a pose (Rcw, tcw): Ow = -Rcw^T tcw (the Frame's mOw,
+    Frame::UpdatePoseMatrices, Frame.cc:271-278; the caller passes its own mOw, so only its
+    value matters here), mfLogScaleFactor = logf(mfScaleFactor) (Frame.cc:82; for 1.2f the
+    double log rounded to float is glibc's logf value, tests/test_frustum.py)."""
+    import math
+    f = np.zeros((), FRAME_POSE_DTYPE)
+    R = np.asarray(Rcw, np.float32).reshape(3, 3)
+    t = np.asarray(tcw, np.float32).reshape(3)
+    f["Rcw"] = R.reshape(9)
+    f["tcw"] = t
+    f["Ow"] = (-(R.astype(np.float64).T @ t.astype(np.float64))).astype(np.float32)
+    f["fx"], f["fy"], f["cx"], f["cy"] = (np.float32(v) for v in np.asarray(K4, np.float32))
+    f["mbf"] = np.float32(mbf)
+    f["min_x"], f["max_x"], f["min_y"], f["max_y"] = (np.float32(b) for b in bounds)
+    sc = np.asarray(scale_factors, np.float32)
+    f["nlevels"] = len(sc)
+    f["scale"][:len(sc)] = sc
+    f["log_scale_factor"] = np.float32(math.log(float(np.float32(scale_factor))))
+    return f
+
+
+def is_in_frustum(frame: np.ndarray, mps: np.ndarray, skip=None, viewing_cos_limit: float = 0.5,
+                  th: float = 1.0, device: int = 0):
+    """Tracking::SearchLocalPoints' projection of one frame's local map on the GPU
+    (Frame::isInFrustum + PredictScale, Frame.cc:285-349, MapPoint.cc:430-444): returns the
+    SearchByProjection queries (PROJ_QUERY_DTYPE, radius -1 = not in view) and nToMatch."""
+    from ._lib import check, load, ptr
+    fr = np.ascontiguousarray(frame, FRAME_POSE_DTYPE).reshape(())
+    m = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+    q = np.zeros(len(m), PROJ_QUERY_DTYPE)
+    nv = ctypes.c_int32(0)
+    check("orbx_is_in_frustum", load().orbx_is_in_frustum(
+        ptr(fr), ptr(m), len(m), ptr(sk), float(viewing_cos_limit), float(th), ptr(q),
+        ctypes.byref(nv), device))
+    return q, nv.value
+
+
+def is_in_frustum_batch_device(d_frames, nframes: int, d_mps, d_mp_off, max_mps: int, d_skip,
+                               d_q, d_nvisible=None, viewing_cos_limit: float = 0.5,
+                               th: float = 1.0, stream: int = 0):
+    """The same for `nframes` frames on device arrays (torch tensors): frame f's MapPoints at
+    [d_mp_off[f], d_mp_off[f+1]) of d_mps, queries into d_q at the same indices."""
+    from ._lib import check, load, ptr
+    check("orbx_is_in_frustum_batch_device", load().orbx_is_in_frustum_batch_device(
+        ptr(d_frames), int(nframes), ptr(d_mps), ptr(d_mp_off), int(max_mps), ptr(d_skip),
+        float(viewing_cos_limit), float(th), ptr(d_q), ptr(d_nvisible), ctypes.c_void_p(stream)))

@@ -272,6 +272,83 @@ def local_map_queries(seed: int, keys_un, desc, n_queries: int, width: int = 752
     return q, np.ascontiguousarray(d[perm])
 
 
+def local_map_points(seed: int, keys_un, desc, n_points: int, K4, bounds, width: int = 752,
+                     height: int = 480, th: float = 1.0, inlier_frac: float = 0.6,
+                     outside_frac: float = 0.12, nlevels: int = 8, scale_factor: float = 1.2,
+                     max_flip: int = 24, skip_frac: float = 0.05, mbf: float = 0.0):
+    """A 3-D local map for one frame (Tracking::SearchLocalPoints inputs, Tracking.cc:1297-1347,
+    before isInFrustum): a camera pose and `n_points` MapPoints (orbx_map_point records) with
+    descriptors.  `inlier_frac` of them are observations of the frame's own features: they
+    project within ~1 px of the feature, with a descriptor 0..max_flip bits away and a
+    mfMaxDistance that puts PredictScale at the feature's octave +-1; the rest land anywhere in
+    the image with random descriptors; `outside_frac` fail one of isInFrustum's tests (behind
+    the camera, outside the image bounds, outside the scale-invariance distances, viewing
+    angle above 60 degrees).  Normals are the viewing direction turned by up to 40 degrees (a
+    tenth of them exactly the viewing direction: RadiusByViewingCos 2.5).  `skip_frac` of the
+    MapPoints are flagged as already matched in the frame (mnLastFrameSeen).  Returns
+    (frame_pose record, map points, descriptors [n, 32], skip mask)."""
+    from .features import MAP_POINT_DTYPE, frame_pose
+    rng = np.random.default_rng(seed)
+    scale, _, _ = scale_tables(nlevels, scale_factor)
+    fx, fy, cx, cy = (float(v) for v in K4)
+    Rcw = _rot(rng, 20.0)
+    tcw = rng.normal(0, 1.0, 3)
+    pose = frame_pose(Rcw, tcw, K4, bounds, scale, mbf=mbf, scale_factor=scale_factor)
+    R = Rcw.astype(np.float64)
+    n = len(keys_un)
+    nin = min(n, int(round(inlier_frac * n_points)))
+    src = rng.choice(n, nin, replace=False) if nin else np.zeros(0, np.int64)
+    u = rng.uniform(bounds[0] + 1, bounds[1] - 1, n_points)
+    v = rng.uniform(bounds[2] + 1, bounds[3] - 1, n_points)
+    u[:nin] = keys_un["x"][src] + rng.normal(0, 0.7, nin)
+    v[:nin] = keys_un["y"][src] + rng.normal(0, 0.7, nin)
+    lvl = rng.integers(0, nlevels, n_points)
+    lvl[:nin] = np.clip(keys_un["octave"][src] + rng.integers(-1, 2, nin), 0, nlevels - 1)
+    Z = rng.uniform(2.0, 30.0, n_points)
+    Pc = np.stack([(u - cx) / fx * Z, (v - cy) / fy * Z, Z], 1)
+    P = (Pc - tcw[None, :]) @ R                      # Rcw^T (Pc - tcw), row vectors
+    Ow = -(R.T @ tcw)
+    PO = P - Ow[None, :]
+    dist = np.linalg.norm(PO, axis=1)
+    # PredictScale = ceil(log(maxD / dist) / log(1.2)) = lvl: maxD = dist * 1.2^(lvl - 0.5)
+    maxd = dist * float(scale_factor) ** (lvl - 0.5)
+    mind = maxd / float(scale[nlevels - 1])
+    # normals: the viewing direction turned by up to 40 degrees
+    dirn = PO / dist[:, None]
+    nrm = np.empty_like(dirn)
+    for i in range(n_points):
+        nrm[i] = _rot(rng, 40.0) @ dirn[i] if rng.random() > 0.1 else dirn[i]
+    # failures of isInFrustum's tests
+    kind = np.where(rng.random(n_points) < outside_frac, rng.integers(0, 5, n_points), -1)
+    kind[:nin] = -1
+    beh = kind == 0                                    # behind the camera
+    P[beh] = ((Pc[beh] * np.array([1, 1, -1.0])) - tcw) @ R
+    side = kind == 1                                   # outside the image bounds
+    P[side] = ((np.stack([(u[side] - cx + width) / fx * Z[side], Pc[side, 1], Z[side]], 1))
+               - tcw) @ R
+    far = kind == 2                                    # beyond 1.2 * mfMaxDistance
+    maxd[far] = dist[far] / 1.5
+    near = kind == 3                                   # below 0.8 * mfMinDistance
+    mind[near] = dist[near] * 1.5
+    maxd[near] = np.maximum(maxd[near], mind[near] * 2)
+    ang = kind == 4                                    # viewing angle above 60 degrees
+    for i in np.nonzero(ang)[0]:
+        ax = np.cross(dirn[i], rng.normal(size=3))
+        ax /= np.linalg.norm(ax)
+        a = np.deg2rad(rng.uniform(65, 120))
+        nrm[i] = dirn[i] * np.cos(a) + np.cross(ax, dirn[i]) * np.sin(a)
+    mp = np.zeros(n_points, MAP_POINT_DTYPE)
+    mp["pos"] = P.astype(np.float32)
+    mp["normal"] = nrm.astype(np.float32)
+    mp["max_dist"] = maxd.astype(np.float32)
+    mp["min_dist"] = mind.astype(np.float32)
+    d = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    d[:nin] = _flip(rng, desc[src], rng.integers(0, max_flip + 1, nin))
+    skip = (rng.random(n_points) < skip_frac).astype(np.uint8)
+    perm = rng.permutation(n_points)   # MapPoint order is unrelated to feature order
+    return pose, mp[perm], np.ascontiguousarray(d[perm]), skip[perm]
+
+
 def _rot(rng, max_deg):
     ax = rng.normal(size=3)
     ax /= np.linalg.norm(ax)

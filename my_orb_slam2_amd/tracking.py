@@ -4,14 +4,17 @@ Per frame, the reference's mono Tracking does (src/Tracking.cc):
   Frame::Frame (mono)      ExtractORB (Frame.cc:204), UndistortKeyPoints (:429-458),
                            AssignFeaturesToGrid (:243-258); image bounds once per camera
                            (ComputeImageBounds :461-489)
-  SearchLocalPoints        ORBmatcher(0.8).SearchByProjection(mCurrentFrame, mvpLocalMapPoints,
-                           th) (Tracking.cc:1297-1347, ORBmatcher.cc:41-136)
+  SearchLocalPoints        Frame::isInFrustum + MapPoint::PredictScale on every local MapPoint
+                           (Tracking.cc:1322-1335, Frame.cc:285-349, MapPoint.cc:430-444),
+                           then ORBmatcher(0.8).SearchByProjection(mCurrentFrame,
+                           mvpLocalMapPoints, th) (Tracking.cc:1337-1346, ORBmatcher.cc:41-136)
 
 ``MonoTrackBatch`` runs those stages for B frames on one HIP stream: one batched extraction
 (orbx_extract_batch_device), one batched undistortion and grid pass (orbx_frame.h batch
-forms), and one batched projection search (orbx_search_by_projection_batch_device) whose job
-j is frame j.  The projected local-map queries (u, v, radius, predicted level: the output of
-Frame::isInFrustum, Frame.cc:268-349, on the host side of Tracking) are inputs.
+forms), one batched projection of the frames' local maps (orbx_is_in_frustum_batch_device:
+the pose, the MapPoints' positions, normals and distances in; the SearchByProjection queries
+out) and one batched projection search (orbx_search_by_projection_batch_device) whose job j is
+frame j.  ``search_local_points`` also takes ready-made queries (the caller's own projection).
 """
 from __future__ import annotations
 
@@ -23,7 +26,7 @@ from ._lib import KEYPOINT_DTYPE, check
 from .extractor import ORBextractor
 from .features import (FRAME_GRID_COLS, FRAME_GRID_ROWS, PROJ_FRAME_MAPPOINTS, PROJ_QUERY_DTYPE,
                        FeatureSetC, assign_grid_batch_device, image_bounds,
-                       undistort_keypoints_batch_device)
+                       is_in_frustum_batch_device, undistort_keypoints_batch_device)
 from .matcher import ORBmatcher
 
 
@@ -93,9 +96,27 @@ class MonoTrackBatch:
             PROJ_FRAME_MAPPOINTS, self, d_qdesc, d_q, d_q_off, d_match, d_nmatches, d_claimed,
             stream=stream)
 
+    def project_local_map(self, d_frames, d_mps, d_mp_off, max_mps: int, d_skip, d_q,
+                          d_nvisible=None, th: float = 1.0, stream: int = 0):
+        """SearchLocalPoints' projection loop for every frame (Tracking.cc:1322-1335): frame j's
+        local MapPoints at [d_mp_off[j], d_mp_off[j+1]) of d_mps (MAP_POINT_DTYPE records),
+        its pose in d_frames[j] (FRAME_POSE_DTYPE); isInFrustum(pMP, 0.5) writes the
+        SearchByProjection query of each MapPoint into d_q (radius -1: not in view or d_skip
+        set, i.e. bad or already matched), nToMatch into d_nvisible[j]."""
+        is_in_frustum_batch_device(d_frames, self.batch, d_mps, d_mp_off, max_mps, d_skip, d_q,
+                                   d_nvisible, 0.5, th, stream)
+
     def __call__(self, images, d_qdesc, d_q, d_q_off, d_match, d_nmatches, d_claimed=None,
-                 stream: int = 0):
+                 stream: int = 0, local_map=None):
+        """One tracking step of the B frames.  With `local_map` = (d_frames, d_mps, max_mps,
+        d_skip, d_nvisible, th) the queries d_q are first projected from the local map
+        (project_local_map, MapPoints indexed like the queries: d_q_off); without it d_q
+        holds the caller's projections."""
         self.frames(images, stream)
+        if local_map is not None:
+            d_frames, d_mps, max_mps, d_skip, d_nvis, th = local_map
+            self.project_local_map(d_frames, d_mps, d_q_off, max_mps, d_skip, d_q, d_nvis, th,
+                                   stream)
         self.search_local_points(d_qdesc, d_q, d_q_off, d_match, d_nmatches, d_claimed, stream)
 
     def fetch_undistorted(self):

@@ -254,3 +254,20 @@ def cvt_gray(img, rgb):
     L.oracle_cvt_gray.argtypes = [_vp, _i, _i, _i, _i, _vp]
     L.oracle_cvt_gray(_a(s), w, h, c, int(rgb), _a(out))
     return out
+
+
+def is_in_frustum(frame, mps, skip=None, viewing_cos_limit=0.5, th=1.0):
+    """Tracking::SearchLocalPoints' projection loop restated (Frame::isInFrustum +
+    MapPoint::PredictScale + the SearchByProjection window, oracle/orb_frame_oracle.cpp):
+    frame is one orbx_frame_pose record, mps orbx_map_point records (numpy structured arrays
+    of my_orb_slam2_amd.features' dtypes).  Returns (queries as uint8 bytes of
+    orbx_proj_query records, nToMatch)."""
+    fr = np.ascontiguousarray(frame)
+    m = np.ascontiguousarray(mps)
+    sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+    q = np.zeros(len(m) * 32, np.uint8)
+    L = lib()
+    L.oracle_is_in_frustum.argtypes = [_vp, _vp, _i, _vp, _f, _f, _vp]
+    L.oracle_is_in_frustum.restype = _i
+    n = L.oracle_is_in_frustum(_a(fr), _a(m), len(m), _a(sk), viewing_cos_limit, th, _a(q))
+    return q, n

@@ -94,3 +94,129 @@ void oracle_cvt_gray(const uint8_t* src, int w, int h, int scn, int rgb, uint8_t
     }
 }
 }
+
+// ---- Frame::isInFrustum (src/Frame.cc:285-349) + MapPoint::PredictScale (MapPoint.cc:430-444),
+// and the query SearchByProjection(Frame&, vpMapPoints, th) builds (ORBmatcher.cc:55-80) -------
+// The cv::Mat arithmetic is restated from OpenCV 3.2 (PARITY UNPINNED against the library):
+//   mRcw*P + mtcw   MatExpr folds into cv::gemm(Rcw, P, 1, tcw, 1); its small-matrix path
+//                   (matmul.cpp, len 3, one output column) sums a_r0*b0 + a_r1*b1 + a_r2*b2 in
+//                   float and stores (float)(t*alpha + c*beta) computed in double
+//   cv::norm(PO)    normL2_<float, double>: squares summed in double, std::sqrt
+//   PO.dot(Pn)      dotProd_32f -> dotProd_<float>: (double)a*b summed in double
+// std::log / std::ceil of floats are logf / ceilf: TemplatedVocabulary.h:36 puts `using
+// namespace std` in scope of MapPoint.cc and Frame.cc, so the float overloads are chosen.
+#include <cmath>
+#include <climits>
+#include <cstring>
+
+namespace {
+struct OMapPoint {
+    float pos[3], min_dist, normal[3], max_dist;
+};
+struct OFrame {
+    float Rcw[9], tcw[3], Ow[3];
+    float fx, fy, cx, cy, mbf;
+    float mnMinX, mnMaxX, mnMinY, mnMaxY;
+    float mfLogScaleFactor;
+    int mnScaleLevels;
+    float mvScaleFactors[16];
+};
+struct OQuery {
+    float u, v, ur, radius;
+    int min_level, max_level, pred_level;
+    float angle;
+};
+
+// MapPoint::PredictScale(const float& currentDist, Frame* pF)
+int predict_scale(const OMapPoint& mp, float currentDist, const OFrame& F) {
+    float ratio = mp.max_dist / currentDist;
+    const float q = std::ceil(std::log(ratio) / F.mfLogScaleFactor);
+    // int nScale = ceil(...): the x86 conversion (cvttss2si) gives INT_MIN out of range
+    int nScale = (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
+    if (nScale < 0)
+        nScale = 0;
+    else if (nScale >= F.mnScaleLevels)
+        nScale = F.mnScaleLevels - 1;
+    return nScale;
+}
+
+// Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit); fills the mTrack* members
+bool is_in_frustum(const OFrame& F, const OMapPoint& mp, float viewingCosLimit, float& u_out,
+                   float& v_out, float& ur_out, int& level_out, float& viewcos_out) {
+    // const cv::Mat Pc = mRcw*P+mtcw;
+    float Pc[3];
+    for (int r = 0; r < 3; ++r) {
+        const float* a = F.Rcw + 3 * r;
+        const float t0 = a[0] * mp.pos[0] + a[1] * mp.pos[1] + a[2] * mp.pos[2];
+        const double alpha = 1.0, beta = 1.0;
+        Pc[r] = (float)(t0 * alpha + F.tcw[r] * beta);
+    }
+    const float& PcX = Pc[0];
+    const float& PcY = Pc[1];
+    const float& PcZ = Pc[2];
+    if (PcZ < 0.0f) return false;
+    const float invz = 1.0f / PcZ;
+    const float u = F.fx * PcX * invz + F.cx;
+    const float v = F.fy * PcY * invz + F.cy;
+    if (u < F.mnMinX || u > F.mnMaxX) return false;
+    if (v < F.mnMinY || v > F.mnMaxY) return false;
+    const float maxDistance = 1.2f * mp.max_dist;   // GetMaxDistanceInvariance
+    const float minDistance = 0.8f * mp.min_dist;   // GetMinDistanceInvariance
+    float PO[3];
+    for (int k = 0; k < 3; ++k) PO[k] = mp.pos[k] - F.Ow[k];
+    double s = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double vk = PO[k];
+        s += vk * vk;
+    }
+    const float dist = (float)std::sqrt(s);
+    if (dist < minDistance || dist > maxDistance) return false;
+    double dot = 0;
+    for (int k = 0; k < 3; ++k) dot += (double)PO[k] * mp.normal[k];
+    const float viewCos = dot / dist;
+    if (viewCos < viewingCosLimit) return false;
+    const int nPredictedLevel = predict_scale(mp, dist, F);
+    u_out = u;
+    ur_out = u - F.mbf * invz;
+    v_out = v;
+    level_out = nPredictedLevel;
+    viewcos_out = viewCos;
+    return true;
+}
+
+// ORBmatcher::RadiusByViewingCos (ORBmatcher.cc:134-140)
+float radius_by_viewing_cos(const float& viewCos) {
+    if (viewCos > 0.998)
+        return 2.5;
+    else
+        return 4.0;
+}
+}  // namespace
+
+extern "C" {
+// Tracking::SearchLocalPoints' projection loop (Tracking.cc:1322-1335) over n MapPoints of one
+// frame, and the window each in-view MapPoint gets in SearchByProjection (ORBmatcher.cc:55-80):
+// q[i] as orbx_proj_query (radius -1 when skip[i] or not in view).  Returns nToMatch.
+int oracle_is_in_frustum(const void* frame, const void* mps, int n, const uint8_t* skip,
+                         float viewingCosLimit, float th, void* q_out) {
+    OFrame F;
+    std::memcpy(&F, frame, sizeof(F));
+    const OMapPoint* M = (const OMapPoint*)mps;
+    OQuery* Q = (OQuery*)q_out;
+    const bool bFactor = th != 1.0;
+    int nToMatch = 0;
+    for (int i = 0; i < n; ++i) {
+        OQuery q = {0.0f, 0.0f, 0.0f, -1.0f, -1, -1, -1, 0.0f};
+        float u, v, ur, viewCos;
+        int level;
+        if (!(skip && skip[i]) && is_in_frustum(F, M[i], viewingCosLimit, u, v, ur, level, viewCos)) {
+            nToMatch++;
+            float r = radius_by_viewing_cos(viewCos);
+            if (bFactor) r *= th;
+            q = {u, v, ur, r * F.mvScaleFactors[level], level - 1, level, level, 0.0f};
+        }
+        Q[i] = q;
+    }
+    return nToMatch;
+}
+}

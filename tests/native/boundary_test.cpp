@@ -14,11 +14,13 @@
 //   F12[9]"); the outputs are written back to DIR as raw little-endian arrays.
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -269,9 +271,19 @@ static int run(const std::string& dir) {
 // the left and right images (Frame.cc:89-92), then ComputeStereoMatches (:102); host images
 // in, host keypoints / descriptors / uRight / depth out.  DIR holds P pairs
 // (pair_<i>_left.raw, pair_<i>_right.raw) and params.txt ("W H nfeatures mbf mb P"); frame f
-// uses pair f % P.  Prints one JSON line with every frame's latency after `warmup` frames,
-// timed with steady_clock like Examples/Stereo/stereo_kitti.cc:80-98.
-static int bench(const std::string& dir, int nframes, int warmup) {
+// uses pair f % P.  `trackers` independent tracking threads (K SLAM sessions sharing the GPU,
+// System.cc:91-101 per session), each with its own left / right handle pair, each running
+// warmup + nframes frames; they start together after every session's warm-up.  Prints one JSON
+// line: every timed frame's latency (steady_clock like Examples/Stereo/stereo_kitti.cc:80-98),
+// the wall time of the timed frames over all trackers, and a digest per tracker of its frames'
+// outputs (the sessions see the same pairs, so equal digests mean equal results).
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+static int bench(const std::string& dir, int nframes, int warmup, int trackers) {
     int W = 0, H = 0, nfeat = 0, P = 0;
     float mbf = 0, mb = 0;
     {
@@ -288,40 +300,93 @@ static int bench(const std::string& dir, int nframes, int warmup) {
             Ls[(size_t)i].size() != (size_t)W * H || Rs[(size_t)i].size() != (size_t)W * H)
             return 2;
     }
+    trackers = std::max(trackers, 1);
+    struct Session {
+        orbx_extractor *hl = nullptr, *hr = nullptr;
+        std::vector<double> ms;
+        long long kp_sum = 0, nv_sum = 0;
+        uint64_t digest = 1469598103934665603ull;
+        orbx_status st = ORBX_OK;
+    };
+    std::vector<Session> ss((size_t)trackers);
     orbx_extractor_params p = {nfeat, 1.2f, 8, 20, 7, 1, 1, 0};
-    orbx_extractor *hl = nullptr, *hr = nullptr;
-    CHECK(orbx_extractor_create(&p, &hl));
-    CHECK(orbx_extractor_create(&p, &hr));
-    std::vector<double> ms;
-    std::vector<float> uR(4096), depth(4096);
-    long long kp_sum = 0, nv_sum = 0;
-    for (int f = 0; f < warmup + nframes; ++f) {
-        const int i = f % P;
-        View vl, vr;
-        const auto t0 = std::chrono::steady_clock::now();
-        std::thread tl(extract, hl, Ls[(size_t)i].data(), W, H, &vl);
-        std::thread tr(extract, hr, Rs[(size_t)i].data(), W, H, &vr);
-        tl.join();
-        tr.join();
-        CHECK(vl.st);
-        CHECK(vr.st);
-        int nvalid = 0;
-        if ((int)uR.size() < vl.n) { uR.resize((size_t)vl.n); depth.resize((size_t)vl.n); }
-        CHECK(orbx_stereo_match(hl, hr, mbf, mb, uR.data(), depth.data(), vl.n, &nvalid));
-        const auto t1 = std::chrono::steady_clock::now();
-        if (f >= warmup) {
-            ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
-            kp_sum += vl.n;
-            nv_sum += nvalid;
-        }
+    for (Session& s : ss) {
+        CHECK(orbx_extractor_create(&p, &s.hl));
+        CHECK(orbx_extractor_create(&p, &s.hr));
     }
-    orbx_extractor_destroy(hl);
-    orbx_extractor_destroy(hr);
-    std::printf("{\"frames\": %d, \"warmup\": %d, \"mean_keypoints_left\": %.3f, "
-                "\"mean_stereo_matches\": %.3f, \"latency_ms\": [",
-                nframes, warmup, (double)kp_sum / std::max(nframes, 1),
-                (double)nv_sum / std::max(nframes, 1));
-    for (size_t k = 0; k < ms.size(); ++k) std::printf("%s%.4f", k ? ", " : "", ms[k]);
+    std::mutex mu;
+    std::condition_variable cv;
+    int warm_done = 0;
+    bool go = false;
+    auto track = [&](Session* s) {
+        std::vector<float> uR(4096), depth(4096);
+        for (int f = 0; f < warmup + nframes; ++f) {
+            if (f == warmup) {   // every session warm, then all timed frames start together
+                std::unique_lock<std::mutex> lk(mu);
+                if (++warm_done == trackers) { go = true; cv.notify_all(); }
+                cv.wait(lk, [&] { return go; });
+            }
+            const int i = f % P;
+            View vl, vr;
+            const auto t0 = std::chrono::steady_clock::now();
+            std::thread tl(extract, s->hl, Ls[(size_t)i].data(), W, H, &vl);
+            std::thread tr(extract, s->hr, Rs[(size_t)i].data(), W, H, &vr);
+            tl.join();
+            tr.join();
+            if (vl.st != ORBX_OK || vr.st != ORBX_OK) { s->st = vl.st != ORBX_OK ? vl.st : vr.st; return; }
+            int nvalid = 0;
+            if ((int)uR.size() < vl.n) { uR.resize((size_t)vl.n); depth.resize((size_t)vl.n); }
+            s->st = orbx_stereo_match(s->hl, s->hr, mbf, mb, uR.data(), depth.data(), vl.n, &nvalid);
+            if (s->st != ORBX_OK) return;
+            const auto t1 = std::chrono::steady_clock::now();
+            if (f >= warmup) {
+                s->ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                s->kp_sum += vl.n;
+                s->nv_sum += nvalid;
+                uint64_t h = fnv1a(s->digest, &vl.n, 4);
+                h = fnv1a(h, vl.kps.data(), vl.kps.size() * sizeof(orbx_keypoint));
+                h = fnv1a(h, vl.desc.data(), vl.desc.size());
+                h = fnv1a(h, vr.kps.data(), vr.kps.size() * sizeof(orbx_keypoint));
+                h = fnv1a(h, vr.desc.data(), vr.desc.size());
+                h = fnv1a(h, uR.data(), (size_t)vl.n * 4);
+                h = fnv1a(h, depth.data(), (size_t)vl.n * 4);
+                s->digest = fnv1a(h, &nvalid, 4);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    std::chrono::steady_clock::time_point t_go;
+    for (Session& s : ss) th.emplace_back(track, &s);
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return go; });
+        t_go = std::chrono::steady_clock::now();
+    }
+    for (std::thread& t : th) t.join();
+    const double wall_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_go).count();
+    long long kp_sum = 0, nv_sum = 0;
+    for (Session& s : ss) {
+        CHECK(s.st);
+        kp_sum += s.kp_sum;
+        nv_sum += s.nv_sum;
+        orbx_extractor_destroy(s.hl);
+        orbx_extractor_destroy(s.hr);
+    }
+    const long long nt = (long long)nframes * trackers;
+    std::printf("{\"frames\": %d, \"warmup\": %d, \"trackers\": %d, \"wall_ms\": %.4f, "
+                "\"mean_keypoints_left\": %.3f, \"mean_stereo_matches\": %.3f, \"digests\": [",
+                nframes, warmup, trackers, wall_ms, (double)kp_sum / std::max(nt, 1LL),
+                (double)nv_sum / std::max(nt, 1LL));
+    for (size_t k = 0; k < ss.size(); ++k)
+        std::printf("%s\"%016llx\"", k ? ", " : "", (unsigned long long)ss[k].digest);
+    std::printf("], \"latency_ms\": [");
+    bool first = true;
+    for (Session& s : ss)
+        for (double v : s.ms) {
+            std::printf("%s%.4f", first ? "" : ", ", v);
+            first = false;
+        }
     std::printf("]}\n");
     return 0;
 }
@@ -467,10 +532,10 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "layout") return layout();
     if (argc >= 3 && std::string(argv[1]) == "run") return run(argv[2]);
     if (argc >= 5 && std::string(argv[1]) == "bench")
-        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]));
+        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc >= 6 ? std::atoi(argv[5]) : 1);
     if (argc >= 5 && std::string(argv[1]) == "tum")
         return tum(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc >= 6 ? argv[5] : "");
-    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP | tum DIR NFRAMES WARMUP [DUMPDIR]\n",
+    std::fprintf(stderr, "usage: %s layout | run DIR | bench DIR NFRAMES WARMUP [TRACKERS] | tum DIR NFRAMES WARMUP [DUMPDIR]\n",
                  argv[0]);
     return 2;
 }

@@ -8,8 +8,10 @@ launch geometry it times, built by bench.py's own input builders.
   orbx_extractor_launch_info); a single image runs 8-row strips and split stereo.  Every slot
   must equal its single-image run, and 16 slots must equal the CPU restatement bit for bit
   (ORBextractor.cc:1065-1154, Frame.cc:496-686).
-* C3 (configs[2]): 256 EuRoC frames through MonoTrackBatch with 2000 projected MapPoints per
-  frame, every slot against the restatement (ORBmatcher.cc:41-136).
+* C3 (configs[2]): 256 EuRoC frames through MonoTrackBatch with a 2000-MapPoint 3-D local map
+  per frame, projected on the device (isInFrustum + PredictScale, Frame.cc:285-349,
+  MapPoint.cc:430-444) inside the step, every slot's queries, in-view count and matches
+  against the restatement (ORBmatcher.cc:41-136).
 * C4 (configs[3]): the 10k-keyframe relocalisation database, 512 sampled keyframes (the 10
   planted true ones among them) against SearchByBoW(KF, F) restated (ORBmatcher.cc:182-319).
 * C4 pure brute force (bench.py --workload bf): one 1000-descriptor query frame against the
@@ -125,7 +127,8 @@ def test_c3_euroc_b256(oracle_mod, orbx_lib, gpu):
     import torch
     from oracle import matcher as om
     from my_orb_slam2_amd import synth
-    from my_orb_slam2_amd.features import PROJ_FRAME_MAPPOINTS, FeatureSet, assign_features_to_grid
+    from my_orb_slam2_amd.features import (PROJ_FRAME_MAPPOINTS, PROJ_QUERY_DTYPE, FeatureSet,
+                                           assign_features_to_grid)
     from my_orb_slam2_amd.tracking import MonoTrackBatch
     B, P, NQ = 256, 32, 2000
     K4, dist = synth.EUROC_CAM
@@ -136,18 +139,18 @@ def test_c3_euroc_b256(oracle_mod, orbx_lib, gpu):
     rows, _ = mt.ext.launch_info(B)
     mt.frames(d_imgs)
     nkp, ku, desc = mt.fetch_undistorted()
-    per = bench.euroc_queries(idx, nkp, ku, desc, NQ, mt.kp_cap)
-    qs = [per[p][0] for p in idx]
-    q_off = np.concatenate([[0], np.cumsum([len(q) for q in qs])]).astype(np.int32)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(gpu)
-    d_q = T(np.concatenate(qs))
-    d_d = T(np.concatenate([per[p][1] for p in idx]))
-    d_cl = T(np.concatenate([per[p][2] for p in idx]))
+    per = bench.euroc_local_maps(idx, nkp, ku, desc, NQ, mt.kp_cap, mt.bounds)
+    inp = bench.euroc_device_inputs(torch, gpu, per, idx)
+    q_off = inp["q_off_h"]
     out = torch.full((int(q_off[-1]),), -7, dtype=torch.int32, device=gpu)
     cnt = torch.full((B,), -7, dtype=torch.int32, device=gpu)
-    mt(d_imgs, d_d, d_q, torch.from_numpy(q_off).to(gpu), out, cnt, d_cl)   # the timed step
+    # the timed step: frames, the local maps' projection (isInFrustum + PredictScale), search
+    mt(d_imgs, inp["desc"], inp["q"], inp["q_off"], out, cnt, inp["claimed"],
+       local_map=(inp["frames"], inp["mps"], inp["max_mps"], inp["skip"], inp["nvis"], 1.0))
     mt.matcher.sync()
     out, cnt = out.cpu().numpy(), cnt.cpu().numpy()
+    qg = inp["q"].cpu().numpy().reshape(-1, 32)
+    nvis = inp["nvis"].cpu().numpy()
     _, kraw, _ = mt.ext.batch_fetch(0, B)
     ref = {}
     for p in range(P):
@@ -157,12 +160,16 @@ def test_c3_euroc_b256(oracle_mod, orbx_lib, gpu):
         ku_o = k_o.copy()
         ku_o["x"], ku_o["y"] = un[:, 0], un[:, 1]
         g = assign_features_to_grid(ku_o, *mt.bounds)
-        q, d, cl = per[p]
-        ref[p] = (k_o, d_o, ku_o, om.search_by_projection(
-            PROJ_FRAME_MAPPOINTS, FeatureSet(ku_o, d_o, None, None, g), q, d, cl[:len(k_o)], None,
-            nnratio=0.8))
+        pose, mps, d, skip, cl = per[p]
+        qb, nv_o = om.is_in_frustum(pose, mps, skip, 0.5, 1.0)
+        ref[p] = (k_o, d_o, ku_o, qb.reshape(-1, 32), nv_o, om.search_by_projection(
+            PROJ_FRAME_MAPPOINTS, FeatureSet(ku_o, d_o, None, None, g),
+            qb.view(PROJ_QUERY_DTYPE), d, cl[:len(k_o)], None, nnratio=0.8))
     for b, p in enumerate(idx):
-        k_o, d_o, ku_o, (n_o, m_o) = ref[p]
+        k_o, d_o, ku_o, q_o, nv_o, (n_o, m_o) = ref[p]
+        assert nvis[b] == nv_o, f"frame {b} MapPoints in view"
+        bad = np.nonzero((qg[q_off[b]:q_off[b + 1]] != q_o).any(1))[0]
+        assert bad.size == 0, f"frame {b}: projections of MapPoints {bad[:8]} differ"
         n = int(nkp[b])
         assert_kps_equal(kraw[b, :n], k_o, f"frame {b} keypoints")
         assert_bytes_equal(desc[b, :n], d_o, f"frame {b} descriptors")

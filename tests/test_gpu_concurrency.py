@@ -168,3 +168,77 @@ def test_batch_fetch_races_extract(orbx_lib, gpu):
                      for j in range(len(nkp)))]
         assert which, "a fetch mixed two extractions"
         seen.add(which[0])
+
+
+def test_k_tracker_sessions(orbx_lib, gpu):
+    """K = 4 tracking sessions sharing the GPU (bench.py --workload dropin --trackers 4): each
+    session has its own left / right handles and runs Frame.cc:89-102 (two extraction threads,
+    then the stereo match) over the same frames at the same time as the others.  Every
+    session's results equal the serial single-session run, bit for bit."""
+    import my_orb_slam2_amd as m
+    mb = float(np.float32(MBF) / np.float32(FX))
+    frames = [synth.stereo_pair(740 + i, 1241, 376) for i in range(4)]
+    K = 4
+    sess = [(m.ORBextractor(2000, 1.2, 8, 20, 7), m.ORBextractor(2000, 1.2, 8, 20, 7))
+            for _ in range(K)]
+    ref = []
+    for L, R in frames:
+        kl, dl = sess[0][0](L)
+        kr, dr = sess[0][1](R)
+        ref.append((kl, dl, kr, dr, *m.compute_stereo_matches(sess[0][0], sess[0][1], MBF, mb)))
+    got = [[] for _ in range(K)]
+    errors = []
+
+    def session(k):
+        gl, gr = sess[k]
+        try:
+            for rnd in range(2):
+                for L, R in frames:
+                    res = {}
+                    tl = threading.Thread(target=lambda: res.__setitem__("l", gl(L)))
+                    tr = threading.Thread(target=lambda: res.__setitem__("r", gr(R)))
+                    tl.start()
+                    tr.start()
+                    tl.join()
+                    tr.join()
+                    got[k].append((*res["l"], *res["r"], *m.compute_stereo_matches(gl, gr, MBF, mb)))
+        except Exception as e:   # pragma: no cover
+            errors.append(e)
+    ths = [threading.Thread(target=session, args=(k,)) for k in range(K)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    for k in range(K):
+        assert len(got[k]) == 2 * len(frames)
+        for i, g in enumerate(got[k]):
+            r = ref[i % len(frames)]
+            assert_kps_equal(g[0], r[0], f"session {k} frame {i} left")
+            assert_bytes_equal(g[1], r[1], f"session {k} frame {i} left desc")
+            assert_kps_equal(g[2], r[2], f"session {k} frame {i} right")
+            assert_bytes_equal(g[3], r[3], f"session {k} frame {i} right desc")
+            assert_f32_bits_equal(g[4], r[4], f"session {k} frame {i} uRight")
+            assert_f32_bits_equal(g[5], r[5], f"session {k} frame {i} depth")
+            assert g[6] == r[6]
+
+
+def test_cpp_tracker_sessions_agree(orbx_lib, gpu, tmp_path):
+    """The C++ K-tracker loop bench.py times (boundary_test `bench DIR N W K`): 4 sessions over
+    the same pairs report the same output digest."""
+    import json
+    import subprocess
+    from my_orb_slam2_amd import build as b
+    binp = b.build_boundary_test()
+    mb = float(np.float32(MBF) / np.float32(FX))
+    for i in range(2):
+        L, R = synth.stereo_pair(750 + i, 1241, 376)
+        L.tofile(tmp_path / f"pair_{i}_left.raw")
+        R.tofile(tmp_path / f"pair_{i}_right.raw")
+    (tmp_path / "params.txt").write_text(f"1241 376 2000 {MBF!r} {mb!r} 2\n")
+    r = subprocess.run([str(binp), "bench", str(tmp_path), "6", "2", "4"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["trackers"] == 4 and len(res["latency_ms"]) == 24
+    assert len(set(res["digests"])) == 1, res["digests"]

@@ -100,3 +100,16 @@ def test_glibc_sincosf_port_exhaustive(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sin_mismatch=0 cos_mismatch=0" in r.stdout
+
+
+def test_glibc_logf_port_exhaustive(tmp_path):
+    """orbx_math.h's logf (MapPoint::PredictScale, Frame::mfLogScaleFactor) == the host glibc
+    logf on every non-negative float bit pattern: zero, subnormals, normals, inf and the NaNs."""
+    exe = tmp_path / "lpc"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-pthread",
+                    str(ROOT / "tests/native/libm_port_check.cpp"), "-o", str(exe), "-lm"],
+                   check=True)
+    r = subprocess.run([str(exe), "logf", "0", "0x80000000"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "checked=2147483648 logf_mismatch=0" in r.stdout
