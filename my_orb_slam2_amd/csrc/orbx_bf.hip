@@ -35,6 +35,10 @@ namespace {
 #ifndef BF_PIPE
 #define BF_PIPE 1      // k_bf_top2: ping-pong row groups (0: 8-row groups, one wait each)
 #endif
+#ifndef BF_PACKED
+#define BF_PACKED 1    // k_bf_top2: packed 16-bit top-2 keys over blocks of BF_BLK rows
+#endif
+#define BF_BLK 256     // rows per packed block (128 pairs: the pair index fits 7 bits)
 
 constexpr uint32_t BF_NONE = 256u << 23;       // (distance 256, row 0): the loop's initial value
 constexpr int BF_ROW_BITS = 23;                 // rows per chunk < 2^23
@@ -90,6 +94,65 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
 #pragma unroll
             for (int k = 0; k < 8; ++k) g[j][k] = p[(size_t)(e0 + j) * 8 + k];
     };
+#if BF_PACKED
+    // Blocks of BF_BLK rows with the top-2 kept as packed 16-bit keys: rows e0 + 2i (low half)
+    // and e0 + 2i + 1 (high half) get the key (distance << 7 | i), built by two v_lshl_or per
+    // row pair; the top-2 update is three v_pk_min/max_u16 per pair (second = max(best,
+    // min(second, key)) for a sorted pair) instead of v_lshl_or + v_med3 + v_min per row.
+    // Each half orders its keys by (distance, row), so at the block's end its best and second
+    // are inserted into the 32-bit (distance << 23 | row) top-2 with their real rows: the
+    // result is the per-row loop's (first row wins a tie).
+    auto pair = [&](const uint32_t* ra, const uint32_t* rb, uint32_t pp, uint32_t& h1,
+                    uint32_t& h2) {
+        uint32_t da = 0, db = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) da = bcnt_acc(a[k] ^ ra[k], da);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) db = bcnt_acc(a[k] ^ rb[k], db);
+        uint32_t x, w;
+        asm("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(x) : "v"(da), "s"(pp));
+        asm("v_lshl_or_b32 %0, %1, 23, %2" : "=v"(w) : "v"(db), "v"(x));
+        uint32_t m;
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(h2), "v"(w));
+        asm("v_pk_max_u16 %0, %1, %2" : "=v"(h2) : "v"(h1), "v"(m));
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(h1) : "v"(h1), "v"(w));
+    };
+    auto ins = [&](uint32_t key) {
+        b2 = med3_u32(b1, b2, key);
+        b1 = min(b1, key);
+    };
+    auto fold = [&](uint32_t h1, uint32_t h2, int e0) {
+        // half key k = d << 7 | i of row e0 + 2i (+1 for the high half)
+        auto full = [&](uint32_t k, int odd) {
+            return ((k >> 7) << BF_ROW_BITS) | (uint32_t)(e0 + 2 * (int)(k & 127u) + odd);
+        };
+        ins(full(h1 & 0xFFFFu, 0));
+        ins(full(h2 & 0xFFFFu, 0));
+        ins(full(h1 >> 16, 1));
+        ins(full(h2 >> 16, 1));
+    };
+    constexpr uint32_t H_NONE = (256u << 7) * 0x10001u;   // (256, pair 0) in both halves
+    for (; e + BF_BLK <= n; e += BF_BLK) {
+        uint32_t h1 = H_NONE, h2 = H_NONE;
+        uint32_t A[BF_G][8], B[BF_G][8];
+        load(A, e);
+        int o = 0;
+        for (; o + 2 * BF_G < BF_BLK; o += 2 * BF_G) {
+            load(B, e + o + BF_G);
+            pair(A[0], A[1], (uint32_t)(o / 2) * 0x10001u, h1, h2);
+            pair(A[2], A[3], (uint32_t)(o / 2 + 1) * 0x10001u, h1, h2);
+            load(A, e + o + 2 * BF_G);
+            pair(B[0], B[1], (uint32_t)(o / 2 + 2) * 0x10001u, h1, h2);
+            pair(B[2], B[3], (uint32_t)(o / 2 + 3) * 0x10001u, h1, h2);
+        }
+        load(B, e + o + BF_G);
+        pair(A[0], A[1], (uint32_t)(o / 2) * 0x10001u, h1, h2);
+        pair(A[2], A[3], (uint32_t)(o / 2 + 1) * 0x10001u, h1, h2);
+        pair(B[0], B[1], (uint32_t)(o / 2 + 2) * 0x10001u, h1, h2);
+        pair(B[2], B[3], (uint32_t)(o / 2 + 3) * 0x10001u, h1, h2);
+        fold(h1, h2, e);
+    }
+#else
     auto group = [&](const uint32_t (&g)[BF_G][8], int e0) {
 #pragma unroll
         for (int j = 0; j < BF_G; ++j) row(g[j], e0 + j);
@@ -118,6 +181,7 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
         group(B, e + BF_G);
         e += 2 * BF_G;
     }
+#endif
 #endif
     for (; e < n; ++e) row(p + (size_t)e * 8, e);
     if (qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1, b2);

@@ -59,6 +59,7 @@ struct orbx_extractor {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_mode = FAST_SIDE, side_at = FAST_SIDE_AT, side_lv = FAST_SIDE_LV;
+    bool side_auto = true;   // the built-in default: no side branch below SIDE_MIN_BATCH images
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -77,14 +78,20 @@ struct orbx_extractor {
     std::vector<uint8_t> ltab;   // k_level per-tile tables (LevelColTab / LevelRowTab)
     int ncap = 0, kcap = 0, ncap1 = 0, kcap1 = 0;
     size_t octree_lds = 0, octree_lds1 = 0, stereo_lds = 0, level_lds = 0;
+    int kcap_small = 0;               // small-batch octree: candidates held in LDS
+    size_t octree_lds_small = 0;
     int cap_batch = 0;
     DevBuf d_geom, d_cells, d_rtab, d_ltab, d_pyr, d_blur, d_ccnt, d_cand, d_ocnt, d_okp, d_kscr,
         d_kps, d_desc, d_nkp, d_uR, d_dep, d_nv, d_sscr;
+    // the extraction outputs as one allocation: [nkp[B] | kps[B][KC] | desc[B][KC][32]]
+    // (d_nkp / d_kps / d_desc are views of it): one DMA returns one image's results
+    DevBuf d_outs;
     long long kscratch_per_image = 0;
     KernelTimer timer;
     // last extraction
     int last_batch = 0;
     bool last_valid = false;
+    int last_n = 0;          // keypoints of the last orbx_extract (host image path)
     // guards every field above against concurrent calls on one handle (const queries too)
     mutable std::mutex mu;
 };
@@ -228,6 +235,37 @@ static void strip_heights(const orbx_extractor* h, int nimg, int* sth) {
 }
 
 static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
+
+// Small-batch launch policies.  Tuning builds (-DORBX_TUNING) read an environment override
+// (tools/variants.py A/B runs); the product library never reads the environment.
+#ifndef OCT_LDS_SMALL_KB
+#define OCT_LDS_SMALL_KB 152   // octree LDS budget for small batches (one workgroup per list)
+#endif
+#ifndef OCT_SMALL_BATCH
+#define OCT_SMALL_BATCH 4      // images per call up to which the octree takes that budget
+#endif
+#ifndef SIDE_MIN_BATCH
+#define SIDE_MIN_BATCH 16      // images per call from which the default side branch forks
+#endif
+static int tuned(const char* name, int def) {
+#ifdef ORBX_TUNING
+    if (const char* e = getenv(name)) return atoi(e);
+#else
+    (void)name;
+#endif
+    return def;
+}
+
+// k_fast cells per wave: FAST_NC (the next cell's ROI loads overlap the current cell) while the
+// launch gives every CU two workgroups, fewer for small batches (a wave's cells run in series,
+// so one image's FAST is a chain of FAST_NC cells otherwise).
+static int fast_cells_per_wave(int ncells, int batch, int ncu) {
+    int nc = tuned("ORBX_FAST_NC", 0);
+    if (nc > 0) return nc;
+    nc = FAST_NC;
+    while (nc > 1 && (long long)ncells * batch / (4 * nc) < 2LL * ncu) nc >>= 1;
+    return nc;
+}
 
 // Orders stream st after all work issued so far for this handle (on whatever stream).
 static bool order_after_last(orbx_extractor* h, hipStream_t st) {
@@ -679,6 +717,13 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         h->octree_lds1 = h->octree_lds;
     }
 #endif
+    {
+        // small batches: the same node arrays, candidates in LDS up to OCT_LDS_SMALL_KB
+        int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
+        while (kc > 64 && octree_lds_bytes(h->ncap, kc) > OCT_LDS_SMALL_KB * 1024) kc -= 64;
+        h->kcap_small = std::max(kc, h->kcap);
+        h->octree_lds_small = std::max(octree_lds_bytes(h->ncap, h->kcap_small), h->octree_lds);
+    }
     G.stereo_ob = G.nlevels;
     h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h, G.stereo_ob);
     if (h->stereo_lds > 160 * 1024) {   // row buckets only (octaves tested per candidate)
@@ -716,7 +761,8 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
             !HIPOK(hipMemcpyAsync(h->d_rtab.p, h->rtab.data(), h->rtab.size() * 2, hipMemcpyHostToDevice, st)))
             return ORBX_ERR_DEVICE;
         if (!HIPOK(hipStreamSynchronize(st))) return ORBX_ERR_DEVICE;
-        if (!HIPOK(prepare_kernels(h->octree_lds, h->stereo_lds, h->level_lds, fast_lds_bytes(h->hg))))
+        if (!HIPOK(prepare_kernels(std::max(h->octree_lds, h->octree_lds_small), h->stereo_lds,
+                                   h->level_lds, fast_lds_bytes(h->hg))))
             return ORBX_ERR_DEVICE;
         h->have_geom = true;
         h->cap_batch = 0;
@@ -736,10 +782,16 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
                   h->d_cand.ensure(B * G.cand_words * 4) &&
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
-                  h->d_kscr.ensure(B * h->kscratch_per_image) &&
-                  h->d_kps.ensure(B * G.kp_cap * sizeof(orbx_keypoint)) &&
-                  h->d_desc.ensure(B * G.kp_cap * 32) && h->d_nkp.ensure(B * 4);
+                  h->d_kscr.ensure(B * h->kscratch_per_image);
+        const size_t o_kps = align_up(B * 4, 256);
+        const size_t o_desc = o_kps + align_up(B * G.kp_cap * sizeof(orbx_keypoint), 256);
+        const size_t o_end = o_desc + B * G.kp_cap * 32;
+        ok = ok && h->d_outs.ensure(o_end);
         if (!ok) return ORBX_ERR_DEVICE;
+        uint8_t* ob = h->d_outs.as<uint8_t>();
+        h->d_nkp.view(ob, B * 4);
+        h->d_kps.view(ob + o_kps, B * G.kp_cap * sizeof(orbx_keypoint));
+        h->d_desc.view(ob + o_desc, B * G.kp_cap * 32);
         h->cap_batch = batch;
     }
     return ORBX_OK;
@@ -782,6 +834,10 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.ncap1 = h->ncap1;
     a.kcap1 = h->kcap1;
     a.octree_lds1 = h->octree_lds1;
+    a.kcap_small = h->kcap_small;
+    a.octree_lds_small = h->octree_lds_small;
+    a.oct_small = batch <= tuned("ORBX_OCT_SMALL_BATCH", OCT_SMALL_BATCH) ? 1 : 0;
+    a.fast_nc = fast_cells_per_wave(h->hg.n_cells, batch, h->ncu);
     a.kps = h->d_kps.as<float>();
     a.desc = h->d_desc.as<uint8_t>();
     a.nkp = h->d_nkp.as<int>();
@@ -789,7 +845,12 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.side = h->side;
     a.ev_fork = h->ev_fork;
     a.ev_join = h->ev_join;
-    a.side_mode = h->side_mode;
+    // the default schedule forks the side branch only for batches that can fill the chip: a
+    // small batch's kernels are latency chains, and the fork / join events between the two
+    // streams cost more than the overlap gives (an explicit orbx_extractor_set_overlap applies
+    // at every batch size)
+    a.side_mode = (h->side_auto && batch < tuned("ORBX_SIDE_MIN_BATCH", SIDE_MIN_BATCH)) ? 0
+                                                                                     : h->side_mode;
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
     strip_heights(h, batch, a.sth);
@@ -797,6 +858,7 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
     h->last_valid = true;
+    h->last_n = -1;   // on the device only (orbx_extract records it once copied back)
     return ORBX_OK;
 }
 
@@ -882,10 +944,12 @@ orbx_status orbx_extractor_set_overlap(orbx_extractor* h, int mode, int fork_lev
         h->side_mode = FAST_SIDE;
         h->side_at = FAST_SIDE_AT;
         h->side_lv = FAST_SIDE_LV;
+        h->side_auto = true;
     } else {
         h->side_mode = mode;
         h->side_at = fork_level;
         h->side_lv = levels;
+        h->side_auto = false;
     }
     return ORBX_OK;
 }
@@ -1003,7 +1067,8 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (h->h_out) (void)hipHostFree(h->h_out);
     DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
-                      &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr};
+                      &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr,
+                      &h->d_outs};
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
     if (h->side) (void)hipStreamSynchronize(h->side);
@@ -1050,9 +1115,12 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     const LevelGeom& L0 = h->hg.lv[0];
     const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)height;
     const size_t KC = (size_t)h->hg.kp_cap;
-    const size_t o_kps = 256, o_desc = o_kps + KC * sizeof(orbx_keypoint);
+    // the outputs' device block (batch 1): nkp at 0, keypoints at o_kps, descriptors at o_desc
+    const size_t o_kps = (size_t)((uint8_t*)h->d_kps.p - (uint8_t*)h->d_outs.p);
+    const size_t o_desc = (size_t)((uint8_t*)h->d_desc.p - (uint8_t*)h->d_outs.p);
+    const size_t o_end = o_desc + KC * 32;
     if (!ensure_pinned(h->h_in, h->h_in_n, img_bytes) ||
-        !ensure_pinned(h->h_out, h->h_out_n, o_desc + KC * 32))
+        !ensure_pinned(h->h_out, h->h_out_n, o_end))
         return ORBX_ERR_DEVICE;
     for (int y = 0; y < height; ++y)
         std::memcpy(h->h_in + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
@@ -1062,15 +1130,13 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
         return ORBX_ERR_DEVICE;
     s = run_extract(h, nullptr, nullptr, 1, 1, 0, 0, st);
     if (s != ORBX_OK) return s;
-    if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(h->h_out + o_kps, h->d_kps.p, KC * sizeof(orbx_keypoint),
-                              hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(h->h_out + o_desc, h->d_desc.p, KC * 32, hipMemcpyDeviceToHost, st)) ||
+    if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) ||
         !mark_done(h, st) || !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
     int n = 0;
     std::memcpy(&n, h->h_out, 4);
     *n_out = n;
+    h->last_n = n;
     const int m = std::min(n, kp_cap);
     if (m > 0) {
         if (kps) std::memcpy(kps, h->h_out + o_kps, (size_t)m * sizeof(orbx_keypoint));
@@ -1235,25 +1301,27 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float
         return ORBX_ERR_STATE;
     (void)hipSetDevice(left->device);
     const size_t KC = (size_t)left->hg.kp_cap;
-    if (!left->d_uR.ensure(KC * 4) || !left->d_dep.ensure(KC * 4) || !left->d_nv.ensure(16))
-        return ORBX_ERR_DEVICE;
-    // results come back in one pinned block: [nkp, nvalid | uRight[KC] | depth[KC]]
+    // the results in one device block, copied back by one DMA into one pinned block:
+    // [nvalid | uRight[KC] | depth[KC]]; the left keypoint count is the handle's own (its
+    // orbx_extract returned it)
     const size_t o_u = 256, o_d = o_u + KC * 4;
+    if (!left->d_uR.ensure(o_d + KC * 4)) return ORBX_ERR_DEVICE;
     if (!ensure_pinned(left->h_out, left->h_out_n, o_d + KC * 4)) return ORBX_ERR_DEVICE;
+    uint8_t* dso = left->d_uR.as<uint8_t>();
     hipStream_t st = left->stream;
-    orbx_status s = run_stereo(left, right, 1, 0, 0, mbf, mb, left->d_uR.as<float>(),
-                               left->d_dep.as<float>(), left->d_nv.as<int>(), st);
+    orbx_status s = run_stereo(left, right, 1, 0, 0, mbf, mb, (float*)(dso + o_u),
+                               (float*)(dso + o_d), (int*)dso, st);
     if (s != ORBX_OK) return s;
     uint8_t* ho = left->h_out;
-    if (!HIPOK(hipMemcpyAsync(ho, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(ho + 4, left->d_nv.p, 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(ho + o_u, left->d_uR.p, KC * 4, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(ho + o_d, left->d_dep.p, KC * 4, hipMemcpyDeviceToHost, st)) ||
+    const bool known = left->last_n >= 0;   // else a batched call of one image set the state
+    if (!HIPOK(hipMemcpyAsync(ho, dso, o_d + KC * 4, hipMemcpyDeviceToHost, st)) ||
+        (!known && !HIPOK(hipMemcpyAsync(ho + 8, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st))) ||
         !mark_done(left, st) || !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
-    int n = 0, nv = 0;
-    std::memcpy(&n, ho, 4);
-    std::memcpy(&nv, ho + 4, 4);
+    int n = left->last_n;
+    if (!known) std::memcpy(&n, ho + 8, 4);
+    int nv = 0;
+    std::memcpy(&nv, ho, 4);
     const int m = std::min(n, n_left);
     if (m > 0) {
         if (uRight) std::memcpy(uRight, ho + o_u, (size_t)m * 4);

@@ -142,9 +142,6 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef FAST_LIST
 #define FAST_LIST 512    // compass survivors listed per row block (a multiple of 256)
 #endif
-#ifndef FAST_NC
-#define FAST_NC 4      // cells per wave (the next cell's ROI loads overlap this cell's work)
-#endif
 #ifndef FAST_PF
 #define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
 #endif
@@ -350,7 +347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                                               const uint8_t* __restrict__ pyr,
                                               int* __restrict__ ccnt,
                                               uint32_t* __restrict__ cand,
-                                              int c_begin, int c_end) {
+                                              int c_begin, int c_end, int nc) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #if FAST_XCD
@@ -361,11 +358,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 #else
     const int bx = blockIdx.x, b = blockIdx.y;
 #endif
-    // one wave owns FAST_NC consecutive cells; no block-level barriers: waves are independent
-    // cells [c_begin, c_end) of every image (a launch may cover a range of levels)
-    const int c_first = __builtin_amdgcn_readfirstlane(c_begin + (bx * 4 + wid) * FAST_NC);
+    // one wave owns nc (FAST_NC, or fewer for a small batch: fast_cells_per_wave) consecutive
+    // cells; no block-level barriers: waves are independent.  Cells [c_begin, c_end) of every
+    // image (a launch may cover a range of levels)
+    const int c_first = __builtin_amdgcn_readfirstlane(c_begin + (bx * 4 + wid) * nc);
     if (c_first >= c_end) return;
-    const int ncw = min(FAST_NC, c_end - c_first);
+    const int ncw = min(nc, c_end - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
 #if FAST_W16
@@ -1565,9 +1563,10 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
     auto fast = [&](int c0, int c1, hipStream_t s) {
         if (c1 <= c0) return;
-        ORBX_TIMED_LAUNCH(T, K_FAST, k_fast, dim3((c1 - c0 + 4 * FAST_NC - 1) / (4 * FAST_NC), a.batch),
+        const int nc = a.fast_nc;
+        ORBX_TIMED_LAUNCH(T, K_FAST, k_fast, dim3((c1 - c0 + 4 * nc - 1) / (4 * nc), a.batch),
                           dim3(256), fast_lds_bytes(G), s, a.dg, a.cells, (const uint8_t*)a.pyr,
-                          a.ccnt, a.cand, c0, c1);
+                          a.ccnt, a.cand, c0, c1, nc);
     };
     // threads per list: OCT_NT, or OCT_NT_SMALL while the batch's lists fit one round on the
     // CUs (each list is a serial chain of rounds with a few barriers each)
@@ -1594,6 +1593,10 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     // the input slot; every other part needs its level (and its blur) launched before the fork.
     const int nside = a.side_lv < G.nlevels - 1 ? a.side_lv : G.nlevels - 1;
     const int mode = a.side_mode;
+    // a small batch's octree lists (a few workgroups on the whole chip) take the large LDS
+    // budget: every level's candidates stay in LDS instead of the global scratch
+    const size_t oct_lds = a.oct_small ? a.octree_lds_small : a.octree_lds;
+    const int oct_kcap = a.oct_small ? a.kcap_small : a.kcap;
     const bool side = mode > 0 && a.side && a.ev_fork && a.ev_join && nside >= 1;
     const int c_l1 = side ? G.lv[nside].cell_begin : G.n_cells;
     const bool side_od = side && mode >= 3 && G.orient_block_begin[nside] < G.orient_blocks;
@@ -1614,21 +1617,21 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         if ((err = hipStreamWaitEvent(a.side, a.ev_fork, 0)) != hipSuccess) return err;
         if (side_l0 && (err = launch_levels(a, a.side, 0, 1)) != hipSuccess) return err;
         fast(0, c_l1, a.side);
-        if (mode >= 2) oct(dim3(nside, a.batch), a.octree_lds, a.ncap, a.kcap, 0, a.side);
+        if (mode >= 2) oct(dim3(nside, a.batch), oct_lds, a.ncap, oct_kcap, 0, a.side);
         if (side_od) orient(0, ob0, -1, a.side);
         if ((err = hipEventRecord(a.ev_join, a.side)) != hipSuccess) return err;
         err = launch_levels(a, st, fork_main, G.nlevels);
         if (err != hipSuccess) return err;
         fast(c_l1, G.n_cells, st);
-        if (mode >= 2) oct(dim3(G.nlevels - nside, a.batch), a.octree_lds, a.ncap, a.kcap, nside, st);
+        if (mode >= 2) oct(dim3(G.nlevels - nside, a.batch), oct_lds, a.ncap, oct_kcap, nside, st);
         if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
-        if (mode < 2) oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
+        if (mode < 2) oct(dim3(G.nlevels, a.batch), oct_lds, a.ncap, oct_kcap, 0, st);
     } else {
         err = launch_levels(a, st, 0, G.nlevels);
         if (err != hipSuccess) return err;
         fast(0, G.n_cells, st);
 #if OCT_MERGED
-        oct(dim3(G.nlevels, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
+        oct(dim3(G.nlevels, a.batch), oct_lds, a.ncap, oct_kcap, 0, st);
 #else
         oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
         if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1, st);

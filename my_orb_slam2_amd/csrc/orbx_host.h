@@ -16,17 +16,26 @@ extern thread_local char g_err[256];
 bool hip_ok(hipError_t e, const char* what);
 #define HIPOK(call) ::orbx::hip_ok((call), #call)
 
-// A growable device allocation (contents are not preserved across growth).
+// A growable device allocation (contents are not preserved across growth), or a view of
+// part of another one (view(): never freed through this object).
 struct DevBuf {
     void* p = nullptr;
     size_t n = 0;
+    bool own = true;
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         n = 0;
+        own = true;
+    }
+    void view(void* base, size_t bytes) {
+        release();
+        p = base;
+        n = bytes;
+        own = false;
     }
     bool ensure(size_t bytes) {
-        if (bytes <= n && p) return true;
+        if (bytes <= n && p && own) return true;
         release();
         if (bytes == 0) bytes = 16;
         if (!HIPOK(hipMalloc(&p, bytes))) { p = nullptr; return false; }

@@ -196,6 +196,10 @@ struct Geometry {
 // compass's b128 reads) with room for the widest lane's reads (16 pixels per lane, 2 lanes
 // per detection row up to 32 columns, else 4).  A bank-conflict-free pitch (24 / 48 dwords)
 // was measured slower: the larger ROI costs a workgroup per CU.
+#ifndef FAST_NC
+#define FAST_NC 4        // k_fast cells per wave at large batches (the next cell's ROI loads
+                         // overlap this cell's work); small batches take fewer
+#endif
 #ifndef FAST_STAGE2D
 #define FAST_STAGE2D 1   // k_fast ROI prefetch on a 16-lanes-per-row grid (no index divisions)
 #endif

@@ -122,6 +122,10 @@ struct ExtractLaunch {
     size_t octree_lds;
     int ncap1, kcap1;        // levels 1.. (a second launch with a smaller LDS footprint)
     size_t octree_lds1;
+    // small batches (a few octree workgroups on the chip): the large LDS budget
+    int oct_small = 0, kcap_small = 0;
+    size_t octree_lds_small = 0;
+    int fast_nc = 4;         // k_fast cells per wave
     float* kps;
     uint8_t* desc;
     int* nkp;

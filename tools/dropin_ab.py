@@ -1,0 +1,60 @@
+"""A/B of the drop-in host path's small-batch policies (run on the GPU box).
+
+Runs tests/native/boundary_test `bench` against a tuning build of liborbx.so
+(tools/_var/tune/liborbx.so, built with -DORBX_TUNING, which reads the ORBX_* overrides of
+orbx_capi.hip) for each setting and K, and prints median / mean latency and pairs/s.
+    python tools/dropin_ab.py build            # here (hipcc)
+    python tools/dropin_ab.py run DIR [K,..]   # on the box, DIR from tools/dropin_data.py
+"""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+VAR = ROOT / "tools" / "_var" / "tune"
+
+SETTINGS = {
+    "r03": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4"},
+    "oct_small": {"ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4"},
+    "no_side": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_FAST_NC": "4"},
+    "fast_nc1": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0"},
+    "all": {},
+}
+
+
+def build():
+    from my_orb_slam2_amd import build as b
+    VAR.mkdir(parents=True, exist_ok=True)
+    srcs = [str(b.CSRC / s) for s in b.SOURCES]
+    cmd = ([b.hipcc()] + b.FLAGS + ["-DORBX_TUNING", f'-DORBX_SRC_HASH="{b.source_hash()}"'] +
+           srcs + ["-o", str(VAR / "liborbx.so")])
+    subprocess.run(cmd, check=True)
+    print(VAR / "liborbx.so")
+
+
+def run(d, ks):
+    binp = ROOT / "tests" / "native" / "boundary_test"
+    for name, env_set in SETTINGS.items():
+        for K in ks:
+            env = dict(os.environ, LD_LIBRARY_PATH=str(VAR), **env_set)
+            frames = 200 if K == 1 else 100
+            r = subprocess.run([str(binp), "bench", d, str(frames), "20", str(K)], env=env,
+                               capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                print(name, K, "FAILED", r.stderr[-1000:], flush=True)
+                raise SystemExit(1)
+            j = json.loads(r.stdout.strip().splitlines()[-1])
+            v = sorted(j["latency_ms"])
+            print(f"{name:10s} K={K}  median {v[len(v) // 2]:.3f} ms  mean {sum(v) / len(v):.3f} ms"
+                  f"  {K * frames / (j['wall_ms'] / 1000):8.0f} pairs/s  agree "
+                  f"{len(set(j['digests'])) == 1}", flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    else:
+        run(sys.argv[2], [int(k) for k in (sys.argv[3] if len(sys.argv) > 3 else "1,8").split(",")])
