@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -60,6 +61,10 @@ struct orbx_extractor {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_mode = FAST_SIDE, side_at = FAST_SIDE_AT, side_lv = FAST_SIDE_LV;
     bool side_auto = true;   // the built-in default: no side branch below SIDE_MIN_BATCH images
+    // orbx_extract's device sequence (H2D, kernels, D2H) as one HIP graph, rebuilt when its
+    // key (image size, effective schedule, every buffer address it names) changes
+    hipGraphExec_t g1 = nullptr;
+    std::vector<const void*> g1key;
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -798,8 +803,10 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
 }
 
 // d_imgs == nullptr: level 0 of every image is already in the pyramid (in place).
-orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
-                        int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
+// The launch descriptor of one batched extraction (d_imgs == nullptr: level 0 of every image
+// is already in the pyramid, in place).
+ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
+                             int split, int batch, size_t stride, size_t batch_stride) {
     ExtractLaunch a;
     a.in_place = d_imgs == nullptr;
     if (a.in_place) {
@@ -854,6 +861,12 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
     strip_heights(h, batch, a.sth);
+    return a;
+}
+
+orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t* d_imgs2,
+                        int split, int batch, size_t stride, size_t batch_stride, hipStream_t st) {
+    const ExtractLaunch a = extract_launch(h, d_imgs, d_imgs2, split, batch, stride, batch_stride);
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
@@ -1071,6 +1084,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
                       &h->d_outs};
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
+    if (h->g1) (void)hipGraphExecDestroy(h->g1);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->done) (void)hipEventDestroy(h->done);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
@@ -1092,6 +1106,40 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
         if (features_per_level) features_per_level[i] = h->nfeat[i];
     }
     return ORBX_OK;
+}
+
+#ifndef EXTRACT_GRAPH
+#define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
+#endif
+
+// The graph of orbx_extract's device sequence for the handle's current state, captured on st
+// when missing or stale.
+static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_t st, int width,
+                           int height, const std::function<bool(const ExtractLaunch&)>& enqueue) {
+    const DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr,
+                            &h->d_blur, &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp,
+                            &h->d_kscr, &h->d_outs};
+    std::vector<const void*> key = {(const void*)(intptr_t)width, (const void*)(intptr_t)height,
+                                    (const void*)(intptr_t)a.side_mode,
+                                    (const void*)(intptr_t)a.side_at,
+                                    (const void*)(intptr_t)a.side_lv, h->h_in, h->h_out};
+    for (const DevBuf* b : bufs) key.push_back(b->p);
+    if (h->g1 && key == h->g1key) return true;
+    if (h->g1) {
+        (void)hipGraphExecDestroy(h->g1);
+        h->g1 = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    if (!HIPOK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal))) return false;
+    const bool ok = enqueue(a);
+    const bool ended = HIPOK(hipStreamEndCapture(st, &g));
+    hipGraphExec_t ex = nullptr;
+    const bool inst = ok && ended && g && HIPOK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    if (g) (void)hipGraphDestroy(g);
+    if (!inst) return false;
+    h->g1 = ex;
+    h->g1key = key;
+    return true;
 }
 
 orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
@@ -1124,15 +1172,24 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
         return ORBX_ERR_DEVICE;
     for (int y = 0; y < height; ++y)
         std::memcpy(h->h_in + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
-    if (!order_after_last(h, st) ||
-        !HIPOK(hipMemcpyAsync(h->d_pyr.as<uint8_t>() + L0.off, h->h_in, img_bytes,
-                              hipMemcpyHostToDevice, st)))
+    if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
+    // the device sequence: one linear DMA into level 0, the kernels, one DMA of the outputs
+    auto enqueue = [&](const ExtractLaunch& a) {
+        return HIPOK(hipMemcpyAsync(h->d_pyr.as<uint8_t>() + L0.off, h->h_in, img_bytes,
+                                    hipMemcpyHostToDevice, st)) &&
+               HIPOK(launch_extract(a, st)) &&
+               HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st));
+    };
+    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 1, 1, 0, 0);
+    // replayed from a graph (one launch instead of ~15 enqueues: several tracking sessions
+    // on one GPU contend for the runtime's per-call work), eagerly when kernels are timed
+    const bool graph = tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
+                       extract1_graph(h, a, st, width, height, enqueue);
+    if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue(a)) || !mark_done(h, st) ||
+        !HIPOK(hipStreamSynchronize(st)))
         return ORBX_ERR_DEVICE;
-    s = run_extract(h, nullptr, nullptr, 1, 1, 0, 0, st);
-    if (s != ORBX_OK) return s;
-    if (!HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) ||
-        !mark_done(h, st) || !HIPOK(hipStreamSynchronize(st)))
-        return ORBX_ERR_DEVICE;
+    h->last_batch = 1;
+    h->last_valid = true;
     int n = 0;
     std::memcpy(&n, h->h_out, 4);
     *n_out = n;

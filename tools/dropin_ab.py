@@ -16,11 +16,15 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 VAR = ROOT / "tools" / "_var" / "tune"
 
+R03 = {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4",
+       "ORBX_EXTRACT_GRAPH": "0"}
 SETTINGS = {
-    "r03": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4"},
-    "oct_small": {"ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4"},
-    "no_side": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_FAST_NC": "4"},
-    "fast_nc1": {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0"},
+    "r03": R03,
+    "oct_small": dict(R03, ORBX_OCT_SMALL_BATCH="4"),
+    "no_side": dict(R03, ORBX_SIDE_MIN_BATCH="16"),
+    "fast_nc1": dict(R03, ORBX_FAST_NC="1"),
+    "graph": dict(R03, ORBX_EXTRACT_GRAPH="1"),
+    "all_nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "all": {},
 }
 
