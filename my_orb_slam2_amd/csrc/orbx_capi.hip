@@ -915,7 +915,8 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
         // (a fixed counter block: one slot per pair of the largest split batch, so a later
         // call with another batch finds its counters zero)
         // (stereo_split(batch) > 1 only for batch <= 128, so 256 counters always suffice)
-        const size_t cnt_bytes = 256 * 4;
+        // (then 256 done-counters of the fused cut, also zero on entry and left zero)
+        const size_t cnt_bytes = 2 * 256 * 4;
         const size_t need = cnt_bytes + (size_t)batch * KC * 6;
         // a reallocation (detected by capacity: the allocator may hand back the same
         // address) starts from zeroed counters

@@ -331,7 +331,29 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             }
         }
     }
-    if (nsplit > 1) return;
+    if (nsplit > 1) {
+#if ST_FUSED_CUT
+        // the pair's last workgroup to finish takes the median over the global scratch (the
+        // others' SADs are visible after their release fence and this one's acquire): no
+        // second launch for the cut
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            tmp[17] = atomicAdd(&scnt[256 + b], 1) == nsplit - 1;
+        }
+        __syncthreads();
+        if (!tmp[17]) return;
+        __threadfence();
+        const int nv = min(__hip_atomic_load(&scnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), KC);
+        __syncthreads();
+        if (tid == 0) {
+            scnt[b] = 0;
+            scnt[256 + b] = 0;
+        }
+        median_cut(nv, ssad + (size_t)b * KC, sidx + (size_t)b * KC, hist, tmp, uR, dep, nvalid, b);
+#endif
+        return;
+    }
     __syncthreads();
     median_cut(tmp[16], vsad, vidx, hist, tmp, uR, dep, nvalid, b);
 }
@@ -430,6 +452,9 @@ hipError_t prepare_stereo(size_t lds) {
 #ifndef ST_SPLIT
 #define ST_SPLIT 4
 #endif
+#ifndef ST_FUSED_CUT
+#define ST_FUSED_CUT 1   // split path: the last workgroup of a pair runs the cut (no k_stereo_cut)
+#endif
 int stereo_split(int batch) {
     int ns = ST_SPLIT;
     while (ns > 1 && batch * ns > 256) ns >>= 1;
@@ -444,10 +469,10 @@ hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {
     if (!e0 || !e1) e0 = e1 = nullptr;
     const int ns = stereo_split(a.batch);
     hipExtLaunchKernelGGL(k_stereo, dim3(a.batch * ns), dim3(ST_THREADS), (uint32_t)a.lds, st, e0,
-                          ns > 1 ? nullptr : e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
+                          (ns > 1 && !ST_FUSED_CUT) ? nullptr : e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
                           a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb, a.uR, a.depth, a.nvalid,
                           ns, a.scnt, a.ssad, a.sidx);
-    if (ns > 1)
+    if (ns > 1 && !ST_FUSED_CUT)
         hipExtLaunchKernelGGL(k_stereo_cut, dim3(a.batch), dim3(ST_THREADS), 0u, st, nullptr, e1, 0u,
                               a.dg, a.uR, a.depth, a.nvalid, a.scnt, (const int*)a.ssad,
                               (const int16_t*)a.sidx);
