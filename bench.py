@@ -99,7 +99,7 @@ def parse():
                          "--db-rows database rows, rows sharded, RCCL all-gather + merge)")
     ap.add_argument("--frames", type=int, default=300,
                     help="dropin: timed stereo frames per tracker (after --warmup frames, at least 20)")
-    ap.add_argument("--trackers", default="1",
+    ap.add_argument("--trackers", default="1,2,4,8",
                     help="dropin: comma-separated numbers of concurrent tracking sessions K (each "
                          "its own left / right handles and threads, sharing the GPU); one result "
                          "line holds every K")

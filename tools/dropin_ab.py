@@ -26,6 +26,8 @@ SETTINGS = {
     "graph": dict(R03, ORBX_EXTRACT_GRAPH="1"),
     "all_nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "all": {},
+    "all_q8": {"GPU_MAX_HW_QUEUES": "8"},
+    "all_q16": {"GPU_MAX_HW_QUEUES": "16"},
 }
 
 
