@@ -1,0 +1,153 @@
+// ORBextractor.h — drop-in replacement for ORB-SLAM2's include/ORBextractor.h (:45-111) and
+// src/ORBextractor.cc, header-only, over liborbx's C ABI (include/orbx.h).
+//
+// A maintainer copies this file over include/ORBextractor.h, deletes src/ORBextractor.cc from
+// the ORB_SLAM2 library sources, adds <repo>/include to the include path and links
+// <repo>/my_orb_slam2_amd/liborbx.so.  Callers (Frame.cc:80-86, :140-146, :195-201 and the
+// ExtractORB threads at Frame.cc:89-92) compile unchanged: the constructor, operator() and the
+// getters keep the reference's signatures and results.
+//
+// One difference: mvImagePyramid is no longer filled by every operator() call.  Its only
+// reader in the reference is Frame::ComputeStereoMatches (Frame.cc:503-619), which the glue in
+// orbx_slam2_glue.h replaces with the device-resident orbx_stereo_match.  Code that still needs
+// the host pyramid calls MaterializePyramid() after operator().
+#ifndef ORBX_INTEGRATION_ORBEXTRACTOR_H
+#define ORBX_INTEGRATION_ORBEXTRACTOR_H
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <opencv2/core/core.hpp>
+
+#include "orbx.h"
+
+namespace ORB_SLAM2 {
+
+class ORBextractor {
+public:
+    enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+    // ORBextractor.cc:410-470: the scale / sigma tables and per-level feature budget come
+    // from liborbx (same float arithmetic as the reference constructor).
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+        : nfeatures(nfeatures), scaleFactor(scaleFactor), nlevels(nlevels),
+          iniThFAST(iniThFAST), minThFAST(minThFAST), cap(std::max(4096, 2 * nfeatures)) {
+        orbx_extractor_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                                /*cv_simd=*/1, /*max_batch=*/1, /*device=*/0};
+        check(orbx_extractor_create(&p, &h), "orbx_extractor_create");
+        mvScaleFactor.resize(nlevels);
+        mvInvScaleFactor.resize(nlevels);
+        mvLevelSigma2.resize(nlevels);
+        mvInvLevelSigma2.resize(nlevels);
+        mnFeaturesPerLevel.resize(nlevels);
+        check(orbx_extractor_tables(h, mvScaleFactor.data(), mvInvScaleFactor.data(),
+                                    mvLevelSigma2.data(), mvInvLevelSigma2.data(),
+                                    mnFeaturesPerLevel.data()),
+              "orbx_extractor_tables");
+    }
+    ~ORBextractor() { orbx_extractor_destroy(h); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    // ORBextractor.cc:1065-1127.  The mask is ignored, as in the reference.
+    void operator()(cv::InputArray _image, cv::InputArray /*mask*/,
+                    std::vector<cv::KeyPoint>& keypoints, cv::OutputArray _descriptors) {
+        if (_image.empty()) return;  // :1068-1069
+        cv::Mat image = _image.getMat();
+        if (image.type() != CV_8UC1)  // :1072 (an assert in the reference)
+            throw std::invalid_argument("ORBextractor: image must be CV_8UC1");
+        static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint),
+                      "cv::KeyPoint and orbx_keypoint must share their 28-byte layout");
+        int n = 0;
+        for (;;) {
+            keypoints.resize(cap);
+            desc.resize((size_t)cap * 32);
+            orbx_status s = orbx_extract(h, image.data, image.cols, image.rows,
+                                         (size_t)image.step,
+                                         reinterpret_cast<orbx_keypoint*>(keypoints.data()),
+                                         cap, desc.data(), &n);
+            if (s == ORBX_ERR_CAPACITY) {  // more keypoints than slots: n holds the count
+                cap = n;
+                continue;
+            }
+            check(s, "orbx_extract");
+            break;
+        }
+        pyramid_valid = false;
+        if (n < 0) {  // empty image inside liborbx as well: outputs untouched
+            keypoints.clear();
+            return;
+        }
+        keypoints.resize(n);
+        if (n == 0) {  // :1086-1088
+            _descriptors.release();
+            return;
+        }
+        _descriptors.create(n, 32, CV_8U);  // :1090-1091
+        cv::Mat d = _descriptors.getMat();
+        if (d.isContinuous()) {
+            std::memcpy(d.data, desc.data(), (size_t)n * 32);
+        } else {
+            for (int i = 0; i < n; ++i) std::memcpy(d.ptr(i), desc.data() + (size_t)i * 32, 32);
+        }
+    }
+
+    int inline GetLevels() { return nlevels; }
+    float inline GetScaleFactor() { return (float)scaleFactor; }
+    std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
+    std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor; }
+    std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
+
+    // Copies the last call's pyramid (ORBextractor.cc:1129-1155's levels, the unblurred
+    // images) into mvImagePyramid; a no-op when it is already current.
+    std::vector<cv::Mat>& MaterializePyramid() {
+        if (!pyramid_valid) {
+            mvImagePyramid.resize(nlevels);
+            for (int l = 0; l < nlevels; ++l) {
+                int w = 0, hh = 0;
+                check(orbx_pyramid_level(h, 0, l, nullptr, &w, &hh), "orbx_pyramid_level");
+                mvImagePyramid[l].create(hh, w, CV_8U);
+                check(orbx_pyramid_level(h, 0, l, mvImagePyramid[l].data, &w, &hh),
+                      "orbx_pyramid_level");
+            }
+            pyramid_valid = true;
+        }
+        return mvImagePyramid;
+    }
+
+    // The liborbx handle, for orbx_stereo_match (orbx_slam2_glue.h).
+    orbx_extractor* handle() const { return h; }
+
+    std::vector<cv::Mat> mvImagePyramid;
+
+protected:
+    static void check(orbx_status s, const char* what) {
+        if (s != ORBX_OK)
+            throw std::runtime_error(std::string(what) + ": " + orbx_last_error());
+    }
+
+    orbx_extractor* h = nullptr;
+    int nfeatures;
+    double scaleFactor;
+    int nlevels;
+    int iniThFAST;
+    int minThFAST;
+    std::vector<int> mnFeaturesPerLevel;
+    std::vector<float> mvScaleFactor;
+    std::vector<float> mvInvScaleFactor;
+    std::vector<float> mvLevelSigma2;
+    std::vector<float> mvInvLevelSigma2;
+
+private:
+    int cap;                       // keypoint slots; grows to the largest count seen
+    std::vector<uint8_t> desc;     // descriptor rows before the copy into _descriptors
+    bool pyramid_valid = false;
+};
+
+}  // namespace ORB_SLAM2
+
+#endif  // ORBX_INTEGRATION_ORBEXTRACTOR_H

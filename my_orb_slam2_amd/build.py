@@ -116,3 +116,31 @@ def build_boundary_test(force: bool = False, verbose: bool = False) -> pathlib.P
     subprocess.run(cmd, check=True)
     os.replace(str(BOUNDARY_BIN) + ".tmp", BOUNDARY_BIN)
     return BOUNDARY_BIN
+
+
+# ---- the drop-in facade compiled as ORB-SLAM2 would include it (tests/native/facade_test.cpp) --
+FACADE_SRC = PKG.parent / "tests" / "native" / "facade_test.cpp"
+FACADE_BIN = PKG.parent / "tests" / "native" / "facade_test"
+
+
+def build_facade_test(force: bool = False, verbose: bool = False) -> pathlib.Path:
+    """g++ on integration/ORBextractor.h + integration/orbx_slam2_glue.h with the cv stand-in
+    headers of tests/native/cv_standin, linked to the in-tree liborbx.so."""
+    root = PKG.parent
+    deps = ([FACADE_SRC] + sorted((root / "include").glob("*.h")) +
+            sorted((root / "integration").glob("*.h")) +
+            sorted((root / "tests" / "native" / "cv_standin").rglob("*.hpp")))
+    newest = max(p.stat().st_mtime for p in deps)
+    if not force and FACADE_BIN.exists() and FACADE_BIN.stat().st_mtime >= newest:
+        return FACADE_BIN
+    build(verbose=verbose)
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-I" + str(root / "include"),
+           "-I" + str(root / "integration"), "-I" + str(root / "tests" / "native" / "cv_standin"),
+           str(FACADE_SRC), "-L" + str(PKG), "-lorbx", "-L/opt/rocm/lib",
+           "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,-rpath,$ORIGIN/../../my_orb_slam2_amd",
+           "-pthread", "-o", str(FACADE_BIN) + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(FACADE_BIN) + ".tmp", FACADE_BIN)
+    return FACADE_BIN

@@ -1,0 +1,217 @@
+// facade_test — the drop-in facade of INTEGRATION.md compiled and run as ORB-SLAM2 would use it:
+// integration/ORBextractor.h (ORB_SLAM2::ORBextractor over liborbx) and
+// integration/orbx_slam2_glue.h (Frame::ComputeStereoMatches, the featureset views,
+// ORBmatcher::SearchByBoW), with Frame / KeyFrame / MapPoint reduced to the members the facade
+// reads.  cv:: comes from tests/native/cv_standin (this image has no OpenCV).
+//
+//   facade_test nogpu     the ORBextractor constructor on a host without a GPU: must throw
+//                         std::runtime_error naming the failing call (no silent fallback)
+//   facade_test run DIR   DIR holds left.raw / right.raw (W*H bytes) and params.txt
+//                         ("W H nfeatures mbf"); writes the same raw arrays as boundary_test
+//                         `run` (n, nr, nvalid, kps/desc of both views, uRight, depth, bow)
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ORBextractor.h"
+#include "orbx_slam2_glue.h"
+
+namespace {
+
+constexpr int FRAME_GRID_COLS = 64;  // Frame.h:33-34
+constexpr int FRAME_GRID_ROWS = 48;
+
+struct MapPoint {
+    bool bad = false;
+    bool isBad() const { return bad; }
+};
+
+// The members of ORB_SLAM2::Frame (Frame.h) the facade reads or writes.
+struct Frame {
+    ORB_SLAM2::ORBextractor* mpORBextractorLeft = nullptr;
+    ORB_SLAM2::ORBextractor* mpORBextractorRight = nullptr;
+    float fx = 0.f, mbf = 0.f;
+    int N = 0;
+    std::vector<cv::KeyPoint> mvKeys, mvKeysRight, mvKeysUn;
+    cv::Mat mDescriptors, mDescriptorsRight;
+    std::vector<float> mvuRight, mvDepth;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    std::vector<std::size_t> mGrid[FRAME_GRID_COLS][FRAME_GRID_ROWS];
+    float mnMinX = 0.f, mnMinY = 0.f, mnMaxX = 0.f, mnMaxY = 0.f;
+    float mfGridElementWidthInv = 0.f, mfGridElementHeightInv = 0.f;
+
+    // Frame.cc:240-249
+    void ExtractORB(int flag, const cv::Mat& im) {
+        if (flag == 0)
+            (*mpORBextractorLeft)(im, cv::Mat(), mvKeys, mDescriptors);
+        else
+            (*mpORBextractorRight)(im, cv::Mat(), mvKeysRight, mDescriptorsRight);
+    }
+};
+
+// The members of ORB_SLAM2::KeyFrame SearchByBoW reads.
+struct KeyFrame {
+    int N = 0;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<MapPoint*> GetMapPointMatches() const { return mvpMapPoints; }
+};
+
+bool read_file(const std::string& path, std::vector<uint8_t>& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize((size_t)n);
+    const bool ok = std::fread(out.data(), 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok;
+}
+
+bool write_file(const std::string& path, const void* p, size_t n) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = n == 0 || std::fwrite(p, 1, n, f) == n;
+    std::fclose(f);
+    return ok;
+}
+
+int nogpu() {
+    try {
+        ORB_SLAM2::ORBextractor ex(1000, 1.2f, 8, 20, 7);
+    } catch (const std::runtime_error& e) {
+        std::printf("facade_test: constructor threw: %s\n", e.what());
+        return std::strstr(e.what(), "orbx_extractor_create") ? 0 : 5;
+    }
+    std::printf("facade_test: constructor succeeded without a GPU\n");
+    return 6;
+}
+
+int run(const std::string& dir) {
+    int W = 0, H = 0, nfeat = 0;
+    float mbf = 0.f;
+    {
+        FILE* f = std::fopen((dir + "/params.txt").c_str(), "r");
+        if (!f) return 2;
+        const int got = std::fscanf(f, "%d %d %d %f", &W, &H, &nfeat, &mbf);
+        std::fclose(f);
+        if (got != 4) return 2;
+    }
+    std::vector<uint8_t> L, R;
+    if (!read_file(dir + "/left.raw", L) || !read_file(dir + "/right.raw", R) ||
+        L.size() != (size_t)W * H || R.size() != (size_t)W * H)
+        return 2;
+
+    // Tracking.cc:136-139: one extractor per camera
+    ORB_SLAM2::ORBextractor left(nfeat, 1.2f, 8, 20, 7), right(nfeat, 1.2f, 8, 20, 7);
+    if (left.GetLevels() != 8 || left.GetScaleFactors().size() != 8 ||
+        left.GetScaleFactor() != 1.2f || left.GetScaleSigmaSquares()[1] != 1.2f * 1.2f) {
+        std::printf("facade_test: scale tables differ\n");
+        return 4;
+    }
+    // an empty image returns without touching the outputs (ORBextractor.cc:1068-1069)
+    {
+        std::vector<cv::KeyPoint> kp(3);
+        cv::Mat d;
+        left(cv::Mat(), cv::Mat(), kp, d);
+        if (kp.size() != 3 || !d.empty()) {
+            std::printf("facade_test: empty image changed the outputs\n");
+            return 4;
+        }
+    }
+    Frame F;
+    F.mpORBextractorLeft = &left;
+    F.mpORBextractorRight = &right;
+    F.mbf = mbf;
+    F.fx = 718.856f;  // KITTI 00-02 (Examples/Stereo/KITTI00-02.yaml)
+    // the image rows are W bytes apart; a Mat over a wider buffer checks `step` handling
+    const size_t pitch = (size_t)W + 24;
+    std::vector<uint8_t> Lp(pitch * H, 0xA5);
+    for (int y = 0; y < H; ++y) std::memcpy(&Lp[(size_t)y * pitch], &L[(size_t)y * W], (size_t)W);
+    const cv::Mat imL(H, W, CV_8UC1, Lp.data(), pitch), imR(H, W, CV_8UC1, R.data());
+    {   // Frame.cc:89-92
+        std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
+        std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
+        tl.join();
+        tr.join();
+    }
+    F.N = (int)F.mvKeys.size();
+    const int nr = (int)F.mvKeysRight.size();
+    if (F.N == 0 || nr == 0 || F.mDescriptors.rows != F.N || F.mDescriptors.cols != 32 ||
+        !F.mDescriptors.isContinuous()) {
+        std::printf("facade_test: bad extraction outputs\n");
+        return 4;
+    }
+    // mvImagePyramid on request: level 0 is the input image
+    {
+        std::vector<cv::Mat>& pyr = left.MaterializePyramid();
+        if (pyr.size() != 8 || pyr[0].rows != H || pyr[0].cols != W) return 4;
+        for (int y = 0; y < H; ++y)
+            if (std::memcmp(pyr[0].ptr(y), &L[(size_t)y * W], (size_t)W) != 0) {
+                std::printf("facade_test: mvImagePyramid[0] differs from the input\n");
+                return 4;
+            }
+    }
+    const int nvalid = orbx_glue::ComputeStereoMatches(F);
+
+    // SearchByBoW(KF = right view, F = left view), one vocabulary node holding every feature
+    F.mvKeysUn = F.mvKeys;
+    for (int i = 0; i < F.N; ++i) F.mFeatVec[0].push_back((unsigned)i);
+    Frame KFf;
+    KFf.N = nr;
+    KFf.mvKeysUn = F.mvKeysRight;
+    KFf.mDescriptors = F.mDescriptorsRight;
+    for (int i = 0; i < nr; ++i) KFf.mFeatVec[0].push_back((unsigned)i);
+    orbx_glue::OrbxView fv, kv;
+    orbx_glue::BuildView(F, fv, FRAME_GRID_COLS, FRAME_GRID_ROWS);
+    orbx_glue::BuildView(KFf, kv, FRAME_GRID_COLS, FRAME_GRID_ROWS);
+    kv.fs.u_right = nullptr;
+    fv.fs.u_right = nullptr;
+    std::vector<MapPoint> points((size_t)nr);
+    KeyFrame KF;
+    KF.N = nr;
+    for (MapPoint& p : points) KF.mvpMapPoints.push_back(&p);
+    orbx_matcher* m = nullptr;
+    const orbx_matcher_params mp = {0.75f, 1, 0};
+    orbx_glue::check(orbx_matcher_create(&mp, &m), "orbx_matcher_create");
+    std::vector<MapPoint*> matches;
+    const int nbow = orbx_glue::SearchByBoW(m, &KF, kv, F, fv, matches);
+    orbx_matcher_destroy(m);
+    std::vector<int32_t> bow(1 + (size_t)F.N, -1);
+    bow[0] = nbow;
+    for (int i = 0; i < F.N; ++i)
+        if (matches[(size_t)i]) bow[1 + (size_t)i] = (int32_t)(matches[(size_t)i] - points.data());
+
+    const bool ok =
+        write_file(dir + "/n.bin", &F.N, 4) && write_file(dir + "/nr.bin", &nr, 4) &&
+        write_file(dir + "/nvalid.bin", &nvalid, 4) &&
+        write_file(dir + "/kps_left.bin", F.mvKeys.data(), F.mvKeys.size() * 28) &&
+        write_file(dir + "/desc_left.bin", F.mDescriptors.data, (size_t)F.N * 32) &&
+        write_file(dir + "/kps_right.bin", F.mvKeysRight.data(), F.mvKeysRight.size() * 28) &&
+        write_file(dir + "/desc_right.bin", F.mDescriptorsRight.data, (size_t)nr * 32) &&
+        write_file(dir + "/uRight.bin", F.mvuRight.data(), F.mvuRight.size() * 4) &&
+        write_file(dir + "/depth.bin", F.mvDepth.data(), F.mvDepth.size() * 4) &&
+        write_file(dir + "/bow.bin", bow.data(), bow.size() * 4);
+    std::printf("facade_test: %d / %d keypoints, %d stereo, %d bow\n", F.N, nr, nvalid, nbow);
+    return ok ? 0 : 3;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "";
+    try {
+        if (mode == "nogpu") return nogpu();
+        if (mode == "run" && argc > 2) return run(argv[2]);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "facade_test: %s\n", e.what());
+        return 1;
+    }
+    std::fprintf(stderr, "usage: facade_test nogpu | run DIR\n");
+    return 2;
+}

@@ -1,0 +1,81 @@
+"""The drop-in facade itself, compiled: integration/ORBextractor.h (ORB_SLAM2::ORBextractor,
+include/ORBextractor.h:45-111 of the reference) and integration/orbx_slam2_glue.h
+(Frame::ComputeStereoMatches, Frame.cc:496-686; ORBmatcher::SearchByBoW, ORBmatcher.cc:182-319)
+built by g++ into tests/native/facade_test.cpp, with the cv:: types from the stand-in headers of
+tests/native/cv_standin (no OpenCV in this image: the stand-in keeps OpenCV's member names and
+semantics, so this proves the facade's marshalling, not OpenCV itself).
+
+* CPU: the program compiles with -Wall -Wextra, and the ORBextractor constructor on a host
+  without a GPU throws std::runtime_error naming the failing call (no silent fallback).
+* GPU: Frame's two ExtractORB threads (Frame.cc:89-92) on the KITTI fixture pair, the left image
+  behind a padded row stride, the stereo glue and SearchByBoW: keypoints, descriptors, uRight and
+  depth equal the committed golden digests (tests/golden/fixtures.json), the matches equal the
+  restated matcher's.
+"""
+import hashlib
+import json
+import pathlib
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+GOLDEN = json.loads((ROOT / "tests" / "golden" / "fixtures.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def facade_bin(orbx_lib):
+    from my_orb_slam2_amd import build as b
+    return b.build_facade_test()
+
+
+def test_facade_fails_loudly_without_gpu(facade_bin):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = subprocess.run([str(facade_bin), "nogpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "orbx_extractor_create" in r.stdout
+
+
+def _sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed):
+    from oracle import matcher as om
+    from my_orb_slam2_amd import synth
+    from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
+    from my_orb_slam2_amd.features import FeatureSet, feature_vector
+    g = GOLDEN[f"kitti_stereo_seed{seed}"]
+    L, R = synth.stereo_pair(seed)
+    assert [_sha(L.tobytes()), _sha(R.tobytes())] == g["input_sha256"]
+    H, W = L.shape
+    (tmp_path / "left.raw").write_bytes(L.tobytes())
+    (tmp_path / "right.raw").write_bytes(R.tobytes())
+    (tmp_path / "params.txt").write_text(f"{W} {H} {g['params'][0]} {g['mbf']!r}\n")
+    r = subprocess.run([str(facade_bin), "run", str(tmp_path)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rd = lambda name: (tmp_path / name).read_bytes()
+    n = int(np.frombuffer(rd("n.bin"), np.int32)[0])
+    nr = int(np.frombuffer(rd("nr.bin"), np.int32)[0])
+    assert (n, nr) == (g["n_left"], g["n_right"])
+    assert int(np.frombuffer(rd("nvalid.bin"), np.int32)[0]) == g["n_valid"]
+    for key, fname in (("kps_left", "kps_left.bin"), ("desc_left", "desc_left.bin"),
+                       ("kps_right", "kps_right.bin"), ("desc_right", "desc_right.bin"),
+                       ("uRight", "uRight.bin"), ("depth", "depth.bin")):
+        assert _sha(rd(fname)) == g["sha256"][key], key
+    kl = np.frombuffer(rd("kps_left.bin"), KEYPOINT_DTYPE)
+    kr = np.frombuffer(rd("kps_right.bin"), KEYPOINT_DTYPE)
+    dl = np.frombuffer(rd("desc_left.bin"), np.uint8).reshape(-1, 32)
+    dr = np.frombuffer(rd("desc_right.bin"), np.uint8).reshape(-1, 32)
+    F = FeatureSet(kl.copy(), dl.copy(), None, feature_vector(np.zeros(n)), None)
+    KF = FeatureSet(kr.copy(), dr.copy(), None, feature_vector(np.zeros(nr)), None)
+    bow = np.frombuffer(rd("bow.bin"), np.int32)
+    n_o, m_o = om.search_by_bow_kf_frame(KF, np.ones(nr, bool), F, 0.75, True)
+    assert bow[0] == n_o and n_o > 0
+    np.testing.assert_array_equal(bow[1:], m_o)
