@@ -25,6 +25,9 @@ namespace orbx {
 #define ST_THREADS 1024
 #endif
 #define ST_WAVES (ST_THREADS / 64)
+#ifndef ST_FUSED_CUT
+#define ST_FUSED_CUT 1   // split path: the last workgroup of a pair runs the cut (no k_stereo_cut)
+#endif
 
 // N bytes of a pyramid row starting at x, as ceil(N/4) dwords realigned to x (bytes of
 // dword i = row[x + 4i .. x + 4i + 3]).  Rows are 64-byte aligned with >= 4 bytes of slack.
@@ -451,9 +454,6 @@ hipError_t prepare_stereo(size_t lds) {
 // 0.080 / 0.070 ms; 512 pairs are not split.
 #ifndef ST_SPLIT
 #define ST_SPLIT 4
-#endif
-#ifndef ST_FUSED_CUT
-#define ST_FUSED_CUT 1   // split path: the last workgroup of a pair runs the cut (no k_stereo_cut)
 #endif
 int stereo_split(int batch) {
     int ns = ST_SPLIT;
