@@ -778,16 +778,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #ifndef STRIP_PEEL
 #define STRIP_PEEL 1   // interior blocks of a walk without store predicates
 #endif
-// BLUR_STRIPE: the blurred rows staged in LDS (7 rows of a wave's 60 groups) and written as
-// 16-byte stripe rows every 7 steps: two buffer_store_dwordx4 per 7 rows, each covering
-// 7-row runs of the wave's 15 stripes, instead of a dword per lane per row scattered over 15
-// stripes (STRIP_BLR_LDS 0)
-#ifndef STRIP_BLR_LDS
-#define STRIP_BLR_LDS 1
-#endif
-#ifndef STRIP_BLR_LDS0
-#define STRIP_BLR_LDS0 0   // also for level 0 (modes 0 / 4: their 7-slot load ring leaves no room)
-#endif
 #ifndef STRIP_NS3
 #define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
 #endif
@@ -1014,38 +1004,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
     auto store_blr = [&](int r, bool ok, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, rblr, ok ? blane_off : 0x80000000u, ok ? r * 16 : 0, STRIP_ST_POLICY);
     };
-    constexpr bool BLR_LDS = STRIP_BLR_LDS && (MODE == 3 || STRIP_BLR_LDS0);
-#if STRIP_BLR_LDS
-    // the wave's 60 output groups (lane l32 of half h: group 30 h + l32 - 1; the other lanes
-    // write the spare slots 60..63) of the last 7 blurred rows, relative row r in slot r % 7
-    __shared__ __attribute__((aligned(16))) uint32_t s_blr[8 * 7 * 64];
-    uint32_t* const wbuf = s_blr + (threadIdx.x >> 6) * (7 * 64);
-    const int gslot = out_lane ? 30 * half + (l32 - 1) : 60 + (lane & 3);
-    // rows yb .. yb + 6 (relative to Y0; slots 0 .. 6): piece p = lane + 64 t (< 105) is stripe
-    // row (j = p / 15, stripe s = p % 15) of the wave's 15 stripes (the wave starts at x = 240
-    // swx, a multiple of 16); rows outside [0, vh) and stripes past the level are dropped (the
-    // buffer's range check for the latter)
-    auto blr_flush = [&](int yb) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const uint32_t soff = yb >= 0 ? 16u * (uint32_t)(Y0 + yb) : 0u;
-        // the lane's pieces are recomputed at every flush (an opaque copy of the lane id):
-        // hoisted out of the walk they would hold registers across every step
-        int ln = (int)threadIdx.x & 63;
-        asm volatile("" : "+v"(ln));
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int p = ln + 64 * t;
-            const int j = (p * 4370) >> 16, sx = p - 15 * j;   // p / 15, p % 15 for p < 128
-            const uint4 v = *(const uint4*)(wbuf + j * 64 + 4 * sx);
-            const int row = yb + j;
-            const bool ok = p < 105 && row >= 0 && row < vh && !(STRIP_DIAG & 1);
-            const uint32_t vo = ok ? (uint32_t)(15 * swx + sx) * (16u * (uint32_t)H) + 16u * (uint32_t)j
-                                   : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rblr, vo, soff,
-                                                   STRIP_ST_POLICY);
-        }
-    };
-#endif
 #else
     auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(rblr, r, ok, v); };
 #endif
@@ -1127,16 +1085,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
                     packed |= min(val, 255u) << (8 * j);
                 }
             }
-#if BLUR_STRIPE && STRIP_BLR_LDS && STRIP_BUFST
-            if constexpr (BLR_LDS) {
-                wbuf[((k + 1) % 7) * 64 + gslot] = packed;   // relative row i - 6 in slot (i - 6) % 7
-                if constexpr (k % 7 == 5) blr_flush(i - 12);
-            } else {
-                store_blr(Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
-            }
-#else
             store_blr(Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
-#endif
         }
     };
     constexpr int U = NS == 7 ? 7 : 7 * NS;   // steps per block: a multiple of NS and of 7
@@ -1172,10 +1121,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
         for (i0 = U; i0 + U <= vh + 3; i0 += U) block(i0, std::true_type{});
 #endif
         for (; i0 < n; i0 += U) block(i0, std::false_type{});
-#if BLUR_STRIPE && STRIP_BLR_LDS && STRIP_BUFST
-        // the rows produced after the last in-walk flush (blocks end on a step = 6 mod 7)
-        if constexpr (BLR_LDS) blr_flush(i0 - 7);
-#endif
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
     if ((L0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
