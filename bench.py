@@ -103,6 +103,9 @@ def parse():
                     help="dropin: comma-separated numbers of concurrent tracking sessions K (each "
                          "its own left / right handles and threads, sharing the GPU); one result "
                          "line holds every K")
+    ap.add_argument("--dropin-via", choices=["facade", "cabi"], default="facade",
+                    help="dropin: the ORB_SLAM2::ORBextractor facade loop (tests/native/"
+                         "facade_test) or the bare C-ABI loop (tests/native/boundary_test)")
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
     ap.add_argument("--db-rows", type=int, default=10_000_000,
                     help="bf: database descriptors (10k keyframes x 1000, SURVEY §8(d) C4)")
@@ -1035,7 +1038,10 @@ def main_dropin(args):
     Lh, Rh, pairs, _ = stereo_inputs(0, B, args.distinct)
     mb = float(np.float32(MBF) / np.float32(FX))
     warm = max(20, args.warmup)
-    binp = os.path.join(ROOT, "tests", "native", "boundary_test")
+    # the loop ORB-SLAM2 runs through the facade (integration/ORBextractor.h: a stereo Frame per
+    # frame, Frame.cc:66-120), or the same calls on the bare C ABI (--dropin-via cabi)
+    binp = os.path.join(ROOT, "tests", "native",
+                        "facade_test" if args.dropin_via == "facade" else "boundary_test")
     ks = [max(1, int(k)) for k in str(args.trackers).split(",")]
     per_k = {}
     with tempfile.TemporaryDirectory() as d:
@@ -1062,8 +1068,10 @@ def main_dropin(args):
         cpu = cpu_baseline(pairs, mb, min(args.cpu_seconds, 6.0))
     k0 = per_k[ks[0]]
     lat = k0["latency"]
-    out = {"metric": "per-stereo-frame latency of the drop-in host path (orbx_extract x2 on 2 "
-                     "threads + orbx_stereo_match), KITTI 1241x376",
+    via = ("ORB_SLAM2::ORBextractor facade: Frame::ExtractORB x2 on 2 threads + "
+           "ComputeStereoMatches" if args.dropin_via == "facade" else
+           "C ABI: orbx_extract x2 on 2 threads + orbx_stereo_match")
+    out = {"metric": f"per-stereo-frame latency of the drop-in host path ({via}), KITTI 1241x376",
            "value": 1000.0 / lat["mean_ms"] if ks[0] == 1 else k0["pairs_per_s"],
            "unit": "frames/sec", "n_gpus": 1,
            "steps": args.frames, "warmup": warm, "ms_per_step": lat["mean_ms"],
@@ -1071,7 +1079,7 @@ def main_dropin(args):
            "data": "synthetic",
            "config": {"workload": "kitti_stereo_dropin_host_path", "width": W, "height": H,
                       "nfeatures": NFEAT, "distinct_pairs": B, "threads_per_tracker": 2,
-                      "trackers": ks,
+                      "trackers": ks, "via": args.dropin_via,
                       "io": "host images in, host keypoints/descriptors/uRight/depth out"},
            "latency": lat, "mean_keypoints_left": k0["mean_keypoints_left"],
            "mean_stereo_matches": k0["mean_stereo_matches"],

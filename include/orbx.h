@@ -73,6 +73,15 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
                          size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
                          int* n_out);
 
+/* orbx_extract without the copies out: *kps / *desc point at the handle's own (pinned host)
+ * output block, *n_out keypoints and n x 32 descriptor bytes, valid until the next call that
+ * uses this handle (an extraction, or orbx_stereo_match with it as either view).  The facade's
+ * ORBextractor::operator() (integration/ORBextractor.h) copies them straight into its
+ * std::vector<cv::KeyPoint> and descriptor cv::Mat.  Empty image: *n_out = -1, NULL views. */
+orbx_status orbx_extract_view(orbx_extractor* h, const uint8_t* img, int width, int height,
+                              size_t stride, const orbx_keypoint** kps, const uint8_t** desc,
+                              int* n_out);
+
 /* Build the geometry and device workspace for width x height images and up to `batch`
  * images per call (otherwise done lazily by the first call); *kp_cap = keypoint slots per
  * image in the batched outputs. */

@@ -14,7 +14,6 @@
 #ifndef ORBX_INTEGRATION_ORBEXTRACTOR_H
 #define ORBX_INTEGRATION_ORBEXTRACTOR_H
 
-#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -34,7 +33,7 @@ public:
     // from liborbx (same float arithmetic as the reference constructor).
     ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
         : nfeatures(nfeatures), scaleFactor(scaleFactor), nlevels(nlevels),
-          iniThFAST(iniThFAST), minThFAST(minThFAST), cap(std::max(4096, 2 * nfeatures)) {
+          iniThFAST(iniThFAST), minThFAST(minThFAST) {
         orbx_extractor_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
                                 /*cv_simd=*/1, /*max_batch=*/1, /*device=*/0};
         check(orbx_extractor_create(&p, &h), "orbx_extractor_create");
@@ -61,27 +60,21 @@ public:
             throw std::invalid_argument("ORBextractor: image must be CV_8UC1");
         static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint),
                       "cv::KeyPoint and orbx_keypoint must share their 28-byte layout");
+        // the outputs stay in liborbx's pinned block; one copy each into the caller's vector
+        // and descriptor Mat
+        const orbx_keypoint* kp = nullptr;
+        const uint8_t* dsc = nullptr;
         int n = 0;
-        for (;;) {
-            keypoints.resize(cap);
-            desc.resize((size_t)cap * 32);
-            orbx_status s = orbx_extract(h, image.data, image.cols, image.rows,
-                                         (size_t)image.step,
-                                         reinterpret_cast<orbx_keypoint*>(keypoints.data()),
-                                         cap, desc.data(), &n);
-            if (s == ORBX_ERR_CAPACITY) {  // more keypoints than slots: n holds the count
-                cap = n;
-                continue;
-            }
-            check(s, "orbx_extract");
-            break;
-        }
+        check(orbx_extract_view(h, image.data, image.cols, image.rows, (size_t)image.step, &kp,
+                                &dsc, &n),
+              "orbx_extract_view");
         pyramid_valid = false;
-        if (n < 0) {  // empty image inside liborbx as well: outputs untouched
+        if (n < 0) {  // empty image inside liborbx as well
             keypoints.clear();
             return;
         }
-        keypoints.resize(n);
+        const cv::KeyPoint* k = reinterpret_cast<const cv::KeyPoint*>(kp);
+        keypoints.assign(k, k + n);
         if (n == 0) {  // :1086-1088
             _descriptors.release();
             return;
@@ -89,9 +82,9 @@ public:
         _descriptors.create(n, 32, CV_8U);  // :1090-1091
         cv::Mat d = _descriptors.getMat();
         if (d.isContinuous()) {
-            std::memcpy(d.data, desc.data(), (size_t)n * 32);
+            std::memcpy(d.data, dsc, (size_t)n * 32);
         } else {
-            for (int i = 0; i < n; ++i) std::memcpy(d.ptr(i), desc.data() + (size_t)i * 32, 32);
+            for (int i = 0; i < n; ++i) std::memcpy(d.ptr(i), dsc + (size_t)i * 32, 32);
         }
     }
 
@@ -143,8 +136,6 @@ protected:
     std::vector<float> mvInvLevelSigma2;
 
 private:
-    int cap;                       // keypoint slots; grows to the largest count seen
-    std::vector<uint8_t> desc;     // descriptor rows before the copy into _descriptors
     bool pyramid_valid = false;
 };
 

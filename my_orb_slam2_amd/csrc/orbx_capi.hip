@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -14,6 +15,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -289,6 +291,28 @@ static bool mark_done(orbx_extractor* h, hipStream_t st) {
 // its buffers grow.  Other streams and handles on the device keep running.
 static bool wait_idle(orbx_extractor* h) {
     return !h->have_done || HIPOK(hipEventSynchronize(h->done));
+}
+
+// The host wait of the single-image calls (orbx_extract, orbx_stereo_match): polls the handle's
+// last event for up to WAIT_SPIN_US (yielding the core between polls) before a blocking wait.
+// A blocking wait returns tens of microseconds after the work ends (the thread sleeps); the
+// drop-in path waits twice per stereo frame on its critical path.
+#ifndef WAIT_SPIN_US
+#define WAIT_SPIN_US 400
+#endif
+static bool wait_done(orbx_extractor* h) {
+    const int spin_us = tuned("ORBX_WAIT_SPIN_US", WAIT_SPIN_US);
+    if (spin_us > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = hipEventQuery(h->done);
+            if (e == hipSuccess) return true;
+            if (e != hipErrorNotReady) return HIPOK(e);
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+            std::this_thread::yield();
+        }
+    }
+    return HIPOK(hipEventSynchronize(h->done));
 }
 
 // Host staging buffer (pinned) of at least n bytes.
@@ -1143,16 +1167,10 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
     return true;
 }
 
-orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
-                         size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
-                         int* n_out) {
-    if (!h || !n_out) return ORBX_ERR_INVALID;
-    if (width <= 0 || height <= 0 || !img) {   // cv::Mat::empty(): silent return
-        *n_out = -1;
-        return ORBX_OK;
-    }
-    if (stride < (size_t)width) return ORBX_ERR_INVALID;
-    std::lock_guard<std::mutex> lk(h->mu);
+// orbx_extract's device sequence for one host image, up to the outputs in the handle's pinned
+// block (nkp at 0, keypoints at *o_kps, descriptors at *o_desc).  Called with h->mu held.
+static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width, int height,
+                                size_t stride, size_t* o_kps_out, size_t* o_desc_out) {
     orbx_status s = ensure_workspace(h, width, height, 1);
     if (s != ORBX_OK) return s;
     hipStream_t st = h->stream;
@@ -1187,20 +1205,58 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     const bool graph = tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
                        extract1_graph(h, a, st, width, height, enqueue);
     if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue(a)) || !mark_done(h, st) ||
-        !HIPOK(hipStreamSynchronize(st)))
+        !wait_done(h))
         return ORBX_ERR_DEVICE;
     h->last_batch = 1;
     h->last_valid = true;
-    int n = 0;
-    std::memcpy(&n, h->h_out, 4);
+    std::memcpy(&h->last_n, h->h_out, 4);
+    *o_kps_out = o_kps;
+    *o_desc_out = o_desc;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height,
+                         size_t stride, orbx_keypoint* kps, int kp_cap, uint8_t* desc,
+                         int* n_out) {
+    if (!h || !n_out) return ORBX_ERR_INVALID;
+    if (width <= 0 || height <= 0 || !img) {   // cv::Mat::empty(): silent return
+        *n_out = -1;
+        return ORBX_OK;
+    }
+    if (stride < (size_t)width) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    size_t o_kps = 0, o_desc = 0;
+    const orbx_status s = extract_host(h, img, width, height, stride, &o_kps, &o_desc);
+    if (s != ORBX_OK) return s;
+    const int n = h->last_n;
     *n_out = n;
-    h->last_n = n;
     const int m = std::min(n, kp_cap);
     if (m > 0) {
         if (kps) std::memcpy(kps, h->h_out + o_kps, (size_t)m * sizeof(orbx_keypoint));
         if (desc) std::memcpy(desc, h->h_out + o_desc, (size_t)m * 32);
     }
     return n > kp_cap ? ORBX_ERR_CAPACITY : ORBX_OK;
+}
+
+orbx_status orbx_extract_view(orbx_extractor* h, const uint8_t* img, int width, int height,
+                              size_t stride, const orbx_keypoint** kps, const uint8_t** desc,
+                              int* n_out) {
+    if (!h || !n_out || !kps || !desc) return ORBX_ERR_INVALID;
+    *kps = nullptr;
+    *desc = nullptr;
+    if (width <= 0 || height <= 0 || !img) {
+        *n_out = -1;
+        return ORBX_OK;
+    }
+    if (stride < (size_t)width) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    size_t o_kps = 0, o_desc = 0;
+    const orbx_status s = extract_host(h, img, width, height, stride, &o_kps, &o_desc);
+    if (s != ORBX_OK) return s;
+    *n_out = h->last_n;
+    *kps = (const orbx_keypoint*)(h->h_out + o_kps);
+    *desc = h->h_out + o_desc;
+    return ORBX_OK;
 }
 
 static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,
@@ -1374,7 +1430,7 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float
     const bool known = left->last_n >= 0;   // else a batched call of one image set the state
     if (!HIPOK(hipMemcpyAsync(ho, dso, o_d + KC * 4, hipMemcpyDeviceToHost, st)) ||
         (!known && !HIPOK(hipMemcpyAsync(ho + 8, left->d_nkp.p, 4, hipMemcpyDeviceToHost, st))) ||
-        !mark_done(left, st) || !HIPOK(hipStreamSynchronize(st)))
+        !mark_done(left, st) || !wait_done(left))
         return ORBX_ERR_DEVICE;
     int n = left->last_n;
     if (!known) std::memcpy(&n, ho + 8, 4);

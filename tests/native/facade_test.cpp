@@ -9,10 +9,23 @@
 //   facade_test run DIR   DIR holds left.raw / right.raw (W*H bytes) and params.txt
 //                         ("W H nfeatures mbf"); writes the same raw arrays as boundary_test
 //                         `run` (n, nr, nvalid, kps/desc of both views, uRight, depth, bow)
+//   facade_test bench DIR FRAMES WARMUP K
+//                         the stereo Frame constructor's extraction and stereo (Frame.cc:66-120:
+//                         two ExtractORB threads, then ComputeStereoMatches) per frame, timed
+//                         (steady_clock, as Examples/Stereo/stereo_kitti.cc:80-98), on K
+//                         independent tracking threads (K SLAM sessions sharing the GPU); DIR as
+//                         boundary_test `bench` (pair_<i>_left/right.raw, params.txt
+//                         "W H nfeatures mbf mb P").  Prints boundary_test bench's JSON line.
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -201,6 +214,137 @@ int run(const std::string& dir) {
     return ok ? 0 : 3;
 }
 
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+int bench(const std::string& dir, int nframes, int warmup, int trackers) {
+    int W = 0, H = 0, nfeat = 0, P = 0;
+    float mbf = 0.f, mb = 0.f;
+    {
+        FILE* f = std::fopen((dir + "/params.txt").c_str(), "r");
+        if (!f) return 2;
+        const int got = std::fscanf(f, "%d %d %d %f %f %d", &W, &H, &nfeat, &mbf, &mb, &P);
+        std::fclose(f);
+        if (got != 6 || P < 1) return 2;
+    }
+    std::vector<std::vector<uint8_t>> Ls((size_t)P), Rs((size_t)P);
+    for (int i = 0; i < P; ++i) {
+        const std::string b = dir + "/pair_" + std::to_string(i);
+        if (!read_file(b + "_left.raw", Ls[(size_t)i]) || !read_file(b + "_right.raw", Rs[(size_t)i]) ||
+            Ls[(size_t)i].size() != (size_t)W * H || Rs[(size_t)i].size() != (size_t)W * H)
+            return 2;
+    }
+    trackers = std::max(trackers, 1);
+    struct Session {
+        std::unique_ptr<ORB_SLAM2::ORBextractor> left, right;   // Tracking.cc:136-139
+        std::vector<double> ms;
+        long long kp_sum = 0, nv_sum = 0;
+        uint64_t digest = 1469598103934665603ull;
+        std::string err;
+    };
+    // Frame::fx such that the glue's mbf / fx is the params' mb exactly (boundary_test `bench`
+    // passes mb itself)
+    float fx = mbf / mb;
+    for (int t = 0; t < 8 && mbf / fx != mb; ++t)
+        fx = std::nextafter(fx, mbf / fx > mb ? 1e30f : 0.f);
+    if (mbf / fx != mb) return 2;
+    std::vector<Session> ss((size_t)trackers);
+    for (Session& s : ss) {
+        s.left.reset(new ORB_SLAM2::ORBextractor(nfeat, 1.2f, 8, 20, 7));
+        s.right.reset(new ORB_SLAM2::ORBextractor(nfeat, 1.2f, 8, 20, 7));
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    int warm_done = 0;
+    bool go = false;
+    auto track = [&](Session* s) {
+        try {
+            for (int f = 0; f < warmup + nframes; ++f) {
+                if (f == warmup) {   // every session warm, then all timed frames start together
+                    std::unique_lock<std::mutex> lk(mu);
+                    if (++warm_done == trackers) { go = true; cv.notify_all(); }
+                    cv.wait(lk, [&] { return go; });
+                }
+                const int i = f % P;
+                const cv::Mat imL(H, W, CV_8UC1, Ls[(size_t)i].data()),
+                    imR(H, W, CV_8UC1, Rs[(size_t)i].data());
+                const auto t0 = std::chrono::steady_clock::now();
+                Frame F;   // the stereo Frame constructor (Frame.cc:66-120)
+                F.mpORBextractorLeft = s->left.get();
+                F.mpORBextractorRight = s->right.get();
+                F.mbf = mbf;
+                F.fx = fx;
+                {
+                    std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
+                    std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
+                    tl.join();
+                    tr.join();
+                }
+                F.N = (int)F.mvKeys.size();
+                const int nvalid = orbx_glue::ComputeStereoMatches(F);
+                const auto t1 = std::chrono::steady_clock::now();
+                if (f >= warmup) {
+                    s->ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                    s->kp_sum += F.N;
+                    s->nv_sum += nvalid;
+                    const int nr = (int)F.mvKeysRight.size();
+                    uint64_t h = fnv1a(s->digest, &F.N, 4);
+                    h = fnv1a(h, F.mvKeys.data(), (size_t)F.N * sizeof(cv::KeyPoint));
+                    h = fnv1a(h, F.mDescriptors.data, (size_t)F.N * 32);
+                    h = fnv1a(h, F.mvKeysRight.data(), (size_t)nr * sizeof(cv::KeyPoint));
+                    h = fnv1a(h, F.mDescriptorsRight.data, (size_t)nr * 32);
+                    h = fnv1a(h, F.mvuRight.data(), (size_t)F.N * 4);
+                    h = fnv1a(h, F.mvDepth.data(), (size_t)F.N * 4);
+                    s->digest = fnv1a(h, &nvalid, 4);
+                }
+            }
+        } catch (const std::exception& e) {
+            s->err = e.what();
+            std::unique_lock<std::mutex> lk(mu);
+            if (!go) { ++warm_done; if (warm_done == trackers) { go = true; cv.notify_all(); } }
+        }
+    };
+    std::vector<std::thread> th;
+    std::chrono::steady_clock::time_point t_go;
+    for (Session& s : ss) th.emplace_back(track, &s);
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return go; });
+        t_go = std::chrono::steady_clock::now();
+    }
+    for (std::thread& t : th) t.join();
+    const double wall_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_go).count();
+    long long kp_sum = 0, nv_sum = 0;
+    for (Session& s : ss) {
+        if (!s.err.empty()) {
+            std::fprintf(stderr, "facade_test bench: %s\n", s.err.c_str());
+            return 1;
+        }
+        kp_sum += s.kp_sum;
+        nv_sum += s.nv_sum;
+    }
+    const long long nt = (long long)nframes * trackers;
+    std::printf("{\"frames\": %d, \"warmup\": %d, \"trackers\": %d, \"wall_ms\": %.4f, "
+                "\"mean_keypoints_left\": %.3f, \"mean_stereo_matches\": %.3f, \"digests\": [",
+                nframes, warmup, trackers, wall_ms, (double)kp_sum / std::max(nt, 1LL),
+                (double)nv_sum / std::max(nt, 1LL));
+    for (size_t k = 0; k < ss.size(); ++k)
+        std::printf("%s\"%016llx\"", k ? ", " : "", (unsigned long long)ss[k].digest);
+    std::printf("], \"latency_ms\": [");
+    bool first = true;
+    for (Session& s : ss)
+        for (double v : s.ms) {
+            std::printf("%s%.4f", first ? "" : ", ", v);
+            first = false;
+        }
+    std::printf("]}\n");
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -208,10 +352,12 @@ int main(int argc, char** argv) {
     try {
         if (mode == "nogpu") return nogpu();
         if (mode == "run" && argc > 2) return run(argv[2]);
+        if (mode == "bench" && argc > 5)
+            return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
     } catch (const std::exception& e) {
         std::fprintf(stderr, "facade_test: %s\n", e.what());
         return 1;
     }
-    std::fprintf(stderr, "usage: facade_test nogpu | run DIR\n");
+    std::fprintf(stderr, "usage: facade_test nogpu | run DIR | bench DIR FRAMES WARMUP K\n");
     return 2;
 }

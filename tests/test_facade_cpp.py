@@ -79,3 +79,30 @@ def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed):
     n_o, m_o = om.search_by_bow_kf_frame(KF, np.ones(nr, bool), F, 0.75, True)
     assert bow[0] == n_o and n_o > 0
     np.testing.assert_array_equal(bow[1:], m_o)
+
+
+@pytest.mark.gpu
+def test_facade_bench_matches_cabi_bench(facade_bin, orbx_lib, gpu, tmp_path):
+    """bench.py --workload dropin's loop through the facade (facade_test `bench`: a Frame per
+    frame, two ExtractORB threads, the stereo glue) and through the bare C ABI (boundary_test
+    `bench`) on the same pairs: 3 tracking sessions each, every session's output digest equal
+    across both programs (the facade adds no result change)."""
+    from my_orb_slam2_amd import build as b
+    from my_orb_slam2_amd import synth
+    mbf, fx = 386.1448, 718.856
+    mb = float(np.float32(mbf) / np.float32(fx))
+    for i in range(2):
+        L, R = synth.stereo_pair(760 + i, 1241, 376)
+        L.tofile(tmp_path / f"pair_{i}_left.raw")
+        R.tofile(tmp_path / f"pair_{i}_right.raw")
+    (tmp_path / "params.txt").write_text(f"1241 376 2000 {mbf!r} {mb!r} 2\n")
+    out = {}
+    for name, binp in (("facade", facade_bin), ("cabi", b.build_boundary_test())):
+        r = subprocess.run([str(binp), "bench", str(tmp_path), "5", "2", "3"],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, name + ": " + r.stderr
+        out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out[name]["trackers"] == 3 and len(out[name]["latency_ms"]) == 15
+    assert len(set(out["facade"]["digests"])) == 1, out["facade"]["digests"]
+    assert out["facade"]["digests"] == out["cabi"]["digests"]
+    assert out["facade"]["mean_stereo_matches"] == out["cabi"]["mean_stereo_matches"] > 0

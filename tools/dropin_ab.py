@@ -1,6 +1,6 @@
 """A/B of the drop-in host path's small-batch policies (run on the GPU box).
 
-Runs tests/native/boundary_test `bench` against a tuning build of liborbx.so
+Runs tests/native/facade_test `bench` (the facade loop) against a tuning build of liborbx.so
 (tools/_var/tune/liborbx.so, built with -DORBX_TUNING, which reads the ORBX_* overrides of
 orbx_capi.hip) for each setting and K, and prints median / mean latency and pairs/s.
     python tools/dropin_ab.py build            # here (hipcc)
@@ -16,18 +16,11 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 VAR = ROOT / "tools" / "_var" / "tune"
 
-R03 = {"ORBX_OCT_SMALL_BATCH": "0", "ORBX_SIDE_MIN_BATCH": "0", "ORBX_FAST_NC": "4",
-       "ORBX_EXTRACT_GRAPH": "0"}
 SETTINGS = {
-    "r03": R03,
-    "oct_small": dict(R03, ORBX_OCT_SMALL_BATCH="4"),
-    "no_side": dict(R03, ORBX_SIDE_MIN_BATCH="16"),
-    "fast_nc1": dict(R03, ORBX_FAST_NC="1"),
-    "graph": dict(R03, ORBX_EXTRACT_GRAPH="1"),
-    "all_nograph": {"ORBX_EXTRACT_GRAPH": "0"},
-    "all": {},
-    "all_q8": {"GPU_MAX_HW_QUEUES": "8"},
-    "all_q16": {"GPU_MAX_HW_QUEUES": "16"},
+    "default": {},
+    "nospin": {"ORBX_WAIT_SPIN_US": "0"},
+    "nograph": {"ORBX_EXTRACT_GRAPH": "0"},
+    "q16": {"GPU_MAX_HW_QUEUES": "16"},
 }
 
 
@@ -42,7 +35,8 @@ def build():
 
 
 def run(d, ks):
-    binp = ROOT / "tests" / "native" / "boundary_test"
+    # the facade loop (bench.py --workload dropin's default), or ORBX_AB_BIN=boundary_test
+    binp = ROOT / "tests" / "native" / os.environ.get("ORBX_AB_BIN", "facade_test")
     for name, env_set in SETTINGS.items():
         for K in ks:
             env = dict(os.environ, LD_LIBRARY_PATH=str(VAR), **env_set)
