@@ -36,14 +36,14 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r03_pmc_fetch_b512.csv", "r03_pmc_write_b512.csv"))
+                       ("r04_pmc_fetch_b512.csv", "r04_pmc_write_b512.csv"))
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                             ("r03_pmc_fetch_euroc.csv", "r03_pmc_write_euroc.csv"))
+                             ("r04_pmc_fetch_euroc.csv", "r04_pmc_write_euroc.csv"))
 # SQ_INSTS_VALU and SQ_ACTIVE_INST_VALU passes (the VALU issue entry beside the HBM roofline)
 DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
-                         ("r03_pmc_insts_b512.csv", "r03_pmc_busy_b512.csv"))
+                         ("r04_pmc_insts_b512.csv", "r04_pmc_busy_b512.csv"))
 DEFAULT_INSTS_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                               ("r03_pmc_insts_euroc.csv", "r03_pmc_busy_euroc.csv"))
+                               ("r04_pmc_insts_euroc.csv", "r04_pmc_busy_euroc.csv"))
 # VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
 # 2 cycles per SIMD for the full-rate class (add / logic / shifts / f32 mul-add), per 4 cycles
 # for the rest (v_dot*, v_perm, v_pk_*, v_bcnt, 32-bit min / max, conversions), measured by
@@ -768,7 +768,7 @@ def valu_from_csv(paths, kernel):
     return counter_from_csv(paths, kernel, "SQ_INSTS_VALU")
 
 
-ISA_MIX = os.path.join(HERE, "profiles", "r03_isa_mix.json")
+ISA_MIX = os.path.join(HERE, "profiles", "r04_isa_mix.json")
 
 
 def _mangled_key(demangled: str) -> str:
@@ -784,7 +784,7 @@ def _mangled_key(demangled: str) -> str:
 
 def mix_cycles_from_csv(paths, kernel, mix_path=None):
     """Mean issue cycles per VALU instruction of a kernel group: each dispatch's SQ_INSTS_VALU
-    weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r03_isa_mix.json)."""
+    weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r04_isa_mix.json)."""
     import csv
     import glob
     try:

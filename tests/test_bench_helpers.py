@@ -141,7 +141,7 @@ def test_valu_entry_from_pmc(tmp_path):
         (100 * 2.5 + 300 * 3.5) / 400)
     b.ISA_MIX = str(mix)
     e = b.valu_entry(str(f), "k_fast", 1e-6)
-    b.ISA_MIX = os.path.join(ROOT, "profiles", "r03_isa_mix.json")
+    b.ISA_MIX = os.path.join(ROOT, "profiles", "r04_isa_mix.json")
     assert e["wave_instr_per_launch"] == pytest.approx(999.0)
     assert e["busy_frac"] == pytest.approx(999.0 * 3.0 / (1024 * 1e-6 * 2.4e9))
     assert e["valubusy_4cycle"] == pytest.approx(4.0 * 1000 / (1024 * 1000))
