@@ -93,7 +93,6 @@ struct orbx_extractor {
     // the extraction outputs as one allocation: [nkp[B] | kps[B][KC] | desc[B][KC][32]]
     // (d_nkp / d_kps / d_desc are views of it): one DMA returns one image's results
     DevBuf d_outs;
-    unsigned* chain_ctr = nullptr;   // k_level_chain's counters, inside d_outs
     long long kscratch_per_image = 0;
     KernelTimer timer;
     // last extraction
@@ -251,9 +250,6 @@ static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
 #endif
 #ifndef OCT_SMALL_BATCH
 #define OCT_SMALL_BATCH 4      // images per call up to which the octree takes that budget
-#endif
-#ifndef CHAIN_MAX_BATCH
-#define CHAIN_MAX_BATCH 4      // images per call up to which the pyramid is one k_level_chain launch
 #endif
 #ifndef SIDE_MIN_BATCH
 #define SIDE_MIN_BATCH 16      // images per call from which the default side branch forks
@@ -816,9 +812,7 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
                   h->d_cand.ensure(B * G.cand_words * 4) &&
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
                   h->d_kscr.ensure(B * h->kscratch_per_image);
-        // nkp [B], then k_level_chain's three counters (chain_ctr) in the 16 bytes before the
-        // keypoints: zero between launches, and the error flag comes back with the outputs
-        const size_t o_kps = align_up(B * 4 + 16, 256);
+        const size_t o_kps = align_up(B * 4, 256);
         const size_t o_desc = o_kps + align_up(B * G.kp_cap * sizeof(orbx_keypoint), 256);
         const size_t o_end = o_desc + B * G.kp_cap * 32;
         ok = ok && h->d_outs.ensure(o_end);
@@ -827,10 +821,6 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         h->d_nkp.view(ob, B * 4);
         h->d_kps.view(ob + o_kps, B * G.kp_cap * sizeof(orbx_keypoint));
         h->d_desc.view(ob + o_desc, B * G.kp_cap * 32);
-        h->chain_ctr = (unsigned*)(ob + o_kps - 16);
-        if (!HIPOK(hipMemsetAsync(h->chain_ctr, 0, 16, h->stream)) ||
-            !HIPOK(hipStreamSynchronize(h->stream)))
-            return ORBX_ERR_DEVICE;
         h->cap_batch = batch;
     }
     return ORBX_OK;
@@ -894,8 +884,6 @@ ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uin
                                                                                      : h->side_mode;
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
-    a.chain = batch <= tuned("ORBX_CHAIN_MAX_BATCH", CHAIN_MAX_BATCH) ? 1 : 0;
-    a.chain_ctr = h->chain_ctr;
     strip_heights(h, batch, a.sth);
     return a;
 }
@@ -1222,14 +1210,6 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
     h->last_batch = 1;
     h->last_valid = true;
     std::memcpy(&h->last_n, h->h_out, 4);
-    unsigned chain_err = 0;
-    std::memcpy(&chain_err, h->h_out + o_kps - 8, 4);
-    if (chain_err) {   // k_level_chain gave up on a barrier: the pyramid is not valid
-        h->last_valid = false;
-        (void)hipMemsetAsync(h->chain_ctr, 0, 16, st);
-        snprintf(g_err, sizeof(g_err), "k_level_chain: grid barrier timed out");
-        return ORBX_ERR_DEVICE;
-    }
     *o_kps_out = o_kps;
     *o_desc_out = o_desc;
     return ORBX_OK;

@@ -141,19 +141,8 @@ struct ExtractLaunch {
     // side branch: 0 off, 1 FAST, 2 + octree, 3 + orientation / descriptors of levels
     // [0, side_lv), forked before level side_at's launch
     int side_mode = 0, side_at = 0, side_lv = 1;
-    // small in-place batches: the whole pyramid in one k_level_chain launch (launch_levels);
-    // chain_ctr = its three device words (phase counter, exit counter, error flag), zero
-    // between launches
-    int chain = 0;
-    unsigned* chain_ctr = nullptr;
 };
 
-// k_level_chain's launch argument: the strip heights of this call and its batch
-struct ChainPlan {
-    int sth[ORBX_MAX_LEVELS];
-    int nlevels;
-    int batch;
-};
 
 struct StereoLaunch {
     const Geometry* dg;

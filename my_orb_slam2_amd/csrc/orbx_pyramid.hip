@@ -13,7 +13,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <algorithm>
 #include <type_traits>
 #include <utility>
 
@@ -1142,87 +1141,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
                            wv, b);
 }
 
-// ---- k_level_chain: every level of a small batch in one launch ----
-// A single-image call's pyramid is a chain of 8 dependent launches of a few microseconds
-// each; their submission by the host runtime (one packet and its bookkeeping per launch) then
-// costs as much as the GPU work, and with several tracking threads on one device it is the
-// bottleneck.  Here a grid of co-resident workgroups walks the levels in phases separated by a
-// grid barrier: phase 0 = level 0 (its blur; in place) with level 1 (resized from the same
-// input slot), phase p = level p + 1.  Each phase's strip waves are the k_level_strip waves of
-// that level, dealt round-robin over the grid's waves; the arithmetic is level_strip_wave's.
-// The grid (<= CHAIN_MAX_WG workgroups, a few per XCD) is always co-resident: other kernels
-// on the device finish without waiting on this one.
-#ifndef CHAIN_MAX_WG
-#define CHAIN_MAX_WG 128   // workgroups of one k_level_chain launch (strip waves loop over them)
-#endif
-#ifndef CHAIN_SPIN_TICKS
-#define CHAIN_SPIN_TICKS 10000000ull   // 100 ms of the 100 MHz real-time counter per barrier
-#endif
-__device__ __forceinline__ void chain_barrier(unsigned* ctr, unsigned target, unsigned* err) {
-    __syncthreads();   // the workgroup's stores of this phase are complete in its L2
-    if (threadIdx.x == 0) {
-        __threadfence();   // ... and written back for the other XCDs
-        atomicAdd(ctr, 1u);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_SPIN_TICKS) {
-                // a grid that is not co-resident (never expected): give up, flag the launch
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        __threadfence();
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_level_chain(
-    const Geometry* __restrict__ g, const uint8_t* __restrict__ ltab, uint8_t* __restrict__ pyr,
-    uint8_t* __restrict__ blur, ChainPlan plan, unsigned* __restrict__ ctr) {
-    const int nw = (int)gridDim.x * 4;   // the grid's waves
-    const int gw = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const size_t pitch0 = (size_t)g->lv[0].pitch, pyrb = (size_t)g->pyr_bytes;
-    unsigned phase = 0;
-    for (int l = 0; l < plan.nlevels; ++l) {
-        if (l > 1) chain_barrier(ctr, ++phase * gridDim.x, ctr + 2);
-        // phase 0 holds levels 0 and 1; the waves of level 0 first
-        const int la = l == 0 ? 0 : l, lb = l == 0 ? (plan.nlevels > 1 ? 1 : 0) : l;
-        const LevelGeom& A = g->lv[la];
-        const int wa = A.snw * ((A.h + plan.sth[la] - 1) / plan.sth[la]);
-        const int na = wa * plan.batch;
-        int nb = 0, wb = 0;
-        if (lb != la) {
-            const LevelGeom& Bv = g->lv[lb];
-            wb = Bv.snw * ((Bv.h + plan.sth[lb] - 1) / plan.sth[lb]);
-            nb = wb * plan.batch;
-        }
-        for (int v = gw; v < na + nb; v += nw) {
-            if (v < na) {
-                const int b = v / wa;
-                if (la == 0)
-                    level_strip_wave<4>(g, ltab, pyr, pyr, plan.batch, pitch0, pyrb, pyr, blur, 0,
-                                        plan.sth[0], 0, v - b * wa, b);
-                else
-                    level_strip_wave<3>(g, ltab, pyr, pyr, plan.batch, pitch0, pyrb, pyr, blur, la,
-                                        plan.sth[la], 0, v - b * wa, b);
-            } else {
-                const int u = v - na, b = u / wb;
-                level_strip_wave<3>(g, ltab, pyr, pyr, plan.batch, pitch0, pyrb, pyr, blur, lb,
-                                    plan.sth[lb], 0, u - b * wb, b);
-            }
-        }
-        if (l == 0) l = lb;   // level 1 done in phase 0
-    }
-    // the last workgroup out leaves the counters zero for the handle's next launch
-    __syncthreads();
-    if (threadIdx.x == 0 &&
-        atomicAdd(ctr + 1, 1u) == gridDim.x - 1) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     (void)ltw;
     (void)lth;
@@ -1253,27 +1171,6 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, in
     const Geometry& G = *a.hg;
     KernelTimer dummy;
     KernelTimer& T = a.timer ? *a.timer : dummy;
-    if (a.chain && a.in_place && a.chain_ctr && l_begin == 0 && l_end >= G.nlevels) {
-        ChainPlan plan;
-        plan.nlevels = G.nlevels;
-        plan.batch = a.batch;
-        int waves = 0;   // the largest phase's strip waves
-        bool strips = true;
-        for (int l = 0; l < G.nlevels; ++l) {
-            const LevelGeom& L = G.lv[l];
-            strips = strips && L.strip && (l == 0 || level_mode(L, l) == 3);
-            plan.sth[l] = a.sth[l];
-            const int w = L.snw * ((L.h + a.sth[l] - 1) / a.sth[l]) * a.batch;
-            if (l == 1) waves += w;   // phase 0: levels 0 and 1
-            else waves = std::max(waves, w);
-        }
-        if (strips) {
-            const int wg = std::min(std::max((waves + 3) / 4, 1), CHAIN_MAX_WG);
-            ORBX_TIMED_LAUNCH(T, K_LEVEL, k_level_chain, dim3(wg), dim3(256), 0, st, a.dg, a.ltab,
-                              a.pyr, a.blur, plan, a.chain_ctr);
-            return hipGetLastError();
-        }
-    }
     for (int l = l_begin; l < l_end && l < G.nlevels; ++l) {
         const LevelGeom& L = G.lv[l];
         const int mode = level_mode(L, l);

@@ -18,7 +18,6 @@ VAR = ROOT / "tools" / "_var" / "tune"
 
 SETTINGS = {
     "default": {},
-    "nochain": {"ORBX_CHAIN_MAX_BATCH": "0"},
     "nospin": {"ORBX_WAIT_SPIN_US": "0"},
     "nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "q16": {"GPU_MAX_HW_QUEUES": "16"},
