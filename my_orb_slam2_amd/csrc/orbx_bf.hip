@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "orbx_device.h"
 #include "orbx_kernels.h"
@@ -39,6 +40,9 @@ namespace {
 #define BF_PACKED 1    // k_bf_top2: packed 16-bit top-2 keys over blocks of BF_BLK rows
 #endif
 #define BF_BLK 256     // rows per packed block (128 pairs: the pair index fits 7 bits)
+#ifndef BF_MFMA
+#define BF_MFMA 1      // the distances on the matrix cores (k_bf_mfma) instead of k_bf_top2
+#endif
 
 constexpr uint32_t BF_NONE = 256u << 23;       // (distance 256, row 0): the loop's initial value
 constexpr int BF_ROW_BITS = 23;                 // rows per chunk < 2^23
@@ -187,6 +191,131 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
     if (qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1, b2);
 }
 
+// ---- k_bf_mfma: the distances on the matrix cores ----
+// With every bit mapped to +-1 (database row: bit 1 -> +1, 0 -> -1; query: 1 -> -1, 0 -> +1),
+// the dot product of two 256-bit descriptors is sum(+1 per differing bit, -1 per equal bit)
+// = 2 * popcount(a ^ b) - 256, exactly, in int32.  v_mfma_i32_32x32x32_i8 forms 32 rows x 32
+// queries of it per 8 instructions (K = 256 = 8 x 32), at the i8 matrix rate, so a distance
+// costs the top-2 update (key build, v_med3, v_min) instead of 8 v_xor + 8 v_bcnt.  The
+// kernel is issue-bound on that update and on the MFMAs, not on HBM (32 B per row per query
+// block).
+//   workgroup: 4 waves x 64 queries (two 32-query tiles per wave, their +-1 bytes held in
+//   registers for the whole chunk) against the chunk's rows in blocks of 32: the block's 1 KB
+//   is read once (a dword per thread), expanded to +-1 bytes in the A-fragment order, staged in
+//   LDS (double-buffered, one barrier per block) and read by every wave (ds_read_b128 per
+//   step).  A fragment element j of lane l (r = l & 31, h = l >> 5) at step s is bit
+//   32 s + 16 h + j of row r, and the B fragment's element j of lane l is the same bit of query
+//   r: the sum over k pairs equal bits whatever k the hardware gives element j, as long as A
+//   and B share it (they do: the parity tests compare every distance-derived output).
+//   Accumulator register i of lane l holds (row (i & 3) + 8 (i >> 2) + 4 h, query r): key =
+//   (acc << 22) + (256 << 22) + row = dist << 23 | row, the k_bf_top2 key, and the same
+//   partials go to k_bf_merge.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// 16 bits -> 16 bytes, byte j = bit j ? 0x01 : 0xFF (off_pattern 0xFFFFFFFF) or the reverse
+// (0x01010101): ((nibble * 0x00204081) & 0x01010101) spreads a nibble's bits to the bytes' low
+// bits, a packed 16-bit multiply by 0xFE (no carries: every byte is 0 or 1) makes 0x00 / 0xFE
+// of them, and the XOR the +-1 bytes
+__device__ __forceinline__ v4i expand16(uint32_t bits, uint32_t off_pattern, uint32_t fe) {
+    v4i r;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const uint32_t t = (((bits >> (4 * n)) & 15u) * 0x00204081u) & 0x01010101u;
+        uint32_t m;
+        asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(t), "v"(fe));
+        r[n] = (int)(m ^ off_pattern);
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q, int nq,
+                                                  const uint32_t* __restrict__ db, long long ndb,
+                                                  int chunk, int nqpad, uint2* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) v4i frag[2][8 * 64];   // [buffer][step * 64 + lane]
+    int bx, c;
+    xcd_block(bx, c);
+    const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const long long r0 = (long long)c * chunk;
+    const int n = (int)min((long long)chunk, ndb - r0);
+    const uint32_t* __restrict__ p = db + r0 * 8;
+    uint32_t fe = 0x00FE00FEu;
+    asm volatile("" : "+v"(fe));   // a register operand for v_pk_mul_lo_u16
+    // the wave's two query tiles as B fragments: query r of tile t, bits 32 s + 16 h ..
+    v4i bq[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int qi = min(bx * 256 + w * 64 + t * 32 + r, nq - 1);
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            bq[t][s] = expand16(q[(size_t)qi * 8 + s] >> (16 * h), 0x01010101u, fe);
+    }
+    // this thread's share of a block: dword (tid & 7) of row (tid >> 3)
+    const int lr = tid >> 3, ls = tid & 7;
+    auto stage = [&](int buf, uint32_t v) {
+        frag[buf][ls * 64 + lr] = expand16(v & 0xFFFFu, 0xFFFFFFFFu, fe);
+        frag[buf][ls * 64 + 32 + lr] = expand16(v >> 16, 0xFFFFFFFFu, fe);
+    };
+    auto fetch = [&](int e0) { return p[(size_t)min(e0 + lr, n - 1) * 8 + ls]; };
+    // key offsets of the lane's 16 accumulator rows in a block: (256 << 22) + row in the block
+    uint32_t koff[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) koff[i] = (256u << 22) + (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h);
+    uint32_t b1[2] = {BF_NONE, BF_NONE}, b2[2] = {BF_NONE, BF_NONE};
+    const int nblk = (n + 31) / 32;
+    if (nblk > 0) stage(0, fetch(0));
+    __syncthreads();
+    // the block's top-2 over its (distance, row-in-block) keys, then its rows offset by e0 and
+    // folded into the chunk's; the tail block drops its rows past n
+    auto block = [&](int buf, int e0, auto tail_c) {
+        constexpr bool TAIL = decltype(tail_c)::value;
+        v16i acc[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = v16i{};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const v4i a = frag[buf][s * 64 + lane];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[t][s], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            uint32_t l1 = 0xFFFFFFFFu, l2 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                uint32_t key = ((uint32_t)acc[t][i] << 22) + koff[i];
+                if (TAIL && e0 + (int)(koff[i] & 31u) >= n) key = 0xFFFFFFFFu;
+                l2 = med3_u32(l1, l2, key);
+                l1 = min(l1, key);
+            }
+            // rows e0 + ..: a block key of 0xFFFFFFFF (no row) stays above every real key
+            const uint32_t o1 = l1 == 0xFFFFFFFFu ? l1 : l1 + (uint32_t)e0;
+            const uint32_t o2 = l2 == 0xFFFFFFFFu ? l2 : l2 + (uint32_t)e0;
+            b2[t] = min(max(b1[t], o1), min(b2[t], o2));
+            b1[t] = min(b1[t], o1);
+        }
+    };
+    const int nfull = n / 32;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int buf = blk & 1, e0 = blk * 32;
+        const uint32_t nxt = blk + 1 < nblk ? fetch(e0 + 32) : 0u;   // in flight meanwhile
+        if (blk < nfull) block(buf, e0, std::false_type{});
+        else block(buf, e0, std::true_type{});
+        if (blk + 1 < nblk) stage(buf ^ 1, nxt);
+        __syncthreads();
+    }
+    // the two half-waves hold the same queries' other 16 rows of every block: fold them
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[t], 32), o2 = (uint32_t)__shfl_xor((int)b2[t], 32);
+        b2[t] = min(max(b1[t], o1), min(b2[t], o2));
+        b1[t] = min(b1[t], o1);
+        const int qi = bx * 256 + w * 64 + t * 32 + r;
+        if (h == 0 && qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1[t], b2[t]);
+    }
+}
+
 // 32 queries per workgroup, 8 threads per query: thread slice s folds the contiguous chunk
 // range [s*L, (s+1)*L) in order, then slice 0 folds the 8 slice results in order (the fold is
 // associative: (earlier, later) -> best of the earlier on a tie).
@@ -269,9 +398,9 @@ hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer)
     if (nchunks > INT32_MAX / 2) return hipErrorInvalidValue;
     hipEvent_t e = timer ? timer->start(st) : nullptr;
     if (nchunks > 0)
-        hipLaunchKernelGGL(k_bf_top2, dim3(nqpad / 256, (unsigned)nchunks), dim3(256), 0, st,
-                           (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db, a.ndb, a.chunk,
-                           nqpad, (uint2*)a.part);
+        hipLaunchKernelGGL(BF_MFMA ? k_bf_mfma : k_bf_top2, dim3(nqpad / 256, (unsigned)nchunks),
+                           dim3(256), 0, st, (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db,
+                           a.ndb, a.chunk, nqpad, (uint2*)a.part);
     hipLaunchKernelGGL(k_bf_merge, dim3((a.nq + 31) / 32), dim3(256), 0, st, (const uint2*)a.part,
                        a.nq, nqpad, (int)nchunks, a.chunk, a.idx_base, a.best_idx, a.best_dist,
                        a.second_dist);
