@@ -1413,6 +1413,9 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 128 lane-ops/clk x 2.4 G
 # cycles per wave64 instruction, v_bcnt_u32_b32 at 4; a 256-bit distance is 8 of each, so one
 # SIMD retires at most 64 distances per 48 cycles.
 DIST_ISSUE_PEAK = 1024 * 2.4e9 * 64 / 48
+# Dense int8 matrix peak (MI355X_MICROARCH.md §Matrix cores: i8 = 2x the bf16 rate, bf16 ~2.5
+# PFLOP/s dense): v_mfma_i32_32x32x32_i8, the k_bf_mfma distances
+I8_MFMA_PEAK_TOPS = 5000.0
 
 
 def _hash_bytes(torch, idx, salt):
@@ -1689,7 +1692,7 @@ def main_bf(args):
     import torch
     import torch.distributed as dist
 
-    from my_orb_slam2_amd import ORBmatcher
+    from my_orb_slam2_amd import ORBmatcher, load
     from my_orb_slam2_amd.distributed import broadcast_query, gather_top2, shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1750,12 +1753,20 @@ def main_bf(args):
         tot_ms, launches = prof["k_bf"]
         avg_s = tot_ms / 1000.0 / launches
         dist_n = float(nq) * (r1 - r0)
-        ops = 16.0 * dist_n                           # 8 XOR + 8 BCNT per 256-bit distance
         dps = dist_n / avg_s
         db_bytes = 32.0 * (r1 - r0) + 32.0 * nq + 12.0 * nq
-        roof = {"kernel": "k_bf_top2 + k_bf_merge", "bound": "valu", "achieved": ops / avg_s / 1e12,
-                "peak": VALU_PEAK_TOPS, "unit": "Tops/s (int32 lane-ops)",
-                "frac": ops / avg_s / 1e12 / VALU_PEAK_TOPS, "traffic": None,
+        kname = load().orbx_bf_kernel().decode()
+        if kname == "k_bf_mfma":
+            # +-1 int8 dot products: 256 multiply-adds (512 int8 ops) per distance, priced
+            # against the dense i8 matrix peak
+            ops = 512.0 * dist_n
+            unit, peak, bound = "TOPS (int8 MFMA)", I8_MFMA_PEAK_TOPS, "mfma"
+        else:
+            ops = 16.0 * dist_n                       # 8 XOR + 8 BCNT per 256-bit distance
+            unit, peak, bound = "Tops/s (int32 lane-ops)", VALU_PEAK_TOPS, "valu"
+        roof = {"kernel": kname + " + k_bf_merge", "bound": bound, "achieved": ops / avg_s / 1e12,
+                "peak": peak, "unit": unit,
+                "frac": ops / avg_s / 1e12 / peak, "traffic": None,
                 "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_s * 1000.0,
                 "distances_per_s": dps, "issue_peak_distances_per_s": DIST_ISSUE_PEAK,
                 "issue_frac": dps / DIST_ISSUE_PEAK,

@@ -260,6 +260,10 @@ orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int
                                         int32_t* d_best_idx, int32_t* d_best_dist,
                                         int32_t* d_second_dist, void* stream);
 
+/* The kernel the brute-force top-2 runs its distances in: "k_bf_mfma" (+-1 int8 dot products
+ * on the matrix cores, the default build) or "k_bf_top2" (v_xor + v_bcnt on the vector ALUs). */
+const char* orbx_bf_kernel(void);
+
 /* Waits for `stream` and returns ORBX_ERR_CAPACITY if a batched call on this matcher met a
  * keyframe above max_feat since the last sync (the flag is then cleared). */
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream);

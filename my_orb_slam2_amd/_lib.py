@@ -102,6 +102,7 @@ SIGNATURES = {
     "orbx_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp]),
     "orbx_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
     "orbx_hamming_bf_top2": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, _vp, _vp, _vp]),
+    "orbx_bf_kernel": (ctypes.c_char_p, []),
     "orbx_hamming_bf_top2_device": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, ctypes.c_int64,
                                          _vp, _vp, _vp, _vp]),
     "orbx_matcher_profile_enable": (_i, [_vp, _i]),

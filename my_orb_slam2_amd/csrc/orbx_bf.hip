@@ -391,6 +391,8 @@ size_t bf_partial_bytes(long long ndb, int nq, int chunk) {
     return (size_t)nchunks * (size_t)nqpad * sizeof(uint2);
 }
 
+const char* bf_kernel_name() { return BF_MFMA ? "k_bf_mfma" : "k_bf_top2"; }
+
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer) {
     if (a.nq <= 0) return hipSuccess;
     const int nqpad = ((a.nq + 255) / 256) * 256;

@@ -819,6 +819,8 @@ orbx_status orbx_hamming_bf_top2(orbx_matcher* m, const uint8_t* q, int32_t nq,
     return ORBX_OK;
 }
 
+const char* orbx_bf_kernel(void) { return orbx::bf_kernel_name(); }
+
 orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int32_t nq,
                                         const uint8_t* d_db, int64_t ndb, int64_t idx_base,
                                         int32_t* d_best_idx, int32_t* d_best_dist,

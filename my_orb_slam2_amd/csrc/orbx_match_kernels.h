@@ -103,6 +103,7 @@ int bf_chunk_rows(long long ndb, int nq, int ncu);
 size_t bf_partial_bytes(long long ndb, int nq, int chunk);
 struct KernelTimer;
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer);
+const char* bf_kernel_name();
 hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, int32_t* best,
                               int* err, hipStream_t st);
 size_t distinctive_lds_bytes();
