@@ -32,8 +32,11 @@ HASH_TAG = b"orbx-src:"
 
 # -ffp-contract=off: every float a*b+c in the path is two roundings, as in the x86 reference
 # (hipcc defaults to fast contraction).  No -ffast-math: IEEE division/rounding throughout.
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs (k_bf_mfma's 16-bit keys are read by
+# VALU min / max straight from them; in AGPRs each read costs a v_accvgpr_read).
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+         "-mllvm", "-amdgpu-mfma-vgpr-form",
          "-I" + str(PKG.parent / "include")]
 
 

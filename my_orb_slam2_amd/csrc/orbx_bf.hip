@@ -192,40 +192,57 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
 }
 
 // ---- k_bf_mfma: the distances on the matrix cores ----
-// With every bit mapped to +-1 (database row: bit 1 -> +1, 0 -> -1; query: 1 -> -1, 0 -> +1),
-// the dot product of two 256-bit descriptors is sum(+1 per differing bit, -1 per equal bit)
-// = 2 * popcount(a ^ b) - 256, exactly, in int32.  v_mfma_i32_32x32x32_i8 forms 32 rows x 32
-// queries of it per 8 instructions (K = 256 = 8 x 32), at the i8 matrix rate, so a distance
-// costs the top-2 update (key build, v_med3, v_min) instead of 8 v_xor + 8 v_bcnt.  The
-// kernel is issue-bound on that update and on the MFMAs, not on HBM (32 B per row per query
-// block).
-//   workgroup: 4 waves x 64 queries (two 32-query tiles per wave, their +-1 bytes held in
+// Every bit maps to a signed byte, database row: bit 1 -> +1, 0 -> -1; query: bit 1 -> -64,
+// 0 -> +64.  The dot product of a row with a query is then +64 per differing bit and -64 per
+// equal bit: 64 (2 popcount(a ^ b) - 256) = 128 dist - 16384, exactly, in int32.
+// v_mfma_i32_32x32x32_i8 forms 32 rows x 32 queries of it per 8 instructions (K = 256 =
+// 8 x 32) at the i8 matrix rate.  Started from C = 16384 + m (m = the row's index in a
+// 128-row superblock), an accumulator IS the 16-bit key dist << 7 | m, so a distance costs
+// three full-rate 16-bit min / max ops of the top-2 update and nothing else (k_bf_top2: 8 v_xor
+// + 8 v_bcnt + the key).  Issue-bound on the MFMAs and that update, not on HBM (32 B per row
+// per query block).
+//   workgroup: 4 waves x 64 queries (two 32-query tiles per wave, their signed bytes held in
 //   registers for the whole chunk) against the chunk's rows in blocks of 32: the block's 1 KB
-//   is read once (a dword per thread), expanded to +-1 bytes in the A-fragment order, staged in
-//   LDS (double-buffered, one barrier per block) and read by every wave (ds_read_b128 per
+//   is read once (a dword per thread), expanded to signed bytes in the A-fragment order, staged
+//   in LDS (double-buffered, one barrier per block) and read by every wave (ds_read_b128 per
 //   step).  A fragment element j of lane l (r = l & 31, h = l >> 5) at step s is bit
-//   32 s + 16 h + j of row r, and the B fragment's element j of lane l is the same bit of query
-//   r: the sum over k pairs equal bits whatever k the hardware gives element j, as long as A
-//   and B share it (they do: the parity tests compare every distance-derived output).
-//   Accumulator register i of lane l holds (row (i & 3) + 8 (i >> 2) + 4 h, query r): key =
-//   (acc << 22) + (256 << 22) + row = dist << 23 | row, the k_bf_top2 key, and the same
-//   partials go to k_bf_merge.
+//   32 s + 16 h + j of row r, and the B fragment's element j of lane l is the same bit of
+//   query r: the sum pairs equal bits whatever k the hardware gives element j, as long as A
+//   and B share it (the parity tests check every distance-derived output).
+//   Accumulator register i of lane l holds (row (i & 3) + 8 (i >> 2) + 4 h of the block,
+//   query r).  A superblock's 16-bit top-2 is folded into the chunk's 32-bit (dist << 23 |
+//   row) top-2, the k_bf_top2 key, and the same partials go to k_bf_merge.
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-// 16 bits -> 16 bytes, byte j = bit j ? 0x01 : 0xFF (off_pattern 0xFFFFFFFF) or the reverse
-// (0x01010101): ((nibble * 0x00204081) & 0x01010101) spreads a nibble's bits to the bytes' low
-// bits, a packed 16-bit multiply by 0xFE (no carries: every byte is 0 or 1) makes 0x00 / 0xFE
-// of them, and the XOR the +-1 bytes
-__device__ __forceinline__ v4i expand16(uint32_t bits, uint32_t off_pattern, uint32_t fe) {
+// 16 bits -> 16 bytes: ((nibble * 0x00204081) & 0x01010101) spreads a nibble's bits to the
+// bytes' low bits (t); rows: byte = t ? 0x01 : 0xFF via a packed 16-bit multiply by 0xFE (no
+// carries: every byte of t is 0 or 1) and a NOT; queries: byte = t ? 0xC0 : 0x40 (t << 7)
+template <bool QUERY>
+__device__ __forceinline__ v4i expand16(uint32_t bits, uint32_t fe) {
     v4i r;
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const uint32_t t = (((bits >> (4 * n)) & 15u) * 0x00204081u) & 0x01010101u;
-        uint32_t m;
-        asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(t), "v"(fe));
-        r[n] = (int)(m ^ off_pattern);
+        if (QUERY) {
+            r[n] = (int)((t << 7) ^ 0x40404040u);
+        } else {
+            uint32_t m;
+            asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(t), "v"(fe));
+            r[n] = (int)~m;
+        }
     }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t min_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t max_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
 
@@ -247,31 +264,43 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
     for (int t = 0; t < 2; ++t) {
         const int qi = min(bx * 256 + w * 64 + t * 32 + r, nq - 1);
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-            bq[t][s] = expand16(q[(size_t)qi * 8 + s] >> (16 * h), 0x01010101u, fe);
+        for (int s = 0; s < 8; ++s) bq[t][s] = expand16<true>(q[(size_t)qi * 8 + s] >> (16 * h), fe);
     }
     // this thread's share of a block: dword (tid & 7) of row (tid >> 3)
     const int lr = tid >> 3, ls = tid & 7;
     auto stage = [&](int buf, uint32_t v) {
-        frag[buf][ls * 64 + lr] = expand16(v & 0xFFFFu, 0xFFFFFFFFu, fe);
-        frag[buf][ls * 64 + 32 + lr] = expand16(v >> 16, 0xFFFFFFFFu, fe);
+        frag[buf][ls * 64 + lr] = expand16<false>(v & 0xFFFFu, fe);
+        frag[buf][ls * 64 + 32 + lr] = expand16<false>(v >> 16, fe);
     };
     auto fetch = [&](int e0) { return p[(size_t)min(e0 + lr, n - 1) * 8 + ls]; };
-    // key offsets of the lane's 16 accumulator rows in a block: (256 << 22) + row in the block
-    uint32_t koff[16];
+    // accumulator starts of the lane's 16 rows of a block at superblock offset 0
+    uint32_t kinit[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) koff[i] = (256u << 22) + (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h);
+    for (int i = 0; i < 16; ++i) kinit[i] = 16384u + (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h);
     uint32_t b1[2] = {BF_NONE, BF_NONE}, b2[2] = {BF_NONE, BF_NONE};
+    uint32_t l1[2] = {0xFFFFu, 0xFFFFu}, l2[2] = {0xFFFFu, 0xFFFFu};
     const int nblk = (n + 31) / 32;
+    // the superblock's 16-bit top-2 -> the chunk's (dist << 23 | row) top-2
+    auto fold = [&](int esb) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint32_t o1 = l1[t] == 0xFFFFu ? 0xFFFFFFFFu
+                                                : ((l1[t] >> 7) << 23) + (uint32_t)esb + (l1[t] & 127u);
+            const uint32_t o2 = l2[t] == 0xFFFFu ? 0xFFFFFFFFu
+                                                : ((l2[t] >> 7) << 23) + (uint32_t)esb + (l2[t] & 127u);
+            b2[t] = min(max(b1[t], o1), min(b2[t], o2));
+            b1[t] = min(b1[t], o1);
+            l1[t] = l2[t] = 0xFFFFu;
+        }
+    };
     if (nblk > 0) stage(0, fetch(0));
     __syncthreads();
-    // the block's top-2 over its (distance, row-in-block) keys, then its rows offset by e0 and
-    // folded into the chunk's; the tail block drops its rows past n
-    auto block = [&](int buf, int e0, auto tail_c) {
-        constexpr bool TAIL = decltype(tail_c)::value;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int buf = blk & 1, e0 = blk * 32, j = blk & 3;
+        const uint32_t nxt = blk + 1 < nblk ? fetch(e0 + 32) : 0u;   // in flight meanwhile
         v16i acc[2];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) acc[t] = v16i{};
+        for (int i = 0; i < 16; ++i) acc[0][i] = acc[1][i] = (int)(kinit[i] + 32u * (uint32_t)j);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const v4i a = frag[buf][s * 64 + lane];
@@ -279,29 +308,27 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
             for (int t = 0; t < 2; ++t)
                 acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[t][s], acc[t], 0, 0, 0);
         }
+        if (e0 + 32 <= n) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            uint32_t l1 = 0xFFFFFFFFu, l2 = 0xFFFFFFFFu;
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                uint32_t key = ((uint32_t)acc[t][i] << 22) + koff[i];
-                if (TAIL && e0 + (int)(koff[i] & 31u) >= n) key = 0xFFFFFFFFu;
-                l2 = med3_u32(l1, l2, key);
-                l1 = min(l1, key);
-            }
-            // rows e0 + ..: a block key of 0xFFFFFFFF (no row) stays above every real key
-            const uint32_t o1 = l1 == 0xFFFFFFFFu ? l1 : l1 + (uint32_t)e0;
-            const uint32_t o2 = l2 == 0xFFFFFFFFu ? l2 : l2 + (uint32_t)e0;
-            b2[t] = min(max(b1[t], o1), min(b2[t], o2));
-            b1[t] = min(b1[t], o1);
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t key = (uint32_t)acc[t][i];
+                    l2[t] = min_u16(l2[t], max_u16(l1[t], key));
+                    l1[t] = min_u16(l1[t], key);
+                }
+        } else {   // the chunk's last, partial block: rows past n dropped
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const bool ok = e0 + (i & 3) + 8 * (i >> 2) + 4 * h < n;
+                    const uint32_t key = ok ? (uint32_t)acc[t][i] : 0xFFFFu;
+                    l2[t] = min_u16(l2[t], max_u16(l1[t], key));
+                    l1[t] = min_u16(l1[t], key);
+                }
         }
-    };
-    const int nfull = n / 32;
-    for (int blk = 0; blk < nblk; ++blk) {
-        const int buf = blk & 1, e0 = blk * 32;
-        const uint32_t nxt = blk + 1 < nblk ? fetch(e0 + 32) : 0u;   // in flight meanwhile
-        if (blk < nfull) block(buf, e0, std::false_type{});
-        else block(buf, e0, std::true_type{});
+        if (j == 3 || blk + 1 == nblk) fold(e0 - 32 * j);
         if (blk + 1 < nblk) stage(buf ^ 1, nxt);
         __syncthreads();
     }
