@@ -103,9 +103,10 @@ def parse():
                     help="dropin: comma-separated numbers of concurrent tracking sessions K (each "
                          "its own left / right handles and threads, sharing the GPU); one result "
                          "line holds every K")
-    ap.add_argument("--dropin-via", choices=["facade", "cabi"], default="facade",
+    ap.add_argument("--dropin-via", choices=["facade", "frame", "cabi"], default="facade",
                     help="dropin: the ORB_SLAM2::ORBextractor facade loop (tests/native/"
-                         "facade_test) or the bare C-ABI loop (tests/native/boundary_test)")
+                         "facade_test), its one-call stereo Frame (orbx_glue::ExtractStereo), "
+                         "or the bare C-ABI loop (tests/native/boundary_test)")
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
     ap.add_argument("--db-rows", type=int, default=10_000_000,
                     help="bf: database descriptors (10k keyframes x 1000, SURVEY §8(d) C4)")
@@ -1041,7 +1042,8 @@ def main_dropin(args):
     # the loop ORB-SLAM2 runs through the facade (integration/ORBextractor.h: a stereo Frame per
     # frame, Frame.cc:66-120), or the same calls on the bare C ABI (--dropin-via cabi)
     binp = os.path.join(ROOT, "tests", "native",
-                        "facade_test" if args.dropin_via == "facade" else "boundary_test")
+                        "boundary_test" if args.dropin_via == "cabi" else "facade_test")
+    extra = ["frame"] if args.dropin_via == "frame" else []
     ks = [max(1, int(k)) for k in str(args.trackers).split(",")]
     per_k = {}
     with tempfile.TemporaryDirectory() as d:
@@ -1051,7 +1053,7 @@ def main_dropin(args):
         with open(os.path.join(d, "params.txt"), "w") as f:
             f.write(f"{W} {H} {NFEAT} {MBF!r} {mb!r} {B}\n")
         for K in ks:
-            r = subprocess.run([binp, "bench", d, str(args.frames), str(warm), str(K)],
+            r = subprocess.run([binp, "bench", d, str(args.frames), str(warm), str(K)] + extra,
                                capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.exit(f"bench.py: {binp} failed ({r.returncode}): {r.stderr[-2000:]}")
@@ -1068,9 +1070,11 @@ def main_dropin(args):
         cpu = cpu_baseline(pairs, mb, min(args.cpu_seconds, 6.0))
     k0 = per_k[ks[0]]
     lat = k0["latency"]
-    via = ("ORB_SLAM2::ORBextractor facade: Frame::ExtractORB x2 on 2 threads + "
-           "ComputeStereoMatches" if args.dropin_via == "facade" else
-           "C ABI: orbx_extract x2 on 2 threads + orbx_stereo_match")
+    via = {"facade": "ORB_SLAM2::ORBextractor facade: Frame::ExtractORB x2 on 2 threads + "
+                     "ComputeStereoMatches",
+           "frame": "facade, the stereo Frame's extraction + matching as one two-image "
+                    "submission (orbx_glue::ExtractStereo)",
+           "cabi": "C ABI: orbx_extract x2 on 2 threads + orbx_stereo_match"}[args.dropin_via]
     out = {"metric": f"per-stereo-frame latency of the drop-in host path ({via}), KITTI 1241x376",
            "value": 1000.0 / lat["mean_ms"] if ks[0] == 1 else k0["pairs_per_s"],
            "unit": "frames/sec", "n_gpus": 1,

@@ -152,6 +152,28 @@ orbx_status orbx_batch_fetch(orbx_extractor* h, int first, int count, int32_t* n
 orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, float mbf, float mb,
                               float* uRight, float* depth, int n_left, int* n_valid);
 
+/* The stereo Frame constructor's extraction and matching (Frame.cc:66-120: ExtractORB of both
+ * views, Frame.cc:89-92, then ComputeStereoMatches, Frame.cc:496-686) in one call on ONE
+ * handle: both host images go into the handle's pinned staging and, by one 2-D DMA, into the
+ * level-0 slots of a two-image batch (left = image 0, right = image 1); the two extractions run
+ * as that batch and the stereo match is appended, and the whole device sequence is replayed from
+ * one HIP graph with one host wait.  The results are the same as two orbx_extract calls on two
+ * handles followed by orbx_stereo_match.  Outputs point into the handle's pinned block, valid
+ * until the next call that uses the handle; n[v] < 0 never happens (an empty image returns
+ * ORBX_ERR_INVALID).  mb as in orbx_stereo_match. */
+typedef struct {
+    const orbx_keypoint* kps[2];  /* [view] (0 = left, 1 = right): n[view] keypoints          */
+    const uint8_t* desc[2];       /* [view]: n[view] x 32 bytes                                 */
+    int32_t n[2];
+    const float* u_right;         /* n[0] floats (-1 = no match)                                */
+    const float* depth;           /* n[0] floats                                                */
+    int32_t n_valid;
+} orbx_stereo_frame_out;
+
+orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_t stride_left,
+                                   const uint8_t* right, size_t stride_right, int width,
+                                   int height, float mbf, float mb, orbx_stereo_frame_out* out);
+
 /* Batched stereo over the last orbx_extract_batch_device calls of both handles (pair i =
  * image i of each).  d_uRight/d_depth: device [batch][kp_cap] floats; d_nvalid: device
  * [batch] (may be NULL). */

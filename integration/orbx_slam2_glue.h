@@ -3,6 +3,8 @@
 // needs nothing from ORB-SLAM2 beyond the members it names.
 //
 //   ComputeStereoMatches(F)         replaces Frame::ComputeStereoMatches (src/Frame.cc:496-686)
+//   ExtractStereo(F, imL, imR)      replaces Frame.cc:89-102 (both ExtractORB threads + the
+//                                   stereo match) by one two-image submission
 //   OrbxView / BuildView(f, view)   the orbx_featureset of a Frame / KeyFrame (mFeatVec, mGrid)
 //   SearchByBoW(m, pKF, F, out)     ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (:182-319)
 //
@@ -11,9 +13,12 @@
 #define ORBX_INTEGRATION_SLAM2_GLUE_H
 
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include <opencv2/core/core.hpp>
 
 #include "orbx.h"
 #include "orbx_match.h"
@@ -37,6 +42,46 @@ int ComputeStereoMatches(Frame& F) {
                             &nvalid),
           "orbx_stereo_match");
     return nvalid;
+}
+
+// Frame.cc:89-102 in one call (the stereo Frame constructor's two ExtractORB threads, then
+// ComputeStereoMatches): both views as one two-image batch on the LEFT extractor's handle with
+// the stereo match appended, one submission and one wait (orbx_stereo_frame_view).  Fills
+// mvKeys / mDescriptors, mvKeysRight / mDescriptorsRight, N, mvuRight / mvDepth with the same
+// values as the two-thread form.  The right extractor's handle is not used.
+template <class Frame>
+int ExtractStereo(Frame& F, const cv::Mat& imLeft, const cv::Mat& imRight) {
+    static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint), "cv::KeyPoint layout");
+    if (imLeft.rows != imRight.rows || imLeft.cols != imRight.cols)
+        throw std::invalid_argument("ExtractStereo: left and right sizes differ");
+    orbx_stereo_frame_out o{};
+    check(orbx_stereo_frame_view(F.mpORBextractorLeft->handle(), imLeft.data,
+                                 (size_t)imLeft.step, imRight.data, (size_t)imRight.step,
+                                 imLeft.cols, imLeft.rows, F.mbf, F.mbf / F.fx, &o),
+          "orbx_stereo_frame_view");
+    auto keys = [](const orbx_keypoint* k, int n) {
+        const cv::KeyPoint* c = reinterpret_cast<const cv::KeyPoint*>(k);
+        return std::vector<cv::KeyPoint>(c, c + n);
+    };
+    auto desc = [](const uint8_t* d, int n, cv::Mat& m) {
+        if (n == 0) {
+            m.release();
+            return;
+        }
+        m.create(n, 32, CV_8U);
+        if (m.isContinuous())
+            std::memcpy(m.data, d, (size_t)n * 32);
+        else
+            for (int i = 0; i < n; ++i) std::memcpy(m.ptr(i), d + (size_t)i * 32, 32);
+    };
+    F.mvKeys = keys(o.kps[0], o.n[0]);
+    F.mvKeysRight = keys(o.kps[1], o.n[1]);
+    desc(o.desc[0], o.n[0], F.mDescriptors);
+    desc(o.desc[1], o.n[1], F.mDescriptorsRight);
+    F.N = o.n[0];
+    F.mvuRight.assign(o.u_right, o.u_right + o.n[0]);
+    F.mvDepth.assign(o.depth, o.depth + o.n[0]);
+    return o.n_valid;
 }
 
 // CSR copies of mFeatVec (after ComputeBoW) and mGrid (after AssignFeaturesToGrid); the other

@@ -56,6 +56,8 @@ SIGNATURES = {
     "orbx_extractor_tables": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "orbx_extractor_prepare": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i)]),
     "orbx_extract": (_i, [_vp, _vp, _i, _i, _sz, _vp, _i, _vp, ctypes.POINTER(_i)]),
+    "orbx_stereo_frame_view": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _i, ctypes.c_float,
+                                    ctypes.c_float, _vp]),
     "orbx_extract_view": (_i, [_vp, _vp, _i, _i, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                ctypes.POINTER(_i)]),
     "orbx_pyramid_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),

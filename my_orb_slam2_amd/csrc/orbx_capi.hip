@@ -67,6 +67,9 @@ struct orbx_extractor {
     // key (image size, effective schedule, every buffer address it names) changes
     hipGraphExec_t g1 = nullptr;
     std::vector<const void*> g1key;
+    // orbx_stereo_frame_view's sequence (2-D H2D, two-image extraction, stereo, D2H) likewise
+    hipGraphExec_t g2 = nullptr;
+    std::vector<const void*> g2key;
     // pinned staging of the host-image path (orbx_extract / orbx_stereo_match)
     uint8_t* h_in = nullptr;
     size_t h_in_n = 0;
@@ -903,16 +906,16 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
 // stream, which orders them with the caller's other default-stream work.
 hipStream_t pick_stream(orbx_extractor*, void* s) { return (hipStream_t)s; }
 
-// Stereo over pairs (image i of L at offset offL, image i of R at offset offR).
-orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL, int offR,
-                       float mbf, float mb, float* d_uR, float* d_dep, int* d_nv, hipStream_t st) {
-    if (!L->last_valid || !R->last_valid) return ORBX_ERR_STATE;
+// The launch of stereo over pairs (image i of L at offset offL, image i of R at offset offR),
+// its scratch allocated: nothing in it allocates or waits, so it can be enqueued in a graph
+// capture.  The images' extraction must be issued (not necessarily run) before the launch.
+orbx_status stereo_launch_args(orbx_extractor* L, orbx_extractor* R, int batch, int offL,
+                               int offR, float mbf, float mb, float* d_uR, float* d_dep,
+                               int* d_nv, hipStream_t st, StereoLaunch& a) {
     if (L->hg.width != R->hg.width || L->hg.height != R->hg.height ||
-        L->hg.nlevels != R->hg.nlevels || L->hg.kp_cap != R->hg.kp_cap ||
-        offL + batch > L->last_batch || offR + batch > R->last_batch)
+        L->hg.nlevels != R->hg.nlevels || L->hg.kp_cap != R->hg.kp_cap)
         return ORBX_ERR_INVALID;
     const size_t KC = (size_t)L->hg.kp_cap;
-    StereoLaunch a;
     a.dg = L->d_geom.as<Geometry>();
     a.batch = batch;
     a.kpsL = L->d_kps.as<float>() + offL * KC * 7;
@@ -955,6 +958,18 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
         a.ssad = (int*)(base + cnt_bytes);
         a.sidx = (int16_t*)(base + cnt_bytes + (size_t)batch * KC * 4);
     }
+    return ORBX_OK;
+}
+
+// Stereo over pairs of the handles' last extractions.
+orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL, int offR,
+                       float mbf, float mb, float* d_uR, float* d_dep, int* d_nv, hipStream_t st) {
+    if (!L->last_valid || !R->last_valid) return ORBX_ERR_STATE;
+    if (offL + batch > L->last_batch || offR + batch > R->last_batch) return ORBX_ERR_INVALID;
+    StereoLaunch a;
+    const orbx_status s = stereo_launch_args(L, R, batch, offL, offR, mbf, mb, d_uR, d_dep, d_nv,
+                                             st, a);
+    if (s != ORBX_OK) return s;
     if (!order_after_last(L, st) || (R != L && !order_after_last(R, st))) return ORBX_ERR_DEVICE;
     if (!HIPOK(launch_stereo(a, st)) || !mark_done(L, st) || (R != L && !mark_done(R, st)))
         return ORBX_ERR_DEVICE;
@@ -1110,6 +1125,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     for (DevBuf* b : bufs) b->release();
     h->timer.destroy();
     if (h->g1) (void)hipGraphExecDestroy(h->g1);
+    if (h->g2) (void)hipGraphExecDestroy(h->g2);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->done) (void)hipEventDestroy(h->done);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
@@ -1140,7 +1156,9 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
 // The graph of orbx_extract's device sequence for the handle's current state, captured on st
 // when missing or stale.
 static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_t st, int width,
-                           int height, const std::function<bool(const ExtractLaunch&)>& enqueue) {
+                           int height, const std::function<bool(const ExtractLaunch&)>& enqueue,
+                           hipGraphExec_t& gx, std::vector<const void*>& gkey,
+                           std::vector<const void*> extra = {}) {
     const DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr,
                             &h->d_blur, &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp,
                             &h->d_kscr, &h->d_outs};
@@ -1149,10 +1167,11 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
                                     (const void*)(intptr_t)a.side_at,
                                     (const void*)(intptr_t)a.side_lv, h->h_in, h->h_out};
     for (const DevBuf* b : bufs) key.push_back(b->p);
-    if (h->g1 && key == h->g1key) return true;
-    if (h->g1) {
-        (void)hipGraphExecDestroy(h->g1);
-        h->g1 = nullptr;
+    key.insert(key.end(), extra.begin(), extra.end());
+    if (gx && key == gkey) return true;
+    if (gx) {
+        (void)hipGraphExecDestroy(gx);
+        gx = nullptr;
     }
     hipGraph_t g = nullptr;
     if (!HIPOK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal))) return false;
@@ -1162,8 +1181,8 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
     const bool inst = ok && ended && g && HIPOK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     if (g) (void)hipGraphDestroy(g);
     if (!inst) return false;
-    h->g1 = ex;
-    h->g1key = key;
+    gx = ex;
+    gkey = key;
     return true;
 }
 
@@ -1203,7 +1222,7 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
     // replayed from a graph (one launch instead of ~15 enqueues: several tracking sessions
     // on one GPU contend for the runtime's per-call work), eagerly when kernels are timed
     const bool graph = tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
-                       extract1_graph(h, a, st, width, height, enqueue);
+                       extract1_graph(h, a, st, width, height, enqueue, h->g1, h->g1key);
     if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue(a)) || !mark_done(h, st) ||
         !wait_done(h))
         return ORBX_ERR_DEVICE;
@@ -1256,6 +1275,80 @@ orbx_status orbx_extract_view(orbx_extractor* h, const uint8_t* img, int width, 
     *n_out = h->last_n;
     *kps = (const orbx_keypoint*)(h->h_out + o_kps);
     *desc = h->h_out + o_desc;
+    return ORBX_OK;
+}
+
+orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_t stride_left,
+                                   const uint8_t* right, size_t stride_right, int width,
+                                   int height, float mbf, float mb, orbx_stereo_frame_out* out) {
+    if (!h || !out || !left || !right || width <= 0 || height <= 0 ||
+        stride_left < (size_t)width || stride_right < (size_t)width)
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    orbx_status s = ensure_workspace(h, width, height, 2);
+    if (s != ORBX_OK) return s;
+    hipStream_t st = h->stream;
+    const LevelGeom& L0 = h->hg.lv[0];
+    const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)height;
+    const size_t KC = (size_t)h->hg.kp_cap;
+    // outputs of both images: [nkp[2] | kps[.][KC] | desc[.][KC][32]] (the handle's output
+    // block), then the stereo block [nvalid | uRight[KC] | depth[KC]], both copied back
+    const size_t o_kps = (size_t)((uint8_t*)h->d_kps.p - (uint8_t*)h->d_outs.p);
+    const size_t o_desc = (size_t)((uint8_t*)h->d_desc.p - (uint8_t*)h->d_outs.p);
+    const size_t o_end = o_desc + 2 * KC * 32;
+    const size_t so_u = 256, so_d = so_u + KC * 4, s_end = so_d + KC * 4;
+    const size_t o_s = align_up(o_end, 256);
+    if (!h->d_uR.ensure(s_end)) return ORBX_ERR_DEVICE;
+    if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes) ||
+        !ensure_pinned(h->h_out, h->h_out_n, o_s + s_end))
+        return ORBX_ERR_DEVICE;
+    for (int v = 0; v < 2; ++v) {
+        const uint8_t* img = v ? right : left;
+        const size_t stride = v ? stride_right : stride_left;
+        uint8_t* dst = h->h_in + (size_t)v * img_bytes;
+        for (int y = 0; y < height; ++y)
+            std::memcpy(dst + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
+    }
+    if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
+    uint8_t* dso = h->d_uR.as<uint8_t>();
+    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
+    StereoLaunch sa;   // pair 0 = (image 0, image 1) of this handle
+    s = stereo_launch_args(h, h, 1, 0, 1, mbf, mb, (float*)(dso + so_u), (float*)(dso + so_d),
+                           (int*)dso, st, sa);
+    if (s != ORBX_OK) return s;
+    // the device sequence: both images into their level-0 slots by one 2-D DMA (a row = one
+    // image), the two-image extraction, the stereo match, the two output blocks back
+    auto enqueue = [&](const ExtractLaunch& ea) {
+        return HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off, (size_t)h->hg.pyr_bytes,
+                                      h->h_in, img_bytes, img_bytes, 2, hipMemcpyHostToDevice,
+                                      st)) &&
+               HIPOK(launch_extract(ea, st)) && HIPOK(launch_stereo(sa, st)) &&
+               HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) &&
+               HIPOK(hipMemcpyAsync(h->h_out + o_s, dso, s_end, hipMemcpyDeviceToHost, st));
+    };
+    uint32_t mbf_bits, mb_bits;
+    std::memcpy(&mbf_bits, &mbf, 4);
+    std::memcpy(&mb_bits, &mb, 4);
+    const bool graph =
+        tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
+        extract1_graph(h, a, st, width, height, enqueue, h->g2, h->g2key,
+                       {h->d_uR.p, h->d_sscr.p, (const void*)(uintptr_t)mbf_bits,
+                        (const void*)(uintptr_t)mb_bits});
+    if (!(graph ? HIPOK(hipGraphLaunch(h->g2, st)) : enqueue(a)) || !mark_done(h, st) ||
+        !wait_done(h))
+        return ORBX_ERR_DEVICE;
+    h->last_batch = 2;
+    h->last_valid = true;
+    h->last_n = -1;   // not the single-image state orbx_stereo_match expects
+    const uint8_t* ho = h->h_out;
+    std::memcpy(out->n, ho, 8);
+    for (int v = 0; v < 2; ++v) {
+        out->kps[v] = (const orbx_keypoint*)(ho + o_kps + (size_t)v * KC * sizeof(orbx_keypoint));
+        out->desc[v] = ho + o_desc + (size_t)v * KC * 32;
+    }
+    std::memcpy(&out->n_valid, ho + o_s, 4);
+    out->u_right = (const float*)(ho + o_s + so_u);
+    out->depth = (const float*)(ho + o_s + so_d);
     return ORBX_OK;
 }
 

@@ -16,6 +16,8 @@
 //                         independent tracking threads (K SLAM sessions sharing the GPU); DIR as
 //                         boundary_test `bench` (pair_<i>_left/right.raw, params.txt
 //                         "W H nfeatures mbf mb P").  Prints boundary_test bench's JSON line.
+//   a trailing "frame" on run / bench: each stereo frame through orbx_glue::ExtractStereo
+//   (both views as one two-image submission with the stereo match appended)
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -105,7 +107,7 @@ int nogpu() {
     return 6;
 }
 
-int run(const std::string& dir) {
+int run(const std::string& dir, bool frame_call) {
     int W = 0, H = 0, nfeat = 0;
     float mbf = 0.f;
     {
@@ -147,7 +149,10 @@ int run(const std::string& dir) {
     std::vector<uint8_t> Lp(pitch * H, 0xA5);
     for (int y = 0; y < H; ++y) std::memcpy(&Lp[(size_t)y * pitch], &L[(size_t)y * W], (size_t)W);
     const cv::Mat imL(H, W, CV_8UC1, Lp.data(), pitch), imR(H, W, CV_8UC1, R.data());
-    {   // Frame.cc:89-92
+    int nvalid = 0;
+    if (frame_call) {   // Frame.cc:89-102 as one two-image submission
+        nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+    } else {   // Frame.cc:89-92
         std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
         std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
         tl.join();
@@ -161,7 +166,7 @@ int run(const std::string& dir) {
         return 4;
     }
     // mvImagePyramid on request: level 0 is the input image
-    {
+    if (!frame_call) {
         std::vector<cv::Mat>& pyr = left.MaterializePyramid();
         if (pyr.size() != 8 || pyr[0].rows != H || pyr[0].cols != W) return 4;
         for (int y = 0; y < H; ++y)
@@ -170,7 +175,7 @@ int run(const std::string& dir) {
                 return 4;
             }
     }
-    const int nvalid = orbx_glue::ComputeStereoMatches(F);
+    if (!frame_call) nvalid = orbx_glue::ComputeStereoMatches(F);
 
     // SearchByBoW(KF = right view, F = left view), one vocabulary node holding every feature
     F.mvKeysUn = F.mvKeys;
@@ -220,7 +225,7 @@ uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     return h;
 }
 
-int bench(const std::string& dir, int nframes, int warmup, int trackers) {
+int bench(const std::string& dir, int nframes, int warmup, int trackers, bool frame_call) {
     int W = 0, H = 0, nfeat = 0, P = 0;
     float mbf = 0.f, mb = 0.f;
     {
@@ -277,14 +282,17 @@ int bench(const std::string& dir, int nframes, int warmup, int trackers) {
                 F.mpORBextractorRight = s->right.get();
                 F.mbf = mbf;
                 F.fx = fx;
-                {
+                int nvalid = 0;
+                if (frame_call) {   // Frame.cc:89-102 as one two-image submission
+                    nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+                } else {
                     std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
                     std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
                     tl.join();
                     tr.join();
+                    F.N = (int)F.mvKeys.size();
+                    nvalid = orbx_glue::ComputeStereoMatches(F);
                 }
-                F.N = (int)F.mvKeys.size();
-                const int nvalid = orbx_glue::ComputeStereoMatches(F);
                 const auto t1 = std::chrono::steady_clock::now();
                 if (f >= warmup) {
                     s->ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
@@ -351,13 +359,17 @@ int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "";
     try {
         if (mode == "nogpu") return nogpu();
-        if (mode == "run" && argc > 2) return run(argv[2]);
+        // a trailing "frame": the stereo Frame's extraction and matching as one call
+        // (orbx_glue::ExtractStereo) instead of two ExtractORB threads + ComputeStereoMatches
+        const bool frame_call = std::string(argv[argc - 1]) == "frame";
+        if (mode == "run" && argc > 2) return run(argv[2], frame_call);
         if (mode == "bench" && argc > 5)
-            return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
+            return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                         frame_call);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "facade_test: %s\n", e.what());
         return 1;
     }
-    std::fprintf(stderr, "usage: facade_test nogpu | run DIR | bench DIR FRAMES WARMUP K\n");
+    std::fprintf(stderr, "usage: facade_test nogpu | run DIR [frame] | bench DIR FRAMES WARMUP K [frame]\n");
     return 2;
 }

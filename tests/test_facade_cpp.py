@@ -44,8 +44,10 @@ def _sha(b: bytes) -> str:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [0, 1])
-def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed):
+@pytest.mark.parametrize("seed,mode", [(0, "threads"), (1, "threads"), (0, "frame"), (1, "frame")])
+def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed, mode):
+    """threads: Frame's two ExtractORB threads + ComputeStereoMatches; frame: the same Frame
+    through orbx_glue::ExtractStereo's single two-image submission (orbx_stereo_frame_view)."""
     from oracle import matcher as om
     from my_orb_slam2_amd import synth
     from my_orb_slam2_amd._lib import KEYPOINT_DTYPE
@@ -57,8 +59,8 @@ def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed):
     (tmp_path / "left.raw").write_bytes(L.tobytes())
     (tmp_path / "right.raw").write_bytes(R.tobytes())
     (tmp_path / "params.txt").write_text(f"{W} {H} {g['params'][0]} {g['mbf']!r}\n")
-    r = subprocess.run([str(facade_bin), "run", str(tmp_path)], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([str(facade_bin), "run", str(tmp_path)] + (["frame"] if mode == "frame" else []),
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     rd = lambda name: (tmp_path / name).read_bytes()
     n = int(np.frombuffer(rd("n.bin"), np.int32)[0])
@@ -83,10 +85,11 @@ def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed):
 
 @pytest.mark.gpu
 def test_facade_bench_matches_cabi_bench(facade_bin, orbx_lib, gpu, tmp_path):
-    """bench.py --workload dropin's loop through the facade (facade_test `bench`: a Frame per
-    frame, two ExtractORB threads, the stereo glue) and through the bare C ABI (boundary_test
-    `bench`) on the same pairs: 3 tracking sessions each, every session's output digest equal
-    across both programs (the facade adds no result change)."""
+    """bench.py --workload dropin's loops on the same pairs, 3 tracking sessions each: through
+    the facade (facade_test `bench`: a Frame per frame, two ExtractORB threads, the stereo
+    glue), through its one-call form (`bench ... frame`: orbx_glue::ExtractStereo) and through
+    the bare C ABI (boundary_test `bench`): every session's output digest equal across all
+    three (neither the facade nor the two-image submission changes a result)."""
     from my_orb_slam2_amd import build as b
     from my_orb_slam2_amd import synth
     mbf, fx = 386.1448, 718.856
@@ -97,12 +100,13 @@ def test_facade_bench_matches_cabi_bench(facade_bin, orbx_lib, gpu, tmp_path):
         R.tofile(tmp_path / f"pair_{i}_right.raw")
     (tmp_path / "params.txt").write_text(f"1241 376 2000 {mbf!r} {mb!r} 2\n")
     out = {}
-    for name, binp in (("facade", facade_bin), ("cabi", b.build_boundary_test())):
-        r = subprocess.run([str(binp), "bench", str(tmp_path), "5", "2", "3"],
+    for name, binp, extra in (("facade", facade_bin, []), ("frame", facade_bin, ["frame"]),
+                              ("cabi", b.build_boundary_test(), [])):
+        r = subprocess.run([str(binp), "bench", str(tmp_path), "5", "2", "3"] + extra,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, name + ": " + r.stderr
         out[name] = json.loads(r.stdout.strip().splitlines()[-1])
         assert out[name]["trackers"] == 3 and len(out[name]["latency_ms"]) == 15
     assert len(set(out["facade"]["digests"])) == 1, out["facade"]["digests"]
-    assert out["facade"]["digests"] == out["cabi"]["digests"]
+    assert out["facade"]["digests"] == out["cabi"]["digests"] == out["frame"]["digests"]
     assert out["facade"]["mean_stereo_matches"] == out["cabi"]["mean_stereo_matches"] > 0

@@ -16,8 +16,10 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 VAR = ROOT / "tools" / "_var" / "tune"
 
-SETTINGS = {
+SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "frame")
     "default": {},
+    "frame": {"_args": "frame"},
+    "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
     "nospin": {"ORBX_WAIT_SPIN_US": "0"},
     "nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "q16": {"GPU_MAX_HW_QUEUES": "16"},
@@ -39,10 +41,12 @@ def run(d, ks):
     binp = ROOT / "tests" / "native" / os.environ.get("ORBX_AB_BIN", "facade_test")
     for name, env_set in SETTINGS.items():
         for K in ks:
-            env = dict(os.environ, LD_LIBRARY_PATH=str(VAR), **env_set)
+            extra = env_set.get("_args", "").split()
+            env = dict(os.environ, LD_LIBRARY_PATH=str(VAR),
+                       **{k: v for k, v in env_set.items() if not k.startswith("_")})
             frames = 200 if K == 1 else 100
-            r = subprocess.run([str(binp), "bench", d, str(frames), "20", str(K)], env=env,
-                               capture_output=True, text=True, timeout=300)
+            r = subprocess.run([str(binp), "bench", d, str(frames), "20", str(K)] + extra,
+                               env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(name, K, "FAILED", r.stderr[-1000:], flush=True)
                 raise SystemExit(1)
