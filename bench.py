@@ -103,7 +103,7 @@ def parse():
                     help="dropin: comma-separated numbers of concurrent tracking sessions K (each "
                          "its own left / right handles and threads, sharing the GPU); one result "
                          "line holds every K")
-    ap.add_argument("--dropin-via", choices=["facade", "frame", "cabi"], default="facade",
+    ap.add_argument("--dropin-via", choices=["facade", "frame", "cabi"], default="frame",
                     help="dropin: the ORB_SLAM2::ORBextractor facade loop (tests/native/"
                          "facade_test), its one-call stereo Frame (orbx_glue::ExtractStereo), "
                          "or the bare C-ABI loop (tests/native/boundary_test)")
@@ -1023,48 +1023,60 @@ def cpu_baseline_throughput(pairs, mb, budget_s, workers=None):
 
 def main_dropin(args):
     """The path INTEGRATION.md installs into ORB-SLAM2, timed as its Tracking thread runs it:
-    per stereo frame, two std::threads call orbx_extract on the left and right host images
-    (src/Frame.cc:89-92), then orbx_stereo_match (:102); host memory in and out (PCIe
-    included).  The loop runs in C++ (tests/native/boundary_test.cpp `bench`, compiled against
-    include/orbx*.h only), so no Python overhead enters the latency.  `--trackers K[,K..]`: K
-    independent sessions (System.cc:91-101 each) run that loop at once on their own handles and
-    threads, sharing the GPU; per K the per-frame median / mean over every session's --frames
-    frames after --warmup (>= 20) frames, and the aggregate pairs/s (all sessions' frames over
-    the wall time of the timed frames).  Every session's output digest must agree (the same
-    pairs in the same order).  Beside it the CPU restatement run the same way on the same
-    pairs."""
+    per stereo frame a Frame through the compiled facade (tests/native/facade_test.cpp
+    `bench`), host memory in and out (PCIe included), so no Python overhead enters the
+    latency.  --dropin-via frame (the default): the stereo Frame's extraction and matching as
+    one call, orbx_glue::ExtractStereo (both views as one two-image submission with the stereo
+    match appended); facade: the reference's two ExtractORB threads (src/Frame.cc:89-92), then
+    ComputeStereoMatches (:102); cabi: the same on the bare C ABI (boundary_test.cpp `bench`).
+    `--trackers K[,K..]`: K independent sessions (System.cc:91-101 each) run that loop at once
+    on their own handles and threads, sharing the GPU; per K the per-frame median / mean over
+    every session's --frames frames after --warmup (>= 20) frames, and the aggregate pairs/s
+    (all sessions' frames over the wall time of the timed frames).  Every session's output
+    digest must agree (the same pairs in the same order).  With --dropin-via frame the
+    two-thread facade loop runs too (`two_thread_facade`), and its digests must equal the
+    one-call loop's.  Beside it the CPU restatement run the same way on the same pairs."""
     import subprocess
     import tempfile
     B = max(1, args.distinct)
     Lh, Rh, pairs, _ = stereo_inputs(0, B, args.distinct)
     mb = float(np.float32(MBF) / np.float32(FX))
     warm = max(20, args.warmup)
-    # the loop ORB-SLAM2 runs through the facade (integration/ORBextractor.h: a stereo Frame per
-    # frame, Frame.cc:66-120), or the same calls on the bare C ABI (--dropin-via cabi)
-    binp = os.path.join(ROOT, "tests", "native",
-                        "boundary_test" if args.dropin_via == "cabi" else "facade_test")
-    extra = ["frame"] if args.dropin_via == "frame" else []
     ks = [max(1, int(k)) for k in str(args.trackers).split(",")]
-    per_k = {}
-    with tempfile.TemporaryDirectory() as d:
-        for i in range(B):
-            Lh[i].tofile(os.path.join(d, f"pair_{i}_left.raw"))
-            Rh[i].tofile(os.path.join(d, f"pair_{i}_right.raw"))
-        with open(os.path.join(d, "params.txt"), "w") as f:
-            f.write(f"{W} {H} {NFEAT} {MBF!r} {mb!r} {B}\n")
+
+    def loop(d, via):
+        binp = os.path.join(ROOT, "tests", "native",
+                            "boundary_test" if via == "cabi" else "facade_test")
+        extra = ["frame"] if via == "frame" else []
+        per_k, digests = {}, {}
         for K in ks:
             r = subprocess.run([binp, "bench", d, str(args.frames), str(warm), str(K)] + extra,
                                capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.exit(f"bench.py: {binp} failed ({r.returncode}): {r.stderr[-2000:]}")
             res = json.loads(r.stdout.strip().splitlines()[-1])
-            lat = latency_stats(res["latency_ms"])
-            per_k[K] = {"trackers": K, "latency": lat,
+            per_k[K] = {"trackers": K, "latency": latency_stats(res["latency_ms"]),
                         "pairs_per_s": K * args.frames / (res["wall_ms"] / 1000.0),
                         "wall_ms": res["wall_ms"],
                         "sessions_agree": len(set(res["digests"])) == 1,
                         "mean_keypoints_left": res["mean_keypoints_left"],
                         "mean_stereo_matches": res["mean_stereo_matches"]}
+            digests[K] = res["digests"]
+        return per_k, digests
+
+    with tempfile.TemporaryDirectory() as d:
+        for i in range(B):
+            Lh[i].tofile(os.path.join(d, f"pair_{i}_left.raw"))
+            Rh[i].tofile(os.path.join(d, f"pair_{i}_right.raw"))
+        with open(os.path.join(d, "params.txt"), "w") as f:
+            f.write(f"{W} {H} {NFEAT} {MBF!r} {mb!r} {B}\n")
+        per_k, dig = loop(d, args.dropin_via)
+        alt = None
+        if args.dropin_via == "frame":
+            alt_k, alt_dig = loop(d, "facade")
+            alt = {"via": "facade (two ExtractORB threads + ComputeStereoMatches)",
+                   "per_trackers": [alt_k[k] for k in ks],
+                   "digests_equal_one_call": alt_dig == dig}
     cpu = None
     if args.cpu_seconds > 0:
         cpu = cpu_baseline(pairs, mb, min(args.cpu_seconds, 6.0))
@@ -1082,12 +1094,13 @@ def main_dropin(args):
            "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic",
            "config": {"workload": "kitti_stereo_dropin_host_path", "width": W, "height": H,
-                      "nfeatures": NFEAT, "distinct_pairs": B, "threads_per_tracker": 2,
+                      "nfeatures": NFEAT, "distinct_pairs": B,
+                      "threads_per_tracker": 1 if args.dropin_via == "frame" else 2,
                       "trackers": ks, "via": args.dropin_via,
                       "io": "host images in, host keypoints/descriptors/uRight/depth out"},
            "latency": lat, "mean_keypoints_left": k0["mean_keypoints_left"],
            "mean_stereo_matches": k0["mean_stereo_matches"],
-           "per_trackers": [per_k[k] for k in ks], "cpu_baseline": cpu}
+           "per_trackers": [per_k[k] for k in ks], "two_thread_facade": alt, "cpu_baseline": cpu}
     if cpu:
         out["speedup_vs_cpu_median"] = cpu["median_ms"] / lat["median_ms"]
     emit(json.dumps(out))
