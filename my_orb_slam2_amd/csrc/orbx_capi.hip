@@ -1152,6 +1152,9 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
 #ifndef EXTRACT_GRAPH
 #define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
 #endif
+#ifndef FRAME_ZEROCOPY
+#define FRAME_ZEROCOPY 0  // orbx_stereo_frame_view: level 0 read from the pinned staging (no H2D)
+#endif
 
 // The graph of orbx_extract's device sequence for the handle's current state, captured on st
 // when missing or stale.
@@ -1311,7 +1314,12 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     }
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     uint8_t* dso = h->d_uR.as<uint8_t>();
-    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
+    // FRAME_ZEROCOPY: level 0's launch reads both images straight from the pinned staging
+    // (mapped host memory, over PCIe) and writes them into their level-0 slots as it blurs
+    // them (k_level_strip mode 0), instead of a DMA into the slots before the first kernel
+    const bool zc = tuned("ORBX_FRAME_ZEROCOPY", FRAME_ZEROCOPY) != 0;
+    const ExtractLaunch a = zc ? extract_launch(h, h->h_in, nullptr, 2, 2, pitch0, img_bytes)
+                               : extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
     StereoLaunch sa;   // pair 0 = (image 0, image 1) of this handle
     s = stereo_launch_args(h, h, 1, 0, 1, mbf, mb, (float*)(dso + so_u), (float*)(dso + so_d),
                            (int*)dso, st, sa);
@@ -1319,9 +1327,9 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     // the device sequence: both images into their level-0 slots by one 2-D DMA (a row = one
     // image), the two-image extraction, the stereo match, the two output blocks back
     auto enqueue = [&](const ExtractLaunch& ea) {
-        return HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off, (size_t)h->hg.pyr_bytes,
-                                      h->h_in, img_bytes, img_bytes, 2, hipMemcpyHostToDevice,
-                                      st)) &&
+        return (zc || HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off,
+                                             (size_t)h->hg.pyr_bytes, h->h_in, img_bytes,
+                                             img_bytes, 2, hipMemcpyHostToDevice, st))) &&
                HIPOK(launch_extract(ea, st)) && HIPOK(launch_stereo(sa, st)) &&
                HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) &&
                HIPOK(hipMemcpyAsync(h->h_out + o_s, dso, s_end, hipMemcpyDeviceToHost, st));
@@ -1333,7 +1341,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
         extract1_graph(h, a, st, width, height, enqueue, h->g2, h->g2key,
                        {h->d_uR.p, h->d_sscr.p, (const void*)(uintptr_t)mbf_bits,
-                        (const void*)(uintptr_t)mb_bits});
+                        (const void*)(uintptr_t)mb_bits, (const void*)(uintptr_t)zc});
     if (!(graph ? HIPOK(hipGraphLaunch(h->g2, st)) : enqueue(a)) || !mark_done(h, st) ||
         !wait_done(h))
         return ORBX_ERR_DEVICE;
