@@ -25,9 +25,6 @@ namespace orbx {
 #define ST_THREADS 1024
 #endif
 #define ST_WAVES (ST_THREADS / 64)
-#ifndef ST_WIDE
-#define ST_WIDE 1        // SAD windows by 16 / 12-byte loads
-#endif
 #ifndef ST_FUSED_CUT
 #define ST_FUSED_CUT 1   // split path: the last workgroup of a pair runs the cut (no k_stereo_cut)
 #endif
@@ -226,25 +223,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         const int shl = (xl - w) & 3, shr = (xr - L5 - w) & 3;
         const int pdw = pitch >> 2;   // rows are 64-byte aligned
         uint32_t lraw[11][4], rraw[11][7];
-#if ST_WIDE
-        // one 16-byte load for the left row, 16 + 12 bytes for the right one (dword-aligned
-        // addresses; 3 load instructions per row instead of 11: the scattered windows of a
-        // wave's 64 keypoints cost the texture addresser per instruction)
-        typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
-        typedef uint32_t u3a __attribute__((ext_vector_type(3), aligned(4)));
-#pragma unroll
-        for (int r = 0; r < 11; ++r) {
-            const u4a l = *(const u4a*)(pl0 + r * pdw);
-            const u4a r0 = *(const u4a*)(pr0 + r * pdw);
-            const u3a r1 = *(const u3a*)(pr0 + r * pdw + 4);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lraw[r][i] = l[i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) rraw[r][i] = r0[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) rraw[r][4 + i] = r1[i];
-        }
-#else
 #pragma unroll
         for (int r = 0; r < 11; ++r) {
 #pragma unroll
@@ -252,7 +230,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
 #pragma unroll
             for (int i = 0; i < 7; ++i) rraw[r][i] = pr0[r * pdw + i];
         }
-#endif
         auto lrow = [&](int r, uint32_t (&o)[3]) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) o[i] = __builtin_amdgcn_alignbyte(lraw[r][i + 1], lraw[r][i], shl);
