@@ -96,6 +96,7 @@ struct orbx_extractor {
     // the extraction outputs as one allocation: [nkp[B] | kps[B][KC] | desc[B][KC][32]]
     // (d_nkp / d_kps / d_desc are views of it): one DMA returns one image's results
     DevBuf d_outs;
+    size_t o_stereo = 0;   // offset of the stereo block in d_outs
     long long kscratch_per_image = 0;
     KernelTimer timer;
     // last extraction
@@ -818,7 +819,10 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
         const size_t o_kps = align_up(B * 4, 256);
         const size_t o_desc = o_kps + align_up(B * G.kp_cap * sizeof(orbx_keypoint), 256);
         const size_t o_end = o_desc + B * G.kp_cap * 32;
-        ok = ok && h->d_outs.ensure(o_end);
+        // then one pair's stereo block [nvalid | uRight[KC] | depth[KC]]
+        // (orbx_stereo_frame_view: its outputs come back with the keypoints in one DMA)
+        h->o_stereo = align_up(o_end, 256);
+        ok = ok && h->d_outs.ensure(h->o_stereo + 256 + 8 * (size_t)G.kp_cap);
         if (!ok) return ORBX_ERR_DEVICE;
         uint8_t* ob = h->d_outs.as<uint8_t>();
         h->d_nkp.view(ob, B * 4);
@@ -1152,9 +1156,6 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
 #ifndef EXTRACT_GRAPH
 #define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
 #endif
-#ifndef FRAME_ZEROCOPY
-#define FRAME_ZEROCOPY 0  // orbx_stereo_frame_view: level 0 read from the pinned staging (no H2D)
-#endif
 
 // The graph of orbx_extract's device sequence for the handle's current state, captured on st
 // when missing or stale.
@@ -1168,7 +1169,11 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
     std::vector<const void*> key = {(const void*)(intptr_t)width, (const void*)(intptr_t)height,
                                     (const void*)(intptr_t)a.side_mode,
                                     (const void*)(intptr_t)a.side_at,
-                                    (const void*)(intptr_t)a.side_lv, h->h_in, h->h_out};
+                                    (const void*)(intptr_t)a.side_lv, h->h_in, h->h_out,
+                                    // the output block's layout (a regrown buffer may come
+                                    // back at the same address)
+                                    (const void*)(intptr_t)h->cap_batch,
+                                    (const void*)(intptr_t)h->hg.kp_cap};
     for (const DevBuf* b : bufs) key.push_back(b->p);
     key.insert(key.end(), extra.begin(), extra.end());
     if (gx && key == gkey) return true;
@@ -1294,43 +1299,49 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     const LevelGeom& L0 = h->hg.lv[0];
     const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)height;
     const size_t KC = (size_t)h->hg.kp_cap;
-    // outputs of both images: [nkp[2] | kps[.][KC] | desc[.][KC][32]] (the handle's output
-    // block), then the stereo block [nvalid | uRight[KC] | depth[KC]], both copied back
+    // outputs of both images: [nkp | kps[.][KC] | desc[.][KC][32]] (the handle's output block,
+    // two images of its capacity), the pair's stereo block [nvalid | uRight[KC] | depth[KC]]
+    // at o_stereo; one DMA back when the block holds just the two images, else two
     const size_t o_kps = (size_t)((uint8_t*)h->d_kps.p - (uint8_t*)h->d_outs.p);
     const size_t o_desc = (size_t)((uint8_t*)h->d_desc.p - (uint8_t*)h->d_outs.p);
     const size_t o_end = o_desc + 2 * KC * 32;
     const size_t so_u = 256, so_d = so_u + KC * 4, s_end = so_d + KC * 4;
-    const size_t o_s = align_up(o_end, 256);
-    if (!h->d_uR.ensure(s_end)) return ORBX_ERR_DEVICE;
+    const size_t o_s = h->o_stereo;
+    const bool one_dma = h->cap_batch == 2;
     if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes) ||
         !ensure_pinned(h->h_out, h->h_out_n, o_s + s_end))
         return ORBX_ERR_DEVICE;
-    for (int v = 0; v < 2; ++v) {
+    auto stage = [&](int v) {
         const uint8_t* img = v ? right : left;
         const size_t stride = v ? stride_right : stride_left;
         uint8_t* dst = h->h_in + (size_t)v * img_bytes;
         for (int y = 0; y < height; ++y)
             std::memcpy(dst + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
-    }
+    };
+    uint8_t* d_l0 = h->d_pyr.as<uint8_t>() + L0.off;   // image 0's level-0 slot
+    const size_t pyrb = (size_t)h->hg.pyr_bytes;
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
-    uint8_t* dso = h->d_uR.as<uint8_t>();
-    // FRAME_ZEROCOPY: level 0's launch reads both images straight from the pinned staging
-    // (mapped host memory, over PCIe) and writes them into their level-0 slots as it blurs
-    // them (k_level_strip mode 0), instead of a DMA into the slots before the first kernel
-    const bool zc = tuned("ORBX_FRAME_ZEROCOPY", FRAME_ZEROCOPY) != 0;
-    const ExtractLaunch a = zc ? extract_launch(h, h->h_in, nullptr, 2, 2, pitch0, img_bytes)
-                               : extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
+    // the left image's DMA runs while the right one is staged
+    stage(0);
+    if (!HIPOK(hipMemcpyAsync(d_l0, h->h_in, img_bytes, hipMemcpyHostToDevice, st)))
+        return ORBX_ERR_DEVICE;
+    stage(1);
+    uint8_t* dso = h->d_outs.as<uint8_t>() + o_s;
+    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
     StereoLaunch sa;   // pair 0 = (image 0, image 1) of this handle
     s = stereo_launch_args(h, h, 1, 0, 1, mbf, mb, (float*)(dso + so_u), (float*)(dso + so_d),
                            (int*)dso, st, sa);
     if (s != ORBX_OK) return s;
-    // the device sequence: both images into their level-0 slots by one 2-D DMA (a row = one
-    // image), the two-image extraction, the stereo match, the two output blocks back
+    // the device sequence: the right image into its level-0 slot, the two-image extraction,
+    // the stereo match, the outputs back
     auto enqueue = [&](const ExtractLaunch& ea) {
-        return (zc || HIPOK(hipMemcpy2DAsync(h->d_pyr.as<uint8_t>() + L0.off,
-                                             (size_t)h->hg.pyr_bytes, h->h_in, img_bytes,
-                                             img_bytes, 2, hipMemcpyHostToDevice, st))) &&
-               HIPOK(launch_extract(ea, st)) && HIPOK(launch_stereo(sa, st)) &&
+        bool ok = HIPOK(hipMemcpyAsync(d_l0 + pyrb, h->h_in + img_bytes, img_bytes,
+                                       hipMemcpyHostToDevice, st)) &&
+                  HIPOK(launch_extract(ea, st)) && HIPOK(launch_stereo(sa, st));
+        if (one_dma)
+            return ok && HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_s + s_end,
+                                              hipMemcpyDeviceToHost, st));
+        return ok &&
                HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) &&
                HIPOK(hipMemcpyAsync(h->h_out + o_s, dso, s_end, hipMemcpyDeviceToHost, st));
     };
@@ -1340,8 +1351,8 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     const bool graph =
         tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
         extract1_graph(h, a, st, width, height, enqueue, h->g2, h->g2key,
-                       {h->d_uR.p, h->d_sscr.p, (const void*)(uintptr_t)mbf_bits,
-                        (const void*)(uintptr_t)mb_bits, (const void*)(uintptr_t)zc});
+                       {h->d_sscr.p, (const void*)(uintptr_t)mbf_bits,
+                        (const void*)(uintptr_t)mb_bits, (const void*)(uintptr_t)one_dma});
     if (!(graph ? HIPOK(hipGraphLaunch(h->g2, st)) : enqueue(a)) || !mark_done(h, st) ||
         !wait_done(h))
         return ORBX_ERR_DEVICE;
