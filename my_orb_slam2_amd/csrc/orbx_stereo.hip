@@ -26,8 +26,20 @@ namespace orbx {
 #endif
 #define ST_WAVES (ST_THREADS / 64)
 #ifndef ST_FUSED_CUT
-#define ST_FUSED_CUT 1   // split path: the last workgroup of a pair runs the cut (no k_stereo_cut)
+// split path: the last workgroup of a pair runs the cut (no k_stereo_cut); 1: its hand-off by
+// an agent-scope fence on both sides, 2: by write-through stores and loads (no fence)
+#define ST_FUSED_CUT 2
 #endif
+// the split path's stores of uRight / depth / SADs: write-through (sc1) under ST_FUSED_CUT 2,
+// so the last workgroup reads them from memory and overwrites them with no fence between
+template <class T>
+__device__ __forceinline__ void split_store(T* p, T v) {
+#if ST_FUSED_CUT == 2
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
 
 // N bytes of a pyramid row starting at x, as ceil(N/4) dwords realigned to x (bytes of
 // dword i = row[x + 4i .. x + 4i + 3]).  Rows are 64-byte aligned with >= 4 bytes of slack.
@@ -146,8 +158,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     const int chunk = (NL + nsplit - 1) / nsplit;
     const int iL0 = slice * chunk, iL1 = min(NL, iL0 + chunk);
     for (int iL = iL0 + tid; iL < iL1; iL += ST_THREADS) {
-        uR[iL] = -1.0f;
-        dep[iL] = -1.0f;
+        if (nsplit > 1) {
+            split_store(uR + iL, -1.0f);
+            split_store(dep + iL, -1.0f);
+        } else {
+            uR[iL] = -1.0f;
+            dep[iL] = -1.0f;
+        }
         const float uL = kL[iL * 7 + 0], vL = kL[iL * 7 + 1];
         const int levelL = ((const int*)kL)[iL * 7 + 5];
         const int row = (int)vL;
@@ -317,25 +334,49 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
                 disparity = (float)0.01;
                 bestuR = (float)((double)uL - 0.01);
             }
-            dep[iL] = mbf / disparity;
-            uR[iL] = bestuR;
             if (nsplit == 1) {
+                dep[iL] = mbf / disparity;
+                uR[iL] = bestuR;
                 const int pos = atomicAdd(&tmp[16], 1);
                 vsad[pos] = bestDist;
                 vidx[pos] = (int16_t)iL;
             } else {
+                split_store(dep + iL, mbf / disparity);
+                split_store(uR + iL, bestuR);
                 // a pair has at most KC accepted SADs; the guard keeps a corrupted counter from
                 // writing past the pair's slots
                 const int pos = atomicAdd(&scnt[b], 1);
                 if (pos < KC) {
-                    ssad[(size_t)b * KC + pos] = bestDist;
-                    sidx[(size_t)b * KC + pos] = (int16_t)iL;
+                    split_store(ssad + (size_t)b * KC + pos, bestDist);
+                    split_store(sidx + (size_t)b * KC + pos, (int16_t)iL);
                 }
             }
         }
     }
     if (nsplit > 1) {
-#if ST_FUSED_CUT
+#if ST_FUSED_CUT == 2
+        // the pair's last workgroup to finish takes the median: every wave's write-through
+        // stores complete, the workgroup's arrival counted by one agent-scope add; the last
+        // one to arrive reads the pair's SADs by write-through loads into LDS (no fence: its
+        // own later stores to uRight / depth cannot be overtaken by older dirty lines, the
+        // others' stores never sat in an L2)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) tmp[17] = atomicAdd(&scnt[256 + b], 1) == nsplit - 1;
+        __syncthreads();
+        if (!tmp[17]) return;
+        const int nv = min(__hip_atomic_load(&scnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), KC);
+        for (int j = tid; j < nv; j += ST_THREADS) {
+            vsad[j] = __hip_atomic_load(ssad + (size_t)b * KC + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            vidx[j] = __hip_atomic_load(sidx + (size_t)b * KC + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            scnt[b] = 0;
+            scnt[256 + b] = 0;
+        }
+        median_cut(nv, vsad, vidx, hist, tmp, uR, dep, nvalid, b);
+#elif ST_FUSED_CUT
         // the pair's last workgroup to finish takes the median over the global scratch (the
         // others' SADs are visible after their release fence and this one's acquire): no
         // second launch for the cut

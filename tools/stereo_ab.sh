@@ -18,5 +18,7 @@ import json; j=json.load(open('$OUT/frame_${v}_k$K.json')); v=sorted(j['latency_
 print('$v K=$K median', v[len(v)//2], 'pairs/s', round(j['trackers']*j['frames']/(j['wall_ms']/1e3)), j['digests'][0])"
   done
 done
-[ "$2" = "headline" ] && timeout -k 10 600 python tools/variants.py run > $OUT/variants.txt 2>&1 || { echo "VARIANTS FAILED"; tail -20 $OUT/variants.txt; exit 1; }
-[ "$2" = "headline" ] && cat $OUT/variants.txt; true
+if [ "$2" = "headline" ]; then
+  timeout -k 10 600 python tools/variants.py run > $OUT/variants.txt 2>&1 || { echo "VARIANTS FAILED"; tail -20 $OUT/variants.txt; exit 1; }
+  cat $OUT/variants.txt
+fi
