@@ -20,6 +20,7 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "default": {},
     "frame": {"_args": "frame"},
     "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
+    "frame_side": {"_args": "frame", "ORBX_SIDE_MIN_BATCH": "1"},
     "nospin": {"ORBX_WAIT_SPIN_US": "0"},
     "nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "q16": {"GPU_MAX_HW_QUEUES": "16"},
