@@ -115,7 +115,7 @@ def parse():
                     help="euroc: projected local-map MapPoints per frame")
     ap.add_argument("--insts-csv", default=None,
                     help="rocprofv3 --pmc CSV holding SQ_INSTS_VALU for the roofline's VALU issue "
-                         "entry (default: the committed profiles/r02_pmc_insts_*.csv)")
+                         "entry (default: the committed profiles/r04_pmc_insts_*.csv)")
     ap.add_argument("--traffic-csv", default=None,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"
