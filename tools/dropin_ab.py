@@ -21,6 +21,8 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "frame": {"_args": "frame"},
     "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
     "frame_side": {"_args": "frame", "ORBX_SIDE_MIN_BATCH": "1"},
+    "frame_th16": {"_args": "frame", "ORBX_STRIP_TH": "16,16,16,16,16,16,16,16"},
+    "frame_th32": {"_args": "frame", "ORBX_STRIP_TH": "32,32,32,32,32,32,32,32"},
     "nospin": {"ORBX_WAIT_SPIN_US": "0"},
     "nograph": {"ORBX_EXTRACT_GRAPH": "0"},
     "q16": {"GPU_MAX_HW_QUEUES": "16"},
