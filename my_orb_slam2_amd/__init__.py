@@ -13,10 +13,10 @@ Everything routes through liborbx.so (include/orbx.h).  There is no CPU fallback
 from __future__ import annotations
 
 from ._lib import KEYPOINT_DTYPE, OrbxError, load
-from .extractor import ORBextractor, compute_stereo_matches, StereoBatch
+from .extractor import ORBextractor, compute_stereo_matches, extract_stereo, StereoBatch
 from .matcher import ORBmatcher, descriptor_distance
 from .vocabulary import Vocabulary, bow_score_l1
 from .kfdb import KeyFrameDatabase
 
-__all__ = ["ORBextractor", "ORBmatcher", "compute_stereo_matches", "descriptor_distance",
+__all__ = ["ORBextractor", "ORBmatcher", "compute_stereo_matches", "extract_stereo", "descriptor_distance",
            "StereoBatch", "Vocabulary", "bow_score_l1", "KeyFrameDatabase", "KEYPOINT_DTYPE", "OrbxError", "load"]

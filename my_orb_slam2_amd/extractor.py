@@ -236,6 +236,46 @@ def compute_stereo_matches(left: ORBextractor, right: ORBextractor, mbf: float, 
     return u[:n], d[:n], nv.value
 
 
+class StereoFrameOut(ctypes.Structure):
+    """orbx_stereo_frame_out (include/orbx.h)."""
+    _fields_ = [("kps", ctypes.c_void_p * 2), ("desc", ctypes.c_void_p * 2),
+                ("n", ctypes.c_int32 * 2), ("u_right", ctypes.c_void_p),
+                ("depth", ctypes.c_void_p), ("n_valid", ctypes.c_int32)]
+
+
+def extract_stereo(ext: ORBextractor, left: np.ndarray, right: np.ndarray, mbf: float,
+                   mb: float):
+    """The stereo Frame constructor's extraction and matching (src/Frame.cc:89-102) as one
+    call on one extractor (orbx_stereo_frame_view: both views as a two-image batch with the
+    stereo match appended, one graph replay, one wait).  Returns (kps_left, desc_left,
+    kps_right, desc_right, mvuRight, mvDepth, n_valid), equal to two extractions +
+    ``compute_stereo_matches``."""
+    L = np.ascontiguousarray(left, dtype=np.uint8)
+    R = np.ascontiguousarray(right, dtype=np.uint8)
+    if L.ndim != 2 or L.shape != R.shape:
+        raise ValueError("extract_stereo expects two single-channel images of one size")
+    h, w = L.shape
+    o = StereoFrameOut()
+    check("orbx_stereo_frame_view", ext._L.orbx_stereo_frame_view(
+        ext._h, ptr(L), w, ptr(R), w, w, h, mbf, mb, ctypes.byref(o)))
+
+    def arr(addr, n, dtype, shape):
+        if n <= 0:
+            return np.zeros(shape, dtype)
+        buf = (ctypes.c_uint8 * (n * np.dtype(dtype).itemsize * int(np.prod(shape[1:]) or 1)))
+        return np.frombuffer(buf.from_address(addr), dtype).reshape(shape).copy()
+
+    nl, nr = o.n[0], o.n[1]
+    kl = arr(o.kps[0], nl, KEYPOINT_DTYPE, (nl,))
+    kr = arr(o.kps[1], nr, KEYPOINT_DTYPE, (nr,))
+    dl = arr(o.desc[0], nl, np.uint8, (nl, 32))
+    dr = arr(o.desc[1], nr, np.uint8, (nr, 32))
+    u = arr(o.u_right, nl, np.float32, (nl,))
+    d = arr(o.depth, nl, np.float32, (nl,))
+    ext._nkp = -1   # the handle now holds a two-image batch, not a single-image extraction
+    return kl, dl, kr, dr, u, d, o.n_valid
+
+
 class StereoBatch:
     """Batched stereo front-end: B rectified pairs per call, all on one HIP stream.
 

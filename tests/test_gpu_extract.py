@@ -414,3 +414,46 @@ def test_overlap_setting_api(orbx_lib, gpu):
     assert e.overlap() == (3, 3, 1)
     with pytest.raises(OrbxError):
         e.set_overlap(7)
+
+
+@pytest.mark.parametrize("params,size", [((2000, 1.2, 8, 20, 7), (1241, 376)),
+                                         ((3000, 1.2, 8, 20, 7), (800, 600)),
+                                         ((500, 1.2, 8, 20, 7), (333, 97))])
+def test_extract_stereo_equals_separate(oracle_mod, orbx_lib, gpu, params, size):
+    """The one-call stereo Frame (orbx_stereo_frame_view: both views as a two-image batch on
+    ONE handle, the stereo match appended, one graph) equals two extractions on two handles
+    + orbx_stereo_match, bit for bit; the handle alternates with single-image extractions and
+    a second size (the graphs' keys and the output block's layout follow)."""
+    import my_orb_slam2_amd as m
+    mb = float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))
+    one = m.ORBextractor(*params)
+    gl, gr = m.ORBextractor(*params), m.ORBextractor(*params)
+    for seed in (40, 41, 42):
+        L, R = synth.stereo_pair(seed, *size)
+        kl, dl, kr, dr, u, d, nv = m.extract_stereo(one, L, R, KITTI_MBF, mb)
+        k1, d1 = gl(L)
+        k2, d2 = gr(R)
+        u1, dd1, n1 = m.compute_stereo_matches(gl, gr, KITTI_MBF, mb)
+        assert_kps_equal(kl, k1, f"seed {seed} left")
+        assert_bytes_equal(dl, d1, f"seed {seed} left desc")
+        assert_kps_equal(kr, k2, f"seed {seed} right")
+        assert_bytes_equal(dr, d2, f"seed {seed} right desc")
+        assert_f32_bits_equal(u, u1, f"seed {seed} uRight")
+        assert_f32_bits_equal(d, dd1, f"seed {seed} depth")
+        assert nv == n1 and (nv > 0 or size[1] < 200)
+        # the same handle as a single-image extractor between stereo frames
+        k3, d3 = one(L)
+        assert_kps_equal(k3, k1, f"seed {seed} single after stereo")
+    if size == (1241, 376):
+        k_o, d_o = oracle_mod.OracleExtractor(*params)(L)
+        assert_kps_equal(kl, k_o, "oracle left")
+        assert_bytes_equal(dl, d_o, "oracle left desc")
+    # another size on the same handle
+    L2, R2 = synth.stereo_pair(43, 640, 480)
+    kl, dl, kr, dr, u, d, nv = m.extract_stereo(one, L2, R2, KITTI_MBF, mb)
+    k1, d1 = gl(L2)
+    gr(R2)
+    u1, _, n1 = m.compute_stereo_matches(gl, gr, KITTI_MBF, mb)
+    assert_kps_equal(kl, k1, "640x480 left")
+    assert_f32_bits_equal(u, u1, "640x480 uRight")
+    assert nv == n1
