@@ -33,7 +33,7 @@ timeout -k 10 300 python bench.py --host-io --steps 20 --warmup 4 --cpu-seconds 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_reloc -o run --output-format csv -- python3 bench.py --workload reloc --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_reloc.log 2>&1 || { echo "RELOC TRACE FAILED"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_tri -o run --output-format csv -- python3 bench.py --workload triangulation --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_tri.log 2>&1 || { echo "TRI TRACE FAILED"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_bf -o run --output-format csv -- python3 bench.py --workload bf --steps 3 --warmup 1 --cpu-seconds 0 --no-kernel-timing > $OUT/prof_bf.log 2>&1 || { echo "BF TRACE FAILED"; exit 1; }
-python tools/dropin_data.py /tmp/dd 8 > /dev/null && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/prof_dropin -o run --output-format csv -- tests/native/facade_test bench /tmp/dd 100 20 1 > $OUT/prof_dropin.log 2>&1 || { echo "DROPIN TRACE FAILED"; exit 1; }
+python tools/dropin_data.py /tmp/dd 8 > /dev/null && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/prof_dropin -o run --output-format csv -- tests/native/facade_test bench /tmp/dd 100 20 1 frame > $OUT/prof_dropin.log 2>&1 || { echo "DROPIN TRACE FAILED"; exit 1; }
 python tools/dropin_data.py /tmp/dd 8 > /dev/null && timeout -k 10 400 python tools/dropin_ab.py run /tmp/dd 1,8 > $OUT/dropin_ab.txt 2>&1 || { echo "DROPIN AB FAILED"; tail -5 $OUT/dropin_ab.txt; exit 1; }
 cat $OUT/dropin_ab.txt
 echo session done
