@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -14,6 +15,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -982,6 +985,157 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 
 }  // namespace
 
+// ---- several sessions' stereo frames as one batch (orbx_stereo_frame_view) -----------------
+// Tracking sessions on one device each call orbx_stereo_frame_view on their own handle.  A
+// call that finds the device's frame server idle runs on its own handle (one graph replay,
+// stereo_frame_solo).  Calls that arrive while another call is being run wait in the server's
+// queue; when the running call returns, one waiting thread takes every queued frame of the
+// same image size and camera (up to FS_MAX_FRAMES) and runs them as ONE batch on the server's
+// own handle: the lefts as images [0, m), the rights as [m, 2m), each frame's two images DMA'd
+// from the pinned staging of its own handle (where its thread put them), one extraction of the
+// 2m images, one stereo launch over the m pairs, the outputs back by two DMAs into one of the
+// server's two pinned blocks.  Each waiting thread then copies its frame's outputs into its
+// own handle's pinned block.  A batch is m + 15 submissions for m frames instead of 14 m: with
+// several sessions the runtime's submission path, not the GPU, bounded the rate.
+#ifndef FS_MAX_FRAMES
+#define FS_MAX_FRAMES 8
+#endif
+#ifndef FRAME_SERVER
+#define FRAME_SERVER 1
+#endif
+struct FsReq {
+    orbx_extractor* h;            // the caller's handle: its h_in holds both images
+    int width, height;
+    float mbf, mb;
+    int slot = -1, buf = -1, m = 0;
+    orbx_status st = ORBX_OK;
+    bool done = false;
+};
+struct FsLayout {                  // the layout of one server output block
+    size_t o_kps = 0, o_desc = 0, o_st = 0, kc = 0;
+    int m = 0;
+};
+struct FrameServer {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool busy = false;
+    std::vector<FsReq*> pending;
+    orbx_extractor* sh = nullptr;  // the server's handle (created on first use)
+    uint8_t* hout[2] = {nullptr, nullptr};
+    size_t hout_n[2] = {0, 0};
+    int readers[2] = {0, 0};       // threads still copying out of each block
+    FsLayout lay[2];
+    int next_buf = 0;
+};
+
+static FrameServer& frame_server(const orbx_extractor* h) {
+    static std::mutex mu;
+    static std::map<std::vector<int>, std::unique_ptr<FrameServer>> servers;
+    const orbx_extractor_params& p = h->prm;
+    int sf;
+    std::memcpy(&sf, &p.scale_factor, 4);
+    const std::vector<int> key = {h->device, p.nfeatures, sf, p.nlevels, p.ini_th_fast,
+                                  p.min_th_fast, p.cv_simd};
+    std::lock_guard<std::mutex> lk(mu);
+    std::unique_ptr<FrameServer>& s = servers[key];
+    if (!s) s.reset(new FrameServer());
+    return *s;
+}
+
+// One batch of m = take.size() frames on the server's handle.
+static orbx_status run_served(FrameServer& fs, const std::vector<FsReq*>& take, int buf) {
+    const FsReq& f = *take[0];
+    const int m = (int)take.size();
+    if (!fs.sh) {
+        orbx_extractor_params p = f.h->prm;
+        p.max_batch = 2 * FS_MAX_FRAMES;
+        const orbx_status s = orbx_extractor_create(&p, &fs.sh);
+        if (s != ORBX_OK) return s;
+    }
+    orbx_extractor* S = fs.sh;
+    std::lock_guard<std::mutex> lk(S->mu);
+    orbx_status s = ensure_workspace(S, f.width, f.height, 2 * m);
+    if (s != ORBX_OK) return s;
+    const LevelGeom& L0 = S->hg.lv[0];
+    const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)f.height;
+    for (const FsReq* q : take)   // the staging layouts must agree (same geometry)
+        if (q->h->hg.lv[0].pitch != L0.pitch) return ORBX_ERR_INVALID;
+    const size_t KC = (size_t)S->hg.kp_cap, pyrb = (size_t)S->hg.pyr_bytes;
+    const size_t o_kps = (size_t)((uint8_t*)S->d_kps.p - (uint8_t*)S->d_outs.p);
+    const size_t o_desc = (size_t)((uint8_t*)S->d_desc.p - (uint8_t*)S->d_outs.p);
+    const size_t o_end = o_desc + 2 * (size_t)m * KC * 32;
+    // stereo block: [nvalid[m] | uRight[m][KC] | depth[m][KC]]
+    const size_t so_u = align_up(4 * (size_t)m, 256), so_d = so_u + (size_t)m * KC * 4;
+    const size_t s_end = so_d + (size_t)m * KC * 4, o_st = align_up(o_end, 256);
+    if (!S->d_uR.ensure(s_end) || !ensure_pinned(fs.hout[buf], fs.hout_n[buf], o_st + s_end))
+        return ORBX_ERR_DEVICE;
+    hipStream_t st = S->stream;
+    if (!order_after_last(S, st)) return ORBX_ERR_DEVICE;
+    uint8_t* d_l0 = S->d_pyr.as<uint8_t>() + L0.off;
+    uint8_t* dso = S->d_uR.as<uint8_t>();
+    // frame i's left into slot i, its right into slot m + i: one 2-D DMA (two rows) per frame
+    for (int i = 0; i < m; ++i)
+        if (!HIPOK(hipMemcpy2DAsync(d_l0 + (size_t)i * pyrb, (size_t)m * pyrb, take[i]->h->h_in,
+                                    img_bytes, img_bytes, 2, hipMemcpyHostToDevice, st)))
+            return ORBX_ERR_DEVICE;
+    const ExtractLaunch a = extract_launch(S, nullptr, nullptr, 2 * m, 2 * m, 0, 0);
+    StereoLaunch sa;
+    s = stereo_launch_args(S, S, m, 0, m, f.mbf, f.mb, (float*)(dso + so_u),
+                           (float*)(dso + so_d), (int*)dso, st, sa);
+    if (s != ORBX_OK) return s;
+    if (!HIPOK(launch_extract(a, st)) || !HIPOK(launch_stereo(sa, st)) ||
+        !HIPOK(hipMemcpyAsync(fs.hout[buf], S->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) ||
+        !HIPOK(hipMemcpyAsync(fs.hout[buf] + o_st, dso, s_end, hipMemcpyDeviceToHost, st)) ||
+        !mark_done(S, st) || !wait_done(S))
+        return ORBX_ERR_DEVICE;
+    S->last_batch = 2 * m;
+    S->last_valid = true;
+    S->last_n = -1;
+    fs.lay[buf] = FsLayout{o_kps, o_desc, o_st, KC, m};
+    return ORBX_OK;
+}
+
+// The waiting thread's own frame, from the server block into its handle's pinned block.
+static orbx_status copy_served(FrameServer& fs, const FsReq& r, orbx_stereo_frame_out* out) {
+    const FsLayout& ly = fs.lay[r.buf];
+    const uint8_t* ho = fs.hout[r.buf];
+    const size_t KC = ly.kc;
+    int32_t n[2];
+    std::memcpy(&n[0], ho + 4 * (size_t)r.slot, 4);
+    std::memcpy(&n[1], ho + 4 * (size_t)(ly.m + r.slot), 4);
+    const size_t nl = (size_t)std::max(n[0], 0), nr = (size_t)std::max(n[1], 0);
+    orbx_extractor* h = r.h;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const size_t need = (nl + nr) * (28 + 32) + nl * 8 + 64;
+    if (!ensure_pinned(h->h_out, h->h_out_n, need)) return ORBX_ERR_DEVICE;
+    uint8_t* o = h->h_out;
+    const size_t img[2] = {(size_t)r.slot, (size_t)(ly.m + r.slot)};
+    const size_t cnt[2] = {nl, nr};
+    for (int v = 0; v < 2; ++v) {
+        std::memcpy(o, ho + ly.o_kps + img[v] * KC * 28, cnt[v] * 28);
+        out->kps[v] = (const orbx_keypoint*)o;
+        o += cnt[v] * 28;
+    }
+    for (int v = 0; v < 2; ++v) {
+        std::memcpy(o, ho + ly.o_desc + img[v] * KC * 32, cnt[v] * 32);
+        out->desc[v] = o;
+        o += cnt[v] * 32;
+    }
+    const uint8_t* sb = ho + ly.o_st;
+    const size_t so_u = align_up(4 * (size_t)ly.m, 256), so_d = so_u + (size_t)ly.m * KC * 4;
+    std::memcpy(&out->n_valid, sb + 4 * (size_t)r.slot, 4);
+    std::memcpy(o, sb + so_u + (size_t)r.slot * KC * 4, nl * 4);
+    out->u_right = (const float*)o;
+    o += nl * 4;
+    std::memcpy(o, sb + so_d + (size_t)r.slot * KC * 4, nl * 4);
+    out->depth = (const float*)o;
+    out->n[0] = n[0];
+    out->n[1] = n[1];
+    // this handle's own workspace does not hold the frame (its pyramid views are stale)
+    h->last_valid = false;
+    return ORBX_OK;
+}
+
 extern "C" {
 
 const char* orbx_version(void) { return ORBX_VERSION; }
@@ -1286,12 +1440,27 @@ orbx_status orbx_extract_view(orbx_extractor* h, const uint8_t* img, int width, 
     return ORBX_OK;
 }
 
-orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_t stride_left,
-                                   const uint8_t* right, size_t stride_right, int width,
-                                   int height, float mbf, float mb, orbx_stereo_frame_out* out) {
-    if (!h || !out || !left || !right || width <= 0 || height <= 0 ||
-        stride_left < (size_t)width || stride_right < (size_t)width)
-        return ORBX_ERR_INVALID;
+// Both images of a stereo frame into the handle's pinned staging, laid out with the pyramid's
+// level-0 pitch (image 0 = left, image 1 = right).  Called with h->mu held.
+static orbx_status stage_frame(orbx_extractor* h, const uint8_t* left, size_t stride_left,
+                               const uint8_t* right, size_t stride_right, int width, int height) {
+    const size_t pitch0 = (size_t)h->hg.lv[0].pitch, img_bytes = pitch0 * (size_t)height;
+    if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes)) return ORBX_ERR_DEVICE;
+    for (int v = 0; v < 2; ++v) {
+        const uint8_t* img = v ? right : left;
+        const size_t stride = v ? stride_right : stride_left;
+        uint8_t* dst = h->h_in + (size_t)v * img_bytes;
+        for (int y = 0; y < height; ++y)
+            std::memcpy(dst + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
+    }
+    return ORBX_OK;
+}
+
+// orbx_stereo_frame_view on the caller's own handle (one graph replay).
+static orbx_status stereo_frame_solo(orbx_extractor* h, const uint8_t* left, size_t stride_left,
+                                     const uint8_t* right, size_t stride_right, int width,
+                                     int height, float mbf, float mb,
+                                     orbx_stereo_frame_out* out) {
     std::lock_guard<std::mutex> lk(h->mu);
     orbx_status s = ensure_workspace(h, width, height, 2);
     if (s != ORBX_OK) return s;
@@ -1308,20 +1477,11 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     const size_t so_u = 256, so_d = so_u + KC * 4, s_end = so_d + KC * 4;
     const size_t o_s = h->o_stereo;
     const bool one_dma = h->cap_batch == 2;
-    if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes) ||
-        !ensure_pinned(h->h_out, h->h_out_n, o_s + s_end))
-        return ORBX_ERR_DEVICE;
-    auto stage = [&](int v) {
-        const uint8_t* img = v ? right : left;
-        const size_t stride = v ? stride_right : stride_left;
-        uint8_t* dst = h->h_in + (size_t)v * img_bytes;
-        for (int y = 0; y < height; ++y)
-            std::memcpy(dst + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
-    };
+    if (!ensure_pinned(h->h_out, h->h_out_n, o_s + s_end)) return ORBX_ERR_DEVICE;
+    if ((s = stage_frame(h, left, stride_left, right, stride_right, width, height)) != ORBX_OK)
+        return s;
     uint8_t* d_l0 = h->d_pyr.as<uint8_t>() + L0.off;   // image 0's level-0 slot
     const size_t pyrb = (size_t)h->hg.pyr_bytes;
-    stage(0);
-    stage(1);
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
     uint8_t* dso = h->d_outs.as<uint8_t>() + o_s;
     const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 2, 2, 0, 0);
@@ -1368,6 +1528,82 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     out->u_right = (const float*)(ho + o_s + so_u);
     out->depth = (const float*)(ho + o_s + so_d);
     return ORBX_OK;
+}
+
+orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_t stride_left,
+                                   const uint8_t* right, size_t stride_right, int width,
+                                   int height, float mbf, float mb, orbx_stereo_frame_out* out) {
+    if (!h || !out || !left || !right || width <= 0 || height <= 0 ||
+        stride_left < (size_t)width || stride_right < (size_t)width)
+        return ORBX_ERR_INVALID;
+    if (!tuned("ORBX_FRAME_SERVER", FRAME_SERVER))
+        return stereo_frame_solo(h, left, stride_left, right, stride_right, width, height, mbf,
+                                 mb, out);
+    FrameServer& fs = frame_server(h);
+    std::unique_lock<std::mutex> lk(fs.mu);
+    if (!fs.busy && fs.pending.empty()) {   // alone on the device: on this handle
+        fs.busy = true;
+        lk.unlock();
+        const orbx_status s = stereo_frame_solo(h, left, stride_left, right, stride_right, width,
+                                                height, mbf, mb, out);
+        lk.lock();
+        fs.busy = false;
+        fs.cv.notify_all();
+        return s;
+    }
+    lk.unlock();
+    {   // the images into this handle's staging; the batch DMAs them from there
+        std::lock_guard<std::mutex> hl(h->mu);
+        orbx_status s = ensure_workspace(h, width, height, 1);
+        if (s == ORBX_OK) s = stage_frame(h, left, stride_left, right, stride_right, width, height);
+        if (s != ORBX_OK) return s;
+    }
+    FsReq r{h, width, height, mbf, mb};
+    lk.lock();
+    fs.pending.push_back(&r);
+    while (!r.done) {
+        if (fs.busy) {
+            fs.cv.wait(lk);
+            continue;
+        }
+        // lead the next batch: every queued frame of the first one's size and camera
+        fs.busy = true;
+        const FsReq* f0 = fs.pending.front();
+        std::vector<FsReq*> take;
+        for (auto it = fs.pending.begin(); it != fs.pending.end() && take.size() < FS_MAX_FRAMES;) {
+            FsReq* q = *it;
+            if (q->width == f0->width && q->height == f0->height &&
+                std::memcmp(&q->mbf, &f0->mbf, 4) == 0 && std::memcmp(&q->mb, &f0->mb, 4) == 0) {
+                q->slot = (int)take.size();
+                take.push_back(q);
+                it = fs.pending.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        const int buf = fs.next_buf;
+        fs.next_buf ^= 1;
+        fs.cv.wait(lk, [&] { return fs.readers[buf] == 0; });   // two batches ago: copied out
+        lk.unlock();
+        const orbx_status bs = run_served(fs, take, buf);
+        lk.lock();
+        for (FsReq* q : take) {
+            q->st = bs;
+            q->buf = buf;
+            q->done = true;
+        }
+        if (bs == ORBX_OK) fs.readers[buf] += (int)take.size();
+        fs.busy = false;
+        fs.cv.notify_all();
+    }
+    lk.unlock();
+    const orbx_status s = r.st == ORBX_OK ? copy_served(fs, r, out) : r.st;
+    if (r.st == ORBX_OK) {
+        lk.lock();
+        --fs.readers[r.buf];
+        fs.cv.notify_all();
+    }
+    return s;
 }
 
 static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,

@@ -19,6 +19,7 @@ VAR = ROOT / "tools" / "_var" / "tune"
 SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "frame")
     "default": {},
     "frame": {"_args": "frame"},
+    "frame_solo": {"_args": "frame", "ORBX_FRAME_SERVER": "0"},
     "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
     "frame_side": {"_args": "frame", "ORBX_SIDE_MIN_BATCH": "1"},
     "frame_th16": {"_args": "frame", "ORBX_STRIP_TH": "16,16,16,16,16,16,16,16"},
