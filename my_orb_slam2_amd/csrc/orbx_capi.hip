@@ -1018,15 +1018,12 @@ struct FsLayout {                  // the layout of one server output block
 struct FrameServer {
     std::mutex mu;
     std::condition_variable cv;
-    bool busy = false;             // a batch is being submitted
-    int inflight = 0;              // batches submitted and not yet ended
+    bool busy = false;
     std::vector<FsReq*> pending;
     orbx_extractor* sh = nullptr;  // the server's handle (created on first use)
     uint8_t* hout[2] = {nullptr, nullptr};
     size_t hout_n[2] = {0, 0};
-    bool inuse[2] = {false, false};  // a batch's outputs land in / are read from the block
     int readers[2] = {0, 0};       // threads still copying out of each block
-    hipEvent_t ev[2] = {nullptr, nullptr};   // the end of the block's batch
     FsLayout lay[2];
     int next_buf = 0;
 };
@@ -1045,9 +1042,8 @@ static FrameServer& frame_server(const orbx_extractor* h) {
     return *s;
 }
 
-// Submits one batch of m = take.size() frames on the server's handle; its end is fs.ev[buf].
-// The next batch may be submitted behind it at once (same stream, its own output block).
-static orbx_status submit_served(FrameServer& fs, const std::vector<FsReq*>& take, int buf) {
+// One batch of m = take.size() frames on the server's handle.
+static orbx_status run_served(FrameServer& fs, const std::vector<FsReq*>& take, int buf) {
     const FsReq& f = *take[0];
     const int m = (int)take.size();
     if (!fs.sh) {
@@ -1055,8 +1051,6 @@ static orbx_status submit_served(FrameServer& fs, const std::vector<FsReq*>& tak
         p.max_batch = 2 * FS_MAX_FRAMES;
         const orbx_status s = orbx_extractor_create(&p, &fs.sh);
         if (s != ORBX_OK) return s;
-        for (hipEvent_t& e : fs.ev)
-            if (!HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming))) return ORBX_ERR_DEVICE;
     }
     orbx_extractor* S = fs.sh;
     std::lock_guard<std::mutex> lk(S->mu);
@@ -1073,8 +1067,6 @@ static orbx_status submit_served(FrameServer& fs, const std::vector<FsReq*>& tak
     // stereo block: [nvalid[m] | uRight[m][KC] | depth[m][KC]]
     const size_t so_u = align_up(4 * (size_t)m, 256), so_d = so_u + (size_t)m * KC * 4;
     const size_t s_end = so_d + (size_t)m * KC * 4, o_st = align_up(o_end, 256);
-    // growing the stereo block frees the old one: the batch in flight must be done with it
-    if (s_end > S->d_uR.n && !wait_idle(S)) return ORBX_ERR_DEVICE;
     if (!S->d_uR.ensure(s_end) || !ensure_pinned(fs.hout[buf], fs.hout_n[buf], o_st + s_end))
         return ORBX_ERR_DEVICE;
     hipStream_t st = S->stream;
@@ -1094,27 +1086,13 @@ static orbx_status submit_served(FrameServer& fs, const std::vector<FsReq*>& tak
     if (!HIPOK(launch_extract(a, st)) || !HIPOK(launch_stereo(sa, st)) ||
         !HIPOK(hipMemcpyAsync(fs.hout[buf], S->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) ||
         !HIPOK(hipMemcpyAsync(fs.hout[buf] + o_st, dso, s_end, hipMemcpyDeviceToHost, st)) ||
-        !mark_done(S, st) || !HIPOK(hipEventRecord(fs.ev[buf], st)))
+        !mark_done(S, st) || !wait_done(S))
         return ORBX_ERR_DEVICE;
     S->last_batch = 2 * m;
     S->last_valid = true;
     S->last_n = -1;
     fs.lay[buf] = FsLayout{o_kps, o_desc, o_st, KC, m};
     return ORBX_OK;
-}
-
-// The end of a submitted batch (polling first, as wait_done).
-static bool wait_event(hipEvent_t e) {
-    const int spin_us = tuned("ORBX_WAIT_SPIN_US", WAIT_SPIN_US);
-    const auto t0 = std::chrono::steady_clock::now();
-    while (spin_us > 0) {
-        const hipError_t q = hipEventQuery(e);
-        if (q == hipSuccess) return true;
-        if (q != hipErrorNotReady) return HIPOK(q);
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
-        std::this_thread::yield();
-    }
-    return HIPOK(hipEventSynchronize(e));
 }
 
 // The waiting thread's own frame, from the server block into its handle's pinned block.
@@ -1563,7 +1541,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
                                  mb, out);
     FrameServer& fs = frame_server(h);
     std::unique_lock<std::mutex> lk(fs.mu);
-    if (!fs.busy && fs.pending.empty() && fs.inflight == 0) {   // alone: on this handle
+    if (!fs.busy && fs.pending.empty()) {   // alone on the device: on this handle
         fs.busy = true;
         lk.unlock();
         const orbx_status s = stereo_frame_solo(h, left, stride_left, right, stride_right, width,
@@ -1584,13 +1562,11 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     lk.lock();
     fs.pending.push_back(&r);
     while (!r.done) {
-        // lead the next batch once a server output block is free: every frame queued by then
-        // of the first one's size and camera (frames keep queueing while both blocks are busy)
-        // (an empty queue: this frame is in a batch another thread submitted)
-        if (fs.busy || fs.inuse[fs.next_buf] || fs.pending.empty()) {
+        if (fs.busy) {
             fs.cv.wait(lk);
             continue;
         }
+        // lead the next batch: every queued frame of the first one's size and camera
         fs.busy = true;
         const FsReq* f0 = fs.pending.front();
         std::vector<FsReq*> take;
@@ -1607,31 +1583,24 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         }
         const int buf = fs.next_buf;
         fs.next_buf ^= 1;
-        fs.inuse[buf] = true;
-        ++fs.inflight;
+        fs.cv.wait(lk, [&] { return fs.readers[buf] == 0; });   // two batches ago: copied out
         lk.unlock();
-        orbx_status bs = submit_served(fs, take, buf);
+        const orbx_status bs = run_served(fs, take, buf);
         lk.lock();
-        fs.busy = false;   // the next batch may be submitted behind this one
-        fs.cv.notify_all();
-        lk.unlock();
-        if (bs == ORBX_OK && !wait_event(fs.ev[buf])) bs = ORBX_ERR_DEVICE;
-        lk.lock();
-        --fs.inflight;
         for (FsReq* q : take) {
             q->st = bs;
             q->buf = buf;
             q->done = true;
         }
-        if (bs == ORBX_OK) fs.readers[buf] = (int)take.size();
-        else fs.inuse[buf] = false;
+        if (bs == ORBX_OK) fs.readers[buf] += (int)take.size();
+        fs.busy = false;
         fs.cv.notify_all();
     }
     lk.unlock();
     const orbx_status s = r.st == ORBX_OK ? copy_served(fs, r, out) : r.st;
     if (r.st == ORBX_OK) {
         lk.lock();
-        if (--fs.readers[r.buf] == 0) fs.inuse[r.buf] = false;
+        --fs.readers[r.buf];
         fs.cv.notify_all();
     }
     return s;
