@@ -49,6 +49,51 @@ bool hip_ok(hipError_t e, const char* what) {
 }
 }  // namespace orbx
 
+// A helper thread that stages the right image of a stereo frame while the calling thread
+// stages the left one (orbx_stereo_frame_view): the copy of a cold 0.47 MB image into pinned
+// memory is tens of microseconds on one core.
+struct OrbxStager {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool has_job = false, done = true, stop = false;
+    std::thread th;
+    OrbxStager() : th([this] { run(); }) {}
+    ~OrbxStager() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    void run() {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return has_job || stop; });
+            if (stop) return;
+            std::function<void()> j = std::move(job);
+            has_job = false;
+            lk.unlock();
+            j();
+            lk.lock();
+            done = true;
+            cv.notify_all();
+        }
+    }
+    void post(std::function<void()> j) {
+        std::lock_guard<std::mutex> lk(mu);
+        job = std::move(j);
+        has_job = true;
+        done = false;
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done; });
+    }
+};
+
 struct orbx_extractor {
     orbx_extractor_params prm;
     int device = 0;
@@ -106,6 +151,7 @@ struct orbx_extractor {
     int last_batch = 0;
     bool last_valid = false;
     int last_n = 0;          // keypoints of the last orbx_extract (host image path)
+    std::unique_ptr<OrbxStager> stager;   // created by the first stereo-frame call
     // guards every field above against concurrent calls on one handle (const queries too)
     mutable std::mutex mu;
 };
@@ -987,16 +1033,28 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 
 // ---- several sessions' stereo frames as one batch (orbx_stereo_frame_view) -----------------
 // Tracking sessions on one device each call orbx_stereo_frame_view on their own handle.  A
-// call that finds the device's frame server idle runs on its own handle (one graph replay,
-// stereo_frame_solo).  Calls that arrive while another call is being run wait in the server's
-// queue; when the running call returns, one waiting thread takes every queued frame of the
-// same image size and camera (up to FS_MAX_FRAMES) and runs them as ONE batch on the server's
-// own handle: the lefts as images [0, m), the rights as [m, 2m), each frame's two images DMA'd
-// from the pinned staging of its own handle (where its thread put them), one extraction of the
-// 2m images, one stereo launch over the m pairs, the outputs back by two DMAs into one of the
-// server's two pinned blocks.  Each waiting thread then copies its frame's outputs into its
-// own handle's pinned block.  A batch is m + 15 submissions for m frames instead of 14 m: with
-// several sessions the runtime's submission path, not the GPU, bounded the rate.
+// call that finds the device's frame server idle (nothing running, nothing queued) runs on its
+// own handle (one graph replay, stereo_frame_solo).  A call that arrives while another runs
+// joins the batch being formed: it stages its two images into its slot of the server's pinned
+// input block and issues that slot's DMA to the server's device staging on the server's copy
+// stream right away (the copy overlaps the running batch).  When the device frees, a waiting
+// thread takes the formed batch (up to FS_MAX_FRAMES frames of one image size and camera) and
+// replays the server's graph for its size on the server's own handle: the lefts as images
+// [0, m), the rights as [m, 2m), one extraction of the 2m images, one stereo launch over the
+// m pairs, the outputs back into the pair's pinned output block.  Each waiting thread then
+// copies its frame's outputs into its own handle's pinned block.  Two block pairs alternate
+// (one forms while the other runs).  With several sessions the runtime's submission path,
+// not the GPU, bounded the rate of one-call frames (14 submissions each).
+#ifndef STAGE_THREAD
+// orbx_stereo_frame_view: the right image staged by a helper thread (0 never, 1 for frames that
+// queue for the frame server, 2 always).  Measured (r04_ab_runs.txt, r4i): the helper's wake-up
+// costs a lone caller with cache-hot images more (0.239 -> 0.257 ms) than it saves on cold ones
+// (0.268 -> 0.259 ms); with 8 sessions it raised 9.4-9.6k to 9.6-9.9k pairs/s.
+#define STAGE_THREAD 1
+#endif
+#ifndef EXTRACT_GRAPH
+#define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
+#endif
 #ifndef FS_MAX_FRAMES
 #define FS_MAX_FRAMES 8
 #endif
@@ -1004,10 +1062,8 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 #define FRAME_SERVER 1
 #endif
 struct FsReq {
-    orbx_extractor* h;            // the caller's handle: its h_in holds both images
-    int width, height;
-    float mbf, mb;
-    int slot = -1, buf = -1, m = 0;
+    orbx_extractor* h;            // the caller's handle (its stager)
+    int slot = -1, blk = -1;      // its frame in the batch, the block pair of that batch
     orbx_status st = ORBX_OK;
     bool done = false;
 };
@@ -1015,17 +1071,59 @@ struct FsLayout {                  // the layout of one server output block
     size_t o_kps = 0, o_desc = 0, o_st = 0, kc = 0;
     int m = 0;
 };
+struct FsBatch {                   // the size and camera of a batch's frames
+    int width = 0, height = 0;
+    float mbf = 0.f, mb = 0.f;
+    size_t pitch0 = 0, img_bytes = 0;
+};
+struct FsGraph {
+    hipGraphExec_t gx = nullptr;
+    std::vector<const void*> key;
+};
 struct FrameServer {
     std::mutex mu;
     std::condition_variable cv;
-    bool busy = false;
-    std::vector<FsReq*> pending;
+    bool busy = false;             // a batch (or a lone call) is on the device
     orbx_extractor* sh = nullptr;  // the server's handle (created on first use)
+    // the batch being formed: n frames joined, `staged` of them copied into input block blk
+    int blk = 0, n = 0, staged = 0;
+    FsBatch geo;
+    FsReq* req[FS_MAX_FRAMES] = {};
+    // block pair i: the input block (frame j's left at 2j, its right at 2j+1, img_bytes each)
+    // and the output block of a batch; the next batch forms in the other pair
+    uint8_t* hin[2] = {nullptr, nullptr};
+    size_t hin_n[2] = {0, 0};
+    // each frame's images go on to the device as soon as they are staged, on the copy stream
+    // (while the batch before runs), into the device staging block of its pair
+    DevBuf dstage[2];
+    hipStream_t cst = nullptr;
+    hipEvent_t cev = nullptr;      // recorded on cst when a batch is taken
     uint8_t* hout[2] = {nullptr, nullptr};
     size_t hout_n[2] = {0, 0};
-    int readers[2] = {0, 0};       // threads still copying out of each block
+    int readers[2] = {0, 0};       // threads still copying out of each output block
     FsLayout lay[2];
-    int next_buf = 0;
+    FsGraph graphs[2][FS_MAX_FRAMES + 1];   // per block pair and batch size
+#ifdef ORBX_TUNING
+    // ORBX_FS_STATS=1: batch sizes and where the device time goes, printed at exit
+    using clk = std::chrono::steady_clock;
+    long st_solo = 0, st_hist[FS_MAX_FRAMES + 1] = {};
+    double st_run_us = 0, st_solo_us = 0, st_idle_us = 0, st_readers_us = 0;
+    clk::time_point st_free = clk::now();
+    static double us(clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+    }
+    ~FrameServer() {
+        if (!getenv("ORBX_FS_STATS")) return;
+        long nb = 0, nf = 0;
+        for (int m = 1; m <= FS_MAX_FRAMES; ++m) nb += st_hist[m], nf += m * st_hist[m];
+        fprintf(stderr, "frame server: %ld solo calls (%.1f us each), %ld batches of %ld frames "
+                "(%.1f us each), device idle %.0f us, readers wait %.0f us; sizes",
+                st_solo, st_solo ? st_solo_us / st_solo : 0.0, nb, nf, nb ? st_run_us / nb : 0.0,
+                st_idle_us, st_readers_us);
+        for (int m = 1; m <= FS_MAX_FRAMES; ++m) fprintf(stderr, " %ld", st_hist[m]);
+        fprintf(stderr, "\n");
+    }
+#endif
 };
 
 static FrameServer& frame_server(const orbx_extractor* h) {
@@ -1042,24 +1140,29 @@ static FrameServer& frame_server(const orbx_extractor* h) {
     return *s;
 }
 
-// One batch of m = take.size() frames on the server's handle.
-static orbx_status run_served(FrameServer& fs, const std::vector<FsReq*>& take, int buf) {
-    const FsReq& f = *take[0];
-    const int m = (int)take.size();
+static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_t st, int width,
+                           int height, const std::function<bool(const ExtractLaunch&)>& enqueue,
+                           hipGraphExec_t& gx, std::vector<const void*>& gkey,
+                           std::vector<const void*> extra);
+
+// One batch of m frames (staged in input block `blk`) on the server's handle, replayed from
+// the server's graph for (blk, m): two 2-D DMAs (the lefts, the rights), the extraction of
+// the 2m images, the stereo match of the m pairs, two DMAs back into output block blk.
+static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, int blk,
+                              const FsBatch& g) {
     if (!fs.sh) {
-        orbx_extractor_params p = f.h->prm;
+        orbx_extractor_params p = h0->prm;
         p.max_batch = 2 * FS_MAX_FRAMES;
         const orbx_status s = orbx_extractor_create(&p, &fs.sh);
         if (s != ORBX_OK) return s;
     }
     orbx_extractor* S = fs.sh;
     std::lock_guard<std::mutex> lk(S->mu);
-    orbx_status s = ensure_workspace(S, f.width, f.height, 2 * m);
+    // the workspace for the largest batch: one layout (and graph key) for every m
+    orbx_status s = ensure_workspace(S, g.width, g.height, 2 * FS_MAX_FRAMES);
     if (s != ORBX_OK) return s;
     const LevelGeom& L0 = S->hg.lv[0];
-    const size_t pitch0 = (size_t)L0.pitch, img_bytes = pitch0 * (size_t)f.height;
-    for (const FsReq* q : take)   // the staging layouts must agree (same geometry)
-        if (q->h->hg.lv[0].pitch != L0.pitch) return ORBX_ERR_INVALID;
+    if ((size_t)L0.pitch != g.pitch0) return ORBX_ERR_INVALID;   // the staging layout
     const size_t KC = (size_t)S->hg.kp_cap, pyrb = (size_t)S->hg.pyr_bytes;
     const size_t o_kps = (size_t)((uint8_t*)S->d_kps.p - (uint8_t*)S->d_outs.p);
     const size_t o_desc = (size_t)((uint8_t*)S->d_desc.p - (uint8_t*)S->d_outs.p);
@@ -1067,38 +1170,61 @@ static orbx_status run_served(FrameServer& fs, const std::vector<FsReq*>& take, 
     // stereo block: [nvalid[m] | uRight[m][KC] | depth[m][KC]]
     const size_t so_u = align_up(4 * (size_t)m, 256), so_d = so_u + (size_t)m * KC * 4;
     const size_t s_end = so_d + (size_t)m * KC * 4, o_st = align_up(o_end, 256);
-    if (!S->d_uR.ensure(s_end) || !ensure_pinned(fs.hout[buf], fs.hout_n[buf], o_st + s_end))
+    const size_t s_max = align_up(4 * (size_t)FS_MAX_FRAMES, 256) + 8 * FS_MAX_FRAMES * KC;
+    const size_t o_max = align_up(o_desc + 2 * (size_t)FS_MAX_FRAMES * KC * 32, 256);
+    if (!S->d_uR.ensure(s_max) || !ensure_pinned(fs.hout[blk], fs.hout_n[blk], o_max + s_max))
         return ORBX_ERR_DEVICE;
     hipStream_t st = S->stream;
     if (!order_after_last(S, st)) return ORBX_ERR_DEVICE;
     uint8_t* d_l0 = S->d_pyr.as<uint8_t>() + L0.off;
     uint8_t* dso = S->d_uR.as<uint8_t>();
-    // frame i's left into slot i, its right into slot m + i: one 2-D DMA (two rows) per frame
-    for (int i = 0; i < m; ++i)
-        if (!HIPOK(hipMemcpy2DAsync(d_l0 + (size_t)i * pyrb, (size_t)m * pyrb, take[i]->h->h_in,
-                                    img_bytes, img_bytes, 2, hipMemcpyHostToDevice, st)))
-            return ORBX_ERR_DEVICE;
+    const uint8_t* dsg = fs.dstage[blk].as<uint8_t>();
+    uint8_t* hout = fs.hout[blk];
+    const size_t ib = g.img_bytes;
     const ExtractLaunch a = extract_launch(S, nullptr, nullptr, 2 * m, 2 * m, 0, 0);
     StereoLaunch sa;
-    s = stereo_launch_args(S, S, m, 0, m, f.mbf, f.mb, (float*)(dso + so_u),
+    s = stereo_launch_args(S, S, m, 0, m, g.mbf, g.mb, (float*)(dso + so_u),
                            (float*)(dso + so_d), (int*)dso, st, sa);
     if (s != ORBX_OK) return s;
-    if (!HIPOK(launch_extract(a, st)) || !HIPOK(launch_stereo(sa, st)) ||
-        !HIPOK(hipMemcpyAsync(fs.hout[buf], S->d_outs.p, o_end, hipMemcpyDeviceToHost, st)) ||
-        !HIPOK(hipMemcpyAsync(fs.hout[buf] + o_st, dso, s_end, hipMemcpyDeviceToHost, st)) ||
-        !mark_done(S, st) || !wait_done(S))
+    // frame i's left into image slot i, its right into slot m + i (from the device staging);
+    // back: the counts and keypoints of the 2m images, their descriptors, the stereo block
+    const size_t kps_end = o_kps + 2 * (size_t)m * KC * sizeof(orbx_keypoint);
+    auto enqueue = [&](const ExtractLaunch& ea) {
+        return HIPOK(hipMemcpy2DAsync(d_l0, pyrb, dsg, 2 * ib, ib, (size_t)m,
+                                      hipMemcpyDeviceToDevice, st)) &&
+               HIPOK(hipMemcpy2DAsync(d_l0 + (size_t)m * pyrb, pyrb, dsg + ib, 2 * ib, ib,
+                                      (size_t)m, hipMemcpyDeviceToDevice, st)) &&
+               HIPOK(launch_extract(ea, st)) && HIPOK(launch_stereo(sa, st)) &&
+               HIPOK(hipMemcpyAsync(hout, S->d_outs.p, kps_end, hipMemcpyDeviceToHost, st)) &&
+               HIPOK(hipMemcpyAsync(hout + o_desc, S->d_outs.as<uint8_t>() + o_desc,
+                                    o_end - o_desc, hipMemcpyDeviceToHost, st)) &&
+               HIPOK(hipMemcpyAsync(hout + o_st, dso, s_end, hipMemcpyDeviceToHost, st));
+    };
+    uint32_t mbf_bits, mb_bits;
+    std::memcpy(&mbf_bits, &g.mbf, 4);
+    std::memcpy(&mb_bits, &g.mb, 4);
+    FsGraph& G = fs.graphs[blk][m];
+    const bool graph =
+        tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !S->timer.on &&
+        extract1_graph(S, a, st, g.width, g.height, enqueue, G.gx, G.key,
+                       {dsg, hout, S->d_sscr.p, dso, (const void*)(uintptr_t)mbf_bits,
+                        (const void*)(uintptr_t)mb_bits, (const void*)(intptr_t)m,
+                        (const void*)ib});
+    if (!HIPOK(hipStreamWaitEvent(st, fs.cev, 0)) ||   // the frames' copies to the device
+        !(graph ? HIPOK(hipGraphLaunch(G.gx, st)) : enqueue(a)) || !mark_done(S, st) ||
+        !wait_done(S))
         return ORBX_ERR_DEVICE;
     S->last_batch = 2 * m;
     S->last_valid = true;
     S->last_n = -1;
-    fs.lay[buf] = FsLayout{o_kps, o_desc, o_st, KC, m};
+    fs.lay[blk] = FsLayout{o_kps, o_desc, o_st, KC, m};
     return ORBX_OK;
 }
 
 // The waiting thread's own frame, from the server block into its handle's pinned block.
 static orbx_status copy_served(FrameServer& fs, const FsReq& r, orbx_stereo_frame_out* out) {
-    const FsLayout& ly = fs.lay[r.buf];
-    const uint8_t* ho = fs.hout[r.buf];
+    const FsLayout& ly = fs.lay[r.blk];
+    const uint8_t* ho = fs.hout[r.blk];
     const size_t KC = ly.kc;
     int32_t n[2];
     std::memcpy(&n[0], ho + 4 * (size_t)r.slot, 4);
@@ -1307,16 +1433,13 @@ orbx_status orbx_extractor_tables(const orbx_extractor* h, float* scale, float* 
     return ORBX_OK;
 }
 
-#ifndef EXTRACT_GRAPH
-#define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
-#endif
 
 // The graph of orbx_extract's device sequence for the handle's current state, captured on st
 // when missing or stale.
 static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_t st, int width,
                            int height, const std::function<bool(const ExtractLaunch&)>& enqueue,
                            hipGraphExec_t& gx, std::vector<const void*>& gkey,
-                           std::vector<const void*> extra = {}) {
+                           std::vector<const void*> extra) {
     const DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr,
                             &h->d_blur, &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp,
                             &h->d_kscr, &h->d_outs};
@@ -1384,7 +1507,7 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
     // replayed from a graph (one launch instead of ~15 enqueues: several tracking sessions
     // on one GPU contend for the runtime's per-call work), eagerly when kernels are timed
     const bool graph = tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
-                       extract1_graph(h, a, st, width, height, enqueue, h->g1, h->g1key);
+                       extract1_graph(h, a, st, width, height, enqueue, h->g1, h->g1key, {});
     if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue(a)) || !mark_done(h, st) ||
         !wait_done(h))
         return ORBX_ERR_DEVICE;
@@ -1440,20 +1563,28 @@ orbx_status orbx_extract_view(orbx_extractor* h, const uint8_t* img, int width, 
     return ORBX_OK;
 }
 
-// Both images of a stereo frame into the handle's pinned staging, laid out with the pyramid's
-// level-0 pitch (image 0 = left, image 1 = right).  Called with h->mu held.
-static orbx_status stage_frame(orbx_extractor* h, const uint8_t* left, size_t stride_left,
-                               const uint8_t* right, size_t stride_right, int width, int height) {
-    const size_t pitch0 = (size_t)h->hg.lv[0].pitch, img_bytes = pitch0 * (size_t)height;
-    if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes)) return ORBX_ERR_DEVICE;
-    for (int v = 0; v < 2; ++v) {
+// Both images of a stereo frame into pinned staging at dst, rows at the pyramid's level-0
+// pitch, the left at dst and the right at dst + img_bytes.  Called with h->mu held.
+static void stage_frame(orbx_extractor* h, uint8_t* dst, size_t pitch0, size_t img_bytes,
+                        const uint8_t* left, size_t stride_left, const uint8_t* right,
+                        size_t stride_right, int width, int height, bool queued) {
+    auto copy = [=](int v) {
         const uint8_t* img = v ? right : left;
         const size_t stride = v ? stride_right : stride_left;
-        uint8_t* dst = h->h_in + (size_t)v * img_bytes;
+        uint8_t* d = dst + (size_t)v * img_bytes;
         for (int y = 0; y < height; ++y)
-            std::memcpy(dst + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
+            std::memcpy(d + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
+    };
+    const int stage_thread = tuned("ORBX_STAGE_THREAD", STAGE_THREAD);
+    if (stage_thread == 2 || (stage_thread == 1 && queued)) {
+        if (!h->stager) h->stager.reset(new OrbxStager());
+        h->stager->post([=] { copy(1); });
+        copy(0);
+        h->stager->wait();
+    } else {
+        copy(0);
+        copy(1);
     }
-    return ORBX_OK;
 }
 
 // orbx_stereo_frame_view on the caller's own handle (one graph replay).
@@ -1478,8 +1609,9 @@ static orbx_status stereo_frame_solo(orbx_extractor* h, const uint8_t* left, siz
     const size_t o_s = h->o_stereo;
     const bool one_dma = h->cap_batch == 2;
     if (!ensure_pinned(h->h_out, h->h_out_n, o_s + s_end)) return ORBX_ERR_DEVICE;
-    if ((s = stage_frame(h, left, stride_left, right, stride_right, width, height)) != ORBX_OK)
-        return s;
+    if (!ensure_pinned(h->h_in, h->h_in_n, 2 * img_bytes)) return ORBX_ERR_DEVICE;
+    stage_frame(h, h->h_in, pitch0, img_bytes, left, stride_left, right, stride_right, width,
+                height, false);
     uint8_t* d_l0 = h->d_pyr.as<uint8_t>() + L0.off;   // image 0's level-0 slot
     const size_t pyrb = (size_t)h->hg.pyr_bytes;
     if (!order_after_last(h, st)) return ORBX_ERR_DEVICE;
@@ -1541,58 +1673,111 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
                                  mb, out);
     FrameServer& fs = frame_server(h);
     std::unique_lock<std::mutex> lk(fs.mu);
-    if (!fs.busy && fs.pending.empty()) {   // alone on the device: on this handle
+    if (!fs.busy && fs.n == 0) {   // alone on the device: on this handle
         fs.busy = true;
+#ifdef ORBX_TUNING
+        const auto t0 = FrameServer::clk::now();
+        fs.st_idle_us += FrameServer::us(fs.st_free, t0);
+#endif
         lk.unlock();
         const orbx_status s = stereo_frame_solo(h, left, stride_left, right, stride_right, width,
                                                 height, mbf, mb, out);
         lk.lock();
+#ifdef ORBX_TUNING
+        fs.st_free = FrameServer::clk::now();
+        fs.st_solo++;
+        fs.st_solo_us += FrameServer::us(t0, fs.st_free);
+#endif
         fs.busy = false;
         fs.cv.notify_all();
         return s;
     }
     lk.unlock();
-    {   // the images into this handle's staging; the batch DMAs them from there
+    FsBatch g{width, height, mbf, mb, 0, 0};
+    {
         std::lock_guard<std::mutex> hl(h->mu);
-        orbx_status s = ensure_workspace(h, width, height, 1);
-        if (s == ORBX_OK) s = stage_frame(h, left, stride_left, right, stride_right, width, height);
+        const orbx_status s = ensure_workspace(h, width, height, 1);   // the level-0 pitch
         if (s != ORBX_OK) return s;
+        g.pitch0 = (size_t)h->hg.lv[0].pitch;
+        g.img_bytes = g.pitch0 * (size_t)height;
     }
-    FsReq r{h, width, height, mbf, mb};
+    auto same = [](const FsBatch& x, const FsBatch& y) {
+        return x.width == y.width && x.height == y.height && x.pitch0 == y.pitch0 &&
+               std::memcmp(&x.mbf, &y.mbf, 4) == 0 && std::memcmp(&x.mb, &y.mb, 4) == 0;
+    };
+    FsReq r{h};
     lk.lock();
-    fs.pending.push_back(&r);
+    // join the batch being formed (after a full one, or one of another size or camera, goes)
+    fs.cv.wait(lk, [&] { return fs.n == 0 || (fs.n < FS_MAX_FRAMES && same(fs.geo, g)); });
+    if (fs.n == 0) {   // open it: its blocks were last used by a batch that has finished
+        const size_t bytes = 2 * FS_MAX_FRAMES * g.img_bytes;
+        if (!HIPOK(hipSetDevice(h->device)) ||
+            (!fs.cst && !HIPOK(hipStreamCreateWithFlags(&fs.cst, hipStreamNonBlocking))) ||
+            (!fs.cev && !HIPOK(hipEventCreateWithFlags(&fs.cev, hipEventDisableTiming))) ||
+            !ensure_pinned(fs.hin[fs.blk], fs.hin_n[fs.blk], bytes) ||
+            !fs.dstage[fs.blk].ensure(bytes))
+            return ORBX_ERR_DEVICE;
+        fs.geo = g;
+    }
+    r.slot = fs.n++;
+    r.blk = fs.blk;
+    fs.req[r.slot] = &r;
+    const size_t fofs = (size_t)r.slot * 2 * g.img_bytes;
+    uint8_t* dst = fs.hin[r.blk] + fofs;
+    uint8_t* ddst = fs.dstage[r.blk].as<uint8_t>() + fofs;
+    lk.unlock();
+    bool copied;
+    {
+        std::lock_guard<std::mutex> hl(h->mu);
+        stage_frame(h, dst, g.pitch0, g.img_bytes, left, stride_left, right, stride_right, width,
+                    height, true);
+        copied = HIPOK(hipSetDevice(h->device)) &&
+                 HIPOK(hipMemcpyAsync(ddst, dst, 2 * g.img_bytes, hipMemcpyHostToDevice, fs.cst));
+    }
+    lk.lock();
+    if (!copied) r.st = ORBX_ERR_DEVICE;   // the batch still counts the slot
+    ++fs.staged;
+    fs.cv.notify_all();
     while (!r.done) {
-        if (fs.busy) {
+        if (fs.busy || fs.n == 0 || fs.staged < fs.n) {
             fs.cv.wait(lk);
             continue;
         }
-        // lead the next batch: every queued frame of the first one's size and camera
+        // lead: the batch being formed goes, the next one forms in the other block pair
+        const int m = fs.n, blk = fs.blk;
+        FsReq* take[FS_MAX_FRAMES];
+        std::copy(fs.req, fs.req + m, take);
+        // every frame's copy is on the stream by now (each was issued before its `staged`)
+        const bool recorded = HIPOK(hipEventRecord(fs.cev, fs.cst));
+        const FsBatch bg = fs.geo;
+        fs.n = fs.staged = 0;
+        fs.blk ^= 1;
         fs.busy = true;
-        const FsReq* f0 = fs.pending.front();
-        std::vector<FsReq*> take;
-        for (auto it = fs.pending.begin(); it != fs.pending.end() && take.size() < FS_MAX_FRAMES;) {
-            FsReq* q = *it;
-            if (q->width == f0->width && q->height == f0->height &&
-                std::memcmp(&q->mbf, &f0->mbf, 4) == 0 && std::memcmp(&q->mb, &f0->mb, 4) == 0) {
-                q->slot = (int)take.size();
-                take.push_back(q);
-                it = fs.pending.erase(it);
-            } else {
-                ++it;
-            }
-        }
-        const int buf = fs.next_buf;
-        fs.next_buf ^= 1;
-        fs.cv.wait(lk, [&] { return fs.readers[buf] == 0; });   // two batches ago: copied out
+        fs.cv.notify_all();
+#ifdef ORBX_TUNING
+        const auto t0 = FrameServer::clk::now();
+        fs.st_idle_us += FrameServer::us(fs.st_free, t0);
+#endif
+        fs.cv.wait(lk, [&] { return fs.readers[blk] == 0; });   // two batches ago: copied out
+#ifdef ORBX_TUNING
+        const auto t1 = FrameServer::clk::now();
+#endif
         lk.unlock();
-        const orbx_status bs = run_served(fs, take, buf);
+        orbx_status bs = recorded ? run_served(fs, take[0]->h, m, blk, bg) : ORBX_ERR_DEVICE;
+        for (int i = 0; i < m; ++i)
+            if (take[i]->st != ORBX_OK) bs = take[i]->st;   // a frame's copy failed
         lk.lock();
-        for (FsReq* q : take) {
-            q->st = bs;
-            q->buf = buf;
-            q->done = true;
+#ifdef ORBX_TUNING
+        fs.st_free = FrameServer::clk::now();
+        fs.st_readers_us += FrameServer::us(t0, t1);
+        fs.st_run_us += FrameServer::us(t1, fs.st_free);
+        fs.st_hist[m]++;
+#endif
+        for (int i = 0; i < m; ++i) {
+            take[i]->st = bs;
+            take[i]->done = true;
         }
-        if (bs == ORBX_OK) fs.readers[buf] += (int)take.size();
+        if (bs == ORBX_OK) fs.readers[blk] += m;
         fs.busy = false;
         fs.cv.notify_all();
     }
@@ -1600,7 +1785,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     const orbx_status s = r.st == ORBX_OK ? copy_served(fs, r, out) : r.st;
     if (r.st == ORBX_OK) {
         lk.lock();
-        --fs.readers[r.buf];
+        --fs.readers[r.blk];
         fs.cv.notify_all();
     }
     return s;

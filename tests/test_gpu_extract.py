@@ -457,3 +457,48 @@ def test_extract_stereo_equals_separate(oracle_mod, orbx_lib, gpu, params, size)
     assert_kps_equal(kl, k1, "640x480 left")
     assert_f32_bits_equal(u, u1, "640x480 uRight")
     assert nv == n1
+
+
+def test_frame_server_mixed_sessions(orbx_lib, gpu):
+    """Six sessions (each its own extractor and thread) call orbx_stereo_frame_view at once
+    with frames of two sizes and two cameras interleaved: the frame server batches the calls
+    that meet (frames of one size and camera per batch, the two block pairs alternating,
+    graphs per batch size), and every frame's outputs equal the same frame run alone."""
+    import threading
+    import my_orb_slam2_amd as m
+    params = (2000, 1.2, 8, 20, 7)
+    cams = [(KITTI_MBF, float(np.float32(KITTI_MBF) / np.float32(KITTI_FX))),
+            (KITTI_MBF * 1.25, float(np.float32(KITTI_MBF * 1.25) / np.float32(KITTI_FX)))]
+    jobs = []
+    for i in range(6):
+        size = (1241, 376) if i % 3 else (640, 480)
+        jobs.append((synth.stereo_pair(70 + i, *size), cams[i % 2]))
+    solo = m.ORBextractor(*params)
+    ref = [m.extract_stereo(solo, L, R, mbf, mb) for (L, R), (mbf, mb) in jobs]
+    n_sessions, rounds = 6, 8
+    exts = [m.ORBextractor(*params) for _ in range(n_sessions)]
+    start = threading.Barrier(n_sessions)
+    errors = []
+
+    def session(t):
+        try:
+            start.wait()
+            for k in range(rounds):
+                j = (t + k) % len(jobs)
+                (L, R), (mbf, mb) = jobs[j]
+                got = m.extract_stereo(exts[t], L, R, mbf, mb)
+                for a, b, what in zip(got[:6], ref[j][:6], ("kl", "dl", "kr", "dr", "u", "d")):
+                    if a.tobytes() != b.tobytes():
+                        errors.append(f"session {t} frame {j} {what}")
+                if got[6] != ref[j][6]:
+                    errors.append(f"session {t} frame {j} n_valid")
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(f"session {t}: {e!r}")
+
+    threads = [threading.Thread(target=session, args=(t,)) for t in range(n_sessions)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a session did not finish"
+    assert not errors, errors[:5]

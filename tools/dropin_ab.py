@@ -20,6 +20,9 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "default": {},
     "frame": {"_args": "frame"},
     "frame_solo": {"_args": "frame", "ORBX_FRAME_SERVER": "0"},
+    "frame_nostage": {"_args": "frame", "ORBX_STAGE_THREAD": "0"},
+    "frame_stage2": {"_args": "frame", "ORBX_STAGE_THREAD": "2"},
+    "frame_nograph": {"_args": "frame", "ORBX_EXTRACT_GRAPH": "0"},
     "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
     "frame_side": {"_args": "frame", "ORBX_SIDE_MIN_BATCH": "1"},
     "frame_th16": {"_args": "frame", "ORBX_STRIP_TH": "16,16,16,16,16,16,16,16"},
@@ -43,7 +46,10 @@ def build():
 def run(d, ks):
     # the facade loop (bench.py --workload dropin's default), or ORBX_AB_BIN=boundary_test
     binp = ROOT / "tests" / "native" / os.environ.get("ORBX_AB_BIN", "facade_test")
+    only = os.environ.get("ORBX_AB_SETTINGS")   # comma-separated subset of SETTINGS
     for name, env_set in SETTINGS.items():
+        if only and name not in only.split(","):
+            continue
         for K in ks:
             extra = env_set.get("_args", "").split()
             env = dict(os.environ, LD_LIBRARY_PATH=str(VAR),
