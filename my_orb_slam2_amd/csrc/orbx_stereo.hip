@@ -61,6 +61,11 @@ __device__ __forceinline__ int byte_of(const uint32_t* w, int k) {   // k compil
 __device__ void median_cut(int nv, const int* vsad, const int16_t* vidx, int* hist, int* tmp,
                            float* uR, float* dep, int* nvalid, int b);
 
+// LPK lanes per left keypoint: 1 for large batches (one lane runs a keypoint's search and SAD);
+// 4 for small ones, where the launch has few keypoints per lane and a keypoint's serial chain
+// is the latency: the lanes split its candidates and its SAD window's rows and combine by
+// lane shuffles (the candidates' minimum is order-free, the SAD sums are exact integers).
+template <int LPK>
 __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restrict__ g,
                                                        const float* __restrict__ kpsL,
                                                        const uint8_t* __restrict__ descL,
@@ -157,10 +162,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
 #endif
     const int chunk = (NL + nsplit - 1) / nsplit;
     const int iL0 = slice * chunk, iL1 = min(NL, iL0 + chunk);
-    for (int iL = iL0 + tid; iL < iL1; iL += ST_THREADS) {
+    const int sub = tid % LPK;   // this lane's share of its keypoint (control flow is per group)
+    for (int iL = iL0 + tid / LPK; iL < iL1; iL += ST_THREADS / LPK) {
         if (nsplit > 1) {
-            split_store(uR + iL, -1.0f);
-            split_store(dep + iL, -1.0f);
+            if (sub == 0) {
+                split_store(uR + iL, -1.0f);
+                split_store(dep + iL, -1.0f);
+            }
         } else {
             uR[iL] = -1.0f;
             dep[iL] = -1.0f;
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             const int r0 = max(row - win, 0), r1 = min(row + win, H - 1);
             const int k0 = o * H + r0;
             const int e1 = bend[o * H + r1];
-            for (int e = k0 > 0 ? bend[k0 - 1] : 0; e < e1; ++e) {
+            for (int e = (k0 > 0 ? bend[k0 - 1] : 0) + sub; e < e1; e += LPK) {
                 const uint3 rc = rrec[e];
                 const int mn = (int)(int16_t)(rc.y & 0xFFFF), mx = (int)(int16_t)(rc.y >> 16);
                 if (mn > row || mx < row) continue;
@@ -209,6 +217,18 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
                         bestR = iR;
                         bestE = e;
                     }
+                }
+            }
+        }
+        if (LPK > 1) {   // the group's minimum of (distance, right index)
+#pragma unroll
+            for (int m = 1; m < LPK; m <<= 1) {
+                const int b2 = __shfl_xor(best, m, LPK), r2 = __shfl_xor(bestR, m, LPK);
+                const int e2 = __shfl_xor(bestE, m, LPK);
+                if (r2 >= 0 && (bestR < 0 || b2 < best || (b2 == best && r2 < bestR))) {
+                    best = b2;
+                    bestR = r2;
+                    bestE = e2;
                 }
             }
         }
@@ -232,78 +252,166 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         const uint8_t* PL = pyrL + (size_t)b * g->pyr_bytes + LV.off;
         const uint8_t* PR = pyrR + (size_t)b * g->pyr_bytes + LV.off;
         const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
-        // all 11 row pairs of the window are loaded before any is used (one memory latency
-        // per keypoint instead of one per row): left x-5..x+5 (4 dwords), right x-10..x+10
-        // (7 dwords), realigned with v_alignbyte
-        const uint32_t* pl0 = (const uint32_t*)(PL + (size_t)(yl - w) * pitch + ((xl - w) & ~3));
-        const uint32_t* pr0 = (const uint32_t*)(PR + (size_t)(yl - w) * pitch + ((xr - L5 - w) & ~3));
-        const int shl = (xl - w) & 3, shr = (xr - L5 - w) & 3;
-        const int pdw = pitch >> 2;   // rows are 64-byte aligned
-        uint32_t lraw[11][4], rraw[11][7];
-#pragma unroll
-        for (int r = 0; r < 11; ++r) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lraw[r][i] = pl0[r * pdw + i];
-#pragma unroll
-            for (int i = 0; i < 7; ++i) rraw[r][i] = pr0[r * pdw + i];
-        }
-        auto lrow = [&](int r, uint32_t (&o)[3]) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) o[i] = __builtin_amdgcn_alignbyte(lraw[r][i + 1], lraw[r][i], shl);
-        };
-        auto rrow = [&](int r, uint32_t (&o)[6]) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) o[i] = __builtin_amdgcn_alignbyte(rraw[r][i + 1], rraw[r][i], shr);
-        };
-        int cL, cR[11];
-        {
-            uint32_t lc[3], rc[6];
-            lrow(w, lc);
-            rrow(w, rc);
-            cL = byte_of(lc, 5);
-#pragma unroll
-            for (int k = 0; k < 11; ++k) cR[k] = byte_of(rc, k + 5);
-        }
-        // sum_x |(l_x - cL) - (r_{k+x} - cR_k)| = sum_x |(l_x + 256) - (r_{k+x} + 256 + cL - cR_k)|
-        // with every operand in [0, 1023]: v_sad_u16 takes two pixels per instruction (pixel
-        // pairs packed as u16 halves by v_perm), the 11th pixel one v_sad_u32-style |a - b|
         int acc[11];
-        uint32_t E[11];
+        if constexpr (LPK == 1) {
+            int accl[11];   // its own array: declared outside, `acc` made this path spill
+            uint32_t E[11];
+            // all 11 row pairs of the window are loaded before any is used (one memory latency
+            // per keypoint instead of one per row): left x-5..x+5 (4 dwords), right x-10..x+10
+            // (7 dwords), realigned with v_alignbyte
+            const uint32_t* pl0 = (const uint32_t*)(PL + (size_t)(yl - w) * pitch + ((xl - w) & ~3));
+            const uint32_t* pr0 = (const uint32_t*)(PR + (size_t)(yl - w) * pitch + ((xr - L5 - w) & ~3));
+            const int shl = (xl - w) & 3, shr = (xr - L5 - w) & 3;
+            const int pdw = pitch >> 2;   // rows are 64-byte aligned
+            uint32_t lraw[11][4], rraw[11][7];
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            acc[k] = 0;
-            E[k] = (uint32_t)(256 + cL - cR[k]) * 0x10001u;
-        }
-        auto pair_sel = [](int s0) {   // bytes s0, s0 + 1 of an 8-byte (hi:lo) pair as u16s
-            return (uint32_t)(s0 & 7) | 0x0C00u | (uint32_t)((s0 + 1) & 7) << 16 | 0x0C000000u;
-        };
+            for (int r = 0; r < 11; ++r) {
 #pragma unroll
-        for (int r = 0; r < 11; ++r) {
-            uint32_t lw[3], rw[6];
-            lrow(r, lw);
-            rrow(r, rw);
-            uint32_t LP[5];
+                for (int i = 0; i < 4; ++i) lraw[r][i] = pl0[r * pdw + i];
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const int b0 = 2 * j;   // bytes b0, b0 + 1 of lw
-                LP[j] = __builtin_amdgcn_perm(lw[(b0 >> 2) + 1 < 3 ? (b0 >> 2) + 1 : 2], lw[b0 >> 2],
-                                              pair_sel(b0 & 3)) + 0x01000100u;
+                for (int i = 0; i < 7; ++i) rraw[r][i] = pr0[r * pdw + i];
             }
-            const int l10 = byte_of(lw, 10) + 256;
-            // right pixel pairs starting at every byte 0..19: RP[m] = (r_m, r_{m+1})
-            uint32_t RP[20];
+            auto lrow = [&](int r, uint32_t (&o)[3]) {
 #pragma unroll
-            for (int m = 0; m < 20; ++m)
-                RP[m] = __builtin_amdgcn_perm(rw[(m >> 2) + 1 < 6 ? (m >> 2) + 1 : 5], rw[m >> 2],
-                                              pair_sel(m & 3));
+                for (int i = 0; i < 3; ++i) o[i] = __builtin_amdgcn_alignbyte(lraw[r][i + 1], lraw[r][i], shl);
+            };
+            auto rrow = [&](int r, uint32_t (&o)[6]) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = __builtin_amdgcn_alignbyte(rraw[r][i + 1], rraw[r][i], shr);
+            };
+            int cL, cR[11];
+            {
+                uint32_t lc[3], rc[6];
+                lrow(w, lc);
+                rrow(w, rc);
+                cL = byte_of(lc, 5);
+#pragma unroll
+                for (int k = 0; k < 11; ++k) cR[k] = byte_of(rc, k + 5);
+            }
+            // sum_x |(l_x - cL) - (r_{k+x} - cR_k)| = sum_x |(l_x + 256) - (r_{k+x} + 256 + cL - cR_k)|
+            // with every operand in [0, 1023]: v_sad_u16 takes two pixels per instruction (pixel
+            // pairs packed as u16 halves by v_perm), the 11th pixel one v_sad_u32-style |a - b|
 #pragma unroll
             for (int k = 0; k < 11; ++k) {
-                uint32_t a = (uint32_t)acc[k];
-#pragma unroll
-                for (int j = 0; j < 5; ++j) a = __builtin_amdgcn_sad_u16(LP[j], RP[k + 2 * j] + E[k], a);
-                const int d = l10 - (byte_of(rw, k + 10) + (int)(E[k] & 0xFFFFu));
-                acc[k] = (int)a + (d < 0 ? -d : d);
+                accl[k] = 0;
+                E[k] = (uint32_t)(256 + cL - cR[k]) * 0x10001u;
             }
+            auto pair_sel = [](int s0) {   // bytes s0, s0 + 1 of an 8-byte (hi:lo) pair as u16s
+                return (uint32_t)(s0 & 7) | 0x0C00u | (uint32_t)((s0 + 1) & 7) << 16 | 0x0C000000u;
+            };
+#pragma unroll
+            for (int r = 0; r < 11; ++r) {
+                uint32_t lw[3], rw[6];
+                lrow(r, lw);
+                rrow(r, rw);
+                uint32_t LP[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int b0 = 2 * j;   // bytes b0, b0 + 1 of lw
+                    LP[j] = __builtin_amdgcn_perm(lw[(b0 >> 2) + 1 < 3 ? (b0 >> 2) + 1 : 2], lw[b0 >> 2],
+                                                  pair_sel(b0 & 3)) + 0x01000100u;
+                }
+                const int l10 = byte_of(lw, 10) + 256;
+                // right pixel pairs starting at every byte 0..19: RP[m] = (r_m, r_{m+1})
+                uint32_t RP[20];
+#pragma unroll
+                for (int m = 0; m < 20; ++m)
+                    RP[m] = __builtin_amdgcn_perm(rw[(m >> 2) + 1 < 6 ? (m >> 2) + 1 : 5], rw[m >> 2],
+                                                  pair_sel(m & 3));
+#pragma unroll
+                for (int k = 0; k < 11; ++k) {
+                    uint32_t a = (uint32_t)accl[k];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) a = __builtin_amdgcn_sad_u16(LP[j], RP[k + 2 * j] + E[k], a);
+                    const int d = l10 - (byte_of(rw, k + 10) + (int)(E[k] & 0xFFFFu));
+                    accl[k] = (int)a + (d < 0 ? -d : d);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 11; ++k) acc[k] = accl[k];
+        } else {
+            const int pdw = pitch >> 2;   // rows are 64-byte aligned
+            const int shl = (xl - w) & 3, shr = (xr - L5 - w) & 3;
+            const uint32_t* pl0 = (const uint32_t*)(PL + (size_t)(yl - w) * pitch + ((xl - w) & ~3));
+            const uint32_t* pr0 = (const uint32_t*)(PR + (size_t)(yl - w) * pitch + ((xr - L5 - w) & ~3));
+            auto align_l = [&](const uint32_t (&raw)[4], uint32_t (&o)[3]) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) o[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], shl);
+            };
+            auto align_r = [&](const uint32_t (&raw)[7], uint32_t (&o)[6]) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) o[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], shr);
+            };
+            // sum_x |(l_x - cL) - (r_{k+x} - cR_k)| = sum_x |(l_x + 256) - (r_{k+x} + 256 + cL - cR_k)|
+            // with every operand in [0, 1023]: v_sad_u16 takes two pixels per instruction (pixel
+            // pairs packed as u16 halves by v_perm), the 11th pixel one v_sad_u32-style |a - b|
+            uint32_t E[11];
+            auto pair_sel = [](int s0) {   // bytes s0, s0 + 1 of an 8-byte (hi:lo) pair as u16s
+                return (uint32_t)(s0 & 7) | 0x0C00u | (uint32_t)((s0 + 1) & 7) << 16 | 0x0C000000u;
+            };
+            auto centre = [&](const uint32_t (&lc)[3], const uint32_t (&rc)[6]) {
+                const int cL = byte_of(lc, 5);
+#pragma unroll
+                for (int k = 0; k < 11; ++k) {
+                    acc[k] = 0;
+                    E[k] = (uint32_t)(256 + cL - byte_of(rc, k + 5)) * 0x10001u;
+                }
+            };
+            auto sad_row = [&](const uint32_t (&lw)[3], const uint32_t (&rw)[6]) {
+                uint32_t LP[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int b0 = 2 * j;   // bytes b0, b0 + 1 of lw
+                    LP[j] = __builtin_amdgcn_perm(lw[(b0 >> 2) + 1 < 3 ? (b0 >> 2) + 1 : 2], lw[b0 >> 2],
+                                                  pair_sel(b0 & 3)) + 0x01000100u;
+                }
+                const int l10 = byte_of(lw, 10) + 256;
+                // right pixel pairs starting at every byte 0..19: RP[m] = (r_m, r_{m+1})
+                uint32_t RP[20];
+#pragma unroll
+                for (int m = 0; m < 20; ++m)
+                    RP[m] = __builtin_amdgcn_perm(rw[(m >> 2) + 1 < 6 ? (m >> 2) + 1 : 5], rw[m >> 2],
+                                                  pair_sel(m & 3));
+#pragma unroll
+                for (int k = 0; k < 11; ++k) {
+                    uint32_t a = (uint32_t)acc[k];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) a = __builtin_amdgcn_sad_u16(LP[j], RP[k + 2 * j] + E[k], a);
+                    const int d = l10 - (byte_of(rw, k + 10) + (int)(E[k] & 0xFFFFu));
+                    acc[k] = (int)a + (d < 0 ? -d : d);
+                }
+            };
+            // lane `sub` of the group takes rows sub, sub + LPK, ... (and reads the centre row
+            // for the offsets); the group's row sums are added by shuffles
+            constexpr int RPL = (11 + LPK - 1) / LPK;
+            uint32_t lraw[RPL + 1][4], rraw[RPL + 1][7];
+#pragma unroll
+            for (int t = 0; t <= RPL; ++t) {
+                const int r = t == RPL ? w : min(sub + LPK * t, 10);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lraw[t][i] = pl0[r * pdw + i];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) rraw[t][i] = pr0[r * pdw + i];
+            }
+            {
+                uint32_t lc[3], rc[6];
+                align_l(lraw[RPL], lc);
+                align_r(rraw[RPL], rc);
+                centre(lc, rc);
+            }
+#pragma unroll
+            for (int t = 0; t < RPL; ++t) {
+                if (sub + LPK * t < 11) {
+                    uint32_t lw[3], rw[6];
+                    align_l(lraw[t], lw);
+                    align_r(rraw[t], rw);
+                    sad_row(lw, rw);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 11; ++k)
+#pragma unroll
+                for (int m = 1; m < LPK; m <<= 1) acc[k] += __shfl_xor(acc[k], m, LPK);
         }
         int bestDist = 0x7FFFFFFF;
         int bestinc = 0;
@@ -334,7 +442,8 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
                 disparity = (float)0.01;
                 bestuR = (float)((double)uL - 0.01);
             }
-            if (nsplit == 1) {
+            if (sub != 0) {
+            } else if (nsplit == 1) {
                 dep[iL] = mbf / disparity;
                 uR[iL] = bestuR;
                 const int pos = atomicAdd(&tmp[16], 1);
@@ -484,9 +593,25 @@ size_t stereo_lds_bytes(int kp_cap, int height, int ob) {
     return s;
 }
 
+// Small batches (at most ST_LPK_BATCH pairs): ST_LPK lanes per left keypoint, ST_LPK_SPLIT
+// workgroups per pair (every keypoint of a 2000-keypoint image in flight at once).
+#ifndef ST_LPK
+#define ST_LPK 4
+#endif
+#ifndef ST_LPK_SPLIT
+#define ST_LPK_SPLIT 8
+#endif
+#ifndef ST_LPK_BATCH
+#define ST_LPK_BATCH 32
+#endif
+
 hipError_t prepare_stereo(size_t lds) {
-    return hipFuncSetAttribute((const void*)k_stereo, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)k_stereo<1>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_stereo<ST_LPK>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    return e;
 }
 
 // Workgroups per pair: up to ST_SPLIT while the launch has at most 256 workgroups (one per
@@ -496,8 +621,9 @@ hipError_t prepare_stereo(size_t lds) {
 #ifndef ST_SPLIT
 #define ST_SPLIT 4
 #endif
+static bool stereo_lpk(int batch) { return ST_LPK > 1 && batch <= ST_LPK_BATCH; }
 int stereo_split(int batch) {
-    int ns = ST_SPLIT;
+    int ns = stereo_lpk(batch) ? ST_LPK_SPLIT : ST_SPLIT;
     while (ns > 1 && batch * ns > 256) ns >>= 1;
     return ns;
 }
@@ -509,7 +635,8 @@ hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {
     hipEvent_t e0 = T ? T->get() : nullptr, e1 = T ? T->get() : nullptr;
     if (!e0 || !e1) e0 = e1 = nullptr;
     const int ns = stereo_split(a.batch);
-    hipExtLaunchKernelGGL(k_stereo, dim3(a.batch * ns), dim3(ST_THREADS), (uint32_t)a.lds, st, e0,
+    hipExtLaunchKernelGGL(stereo_lpk(a.batch) ? k_stereo<ST_LPK> : k_stereo<1>,
+                          dim3(a.batch * ns), dim3(ST_THREADS), (uint32_t)a.lds, st, e0,
                           (ns > 1 && !ST_FUSED_CUT) ? nullptr : e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
                           a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb, a.uR, a.depth, a.nvalid,
                           ns, a.scnt, a.ssad, a.sidx);
