@@ -1042,8 +1042,9 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 // replays the server's graph for its size on the server's own handle: the lefts as images
 // [0, m), the rights as [m, 2m), one extraction of the 2m images, one stereo launch over the
 // m pairs, the outputs back into the pair's pinned output block.  Each waiting thread then
-// copies its frame's outputs into its own handle's pinned block.  Two block pairs alternate
-// (one forms while the other runs).  With several sessions the runtime's submission path,
+// copies its frame's outputs into its own handle's pinned block.  Two block pairs alternate,
+// each with its own server handle: a batch forms in one while the other's runs, and up to
+// FS_INFLIGHT batches run at once.  With several sessions the runtime's submission path,
 // not the GPU, bounded the rate of one-call frames (14 submissions each).
 #ifndef STAGE_THREAD
 // orbx_stereo_frame_view: the right image staged by a helper thread (0 never, 1 for frames that
@@ -1054,6 +1055,12 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 #endif
 #ifndef EXTRACT_GRAPH
 #define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
+#endif
+// Batches on the device at once (each on its block pair's own server handle): a batch of a
+// few frames is a latency-bound chain that leaves most of the GPU idle, so the next one runs
+// beside it.
+#ifndef FS_INFLIGHT
+#define FS_INFLIGHT 2
 #endif
 #ifndef FS_MAX_FRAMES
 #define FS_MAX_FRAMES 8
@@ -1083,8 +1090,9 @@ struct FsGraph {
 struct FrameServer {
     std::mutex mu;
     std::condition_variable cv;
-    bool busy = false;             // a batch (or a lone call) is on the device
-    orbx_extractor* sh = nullptr;  // the server's handle (created on first use)
+    int inflight = 0;              // batches (and lone calls) on the device
+    bool pair_busy[2] = {false, false};   // a batch of block pair i is on the device
+    orbx_extractor* sh[2] = {nullptr, nullptr};   // the server's handle per block pair
     // the batch being formed: n frames joined, `staged` of them copied into input block blk
     int blk = 0, n = 0, staged = 0;
     FsBatch geo;
@@ -1097,7 +1105,7 @@ struct FrameServer {
     // (while the batch before runs), into the device staging block of its pair
     DevBuf dstage[2];
     hipStream_t cst = nullptr;
-    hipEvent_t cev = nullptr;      // recorded on cst when a batch is taken
+    hipEvent_t cev[2] = {nullptr, nullptr};   // recorded on cst when a pair's batch is taken
     uint8_t* hout[2] = {nullptr, nullptr};
     size_t hout_n[2] = {0, 0};
     int readers[2] = {0, 0};       // threads still copying out of each output block
@@ -1150,13 +1158,13 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
 // the 2m images, the stereo match of the m pairs, two DMAs back into output block blk.
 static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, int blk,
                               const FsBatch& g) {
-    if (!fs.sh) {
+    if (!fs.sh[blk]) {
         orbx_extractor_params p = h0->prm;
         p.max_batch = 2 * FS_MAX_FRAMES;
-        const orbx_status s = orbx_extractor_create(&p, &fs.sh);
+        const orbx_status s = orbx_extractor_create(&p, &fs.sh[blk]);
         if (s != ORBX_OK) return s;
     }
-    orbx_extractor* S = fs.sh;
+    orbx_extractor* S = fs.sh[blk];
     std::lock_guard<std::mutex> lk(S->mu);
     // the workspace for the largest batch: one layout (and graph key) for every m
     orbx_status s = ensure_workspace(S, g.width, g.height, 2 * FS_MAX_FRAMES);
@@ -1210,7 +1218,7 @@ static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, 
                        {dsg, hout, S->d_sscr.p, dso, (const void*)(uintptr_t)mbf_bits,
                         (const void*)(uintptr_t)mb_bits, (const void*)(intptr_t)m,
                         (const void*)ib});
-    if (!HIPOK(hipStreamWaitEvent(st, fs.cev, 0)) ||   // the frames' copies to the device
+    if (!HIPOK(hipStreamWaitEvent(st, fs.cev[blk], 0)) ||   // the frames' copies to the device
         !(graph ? HIPOK(hipGraphLaunch(G.gx, st)) : enqueue(a)) || !mark_done(S, st) ||
         !wait_done(S))
         return ORBX_ERR_DEVICE;
@@ -1672,9 +1680,10 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         return stereo_frame_solo(h, left, stride_left, right, stride_right, width, height, mbf,
                                  mb, out);
     FrameServer& fs = frame_server(h);
+    const int inflight_max = tuned("ORBX_FS_INFLIGHT", FS_INFLIGHT);
     std::unique_lock<std::mutex> lk(fs.mu);
-    if (!fs.busy && fs.n == 0) {   // alone on the device: on this handle
-        fs.busy = true;
+    if (fs.inflight == 0 && fs.n == 0) {   // alone on the device: on this handle
+        ++fs.inflight;
 #ifdef ORBX_TUNING
         const auto t0 = FrameServer::clk::now();
         fs.st_idle_us += FrameServer::us(fs.st_free, t0);
@@ -1688,7 +1697,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         fs.st_solo++;
         fs.st_solo_us += FrameServer::us(t0, fs.st_free);
 #endif
-        fs.busy = false;
+        --fs.inflight;
         fs.cv.notify_all();
         return s;
     }
@@ -1708,12 +1717,16 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     FsReq r{h};
     lk.lock();
     // join the batch being formed (after a full one, or one of another size or camera, goes)
-    fs.cv.wait(lk, [&] { return fs.n == 0 || (fs.n < FS_MAX_FRAMES && same(fs.geo, g)); });
+    // (a batch opens in a block pair whose last batch has finished)
+    fs.cv.wait(lk, [&] {
+        return fs.n == 0 ? !fs.pair_busy[fs.blk] : fs.n < FS_MAX_FRAMES && same(fs.geo, g);
+    });
     if (fs.n == 0) {   // open it: its blocks were last used by a batch that has finished
         const size_t bytes = 2 * FS_MAX_FRAMES * g.img_bytes;
         if (!HIPOK(hipSetDevice(h->device)) ||
             (!fs.cst && !HIPOK(hipStreamCreateWithFlags(&fs.cst, hipStreamNonBlocking))) ||
-            (!fs.cev && !HIPOK(hipEventCreateWithFlags(&fs.cev, hipEventDisableTiming))) ||
+            (!fs.cev[fs.blk] &&
+             !HIPOK(hipEventCreateWithFlags(&fs.cev[fs.blk], hipEventDisableTiming))) ||
             !ensure_pinned(fs.hin[fs.blk], fs.hin_n[fs.blk], bytes) ||
             !fs.dstage[fs.blk].ensure(bytes))
             return ORBX_ERR_DEVICE;
@@ -1739,7 +1752,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     ++fs.staged;
     fs.cv.notify_all();
     while (!r.done) {
-        if (fs.busy || fs.n == 0 || fs.staged < fs.n) {
+        if (fs.inflight >= inflight_max || fs.n == 0 || fs.staged < fs.n) {
             fs.cv.wait(lk);
             continue;
         }
@@ -1748,11 +1761,12 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         FsReq* take[FS_MAX_FRAMES];
         std::copy(fs.req, fs.req + m, take);
         // every frame's copy is on the stream by now (each was issued before its `staged`)
-        const bool recorded = HIPOK(hipEventRecord(fs.cev, fs.cst));
+        const bool recorded = HIPOK(hipEventRecord(fs.cev[blk], fs.cst));
         const FsBatch bg = fs.geo;
         fs.n = fs.staged = 0;
         fs.blk ^= 1;
-        fs.busy = true;
+        ++fs.inflight;
+        fs.pair_busy[blk] = true;
         fs.cv.notify_all();
 #ifdef ORBX_TUNING
         const auto t0 = FrameServer::clk::now();
@@ -1778,7 +1792,8 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
             take[i]->done = true;
         }
         if (bs == ORBX_OK) fs.readers[blk] += m;
-        fs.busy = false;
+        --fs.inflight;
+        fs.pair_busy[blk] = false;
         fs.cv.notify_all();
     }
     lk.unlock();
