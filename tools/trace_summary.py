@@ -15,7 +15,7 @@ def main(d):
     ker = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     ks = sorted((int(k["Start_Timestamp"]), int(k["End_Timestamp"]), k["Queue_Id"],
                  k["Kernel_Name"].split("(")[0].replace("void ", "")) for k in ker)
-    stereo = [k for k in ks if k[3].endswith("k_stereo")]
+    stereo = [k for k in ks if "k_stereo" in k[3] and "cut" not in k[3]]
     a, b = stereo[len(stereo) // 5][0], stereo[4 * len(stereo) // 5][0]
     ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "API t" + r["Thread_Id"][-3:],
            r["Function"]) for r in api]
