@@ -24,6 +24,7 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "frame_stage2": {"_args": "frame", "ORBX_STAGE_THREAD": "2"},
     "frame_nograph": {"_args": "frame", "ORBX_EXTRACT_GRAPH": "0"},
     "frame_if1": {"_args": "frame", "ORBX_FS_INFLIGHT": "1"},
+    "frame_oct16": {"_args": "frame", "ORBX_OCT_SMALL_BATCH": "16"},
     "frame_if3": {"_args": "frame", "ORBX_FS_INFLIGHT": "3"},
     "frame_q16": {"_args": "frame", "GPU_MAX_HW_QUEUES": "16"},
     "frame_side": {"_args": "frame", "ORBX_SIDE_MIN_BATCH": "1"},
