@@ -153,6 +153,29 @@ orbx_status orbx_search_by_projection(orbx_matcher* m, int32_t mode,
                                       int32_t nq, const float* inv_sigma2, int32_t nlevels,
                                       int32_t orb_dist, int32_t* match_q, int32_t* nmatches);
 
+/* orbx_search_by_projection with per-query flags and call flags.
+ * qflags[nq] (may be NULL = all 0): ORBX_QF_NO_CLAIM marks a query whose MapPoint has no
+ * observations (Observations() == 0, e.g. the stereo "temporal" points Tracking::UpdateLastFrame
+ * puts into the last frame).  The reference's skip test for an already matched feature is
+ * F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0 (:90-92, :1471-1473), so such a
+ * query's match does not keep later queries off its feature (a later match overwrites it).
+ * Only the FRAME_MAPPOINTS and LAST_FRAME modes read the flag.
+ * flags: ORBX_PROJ_PREFILTER returns every accepted query's feature without the
+ * rotation-consistency filter (LAST_FRAME / KEYFRAME), *nmatches = the accepted count, so the
+ * caller can apply the reference's per-feature filter itself (rotHist holds feature indices,
+ * :1508 / :1637: with overwritten matches a feature can sit in two bins).
+ * Replaces the same ORBmatcher methods as orbx_search_by_projection, which equals this call
+ * with qflags = NULL and flags = 0. */
+enum { ORBX_QF_NO_CLAIM = 1 };
+enum { ORBX_PROJ_PREFILTER = 1 };
+orbx_status orbx_search_by_projection_ex(orbx_matcher* m, int32_t mode,
+                                         const orbx_featureset* target, const uint8_t* claimed,
+                                         const uint8_t* qdesc, const orbx_proj_query* q,
+                                         const uint8_t* qflags, int32_t nq,
+                                         const float* inv_sigma2, int32_t nlevels,
+                                         int32_t orb_dist, int32_t flags, int32_t* match_q,
+                                         int32_t* nmatches);
+
 /* ORBmatcher::SearchBySim3 (:1158-1382).  q12[n1]: KF1 feature i's MapPoint projected into
  * KF2 (radius < 0 when the reference skips i1: no MapPoint, already matched, bad, or failed
  * the depth/image/distance tests); qdesc1: n1 x 32 MapPoint descriptors.  q21[n2] likewise

@@ -93,6 +93,8 @@ SIGNATURES = {
     "orbx_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _i,
                                            _i, _vp, _i, _vp]),
     "orbx_search_by_projection": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _i, _i, _vp, _vp]),
+    "orbx_search_by_projection_ex": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _i, _i,
+                                          _vp, _vp]),
     "orbx_search_by_sim3": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp]),
     "orbx_search_for_initialization": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orbx_search_by_bow_kf_frame_batch_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

@@ -147,3 +147,45 @@ def build_facade_test(force: bool = False, verbose: bool = False) -> pathlib.Pat
     subprocess.run(cmd, check=True)
     os.replace(str(FACADE_BIN) + ".tmp", FACADE_BIN)
     return FACADE_BIN
+
+
+# ---- the ORBmatcher drop-in compiled as ORB-SLAM2 would include it (tests/native/matcher_test.cpp)
+MATCHER_SRC = PKG.parent / "tests" / "native" / "matcher_test.cpp"
+MATCHER_BIN = PKG.parent / "tests" / "native" / "matcher_test"
+MATCHER_CPU_BIN = PKG.parent / "tests" / "native" / "matcher_test_cpu"
+
+
+def build_matcher_test(force: bool = False, verbose: bool = False, cpu: bool = False) -> pathlib.Path:
+    """g++ on integration/ORBmatcher.h with the ORB-SLAM2 stand-in classes
+    (tests/native/slam2_standin) and the cv stand-in, plus the CPU restatement it is checked
+    against (oracle/orb_matcher_objects.h).  cpu=False: linked to the in-tree liborbx.so (the
+    searches run on the GPU).  cpu=True: matcher_test_cpu, linked instead to the C-ABI test
+    double tests/native/oracle_abi.cpp over oracle/orb_matcher_oracle.cpp (no GPU, no liborbx),
+    for the CPU test suite."""
+    root = PKG.parent
+    native = root / "tests" / "native"
+    out = MATCHER_CPU_BIN if cpu else MATCHER_BIN
+    deps = ([MATCHER_SRC, native / "oracle_abi.cpp", root / "oracle" / "orb_matcher_oracle.cpp",
+             root / "oracle" / "orb_matcher_objects.h"] + sorted((root / "include").glob("*.h")) +
+            sorted((root / "integration").glob("*.h")) +
+            sorted((native / "cv_standin").rglob("*.hpp")) + sorted((native / "slam2_standin").glob("*.h")))
+    newest = max(p.stat().st_mtime for p in deps)
+    if not force and out.exists() and out.stat().st_mtime >= newest:
+        return out
+    # -ffp-contract=off: the facade's and the restatement's float expressions as written
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-ffp-contract=off",
+           "-I" + str(root / "include"), "-I" + str(root / "integration"),
+           "-I" + str(root / "oracle"), "-I" + str(native / "cv_standin"),
+           "-I" + str(native / "slam2_standin"), str(MATCHER_SRC)]
+    if cpu:
+        cmd += [str(native / "oracle_abi.cpp"), str(root / "oracle" / "orb_matcher_oracle.cpp")]
+    else:
+        build(verbose=verbose)
+        cmd += ["-L" + str(PKG), "-lorbx", "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib",
+                "-Wl,-rpath,$ORIGIN/../../my_orb_slam2_amd"]
+    cmd += ["-pthread", "-o", str(out) + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(out) + ".tmp", out)
+    return out

@@ -826,6 +826,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
         const int qi = q0 + qb + lane;
         const bool mine = lane < cnt;
         const int nc = mine ? g.ncand[qi] : 0;
+        // a query whose MapPoint has no observations leaves its feature unclaimed (:90-92,
+        // :1471-1473 test Observations() > 0 of the MapPoint already there)
+        const bool claims = !(mine && g.qflags && (g.qflags[qi] & ORBX_QF_NO_CLAIM));
         const int nv = min(nc, PROJ_K);
         int2 L[PROJ_K];
         {
@@ -864,13 +867,13 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
             acc = acc && act && !rescan;
             int f = start + 1;
             if (par) {
-                if (acc) atomicMin(&owner[b.i], lane);
+                if (acc && claims) atomicMin(&owner[b.i], lane);
                 bool wait = rescan && lane > start;
                 if (act && lane > start) {
                     if (b.i >= 0 && owner[b.i] < lane) wait = true;
                     if (c.i >= 0 && owner[c.i] < lane) wait = true;
                 }
-                if (acc) owner[b.i] = 64;
+                if (acc && claims) owner[b.i] = 64;
                 const uint64_t w = __ballot(wait);
                 f = w ? (int)__builtin_ctzll(w) : cnt;
             }
@@ -894,7 +897,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
                 if (lane == start) {
                     res = racc ? rb.i : -1;
                     if (racc) {
-                        claimed[rb.i] = 1;
+                        if (claims) claimed[rb.i] = 1;
                         rbin = rb.bin;
                         if (mi.rot && g.check_ori) atomicAdd(&hist[rb.bin], 1);
                     }
@@ -905,7 +908,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
             if (lane >= start && lane < f) {
                 res = acc ? b.i : -1;
                 if (acc) {
-                    claimed[b.i] = 1;
+                    if (claims) claimed[b.i] = 1;
                     rbin = b.bin;
                     if (mi.rot && g.check_ori) atomicAdd(&hist[b.bin], 1);
                 }
@@ -991,7 +994,7 @@ __global__ __launch_bounds__(256) void k_proj_finish(ProjLaunch g) {
     __shared__ int h[32];
     const int tid = threadIdx.x;
     const ModeInfo mi = mode_info(g.mode, g.orb_dist);
-    const bool filt = mi.rot && g.check_ori;
+    const bool filt = mi.rot && g.check_ori && !g.prefilter;
     const int job = blockIdx.x;
     const int q0 = job_first_query(g, job), q1 = job_end_query(g, job);
     if (tid < 32) h[tid] = filt ? g.hist[32 * job + tid] : 0;

@@ -267,7 +267,7 @@ orbx_status bow_common(orbx_matcher* m, const orbx_featureset* a, const uint8_t*
 orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
                         const uint8_t* claimed, const uint8_t* qdesc, const orbx_proj_query* q,
                         int nq, const float* inv_sigma2, int nlevels, int orb_dist, int32_t* out,
-                        int32_t* nmatches) {
+                        int32_t* nmatches, const uint8_t* qflags = nullptr, int flags = 0) {
     if (!m || !out || !nmatches || nq < 0 || nq > (1 << 22)) return ORBX_ERR_INVALID;
     if (nq > 0 && (!qdesc || !q)) return ORBX_ERR_INVALID;
     if (!valid_feat(T, false, true)) return ORBX_ERR_INVALID;
@@ -281,8 +281,9 @@ orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
     const FeatOffsets ot = pack_feat(P, T);
     const size_t oq = P.add(q, sizeof(orbx_proj_query) * (size_t)nq);
     const size_t od = P.add(qdesc, 32 * (size_t)nq);
-    size_t oc = 0;
+    size_t oc = 0, of = 0;
     if (claimed) oc = P.add(claimed, (size_t)T->n);
+    if (qflags) of = P.add(qflags, (size_t)nq);
     orbx_status s = upload(m);
     if (s != ORBX_OK) return s;
     // outputs: nmatches(64 ints) | out[nq] | hist[32] | top2[nq] | bins[nq] | cand | ncand
@@ -308,6 +309,8 @@ orbx_status proj_common(orbx_matcher* m, int mode, const orbx_featureset* T,
     L.ratio = m->prm.nnratio;
     L.check_ori = m->prm.check_orientation;
     L.claimed_in = claimed ? base + oc : nullptr;
+    L.qflags = qflags ? base + of : nullptr;
+    L.prefilter = (flags & ORBX_PROJ_PREFILTER) != 0;
     L.out = (int32_t*)(ob + o_out);
     L.top2 = (int4*)(ob + o_top);
     L.cand = (int2*)(ob + o_cand);
@@ -492,6 +495,19 @@ orbx_status orbx_search_by_projection(orbx_matcher* m, int32_t mode,
     if (mode < 0 || mode >= ORBX_PROJ_MODE_COUNT) return ORBX_ERR_INVALID;
     return proj_common(m, mode, target, claimed, qdesc, q, nq, inv_sigma2, nlevels, orb_dist,
                        match_q, nmatches);
+}
+
+orbx_status orbx_search_by_projection_ex(orbx_matcher* m, int32_t mode,
+                                         const orbx_featureset* target, const uint8_t* claimed,
+                                         const uint8_t* qdesc, const orbx_proj_query* q,
+                                         const uint8_t* qflags, int32_t nq,
+                                         const float* inv_sigma2, int32_t nlevels,
+                                         int32_t orb_dist, int32_t flags, int32_t* match_q,
+                                         int32_t* nmatches) {
+    if (mode < 0 || mode >= ORBX_PROJ_MODE_COUNT || (flags & ~ORBX_PROJ_PREFILTER))
+        return ORBX_ERR_INVALID;
+    return proj_common(m, mode, target, claimed, qdesc, q, nq, inv_sigma2, nlevels, orb_dist,
+                       match_q, nmatches, qflags, flags);
 }
 
 orbx_status orbx_search_by_sim3(orbx_matcher* m, const orbx_featureset* kf1,

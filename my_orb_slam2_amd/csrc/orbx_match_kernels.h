@@ -64,6 +64,8 @@ struct ProjLaunch {
     float ratio;
     int check_ori;
     const uint8_t* claimed_in;   // may be null
+    const uint8_t* qflags;       // nq ORBX_QF_* per query, may be null
+    int prefilter;               // ORBX_PROJ_PREFILTER: no rotation-consistency filter
     int32_t* out;                // nq
     int4* top2;                  // nq (PROJ_INIT: static best and second)
     int2* cand;                  // nq x PROJ_K (claim modes: sorted candidate lists)

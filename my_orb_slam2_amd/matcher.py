@@ -158,6 +158,27 @@ class ORBmatcher:
             0 if isg is None else len(isg), int(orb_dist), ptr(out), ctypes.byref(n)))
         return n.value, out[:len(q)]
 
+    def search_by_projection_ex(self, mode: int, target: FeatureSet, queries, qdesc,
+                                qflags=None, claimed=None, inv_sigma2=None, orb_dist: int = 0,
+                                prefilter: bool = False):
+        """orbx_search_by_projection_ex: per-query ORBX_QF_* flags (qflags) and the
+        ORBX_PROJ_PREFILTER call flag -> (nmatches, target index per query)."""
+        q = _queries(queries)
+        d = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+        if len(d) != len(q):
+            raise ValueError("one descriptor per query")
+        t = featureset_c(target)
+        cl = None if claimed is None else _u8(claimed, target.n)
+        qf = None if qflags is None else _u8(qflags, len(q))
+        isg = None if inv_sigma2 is None else np.ascontiguousarray(inv_sigma2, np.float32)
+        out = np.full(max(len(q), 1), -1, np.int32)
+        n = ctypes.c_int32()
+        check("orbx_search_by_projection_ex", self._lib.orbx_search_by_projection_ex(
+            self._h, int(mode), ctypes.byref(t), ptr(cl), ptr(d), ptr(q), ptr(qf), len(q),
+            ptr(isg), 0 if isg is None else len(isg), int(orb_dist), int(bool(prefilter)),
+            ptr(out), ctypes.byref(n)))
+        return n.value, out[:len(q)]
+
     def SearchByProjection(self, target: FeatureSet, queries, qdesc, claimed=None,
                            variant: str = "mappoints", orb_dist: int = TH_HIGH):
         """The four SearchByProjection overloads: variant "mappoints" (:46-132), "kf_scw"

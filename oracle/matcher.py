@@ -61,6 +61,8 @@ def lib():
                                                       _i, _i, _vp]
         L.oracle_search_by_projection.argtypes = [_i, _vp, _vp, _vp, _vp, _i, _vp, _i, _f, _i,
                                                   _vp]
+        L.oracle_search_by_projection_ex.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i,
+                                                     _f, _i, _i, _vp]
         L.oracle_search_by_sim3.argtypes = [_vp, _vp, _vp, _vp, _i, _vp, _vp, _i, _vp]
         L.oracle_search_for_initialization.argtypes = [_vp, _vp, _vp, _i, _f, _i, _vp]
         L.oracle_descriptor_distance_m.argtypes = [_vp, _vp]
@@ -132,6 +134,22 @@ def search_by_projection(mode, target, queries, qdesc, claimed=None, inv_sigma2=
     n = lib().oracle_search_by_projection(int(mode), ctypes.byref(t), _a(cl), _a(d), _a(q),
                                           len(q), _a(isg), int(orb_dist), nnratio,
                                           int(check_ori), _a(out))
+    return n, out[:len(q)]
+
+
+def search_by_projection_ex(mode, target, queries, qdesc, qflags=None, claimed=None,
+                            inv_sigma2=None, orb_dist=0, nnratio=0.6, check_ori=True,
+                            prefilter=False):
+    q = np.ascontiguousarray(queries)
+    d = np.ascontiguousarray(qdesc, np.uint8)
+    out = np.zeros(max(len(q), 1), np.int32)
+    t = _feat(target)
+    cl = None if claimed is None else _u8(claimed, len(target.keys))
+    qf = None if qflags is None else _u8(qflags, len(q))
+    isg = None if inv_sigma2 is None else np.ascontiguousarray(inv_sigma2, np.float32)
+    n = lib().oracle_search_by_projection_ex(int(mode), ctypes.byref(t), _a(cl), _a(d), _a(q),
+                                             _a(qf), len(q), _a(isg), int(orb_dist), nnratio,
+                                             int(check_ori), int(prefilter), _a(out))
     return n, out[:len(q)]
 
 

@@ -346,15 +346,22 @@ int oracle_search_for_triangulation(const orbx_featureset* K1, const uint8_t* ha
 }
 
 // The projection searches (include/orbx_match.h orbx_proj_mode).  claimed may be NULL.
-int oracle_search_by_projection(int mode, const orbx_featureset* T, const uint8_t* claimed_in,
-                                const uint8_t* qdesc, const orbx_proj_query* Q, int nq,
-                                const float* inv_sigma2, int orb_dist, float nnratio,
-                                int checkOri, int32_t* match_q) {
+// qflags (may be NULL): ORBX_QF_NO_CLAIM = the query's MapPoint has no observations, so its
+// match does not count as "already matched" for later queries (:90-92, :1471-1473).
+// prefilter: return the accepted matches without the rotation-consistency filter.  The filter
+// otherwise drops, per query, every match whose bin is not among the three maxima (with
+// claims a feature has one match, so this is the reference's per-feature loop).
+int oracle_search_by_projection_ex(int mode, const orbx_featureset* T, const uint8_t* claimed_in,
+                                   const uint8_t* qdesc, const orbx_proj_query* Q,
+                                   const uint8_t* qflags, int nq, const float* inv_sigma2,
+                                   int orb_dist, float nnratio, int checkOri, int prefilter,
+                                   int32_t* match_q) {
     std::vector<char> claimed(T->n, 0);
     const bool greedy = mode <= ORBX_PROJ_KEYFRAME;
     if (claimed_in && greedy)
         for (int i = 0; i < T->n; i++) claimed[i] = claimed_in[i] != 0;
-    std::vector<int> owner(T->n, -1);   // feature -> query that claimed it (for the filter)
+    auto claims = [&](int iq) { return !(qflags && (qflags[iq] & ORBX_QF_NO_CLAIM)); };
+    std::vector<int> qbin(nq, -1);      // rotation bin of each accepted query
     std::vector<int> rotHist[HISTO_LENGTH];
     int nmatches = 0;
     for (int iq = 0; iq < nq; iq++) {
@@ -384,7 +391,7 @@ int oracle_search_by_projection(int mode, const orbx_featureset* T, const uint8_
             }
             if (bestDist <= TH_HIGH) {   // :121-128
                 if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
-                claimed[bestIdx] = 1;
+                if (claims(iq)) claimed[bestIdx] = 1;
                 match_q[iq] = bestIdx;
                 nmatches++;
             }
@@ -405,11 +412,13 @@ int oracle_search_by_projection(int mode, const orbx_featureset* T, const uint8_
             }
             const int th = mode == ORBX_PROJ_LAST_FRAME ? TH_HIGH : orb_dist;
             if (bestDist <= th) {
-                claimed[bestIdx2] = 1;
-                owner[bestIdx2] = iq;
+                if (mode == ORBX_PROJ_KEYFRAME || claims(iq)) claimed[bestIdx2] = 1;
                 match_q[iq] = bestIdx2;
                 nmatches++;
-                if (checkOri) rotHist[rot_bin(q.angle, T->keys[bestIdx2].angle)].push_back(bestIdx2);
+                if (checkOri) {
+                    qbin[iq] = rot_bin(q.angle, T->keys[bestIdx2].angle);
+                    rotHist[qbin[iq]].push_back(bestIdx2);
+                }
             }
         } else {
             // KeyFrame grid searches: KF_SCW :393-429, FUSE :946-1024, FUSE_SCW :1107-1151,
@@ -445,12 +454,24 @@ int oracle_search_by_projection(int mode, const orbx_featureset* T, const uint8_
             }
         }
     }
-    if (checkOri && (mode == ORBX_PROJ_LAST_FRAME || mode == ORBX_PROJ_KEYFRAME))
-        nmatches -= rotation_filter(rotHist, [&](int idx) {
-            match_q[owner[idx]] = -1;   // CurrentFrame.mvpMapPoints[idx] = NULL
-            return 1;
-        });
+    if (checkOri && !prefilter && (mode == ORBX_PROJ_LAST_FRAME || mode == ORBX_PROJ_KEYFRAME)) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int iq = 0; iq < nq; iq++)   // CurrentFrame.mvpMapPoints[idx] = NULL
+            if (match_q[iq] >= 0 && qbin[iq] != ind1 && qbin[iq] != ind2 && qbin[iq] != ind3) {
+                match_q[iq] = -1;
+                nmatches--;
+            }
+    }
     return nmatches;
+}
+
+int oracle_search_by_projection(int mode, const orbx_featureset* T, const uint8_t* claimed_in,
+                                const uint8_t* qdesc, const orbx_proj_query* Q, int nq,
+                                const float* inv_sigma2, int orb_dist, float nnratio,
+                                int checkOri, int32_t* match_q) {
+    return oracle_search_by_projection_ex(mode, T, claimed_in, qdesc, Q, nullptr, nq, inv_sigma2,
+                                          orb_dist, nnratio, checkOri, 0, match_q);
 }
 
 // SearchBySim3 — ORBmatcher.cc:1158-1382 (the two projection loops + agreement check).

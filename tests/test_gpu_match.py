@@ -104,6 +104,37 @@ def test_projection_large_target(oracle_mod, orbx_lib, gpu, mode):
     np.testing.assert_array_equal(m_g, m_o)
 
 
+@pytest.mark.parametrize("mode,seed,th,prefilter", [
+    (PROJ_FRAME_MAPPOINTS, 11, 15.0, False), (PROJ_LAST_FRAME, 12, 7.0, True),
+    (PROJ_LAST_FRAME, 13, 25.0, True), (PROJ_LAST_FRAME, 14, 25.0, False),
+    (PROJ_KEYFRAME, 15, 10.0, True)])
+def test_projection_no_claim_queries(oracle_mod, orbx_lib, gpu, mode, seed, th, prefilter):
+    """orbx_search_by_projection_ex: a third of the queries are MapPoints without
+    observations (ORBX_QF_NO_CLAIM), whose matches later queries may take over (ORBmatcher.cc
+    :90-92, :1471-1473), with and without the rotation filter."""
+    from oracle import matcher as om
+    f1, f2, t = synth.feature_pair(seed + 40, n1=1500, n2=1200, dup_frac=0.1)
+    q, d = synth.projection_queries(seed, f1, f2, t, th=th,
+                                    mode_levels="frame" if mode in (0, 2, 3) else "kf")
+    rng = np.random.default_rng(seed)
+    claimed = rng.random(f2.n) < 0.1
+    qflags = (rng.random(len(q)) < 0.33).astype(np.uint8)
+    # the first 300 queries once more in front, as MapPoints without observations: their
+    # matches stay unclaimed, so the same queries later take those features again
+    q, d = np.concatenate([q[:300], q]), np.concatenate([d[:300], d])
+    qflags = np.concatenate([np.ones(300, np.uint8), qflags])
+    m = _matcher(0.8, True)
+    n_g, m_g = m.search_by_projection_ex(mode, f2, q, d, qflags, claimed, orb_dist=64,
+                                         prefilter=prefilter)
+    n_o, m_o = om.search_by_projection_ex(mode, f2, q, d, qflags, claimed, orb_dist=64,
+                                          nnratio=0.8, prefilter=prefilter)
+    assert n_g == n_o and n_o > 0
+    np.testing.assert_array_equal(m_g, m_o)
+    if mode != PROJ_KEYFRAME:   # some feature is matched by two queries
+        hit = m_o[m_o >= 0]
+        assert len(np.unique(hit)) < len(hit) - 50
+
+
 def test_sim3(oracle_mod, orbx_lib, gpu):
     from oracle import matcher as om
     f1, f2, t = synth.feature_pair(60, n1=1000, n2=1000)

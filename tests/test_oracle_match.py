@@ -223,10 +223,11 @@ def area_py(fs, x, y, r, minl, maxl):
     return out
 
 
-def projection_py(mode, T, q, qdesc, claimed, ratio, check_ori, orb_dist=100, inv_sigma2=None):
+def projection_py(mode, T, q, qdesc, claimed, ratio, check_ori, orb_dist=100, inv_sigma2=None,
+                  qflags=None, prefilter=False):
     cl = [bool(c) for c in claimed] if claimed is not None else [False] * T.n
     out = [-1] * len(q)
-    owner = {}
+    qbin = {}
     hist = [[] for _ in range(30)]
     n = 0
     for iq, qq in enumerate(q):
@@ -268,20 +269,20 @@ def projection_py(mode, T, q, qdesc, claimed, ratio, check_ori, orb_dist=100, in
         if bd <= th:
             if mode == PROJ_FRAME_MAPPOINTS and bl == bl2 and f32(bd) > f32(ratio) * f32(bd2):
                 continue
-            if mode != PROJ_FUSE:
+            no_claim = qflags is not None and mode != PROJ_KEYFRAME and qflags[iq] & 1
+            if mode != PROJ_FUSE and not no_claim:
                 cl[bi] = True
             out[iq] = bi
-            owner[bi] = iq
             n += 1
             if check_ori and mode in (PROJ_LAST_FRAME, PROJ_KEYFRAME):
-                hist[rot_bin(qq["angle"], T.keys["angle"][bi])].append(bi)
-    if check_ori and mode in (PROJ_LAST_FRAME, PROJ_KEYFRAME):
+                qbin[iq] = rot_bin(qq["angle"], T.keys["angle"][bi])
+                hist[qbin[iq]].append(bi)
+    if check_ori and not prefilter and mode in (PROJ_LAST_FRAME, PROJ_KEYFRAME):
         t = three_maxima_py([len(h) for h in hist])
-        for b in range(30):
+        for iq, b in qbin.items():
             if b not in t:
-                for j in hist[b]:
-                    out[owner[j]] = -1
-                    n -= 1
+                out[iq] = -1
+                n -= 1
     return n, np.array(out, np.int32)
 
 
@@ -324,6 +325,30 @@ def test_projection_crosscheck(mode):
     n_p, m_p = projection_py(mode, f2, q, d, claimed, 0.8, True, orb_dist=64, inv_sigma2=isg)
     assert n_o == n_p and n_o > 0
     np.testing.assert_array_equal(m_o, m_p)
+
+
+@pytest.mark.parametrize("mode,prefilter", [(PROJ_FRAME_MAPPOINTS, False),
+                                            (PROJ_LAST_FRAME, False), (PROJ_LAST_FRAME, True),
+                                            (PROJ_KEYFRAME, True)])
+def test_projection_ex_crosscheck(mode, prefilter):
+    """orbx_search_by_projection_ex's per-query no-claim flag and the prefilter call flag."""
+    f1, f2, t = synth.feature_pair(31 + mode, n1=150, n2=160, dup_frac=0.15)
+    q, d = synth.projection_queries(9 + mode, f1, f2, t, th=12.0,
+                                    mode_levels="frame" if mode in (0, 2, 3) else "kf")
+    rng = np.random.default_rng(mode + 3)
+    claimed = rng.random(f2.n) < 0.1
+    qflags = (rng.random(len(q)) < 0.4).astype(np.uint8)
+    q, d = np.concatenate([q[:40], q]), np.concatenate([d[:40], d])   # see test_gpu_match
+    qflags = np.concatenate([np.ones(40, np.uint8), qflags])
+    n_o, m_o = om.search_by_projection_ex(mode, f2, q, d, qflags, claimed, orb_dist=64,
+                                          nnratio=0.8, prefilter=prefilter)
+    n_p, m_p = projection_py(mode, f2, q, d, claimed, 0.8, True, orb_dist=64, qflags=qflags,
+                             prefilter=prefilter)
+    assert n_o == n_p and n_o > 0
+    np.testing.assert_array_equal(m_o, m_p)
+    if mode != PROJ_KEYFRAME:
+        hit = m_o[m_o >= 0]
+        assert len(np.unique(hit)) < len(hit)
 
 
 def _distinctive_case(seed, npts=60, maxn=40):

@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU session on the box: the steps named on the command line, in order, each under its own
+# time limit, stopping at the first failure.
+# usage: tools/session.sh TAG step [step ...]
+#   steps: tests (pytest -m gpu), smoke, bench (default headline line), prof (rocprofv3 kernel
+#          stats of a short headline run), dropin (drop-in line), pmc (HBM fetch/write passes),
+#          k=<pytest -k expr> (a subset of the GPU tests)
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+      tail -1 $OUT/pytest_gpu.log ;;
+    k=*)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "${step#k=}" > $OUT/pytest_k.log 2>&1 \
+        || { echo "GPU TESTS (-k) FAILED"; tail -40 $OUT/pytest_k.log; exit 1; }
+      tail -3 $OUT/pytest_k.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+        || { echo "SMOKE FAILED"; tail -20 $OUT/smoke.log; exit 1; }
+      tail -1 $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err \
+        || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
+      python -c "import json,sys; j=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print('bench', j['value'], j['ms_per_step'], json.dumps(j.get('roofline'))[:400])" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/prof.log 2>&1 \
+        || { echo "PROF FAILED"; tail -20 $OUT/prof.log; exit 1; }
+      echo prof done ;;
+    dropin)
+      timeout -k 10 600 python bench.py --workload dropin --frames 300 > $OUT/dropin.json 2> $OUT/dropin.err \
+        || { echo "DROPIN BENCH FAILED"; tail -20 $OUT/dropin.err; exit 1; }
+      echo dropin done ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo session done
