@@ -174,6 +174,47 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
                                    const uint8_t* right, size_t stride_right, int width,
                                    int height, float mbf, float mb, orbx_stereo_frame_out* out);
 
+/* The pyramid after orbx_stereo_frame_view (ORBextractor::mvImagePyramid, ORBextractor.h:85,
+ * filled by every operator() in the reference, ORBextractor.cc:1129-1154).  Calls on several
+ * sessions' handles that meet are served as one batch on the device's frame server, so the
+ * frame's pyramids may live in the server's workspace, not the caller's.  The contract is the
+ * same either way:
+ *   keep_pyramid off (the default): after orbx_stereo_frame_view, orbx_pyramid_level on the
+ *     handle returns ORBX_ERR_STATE, whether the frame ran alone or in a batch;
+ *   keep_pyramid on: orbx_pyramid_level(h, 0, l, ...) returns level l of the left view and
+ *     (h, 1, l, ...) of the right view, whether the frame ran alone or in a batch (a served
+ *     frame's two pyramid blocks are copied device to device into the handle: about 3 MB at
+ *     KITTI size).
+ * Any other extraction on the handle (orbx_extract, the batched calls) leaves the pyramids of
+ * all its images, as before.  orbx_blurred_level needs the frame to have run on the handle
+ * itself (it returns ORBX_ERR_STATE after a served frame). */
+orbx_status orbx_extractor_keep_pyramid(orbx_extractor* h, int on);
+
+/* Counters of the frame server that orbx_stereo_frame_view calls on handles with h's device and
+ * parameters go to.  batches_of_size[m] = batches that held m frames (1 <= m <= 8);
+ * batches_per_pair[i] = batches run in block pair i (the two pairs alternate);
+ * peak_inflight = most batches (plus a lone call) on the device at once; users = live handles
+ * that have called orbx_stereo_frame_view; resident = whether the server holds device / pinned
+ * resources.  reset != 0 zeroes the counters after reading them. */
+typedef struct {
+    int64_t solo_calls;           /* calls that found the server idle and ran on their handle  */
+    int64_t batches;
+    int64_t served_frames;
+    int64_t batches_of_size[9];
+    int64_t batches_per_pair[2];
+    int32_t peak_inflight;
+    int32_t users;
+    int32_t resident;
+} orbx_frame_server_stats;
+orbx_status orbx_frame_server_get_stats(const orbx_extractor* h, orbx_frame_server_stats* out,
+                                        int reset);
+
+/* Frees the frame server's resources (its two server handles with their workspaces, pinned
+ * input / output blocks, device staging, graphs, stream) now; ORBX_ERR_STATE while a batch is
+ * forming or running.  The next orbx_stereo_frame_view recreates them.  The server also
+ * releases itself when the last handle that used it is destroyed. */
+orbx_status orbx_frame_server_release(const orbx_extractor* h);
+
 /* Batched stereo over the last orbx_extract_batch_device calls of both handles (pair i =
  * image i of each).  d_uRight/d_depth: device [batch][kp_cap] floats; d_nvalid: device
  * [batch] (may be NULL). */

@@ -10,7 +10,10 @@
 // One difference: mvImagePyramid is no longer filled by every operator() call.  Its only
 // reader in the reference is Frame::ComputeStereoMatches (Frame.cc:503-619), which the glue in
 // orbx_slam2_glue.h replaces with the device-resident orbx_stereo_match.  Code that still needs
-// the host pyramid calls MaterializePyramid() after operator().
+// the host pyramid calls MaterializePyramid() after operator().  After the one-call stereo Frame
+// (orbx_glue::ExtractStereo) both extractors' MaterializePyramid() return their view's levels
+// when the LEFT extractor has KeepPyramid(true), and throw otherwise, whether the frame ran
+// alone or in a frame-server batch (include/orbx.h orbx_extractor_keep_pyramid).
 #ifndef ORBX_INTEGRATION_ORBEXTRACTOR_H
 #define ORBX_INTEGRATION_ORBEXTRACTOR_H
 
@@ -69,6 +72,8 @@ public:
                                 &dsc, &n),
               "orbx_extract_view");
         pyramid_valid = false;
+        pyr_src = h;
+        pyr_index = 0;
         if (n < 0) {  // empty image inside liborbx as well
             keypoints.clear();
             return;
@@ -96,20 +101,34 @@ public:
     std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
     // Copies the last call's pyramid (ORBextractor.cc:1129-1155's levels, the unblurred
-    // images) into mvImagePyramid; a no-op when it is already current.
+    // images) into mvImagePyramid; a no-op when it is already current.  Throws when the last
+    // call left no pyramid (a stereo Frame without KeepPyramid, see the file comment).
     std::vector<cv::Mat>& MaterializePyramid() {
         if (!pyramid_valid) {
             mvImagePyramid.resize(nlevels);
             for (int l = 0; l < nlevels; ++l) {
                 int w = 0, hh = 0;
-                check(orbx_pyramid_level(h, 0, l, nullptr, &w, &hh), "orbx_pyramid_level");
+                check(orbx_pyramid_level(pyr_src, pyr_index, l, nullptr, &w, &hh),
+                      "orbx_pyramid_level");
                 mvImagePyramid[l].create(hh, w, CV_8U);
-                check(orbx_pyramid_level(h, 0, l, mvImagePyramid[l].data, &w, &hh),
+                check(orbx_pyramid_level(pyr_src, pyr_index, l, mvImagePyramid[l].data, &w, &hh),
                       "orbx_pyramid_level");
             }
             pyramid_valid = true;
         }
         return mvImagePyramid;
+    }
+
+    // orbx_extractor_keep_pyramid on this extractor's handle: a stereo Frame extracted through
+    // it (orbx_glue::ExtractStereo, this being the LEFT extractor) leaves both views' pyramids.
+    void KeepPyramid(bool on) { check(orbx_extractor_keep_pyramid(h, on ? 1 : 0), "orbx_extractor_keep_pyramid"); }
+
+    // Where MaterializePyramid reads from after a call this extractor did not make itself: the
+    // stereo Frame ran on `from`'s handle, this view is image `index` of it (the glue sets it).
+    void SetPyramidSource(const ORBextractor* from, int index) {
+        pyramid_valid = false;
+        pyr_src = from->h;
+        pyr_index = index;
     }
 
     // The liborbx handle, for orbx_stereo_match (orbx_slam2_glue.h).
@@ -137,6 +156,8 @@ protected:
 
 private:
     bool pyramid_valid = false;
+    orbx_extractor* pyr_src = nullptr;   // the handle and image holding this view's pyramid
+    int pyr_index = 0;
 };
 
 }  // namespace ORB_SLAM2

@@ -49,9 +49,22 @@ int ComputeStereoMatches(Frame& F) {
 // the stereo match appended, one submission and one wait (orbx_stereo_frame_view).  Fills
 // mvKeys / mDescriptors, mvKeysRight / mDescriptorsRight, N, mvuRight / mvDepth with the same
 // values as the two-thread form.  The right extractor's handle is not used.
+//
+// An empty image: each ExtractORB returns without touching its outputs (ORBextractor.cc:
+// 1068-1069), so the views go through the extractors' operator() one by one and no stereo
+// match is made (the reference would take the median of an empty vector, Frame.cc:673).
+// mvImagePyramid afterwards: see integration/ORBextractor.h (KeepPyramid on the left one).
 template <class Frame>
 int ExtractStereo(Frame& F, const cv::Mat& imLeft, const cv::Mat& imRight) {
     static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint), "cv::KeyPoint layout");
+    if (imLeft.empty() || imRight.empty()) {
+        (*F.mpORBextractorLeft)(imLeft, cv::Mat(), F.mvKeys, F.mDescriptors);
+        (*F.mpORBextractorRight)(imRight, cv::Mat(), F.mvKeysRight, F.mDescriptorsRight);
+        F.N = (int)F.mvKeys.size();
+        F.mvuRight.assign((size_t)F.N, -1.0f);
+        F.mvDepth.assign((size_t)F.N, -1.0f);
+        return 0;
+    }
     if (imLeft.rows != imRight.rows || imLeft.cols != imRight.cols)
         throw std::invalid_argument("ExtractStereo: left and right sizes differ");
     orbx_stereo_frame_out o{};
@@ -59,6 +72,8 @@ int ExtractStereo(Frame& F, const cv::Mat& imLeft, const cv::Mat& imRight) {
                                  (size_t)imLeft.step, imRight.data, (size_t)imRight.step,
                                  imLeft.cols, imLeft.rows, F.mbf, F.mbf / F.fx, &o),
           "orbx_stereo_frame_view");
+    F.mpORBextractorLeft->SetPyramidSource(F.mpORBextractorLeft, 0);
+    F.mpORBextractorRight->SetPyramidSource(F.mpORBextractorLeft, 1);
     auto keys = [](const orbx_keypoint* k, int n) {
         const cv::KeyPoint* c = reinterpret_cast<const cv::KeyPoint*>(k);
         return std::vector<cv::KeyPoint>(c, c + n);

@@ -61,6 +61,9 @@ SIGNATURES = {
     "orbx_extract_view": (_i, [_vp, _vp, _i, _i, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                ctypes.POINTER(_i)]),
     "orbx_pyramid_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "orbx_extractor_keep_pyramid": (_i, [_vp, _i]),
+    "orbx_frame_server_get_stats": (_i, [_vp, _vp, _i]),
+    "orbx_frame_server_release": (_i, [_vp]),
     "orbx_blur_level": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orbx_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp]),
     "orbx_batch_view_get": (_i, [_vp, ctypes.POINTER(BatchView)]),

@@ -151,6 +151,12 @@ struct orbx_extractor {
     int last_batch = 0;
     bool last_valid = false;
     int last_n = 0;          // keypoints of the last orbx_extract (host image path)
+    // images [0, pyr_images) of d_pyr hold the raw pyramids of the last call (mvImagePyramid,
+    // orbx_pyramid_level).  A stereo frame (orbx_stereo_frame_view) leaves them only when
+    // keep_pyr is set, solo or served alike (orbx_extractor_keep_pyramid)
+    int pyr_images = 0;
+    bool keep_pyr = false;
+    bool fs_user = false;    // counted as a user of its frame server (released with the last)
     std::unique_ptr<OrbxStager> stager;   // created by the first stereo-frame call
     // guards every field above against concurrent calls on one handle (const queries too)
     mutable std::mutex mu;
@@ -954,6 +960,7 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     if (!HIPOK(launch_extract(a, st)) || !mark_done(h, st)) return ORBX_ERR_DEVICE;
     h->last_batch = batch;
     h->last_valid = true;
+    h->pyr_images = h->last_batch;
     h->last_n = -1;   // on the device only (orbx_extract records it once copied back)
     return ORBX_OK;
 }
@@ -1075,6 +1082,7 @@ struct FsReq {
     orbx_extractor* h;            // the caller's handle (its stager)
     int slot = -1, blk = -1;      // its frame in the batch, the block pair of that batch
     orbx_status st = ORBX_OK;
+    bool taken = false;           // its batch has a lead (only an untaken frame may lead)
     bool done = false;
 };
 struct FsLayout {                  // the layout of one server output block
@@ -1114,6 +1122,39 @@ struct FrameServer {
     int readers[2] = {0, 0};       // threads still copying out of each output block
     FsLayout lay[2];
     FsGraph graphs[2][FS_MAX_FRAMES + 1];   // per block pair and batch size
+    int users = 0;                 // live handles that called orbx_stereo_frame_view
+    orbx_frame_server_stats stats{};   // always counted (orbx_frame_server_get_stats)
+    // Frees every device / pinned resource (server handles, graphs, staging, streams); the
+    // object itself (mutex, condition variable) stays, so references held by callers stay
+    // valid.  Only when idle: nothing forming, running or being copied out.
+    bool idle() const { return n == 0 && inflight == 0 && readers[0] == 0 && readers[1] == 0; }
+    void release_resources() {
+        for (int b = 0; b < 2; ++b) {
+            for (FsGraph& G : graphs[b]) {
+                if (G.gx) (void)hipGraphExecDestroy(G.gx);
+                G.gx = nullptr;
+                G.key.clear();
+            }
+            if (sh[b]) (void)orbx_extractor_destroy(sh[b]);
+            sh[b] = nullptr;
+            if (hin[b]) (void)hipHostFree(hin[b]);
+            if (hout[b]) (void)hipHostFree(hout[b]);
+            hin[b] = hout[b] = nullptr;
+            hin_n[b] = hout_n[b] = 0;
+            dstage[b].release();
+            if (cev[b]) (void)hipEventDestroy(cev[b]);
+            cev[b] = nullptr;
+            pair_busy[b] = false;
+            lay[b] = FsLayout{};
+        }
+        if (cst) {
+            (void)hipStreamSynchronize(cst);
+            (void)hipStreamDestroy(cst);
+        }
+        cst = nullptr;
+        blk = n = staged = 0;
+        stats.resident = 0;
+    }
 #ifdef ORBX_TUNING
     // ORBX_FS_STATS=1: batch sizes and where the device time goes, printed at exit
     using clk = std::chrono::steady_clock;
@@ -1137,18 +1178,40 @@ struct FrameServer {
 #endif
 };
 
-static FrameServer& frame_server(const orbx_extractor* h) {
+// One server per (device, extractor parameters).  The registry owns them for the life of the
+// process; their resources are freed when the last handle that used one is destroyed
+// (frame_server_unuse) or on orbx_frame_server_release.
+static std::mutex& fs_registry_mu() {
     static std::mutex mu;
+    return mu;
+}
+static FrameServer& frame_server(const orbx_extractor* h) {
     static std::map<std::vector<int>, std::unique_ptr<FrameServer>> servers;
     const orbx_extractor_params& p = h->prm;
     int sf;
     std::memcpy(&sf, &p.scale_factor, 4);
     const std::vector<int> key = {h->device, p.nfeatures, sf, p.nlevels, p.ini_th_fast,
                                   p.min_th_fast, p.cv_simd};
-    std::lock_guard<std::mutex> lk(mu);
+    std::lock_guard<std::mutex> lk(fs_registry_mu());
     std::unique_ptr<FrameServer>& s = servers[key];
     if (!s) s.reset(new FrameServer());
     return *s;
+}
+
+// A handle that called orbx_stereo_frame_view counts as a user of its server until destroyed.
+static void frame_server_use(orbx_extractor* h, FrameServer& fs) {
+    std::lock_guard<std::mutex> hl(h->mu);
+    if (h->fs_user) return;
+    h->fs_user = true;
+    std::lock_guard<std::mutex> lk(fs.mu);
+    ++fs.users;
+}
+void frame_server_unuse(orbx_extractor* h) {
+    if (!h->fs_user) return;
+    FrameServer& fs = frame_server(h);
+    std::lock_guard<std::mutex> lk(fs.mu);
+    h->fs_user = false;
+    if (--fs.users == 0 && fs.idle()) fs.release_resources();
 }
 
 static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_t st, int width,
@@ -1227,13 +1290,15 @@ static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, 
         return ORBX_ERR_DEVICE;
     S->last_batch = 2 * m;
     S->last_valid = true;
+    S->pyr_images = 2 * m;
     S->last_n = -1;
     fs.lay[blk] = FsLayout{o_kps, o_desc, o_st, KC, m};
     return ORBX_OK;
 }
 
 // The waiting thread's own frame, from the server block into its handle's pinned block.
-static orbx_status copy_served(FrameServer& fs, const FsReq& r, orbx_stereo_frame_out* out) {
+static orbx_status copy_served(FrameServer& fs, const FsReq& r, const FsBatch& g,
+                               orbx_stereo_frame_out* out) {
     const FsLayout& ly = fs.lay[r.blk];
     const uint8_t* ho = fs.hout[r.blk];
     const size_t KC = ly.kc;
@@ -1268,8 +1333,29 @@ static orbx_status copy_served(FrameServer& fs, const FsReq& r, orbx_stereo_fram
     out->depth = (const float*)o;
     out->n[0] = n[0];
     out->n[1] = n[1];
-    // this handle's own workspace does not hold the frame (its pyramid views are stale)
+    // this handle's own workspace does not hold the frame's keypoints ...
     h->last_valid = false;
+    h->pyr_images = 0;
+    if (!h->keep_pyr) return ORBX_OK;
+    // ... but its pyramids when asked for (orbx_extractor_keep_pyramid): both views' blocks,
+    // device to device from the server handle, whose workspace this block pair's next batch
+    // does not touch while this thread holds its reader count
+    const orbx_extractor* S = fs.sh[r.blk];
+    orbx_status s = ensure_workspace(h, g.width, g.height, 2);
+    if (s != ORBX_OK) return s;
+    const size_t pyrb = (size_t)h->hg.pyr_bytes;
+    if (!S || (size_t)S->hg.pyr_bytes != pyrb || S->hg.lv[0].pitch != h->hg.lv[0].pitch)
+        return ORBX_ERR_STATE;
+    const uint8_t* src = S->d_pyr.as<uint8_t>();
+    uint8_t* dst = h->d_pyr.as<uint8_t>();
+    if (!HIPOK(hipSetDevice(h->device)) || !order_after_last(h, h->stream) ||
+        !HIPOK(hipMemcpyAsync(dst, src + img[0] * pyrb, pyrb, hipMemcpyDeviceToDevice, h->stream)) ||
+        !HIPOK(hipMemcpyAsync(dst + pyrb, src + img[1] * pyrb, pyrb, hipMemcpyDeviceToDevice,
+                              h->stream)) ||
+        !mark_done(h, h->stream) || !wait_done(h))
+        return ORBX_ERR_DEVICE;
+    h->last_batch = 2;
+    h->pyr_images = 2;
     return ORBX_OK;
 }
 
@@ -1408,6 +1494,7 @@ orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor
 
 orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (!h) return ORBX_ERR_INVALID;
+    frame_server_unuse(h);
     (void)hipSetDevice(h->device);
     (void)wait_idle(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
@@ -1524,6 +1611,7 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
         return ORBX_ERR_DEVICE;
     h->last_batch = 1;
     h->last_valid = true;
+    h->pyr_images = h->last_batch;
     std::memcpy(&h->last_n, h->h_out, 4);
     *o_kps_out = o_kps;
     *o_desc_out = o_desc;
@@ -1660,6 +1748,7 @@ static orbx_status stereo_frame_solo(orbx_extractor* h, const uint8_t* left, siz
         return ORBX_ERR_DEVICE;
     h->last_batch = 2;
     h->last_valid = true;
+    h->pyr_images = h->keep_pyr ? 2 : 0;   // the stereo-frame pyramid contract (keep_pyr)
     h->last_n = -1;   // not the single-image state orbx_stereo_match expects
     const uint8_t* ho = h->h_out;
     std::memcpy(out->n, ho, 8);
@@ -1683,10 +1772,12 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         return stereo_frame_solo(h, left, stride_left, right, stride_right, width, height, mbf,
                                  mb, out);
     FrameServer& fs = frame_server(h);
+    frame_server_use(h, fs);
     const int inflight_max = tuned("ORBX_FS_INFLIGHT", FS_INFLIGHT);
     std::unique_lock<std::mutex> lk(fs.mu);
     if (fs.inflight == 0 && fs.n == 0) {   // alone on the device: on this handle
         ++fs.inflight;
+        fs.stats.solo_calls++;
 #ifdef ORBX_TUNING
         const auto t0 = FrameServer::clk::now();
         fs.st_idle_us += FrameServer::us(fs.st_free, t0);
@@ -1755,7 +1846,10 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     ++fs.staged;
     fs.cv.notify_all();
     while (!r.done) {
-        if (fs.inflight >= inflight_max || fs.n == 0 || fs.staged < fs.n) {
+        // only a frame of the batch being formed leads it (a frame whose batch already has a
+        // lead waits for it, instead of leading someone else's batch and holding its reader
+        // slot meanwhile)
+        if (r.taken || fs.inflight >= inflight_max || fs.n == 0 || fs.staged < fs.n) {
             fs.cv.wait(lk);
             continue;
         }
@@ -1763,6 +1857,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         const int m = fs.n, blk = fs.blk;
         FsReq* take[FS_MAX_FRAMES];
         std::copy(fs.req, fs.req + m, take);
+        for (int i = 0; i < m; ++i) take[i]->taken = true;
         // every frame's copy is on the stream by now (each was issued before its `staged`)
         const bool recorded = HIPOK(hipEventRecord(fs.cev[blk], fs.cst));
         const FsBatch bg = fs.geo;
@@ -1770,6 +1865,12 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         fs.blk ^= 1;
         ++fs.inflight;
         fs.pair_busy[blk] = true;
+        fs.stats.batches++;
+        fs.stats.served_frames += m;
+        fs.stats.batches_of_size[m]++;
+        fs.stats.batches_per_pair[blk]++;
+        fs.stats.peak_inflight = std::max(fs.stats.peak_inflight, fs.inflight);
+        fs.stats.resident = 1;
         fs.cv.notify_all();
 #ifdef ORBX_TUNING
         const auto t0 = FrameServer::clk::now();
@@ -1800,7 +1901,7 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         fs.cv.notify_all();
     }
     lk.unlock();
-    const orbx_status s = r.st == ORBX_OK ? copy_served(fs, r, out) : r.st;
+    const orbx_status s = r.st == ORBX_OK ? copy_served(fs, r, g, out) : r.st;
     if (r.st == ORBX_OK) {
         lk.lock();
         --fs.readers[r.blk];
@@ -1809,13 +1910,45 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     return s;
 }
 
+orbx_status orbx_extractor_keep_pyramid(orbx_extractor* h, int on) {
+    if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->keep_pyr = on != 0;
+    return ORBX_OK;
+}
+
+orbx_status orbx_frame_server_get_stats(const orbx_extractor* h, orbx_frame_server_stats* out,
+                                        int reset) {
+    if (!h || !out) return ORBX_ERR_INVALID;
+    FrameServer& fs = frame_server(h);
+    std::lock_guard<std::mutex> lk(fs.mu);
+    *out = fs.stats;
+    out->users = fs.users;
+    if (reset) {
+        const int32_t resident = fs.stats.resident;
+        fs.stats = orbx_frame_server_stats{};
+        fs.stats.resident = resident;
+    }
+    return ORBX_OK;
+}
+
+orbx_status orbx_frame_server_release(const orbx_extractor* h) {
+    if (!h) return ORBX_ERR_INVALID;
+    FrameServer& fs = frame_server(h);
+    std::lock_guard<std::mutex> lk(fs.mu);
+    if (!fs.idle()) return ORBX_ERR_STATE;
+    fs.release_resources();
+    return ORBX_OK;
+}
+
 static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, int level,
                               uint8_t* out, int* width, int* height, bool blurred = false) {
     if (!h) return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(h->mu);
-    if (!h->last_valid || level < 0 || level >= h->hg.nlevels || index < 0 ||
-        index >= h->last_batch)
-        return ORBX_ERR_INVALID;
+    if (level < 0 || level >= h->hg.nlevels || index < 0) return ORBX_ERR_INVALID;
+    // the raw pyramid of images [0, pyr_images); the blurred one of a full last call only
+    if (index >= h->pyr_images || (blurred && (!h->last_valid || index >= h->last_batch)))
+        return ORBX_ERR_STATE;
     const LevelGeom& lv = h->hg.lv[level];
     if (width) *width = lv.w;
     if (height) *height = lv.h;

@@ -828,7 +828,10 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjLaunch g) {
         const int nc = mine ? g.ncand[qi] : 0;
         // a query whose MapPoint has no observations leaves its feature unclaimed (:90-92,
         // :1471-1473 test Observations() > 0 of the MapPoint already there)
-        const bool claims = !(mine && g.qflags && (g.qflags[qi] & ORBX_QF_NO_CLAIM));
+        // (only FRAME_MAPPOINTS and LAST_FRAME test Observations(); KEYFRAME / KF_SCW skip any
+        // matched feature, :1609-1610, :406)
+        const bool claims = !(mine && g.qflags && (g.qflags[qi] & ORBX_QF_NO_CLAIM) &&
+                              (g.mode == ORBX_PROJ_FRAME_MAPPOINTS || g.mode == ORBX_PROJ_LAST_FRAME));
         const int nv = min(nc, PROJ_K);
         int2 L[PROJ_K];
         {

@@ -134,6 +134,29 @@ class ORBextractor:
             self._h, index, level, ptr(out), ctypes.byref(w), ctypes.byref(h)))
         return out
 
+    def keep_pyramid(self, on: bool = True):
+        """orbx_extractor_keep_pyramid: after ``extract_stereo`` the handle holds both views'
+        pyramids (image 0 = left, 1 = right) whether the frame ran alone or in a frame-server
+        batch; off (the default) none in either case."""
+        check("orbx_extractor_keep_pyramid", self._L.orbx_extractor_keep_pyramid(self._h, int(on)))
+
+    def frame_server_stats(self, reset: bool = False) -> dict:
+        """Counters of the frame server this handle's ``extract_stereo`` calls go to
+        (orbx_frame_server_get_stats)."""
+        st = FrameServerStats()
+        check("orbx_frame_server_get_stats", self._L.orbx_frame_server_get_stats(
+            self._h, ctypes.byref(st), int(reset)))
+        return {"solo_calls": st.solo_calls, "batches": st.batches,
+                "served_frames": st.served_frames,
+                "batches_of_size": list(st.batches_of_size),
+                "batches_per_pair": list(st.batches_per_pair),
+                "peak_inflight": st.peak_inflight, "users": st.users,
+                "resident": bool(st.resident)}
+
+    def frame_server_release(self):
+        """orbx_frame_server_release: free the frame server's resources now."""
+        check("orbx_frame_server_release", self._L.orbx_frame_server_release(self._h))
+
     # ---- batched device path ----
     def prepare(self, width: int, height: int, batch: int) -> int:
         """Allocate the workspace for `batch` images of width x height; returns kp_cap."""
@@ -234,6 +257,14 @@ def compute_stereo_matches(left: ORBextractor, right: ORBextractor, mbf: float, 
     check("orbx_stereo_match", left._L.orbx_stereo_match(
         left._h, right._h, mbf, mb, ptr(u), ptr(d), n, ctypes.byref(nv)))
     return u[:n], d[:n], nv.value
+
+
+class FrameServerStats(ctypes.Structure):
+    """orbx_frame_server_stats (include/orbx.h)."""
+    _fields_ = [("solo_calls", ctypes.c_int64), ("batches", ctypes.c_int64),
+                ("served_frames", ctypes.c_int64), ("batches_of_size", ctypes.c_int64 * 9),
+                ("batches_per_pair", ctypes.c_int64 * 2), ("peak_inflight", ctypes.c_int32),
+                ("users", ctypes.c_int32), ("resident", ctypes.c_int32)]
 
 
 class StereoFrameOut(ctypes.Structure):

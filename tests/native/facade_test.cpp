@@ -151,6 +151,28 @@ int run(const std::string& dir, bool frame_call) {
     const cv::Mat imL(H, W, CV_8UC1, Lp.data(), pitch), imR(H, W, CV_8UC1, R.data());
     int nvalid = 0;
     if (frame_call) {   // Frame.cc:89-102 as one two-image submission
+        // without KeepPyramid no pyramid is left (a fixed state, solo or served) ...
+        nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+        try {
+            left.MaterializePyramid();
+            std::printf("facade_test: a pyramid after ExtractStereo without KeepPyramid\n");
+            return 4;
+        } catch (const std::runtime_error&) {
+        }
+        // ... with it both views' pyramids (checked below); the outputs are the same
+        left.KeepPyramid(true);
+        nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+        // an empty view: the extractors return silently (ORBextractor.cc:1068-1069)
+        Frame E;
+        E.mpORBextractorLeft = &left;
+        E.mpORBextractorRight = &right;
+        E.mbf = F.mbf;
+        E.fx = F.fx;
+        if (orbx_glue::ExtractStereo(E, cv::Mat(), imR) != 0 || E.N != 0 || !E.mvKeys.empty() ||
+            E.mvKeysRight.empty()) {
+            std::printf("facade_test: ExtractStereo with an empty left image\n");
+            return 4;
+        }
         nvalid = orbx_glue::ExtractStereo(F, imL, imR);
     } else {   // Frame.cc:89-92
         std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
@@ -165,13 +187,14 @@ int run(const std::string& dir, bool frame_call) {
         std::printf("facade_test: bad extraction outputs\n");
         return 4;
     }
-    // mvImagePyramid on request: level 0 is the input image
-    if (!frame_call) {
-        std::vector<cv::Mat>& pyr = left.MaterializePyramid();
+    // mvImagePyramid on request: level 0 is the input image (both views after ExtractStereo)
+    for (int v = 0; v < (frame_call ? 2 : 1); ++v) {
+        std::vector<cv::Mat>& pyr = (v ? right : left).MaterializePyramid();
+        const std::vector<uint8_t>& img = v ? R : L;
         if (pyr.size() != 8 || pyr[0].rows != H || pyr[0].cols != W) return 4;
         for (int y = 0; y < H; ++y)
-            if (std::memcmp(pyr[0].ptr(y), &L[(size_t)y * W], (size_t)W) != 0) {
-                std::printf("facade_test: mvImagePyramid[0] differs from the input\n");
+            if (std::memcmp(pyr[0].ptr(y), &img[(size_t)y * W], (size_t)W) != 0) {
+                std::printf("facade_test: mvImagePyramid[0] of view %d differs from the input\n", v);
                 return 4;
             }
     }

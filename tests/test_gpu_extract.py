@@ -477,6 +477,7 @@ def test_frame_server_mixed_sessions(orbx_lib, gpu):
     ref = [m.extract_stereo(solo, L, R, mbf, mb) for (L, R), (mbf, mb) in jobs]
     n_sessions, rounds = 6, 8
     exts = [m.ORBextractor(*params) for _ in range(n_sessions)]
+    solo.frame_server_stats(reset=True)
     start = threading.Barrier(n_sessions)
     errors = []
 
@@ -502,3 +503,84 @@ def test_frame_server_mixed_sessions(orbx_lib, gpu):
         th.join(timeout=100)
     assert not any(th.is_alive() for th in threads), "a session did not finish"
     assert not errors, errors[:5]
+    # the batched path ran: batches of several frames, in both block pairs
+    st = solo.frame_server_stats()
+    assert st["solo_calls"] + st["served_frames"] == n_sessions * rounds, st
+    assert sum(st["batches_of_size"][2:]) > 0, st
+    assert min(st["batches_per_pair"]) > 0, st
+    assert st["batches"] == sum(st["batches_per_pair"]) == sum(st["batches_of_size"]), st
+    assert st["served_frames"] == sum(k * v for k, v in enumerate(st["batches_of_size"])), st
+    assert st["users"] >= n_sessions + 1 and st["resident"], st
+    assert st["peak_inflight"] >= 1, st
+
+
+def test_stereo_frame_pyramid_contract(oracle_mod, orbx_lib, gpu):
+    """mvImagePyramid after the one-call stereo Frame (include/orbx.h keep_pyramid): six
+    sessions at once, so frames are served both alone and in frame-server batches.  With
+    keep_pyramid every frame leaves both views' levels on its handle, equal to the reference
+    pyramid of ORBextractor.cc:1129-1154 (the oracle's); without it no frame leaves a pyramid
+    (ORBX_ERR_STATE), alone or batched.  Then the server's resources are released: explicitly
+    while idle, and again when the last session's handle is destroyed."""
+    import threading
+    import my_orb_slam2_amd as m
+    from my_orb_slam2_amd._lib import OrbxError
+    params = (1100, 1.2, 8, 20, 7)   # parameters no other test uses: its own frame server
+    size = (752, 480)
+    mbf = KITTI_MBF
+    mb = float(np.float32(mbf) / np.float32(KITTI_FX))
+    pairs = [synth.stereo_pair(90 + i, *size) for i in range(3)]
+    levels = []
+    for L, R in pairs:
+        o = [oracle_mod.OracleExtractor(*params), oracle_mod.OracleExtractor(*params)]
+        o[0](L)
+        o[1](R)
+        levels.append([[o[v].level(l) for l in range(8)] for v in range(2)])
+    n_sessions, rounds = 6, 6
+    exts = [m.ORBextractor(*params) for _ in range(n_sessions)]
+    for t, e in enumerate(exts):
+        e.keep_pyramid(t % 2 == 0)   # even sessions keep their pyramids, odd ones do not
+    exts[0].frame_server_stats(reset=True)
+    start = threading.Barrier(n_sessions)
+    errors = []
+
+    def session(t):
+        try:
+            start.wait()
+            for k in range(rounds):
+                j = (t + k) % len(pairs)
+                m.extract_stereo(exts[t], *pairs[j], mbf, mb)
+                if t % 2:
+                    try:
+                        exts[t].pyramid_level(0, 0)
+                        errors.append(f"session {t} frame {j}: a pyramid without keep_pyramid")
+                    except OrbxError:
+                        pass
+                    continue
+                for v in range(2):
+                    for l in range(8):
+                        if not np.array_equal(exts[t].pyramid_level(l, v), levels[j][v][l]):
+                            errors.append(f"session {t} frame {j} view {v} level {l}")
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(f"session {t}: {e!r}")
+
+    threads = [threading.Thread(target=session, args=(t,)) for t in range(n_sessions)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a session did not finish"
+    assert not errors, errors[:5]
+    st = exts[0].frame_server_stats()
+    assert st["served_frames"] > 0 and st["solo_calls"] + st["served_frames"] == n_sessions * rounds, st
+    assert st["resident"] and st["users"] == n_sessions, st
+    # explicit release while idle, then a frame recreates the resources
+    exts[1].frame_server_release()
+    assert not exts[0].frame_server_stats()["resident"]
+    m.extract_stereo(exts[2], *pairs[0], mbf, mb)
+    assert np.array_equal(exts[2].pyramid_level(3, 1), levels[0][1][3])
+    # destroying every session's handle releases the server (the last user goes)
+    probe = m.ORBextractor(*params)   # same device and parameters, never a user
+    for e in exts:
+        e.close()
+    st = probe.frame_server_stats()
+    assert st["users"] == 0 and not st["resident"], st
