@@ -704,7 +704,40 @@ def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv
         se = roof["per_kernel"][dom]
         roof["serial_pass"] = {"avg_launch_ms": se["avg_launch_ms"], "achieved": se["achieved"],
                                "frac": se["frac"], "launches_per_step": se["launches_per_step"]}
+    # the kernel group that takes the most time per step in the timed (scheduled) region, the
+    # one a rocprofv3 summary of this command ranks first
+    tdom = max((k for k in gt if k in HEADLINE_GROUPS), key=lambda k: gt[k][0], default=None)
+    if tdom:
+        tot = sum(v[0] for v in gt.values())
+        roof["timed_dominant"] = {"kernel": tdom, "ms_per_step": round(gt[tdom][0] / max(steps, 1), 4),
+                                  "share_of_kernel_time": round(gt[tdom][0] / tot, 4) if tot else None,
+                                  "hbm_frac": roofline_entry(tdom, *gt[tdom], steps, geo.get(tdom),
+                                                             traffic_per_step(traffic_csv, tdom))["frac"]}
+    for e in [roof] + list(roof["per_kernel"].values()):
+        label_binding_roof(e)
     return roof
+
+
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 1e12   # T SIMD issue cycles/s (1024 SIMDs at 2.4 GHz)
+
+
+def label_binding_roof(e):
+    """Name the roof the counters show for a roofline entry.  The integer kernels are bound by
+    VALU issue, not HBM: when the PMC pass shows the SIMDs issuing VALU work most of the launch
+    (the mix-aware busy fraction >= 0.7, or rocprof's 4-cycle VALUBusy >= 0.9) and that exceeds
+    the HBM fraction, `bound` is "valu" and achieved / peak / frac are VALU issue cycles per
+    second against 1024 SIMDs x 2.4 GHz; the HBM figures move to `hbm`.  `traffic` stays the
+    PMC HBM bytes per launch either way."""
+    v = e.get("valu") or {}
+    busy, b4 = v.get("busy_frac"), v.get("valubusy_4cycle")
+    hbm = {"achieved": e.get("achieved"), "peak": e.get("peak"), "unit": e.get("unit"),
+           "frac": e.get("frac")}
+    if busy is None or not ((b4 or 0) >= 0.9 or busy >= 0.7) or busy <= (e.get("frac") or 0):
+        e["hbm"] = hbm
+        return
+    ach = v["wave_instr_per_launch"] * v["mean_issue_cycles"] / (e["avg_launch_ms"] / 1000.0) / 1e12
+    e.update({"bound": "valu", "achieved": ach, "peak": VALU_ISSUE_PEAK,
+              "unit": "T VALU issue cycles/s", "frac": ach / VALU_ISSUE_PEAK, "hbm": hbm})
 
 
 def counted_bytes(requested, traffic):

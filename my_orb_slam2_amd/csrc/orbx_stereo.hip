@@ -465,13 +465,16 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     if (nsplit > 1) {
 #if ST_FUSED_CUT == 2
         // the pair's last workgroup to finish takes the median: every wave's write-through
-        // stores complete, the workgroup's arrival counted by one agent-scope add; the last
-        // one to arrive reads the pair's SADs by write-through loads into LDS (no fence: its
-        // own later stores to uRight / depth cannot be overtaken by older dirty lines, the
-        // others' stores never sat in an L2)
+        // stores complete, then the workgroup's arrival is one agent-scope acq_rel add (its
+        // release orders this workgroup's stores, ordered before it by the barrier, ahead of
+        // the arrival; its acquire makes every earlier arrival's stores visible to the last
+        // workgroup, whose barrier passes that on to its other waves); the last one reads the
+        // pair's SADs by write-through loads into LDS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) tmp[17] = atomicAdd(&scnt[256 + b], 1) == nsplit - 1;
+        if (tid == 0)
+            tmp[17] = __hip_atomic_fetch_add(&scnt[256 + b], 1, __ATOMIC_ACQ_REL,
+                                             __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
         __syncthreads();
         if (!tmp[17]) return;
         const int nv = min(__hip_atomic_load(&scnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), KC);

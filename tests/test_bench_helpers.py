@@ -35,10 +35,32 @@ def test_headline_traffic_matches_committed_pmc():
     t = b.traffic_per_step(b.DEFAULT_PMC, roof["kernel"])
     assert t is not None and t > 0
     assert t / roof["launches_per_step"] == pytest.approx(roof["traffic"], rel=1e-9)
-    # the algorithmic bytes and the achieved rate are consistent with the launch time
-    assert roof["achieved"] == pytest.approx(
+    # the algorithmic bytes and the achieved rate are consistent with the launch time (the HBM
+    # figures sit in `hbm` when the counters name VALU issue as the binding roof)
+    hbm = roof["hbm"] if roof.get("bound") == "valu" else roof
+    assert hbm["achieved"] == pytest.approx(
         roof["algorithmic_bytes_per_launch"] / (roof["avg_launch_ms"] / 1000.0) / 1e9, rel=1e-9)
     assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-9)
+
+
+def test_binding_roof_label():
+    """`bound` names the roof the counters show.  A launch whose SIMDs issue VALU
+    work most of the time is labelled "valu" (its fraction = the mix-aware busy fraction, the
+    HBM figures kept beside it); one that does not stays "hbm"."""
+    b = _bench()
+    e = b.roofline_entry("k_fast", 10.0, 10, 10, 7.0e8, None)
+    # 0.75 of 1024 SIMDs x 1 ms x 2.4 GHz at 3 cycles per instruction
+    e["valu"] = {"busy_frac": 0.75, "valubusy_4cycle": 1.01, "wave_instr_per_launch": 6.144e8,
+                 "mean_issue_cycles": 3.0}
+    hbm_frac = e["frac"]
+    b.label_binding_roof(e)
+    assert e["bound"] == "valu" and e["frac"] == pytest.approx(0.75) and e["hbm"]["frac"] == hbm_frac
+    assert e["frac"] == pytest.approx(e["achieved"] / e["peak"], rel=1e-9)
+    e = b.roofline_entry("k_level1_7", 10.0, 70, 10, 3.4e9, None)
+    e["valu"] = {"busy_frac": 0.60, "valubusy_4cycle": 0.64, "wave_instr_per_launch": 7e7,
+                 "mean_issue_cycles": 3.66}
+    b.label_binding_roof(e)
+    assert e["bound"] == "hbm" and e["hbm"]["frac"] == e["frac"]
 
 
 def test_roofline_entries_per_launch():
