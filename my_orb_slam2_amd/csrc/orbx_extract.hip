@@ -175,6 +175,12 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef OCTREE_PACKED
 #define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
 #endif
+#ifndef OCT_GATHER2
+#define OCT_GATHER2 1       // candidate gather: two cells per thread, one scan per 2 NT cells
+#endif
+#ifndef OCT_BUCKET_SORT
+#define OCT_BUCKET_SORT 1   // phase-2 order by size buckets, then ranks inside a bucket
+#endif
 #ifndef OD_WPE
 #define OD_WPE 5       // at most 96 VGPRs: five waves per SIMD (6: spills)
 #endif
@@ -762,7 +768,8 @@ struct OctreeSmem {
     int32_t* pre;     // [NCAP] scratch prefix (children before)
     int32_t* pre2;    // [NCAP] scratch prefix (survivors before)
     uint64_t* sortb;  // [NCAP_POW2]
-    int* tmp;         // [16] scan scratch + scalars
+    int* tmp;         // [224] scan scratch + scalars, then the phase-2 bucket arrays
+    int ncap;
 };
 
 __device__ __forceinline__ void split_lines(int x0, int y0, int x1, int y1, int& sx, int& sy) {
@@ -864,18 +871,38 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
             sm.cc[i * 4 + 2] = 0; sm.cc[i * 4 + 3] = 0;
             sm.pord[i] = -1;
+            // a multi-key node's split lines, once per node (cpos is free until the node pass)
+            if (cur.cnt[i] > 1) {
+                int sx, sy;
+                split_lines(cur.x0[i], cur.y0[i], cur.x1[i], cur.y1[i], sx, sy);
+                sm.cpos[i * 4] = (int16_t)sx;
+                sm.cpos[i * 4 + 1] = (int16_t)sy;
+            }
         }
         __syncthreads();
-        for (int k = tid; k < ncand; k += NT) {
-            const int n = knode[k];
-            if (cur.cnt[n] > 1) {
-                int sx, sy;
-                split_lines(cur.x0[n], cur.y0[n], cur.x1[n], cur.y1[n], sx, sy);
-                const uint32_t kd = kdata[k];
-                const int x = cand_x(kd), y = cand_y(kd);
-                const int q = (x < sx) ? (y < sy ? 0 : 2) : (y < sy ? 1 : 3);
-                kq[k] = (uint8_t)q;
-                atomicAdd(&sm.cc[n * 4 + q], 1);
+        // four candidates per thread per trip: their dependent LDS reads (node, then its size
+        // and split lines) overlap instead of running one chain after another
+        for (int k0 = tid; k0 < ncand; k0 += 4 * NT) {
+            int n[4], c[4];
+            uint32_t kd[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = min(k0 + u * NT, ncand - 1);
+                n[u] = knode[k];
+                kd[u] = kdata[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = cur.cnt[n[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * NT;
+                if (k < ncand && c[u] > 1) {
+                    const int sx = sm.cpos[n[u] * 4], sy = sm.cpos[n[u] * 4 + 1];
+                    const int x = cand_x(kd[u]), y = cand_y(kd[u]);
+                    const int q = (x < sx) ? (y < sy ? 0 : 2) : (y < sy ? 1 : 3);
+                    kq[k] = (uint8_t)q;
+                    atomicAdd(&sm.cc[n[u] * 4 + q], 1);
+                }
             }
         }
         __syncthreads();
@@ -963,6 +990,41 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                                        ((uint64_t)(uint32_t)cur.seq[i] << 16) | (uint64_t)i;
                 });
             __syncthreads();
+#if OCT_BUCKET_SORT
+            if (nV <= sm.ncap) {
+                // bucket-then-rank sort, descending: keys go to buckets by size (min(cnt, 63),
+                // larger sizes first), and a key's place inside its bucket is the number of
+                // larger keys there (keys are unique: they end in the node index).  The
+                // comparisons run over one bucket (the nodes of one size) instead of all nV.
+                int* hist = tmp + 32;     // [64] keys per bucket
+                int* start = tmp + 96;    // [64] first position of each bucket
+                int* fill = tmp + 160;    // [64] fill cursor
+                uint64_t* stage = (uint64_t*)sm.cpos;   // free until the node pass below
+                auto bucket = [](uint64_t k) { return min((int)(k >> 40), 63); };
+                for (int i = tid; i < 64; i += NT) { hist[i] = 0; fill[i] = 0; }
+                __syncthreads();
+                for (int j = tid; j < nV; j += NT) atomicAdd(&hist[bucket(sm.sortb[j])], 1);
+                __syncthreads();
+                if (tid < 64) {   // one wave: exclusive scan from bucket 63 down
+                    const int v = hist[63 - tid];
+                    start[63 - tid] = wave_incl_scan(v) - v;
+                }
+                __syncthreads();
+                for (int j = tid; j < nV; j += NT) {
+                    const uint64_t k = sm.sortb[j];
+                    const int bk = bucket(k);
+                    stage[start[bk] + atomicAdd(&fill[bk], 1)] = k;
+                }
+                __syncthreads();
+                for (int q = tid; q < nV; q += NT) {
+                    const uint64_t k = stage[q];
+                    const int bk = bucket(k), s0 = start[bk], s1 = s0 + hist[bk];
+                    int rank = 0;
+                    for (int t = s0; t < s1; ++t) rank += stage[t] > k ? 1 : 0;
+                    sm.sortb[s0 + rank] = k;
+                }
+            } else
+#endif
             if (nV <= 4 * NT) {
                 // rank sort, descending: a key's position is the number of larger keys (keys
                 // are unique: they end in the node index); two barriers instead of bitonic's
@@ -1003,16 +1065,24 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     }
                 }
             }
-            // running size after processing j (descending order); stop once >= N
+            // running size after processing j (descending order); stop once >= N.  The running
+            // size only grows, so J is the first j past N: one atomic per wave (its first lane
+            // past N), and no chunk after the one that holds J
             if (tid == 0) tmp[24] = nV - 1;   // past the scan's NT / 64 partials
             __syncthreads();
-            chunked_scan<NT>(
-                nV, tmp,
-                [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1; },
-                [&](int j, int ex) {
-                    const int delta = nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1;
-                    if (S + ex + delta >= N) atomicMin(&tmp[24], j);
-                });
+            {
+                int carry = 0;
+                for (int c0 = 0; c0 < nV; c0 += NT) {
+                    const int j = c0 + tid;
+                    const int delta = j < nV ? nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1 : 0;
+                    int tot;
+                    const int ex = block_excl_scan<NT / 64>(delta, tmp, tot);
+                    const uint64_t past = __ballot(j < nV && S + carry + ex + delta >= N);
+                    if (past && (threadIdx.x & 63) == (int)__builtin_ctzll(past)) atomicMin(&tmp[24], j);
+                    carry += tot;
+                    if (S + carry >= N) break;   // block-uniform
+                }
+            }
             __syncthreads();
             const int J = tmp[24];
             __syncthreads();
@@ -1061,9 +1131,22 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             }
         }
         __syncthreads();
-        for (int k = tid; k < ncand; k += NT) {
-            const int n = knode[k];
-            knode[k] = sm.pord[n] >= 0 ? sm.cpos[n * 4 + kq[k]] : sm.npos[n];
+        for (int k0 = tid; k0 < ncand; k0 += 4 * NT) {   // four chains per trip, as above
+            int n[4], q[4], o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = min(k0 + u * NT, ncand - 1);
+                n[u] = knode[k];
+                q[u] = kq[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u] = sm.pord[n[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * NT;
+                const int t = o[u] >= 0 ? sm.cpos[n[u] * 4 + q[u]] : sm.npos[n[u]];
+                if (k < ncand) knode[k] = (int16_t)t;
+            }
         }
         __syncthreads();
         NodeArrays t2 = cur; cur = nxt; nxt = t2;
@@ -1114,7 +1197,8 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     OctreeSmem sm;
     int NP2 = 1;
     while (NP2 < NCAP) NP2 <<= 1;
-    sm.tmp = (int*)take(32 * sizeof(int));
+    sm.tmp = (int*)take(224 * sizeof(int));
+    sm.ncap = NCAP;
     sm.sortb = (uint64_t*)take((size_t)NP2 * 8);
     sm.A.x0 = (int16_t*)take(NCAP * 2); sm.A.y0 = (int16_t*)take(NCAP * 2);
     sm.A.x1 = (int16_t*)take(NCAP * 2); sm.A.y1 = (int16_t*)take(NCAP * 2);
@@ -1152,6 +1236,38 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     // gather candidates in cell order (cell-major, raster inside a cell)
     const uint32_t* cbase = cand + (size_t)b * g->cand_words;
     const CellDesc* lc = cells + L.cell_begin;
+#if OCT_GATHER2
+    // two adjacent cells per thread, their offsets from one scan of the pairs' sums, and the
+    // first 8 candidates of both cells loaded at once (addresses clamped into each cell's
+    // slot, so no load is guarded): a level of up to 2 NT cells costs one memory round trip
+    // for cells of up to 8 candidates
+    {
+        int carry = 0;
+        for (int c0 = 0; c0 < L.ncells; c0 += 2 * NT) {
+            const int ca = c0 + 2 * tid, cb = ca + 1;
+            const int na = ca < L.ncells ? cc[ca] : 0, nb = cb < L.ncells ? cc[cb] : 0;
+            int tot;
+            const int exa = carry + block_excl_scan<NT / 64>(na + nb, sm.tmp, tot);
+            const int exb = exa + na;
+            carry += tot;
+            const uint32_t* sa = cbase + (na > 0 ? lc[ca].slot : 0);
+            const uint32_t* sb = cbase + (nb > 0 ? lc[cb].slot : 0);
+            for (int e0 = 0; e0 < max(na, nb); e0 += 8) {
+                uint32_t va[8], vb[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    va[j] = sa[max(min(e0 + j, na - 1), 0)];
+                    vb[j] = sb[max(min(e0 + j, nb - 1), 0)];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (e0 + j < na) kdata[exa + e0 + j] = va[j];
+                    if (e0 + j < nb) kdata[exb + e0 + j] = vb[j];
+                }
+            }
+        }
+    }
+#else
     chunked_scan<NT>(
         L.ncells, sm.tmp, [&](int c) { return cc[c]; },
         [&](int c, int ex) {
@@ -1168,6 +1284,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                     if (e0 + j < n) kdata[ex + e0 + j] = v[j];
             }
         });
+#endif
     __syncthreads();
     if (in_lds)
         octree_level<NT, true>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
@@ -1646,7 +1763,7 @@ size_t octree_lds_bytes(int ncap, int kcap) {
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
     int np2 = 1;
     while (np2 < ncap) np2 <<= 1;
-    size_t s = r(32 * 4) + r((size_t)np2 * 8);
+    size_t s = r(224 * 4) + r((size_t)np2 * 8);
     s += 2 * (4 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4));
     s += r((size_t)ncap * 16) + r((size_t)ncap * 8) + 2 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4);
     s += r((size_t)kcap * 4) + r((size_t)kcap * 2) + r((size_t)kcap);

@@ -11,12 +11,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from my_orb_slam2_amd import build as b  # noqa: E402
 
-DIAG = os.path.join(ROOT, "tools", "_diag", "liborbx_octdiag.so")
+IMG = int(os.environ.get("OCT_STAMP_IMG", "5"))   # blockIdx.y whose lists are stamped
+DIAG = os.path.join(ROOT, "tools", "_diag", f"liborbx_octdiag{IMG}.so")
 os.makedirs(os.path.dirname(DIAG), exist_ok=True)
 srcs = [str(b.CSRC / s) for s in b.SOURCES if (b.CSRC / s).exists()]
 newest = max(os.path.getmtime(str(b.CSRC / f)) for f in os.listdir(b.CSRC))
 if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < newest:
-    subprocess.run([b.hipcc()] + b.FLAGS + ["-DORBX_OCT_STAMPS=5"] + srcs + ["-o", DIAG], check=True)
+    subprocess.run([b.hipcc()] + b.FLAGS + [f"-DORBX_OCT_STAMPS={IMG}"] + srcs + ["-o", DIAG], check=True)
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     sys.exit(0)
 import torch  # noqa: E402
