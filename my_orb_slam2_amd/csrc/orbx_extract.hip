@@ -78,6 +78,47 @@ __device__ __forceinline__ int fast_arc_score(const uint8_t* roi, int cols, int 
     return max(best_dark, -best_min_max);
 }
 
+// The same score with both polarities in the halves of one packed-f16 register, so every
+// run min / max is one v_pk_minimum3 / v_pk_maximum3 for dark and bright together (40 of
+// them instead of 80).  A circle pixel n enters as the f16 whose bits are n (a subnormal:
+// f16 order = integer order, and the f16 modes keep subnormals), the low half negated:
+// y = (-n, n).  Then low = max_arcs min_9 (-n) = -(min_arcs max_9 n) and high =
+// max_arcs min_9 n, read back as the low 10 bits of each half (n <= 255, no rounding
+// anywhere: min / max only select).  dark = v - min max n, bright = max min n - v.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f16x2 arc_y(const uint8_t* p) {
+    const _Float16 f = __builtin_bit_cast(_Float16, (unsigned short)*p);
+    return f16x2{-f, f};   // folded into neg_lo / op_sel_hi source modifiers
+}
+__device__ __forceinline__ int fast_arc_score_pk(const uint8_t* roi, int cols, int r, int c) {
+    const uint8_t* p = roi + r * cols + c;
+    const int v = p[0];
+    f16x2 y[16];
+    y[0] = arc_y(p + 3 * cols);       y[1] = arc_y(p + 3 * cols + 1);
+    y[2] = arc_y(p + 2 * cols + 2);   y[3] = arc_y(p + cols + 3);
+    y[4] = arc_y(p + 3);              y[5] = arc_y(p - cols + 3);
+    y[6] = arc_y(p - 2 * cols + 2);   y[7] = arc_y(p - 3 * cols + 1);
+    y[8] = arc_y(p - 3 * cols);       y[9] = arc_y(p - 3 * cols - 1);
+    y[10] = arc_y(p - 2 * cols - 2);  y[11] = arc_y(p - cols - 3);
+    y[12] = arc_y(p - 3);             y[13] = arc_y(p + cols - 3);
+    y[14] = arc_y(p + 2 * cols - 2);  y[15] = arc_y(p + 3 * cols - 1);
+#define PMN3(a, b, c) __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c)
+#define PMX3(a, b, c) __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c)
+    f16x2 m3[16], m9[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m3[i] = PMN3(y[i], y[(i + 1) & 15], y[(i + 2) & 15]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m9[i] = PMN3(m3[i], m3[(i + 3) & 15], m3[(i + 6) & 15]);
+    f16x2 b = PMX3(m9[0], m9[1], m9[2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) b = PMX3(b, m9[i], m9[i + 1]);
+    b = __builtin_elementwise_maximum(b, m9[15]);
+#undef PMN3
+#undef PMX3
+    const uint32_t bits = __builtin_bit_cast(uint32_t, b);
+    return max(v - (int)(bits & 0x3FFu), (int)((bits >> 16) & 0x3FFu) - v);
+}
+
 // Exact necessary condition for M > t: the 9 circle indices of any arc include 4 or 5
 // consecutive even indices, so a corner at t has 4 cyclically consecutive even-index pixels
 // (0, 2, .., 14) all darker than v - t or all brighter than v + t.  8 reads instead of 16.
@@ -157,6 +198,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #endif
 #ifndef FAST_2PASS
 #define FAST_2PASS 1   // detect at iniThFAST first, minThFAST only for cells without a keypoint
+#endif
+#ifndef FAST_ARC_PK
+#define FAST_ARC_PK 1   // arc score with both polarities in one packed-f16 register
 #endif
 #ifndef FAST_PRE8
 #define FAST_PRE8 0    // even-point segment test before the arc score (measured slower: off)
@@ -666,7 +710,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 if (j < nlist) {
                     pe = list[lb + j];
                     const int rr = pe >> 6, cc = pe & 63;
+#if FAST_ARC_PK
+                    m = fast_arc_score_pk(roi, rp, rr + 3, cc + 3);
+#else
                     m = fast_arc_score(roi, rp, rr + 3, cc + 3);
+#endif
                     mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
                 }
                 const bool corner = j < nlist && m > tq;
