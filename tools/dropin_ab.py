@@ -20,6 +20,7 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "default": {},
     "frame": {"_args": "frame"},
     "frame_solo": {"_args": "frame", "ORBX_FRAME_SERVER": "0"},
+    "frame_nochain": {"_args": "frame", "ORBX_CHAIN_MAX_BATCH": "0"},
     "frame_nostage": {"_args": "frame", "ORBX_STAGE_THREAD": "0"},
     "frame_stage2": {"_args": "frame", "ORBX_STAGE_THREAD": "2"},
     "frame_nograph": {"_args": "frame", "ORBX_EXTRACT_GRAPH": "0"},

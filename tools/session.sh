@@ -4,7 +4,11 @@
 # usage: tools/session.sh TAG step [step ...]
 #   steps: tests (pytest -m gpu), smoke, bench (default headline line), prof (rocprofv3 kernel
 #          stats of a short headline run), dropin (drop-in line), pmc (HBM fetch/write passes),
-#          k=<pytest -k expr> (a subset of the GPU tests)
+#          k=<pytest -k expr> (a subset of the GPU tests), counters (kernel trace + PMC passes,
+#          tools/prof_counters.sh), workloads (the side-row benches: euroc, reloc, tri, bf, kfdb,
+#          tum, host-io), dropin_ab (the one-call Frame with / without the pyramid chain),
+#          frame_trace (kernel + API trace of the one-call Frame, K = 1 and 8)
+# Copy what is kept into profiles/ with tools/collect_profiles.sh.
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -36,6 +40,25 @@ for step in "$@"; do
       timeout -k 10 600 python bench.py --workload dropin --frames 300 > $OUT/dropin.json 2> $OUT/dropin.err \
         || { echo "DROPIN BENCH FAILED"; tail -20 $OUT/dropin.err; exit 1; }
       echo dropin done ;;
+    counters)
+      timeout -k 10 1200 bash tools/prof_counters.sh $OUT/prof --steps 10 --warmup 3 > $OUT/counters.log 2>&1 \
+        || { echo "COUNTERS FAILED"; tail -20 $OUT/counters.log; exit 1; }
+      echo counters done ;;
+    workloads)
+      for w in euroc reloc triangulation bf kfdb tum; do
+        timeout -k 10 300 python bench.py --workload $w --cpu-seconds 5 > $OUT/$w.json 2> $OUT/$w.err \
+          || { echo "WORKLOAD $w FAILED"; tail -20 $OUT/$w.err; exit 1; }
+      done
+      timeout -k 10 300 python bench.py --host-io --cpu-seconds 0 > $OUT/hostio.json 2> $OUT/hostio.err \
+        || { echo "HOST-IO FAILED"; tail -20 $OUT/hostio.err; exit 1; }
+      echo workloads done ;;
+    dropin_ab)
+      python tools/dropin_data.py /tmp/dd 32 > /dev/null || exit 1
+      ORBX_AB_SETTINGS=frame,frame_nochain timeout -k 10 400 python tools/dropin_ab.py run /tmp/dd 1,8 > $OUT/dropin_ab.txt 2>&1 \
+        || { echo "DROPIN AB FAILED"; tail -5 $OUT/dropin_ab.txt; exit 1; }
+      cat $OUT/dropin_ab.txt ;;
+    frame_trace)
+      bash tools/frame_trace.sh ${OUT#gpurun_out/}/tr || exit 1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
