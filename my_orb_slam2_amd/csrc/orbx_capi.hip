@@ -313,6 +313,9 @@ static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
 // with 16 instead of 4, r4aa)
 #define OCT_SMALL_BATCH 16
 #endif
+#ifndef CHAIN_MAX_BATCH
+#define CHAIN_MAX_BATCH 16     // images per call up to which the pyramid is one k_pyr_chain launch
+#endif
 #ifndef SIDE_MIN_BATCH
 #define SIDE_MIN_BATCH 16      // images per call from which the default side branch forks
 #endif
@@ -459,6 +462,105 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
 }
 
 // Per-size geometry.  Returns ORBX_OK or ORBX_ERR_UNSUPPORTED.
+// k_pyr_chain tiles (orbx_pyramid.hip): per tile of a gx x gy grid and per level, the owned
+// rectangle and the footprint, built from the deepest level up: a level's footprint is its
+// owned rectangle + the blur halo, joined with the source rows / columns the next level's
+// footprint reads through the resize tables (xofs / yofs of level l + 1, as cv::resize's
+// HResizeLinear / VResizeLinear index them).  chain_ok stays 0 (per-level launches) unless
+// every level l >= 1 is INTER_LINEAR and the two level buffers + row sums fit the LDS.
+static void build_chain(orbx_extractor* h) {
+    Geometry& G = h->hg;
+    const int L = G.nlevels;
+    G.chain_ok = 0;
+    G.chain_gx = G.chain_gy = 1;
+    G.chain_tab = G.chain_toffs = 0;
+    G.chain_buf = G.chain_rs = G.chain_lds = 0;
+    for (int l = 1; l < L; ++l)
+        if (G.lv[l].copy || G.lv[l].area2) return;
+    const int gx = std::max(1, (G.lv[0].w + CHAIN_TW - 1) / CHAIN_TW);
+    const int gy = std::max(1, (G.lv[0].h + CHAIN_TH - 1) / CHAIN_TH);
+    std::vector<ChainRect> rects((size_t)gx * gy * L);
+    std::vector<int32_t> toffs((size_t)gx * gy * (L + 1), 0);   // k_pyr_chain table offsets
+    size_t buf = 16, rs = 16, ct = 16;
+    for (int ty = 0; ty < gy; ++ty)
+        for (int tx = 0; tx < gx; ++tx) {
+            size_t tab = 0;   // table entries of the tile's levels 1.. (k_pyr_chain phase 1)
+            bool have_next = false;
+            int nx0 = 0, nx1 = -1, ny0 = 0, ny1 = -1;   // footprint of level l + 1
+            for (int l = L - 1; l >= 0; --l) {
+                const LevelGeom& lv = G.lv[l];
+                const int W = lv.w, Hh = lv.h;
+                const int ox0 = tx == 0 ? 0 : ((int)((long long)tx * W / gx) & ~3);
+                const int ox1 = std::max(ox0, tx == gx - 1 ? W : ((int)((long long)(tx + 1) * W / gx) & ~3));
+                const int oy0 = (int)((long long)ty * Hh / gy);
+                const int oy1 = std::max(oy0, ty == gy - 1 ? Hh : (int)((long long)(ty + 1) * Hh / gy));
+                int fx0 = INT_MAX, fx1 = -1, fy0 = INT_MAX, fy1 = -1;
+                if (ox1 > ox0 && oy1 > oy0) {
+                    fx0 = std::max(ox0 - 3, 0);
+                    fx1 = std::min(ox1 + 2, W - 1);
+                    fy0 = std::max(oy0 - 3, 0);
+                    fy1 = std::min(oy1 + 2, Hh - 1);
+                }
+                if (have_next) {
+                    const LevelGeom& D = G.lv[l + 1];
+                    const int16_t* xofs = h->rtab.data() + D.rtab_off;
+                    const int16_t* yofs = xofs + 3 * D.w;
+                    fx0 = std::min(fx0, std::min(std::max((int)xofs[nx0], 0), W - 1));
+                    fx1 = std::max(fx1, std::min((int)xofs[nx1] + 1, W - 1));
+                    fy0 = std::min(fy0, std::min(std::max((int)yofs[ny0], 0), Hh - 1));
+                    fy1 = std::max(fy1, std::min(std::max((int)yofs[ny1] + 1, 0), Hh - 1));
+                }
+                ChainRect& c = rects[((size_t)ty * gx + tx) * L + l];
+                c.ox0 = (int16_t)ox0;
+                c.ox1 = (int16_t)ox1;
+                c.oy0 = (int16_t)oy0;
+                c.oy1 = (int16_t)oy1;
+                if (fx1 < 0) {
+                    c.fx0 = c.fy0 = 0;
+                    c.fx1 = c.fy1 = -1;
+                    have_next = false;
+                    continue;
+                }
+                fx0 &= ~3;
+                c.fx0 = (int16_t)fx0;
+                c.fx1 = (int16_t)fx1;
+                c.fy0 = (int16_t)fy0;
+                c.fy1 = (int16_t)fy1;
+                have_next = true;
+                nx0 = fx0;
+                nx1 = fx1;
+                ny0 = fy0;
+                ny1 = fy1;
+                const int fw = fx1 - fx0 + 1;
+                buf = std::max(buf, (size_t)chain_pitch(fw) * (fy1 - fy0 + 1) + 16);
+                rs = std::max(rs, (size_t)4 * ((ox1 - ox0 + 3) & ~3) * (oy1 - oy0 + 6));
+                if (l > 0) tab += (size_t)((fw + 3) & ~3) + ((fy1 - fy0 + 2) & ~1);
+            }
+            ct = std::max(ct, 8 * tab);
+            int32_t* to = &toffs[((size_t)ty * gx + tx) * (L + 1)];
+            for (int l = 1; l < L; ++l) {
+                const ChainRect& c = rects[((size_t)ty * gx + tx) * L + l];
+                const int fw = c.fx1 - c.fx0 + 1;
+                to[l + 1] = to[l] + (fw > 0 ? ((fw + 3) & ~3) + ((c.fy1 - c.fy0 + 2) & ~1) : 0);
+            }
+        }
+    auto r16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    const size_t lds = 2 * r16(buf) + r16(rs) + r16(ct);
+    if (lds > 150 * 1024) return;
+    G.chain_gx = gx;
+    G.chain_gy = gy;
+    G.chain_buf = (int)r16(buf);
+    G.chain_rs = (int)r16(rs);
+    G.chain_lds = (int)lds;
+    while (h->ltab.size() % 16) h->ltab.push_back(0);
+    G.chain_tab = (int)h->ltab.size();
+    h->ltab.insert(h->ltab.end(), (const uint8_t*)rects.data(), (const uint8_t*)(rects.data() + rects.size()));
+    while (h->ltab.size() % 16) h->ltab.push_back(0);
+    G.chain_toffs = (int)h->ltab.size();
+    h->ltab.insert(h->ltab.end(), (const uint8_t*)toffs.data(), (const uint8_t*)(toffs.data() + toffs.size()));
+    G.chain_ok = 1;
+}
+
 orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     Geometry& G = h->hg;
     memset(&G, 0, sizeof(G));
@@ -750,6 +852,7 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                        (const uint8_t*)(rt.data() + rt.size()));
         build_strip_tables(h, l, mode, xofs, alpha, yofs, beta);
     }
+    build_chain(h);
     h->level_lds = level_lds_bytes(G.ltw, G.lth, G.win_cap);
     if (h->level_lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     G.blur_tile_begin[L] = blur_tiles;
@@ -853,7 +956,7 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
             return ORBX_ERR_DEVICE;
         if (!HIPOK(hipStreamSynchronize(st))) return ORBX_ERR_DEVICE;
         if (!HIPOK(prepare_kernels(std::max(h->octree_lds, h->octree_lds_small), h->stereo_lds,
-                                   h->level_lds, fast_lds_bytes(h->hg))))
+                                   std::max(h->level_lds, (size_t)h->hg.chain_lds), fast_lds_bytes(h->hg))))
             return ORBX_ERR_DEVICE;
         h->have_geom = true;
         h->cap_batch = 0;
@@ -949,6 +1052,8 @@ ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uin
                                                                                      : h->side_mode;
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
+    a.chain = (h->hg.chain_ok && a.in_place && a.side_mode == 0 &&
+               batch <= tuned("ORBX_CHAIN_MAX_BATCH", CHAIN_MAX_BATCH)) ? 1 : 0;
     strip_heights(h, batch, a.sth);
     return a;
 }

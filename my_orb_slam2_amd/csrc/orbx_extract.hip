@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 #include <stdint.h>
 
 #include "orbx_device.h"
@@ -223,7 +224,8 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define OCT_GATHER2 1       // candidate gather: two cells per thread, one scan per 2 NT cells
 #endif
 #ifndef OCT_BUCKET_SORT
-#define OCT_BUCKET_SORT 1   // phase-2 order by size buckets, then ranks inside a bucket
+#define OCT_BUCKET_SORT 2   // phase-2 order by size buckets: 1 ranks inside a bucket, 2 a stable
+                            // counting sort (the list order is the seq order)
 #endif
 #ifndef OD_WPE
 #define OD_WPE 5       // at most 96 VGPRs: five waves per SIMD (6: spills)
@@ -1039,17 +1041,28 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 });
             __syncthreads();
 #if OCT_BUCKET_SORT
-            if (nV <= sm.ncap) {
-                // bucket-then-rank sort, descending: keys go to buckets by size (min(cnt, 63),
-                // larger sizes first), and a key's place inside its bucket is the number of
-                // larger keys there (keys are unique: they end in the node index).  The
-                // comparisons run over one bucket (the nodes of one size) instead of all nV.
+            if (nV <= sm.ncap && (OCT_BUCKET_SORT < 2 || sm.ncap >= NT)) {
+                // bucket sort, descending: keys go to buckets by size (min(cnt, 63), larger
+                // sizes first).  OCT_BUCKET_SORT 1: a key's place inside its bucket is the
+                // number of larger keys there (keys are unique: they end in the node index).
+                // 2: a stable counting sort.  In phase 2 no root is expandable (phase 1's first
+                // round split them all), and every other node's seq falls strictly with its
+                // position in the list (children go to the front with the highest seqs, and the
+                // survivors keep their order), so sortb, built in list order, is already in
+                // descending (seq, node) order inside every size: placing the keys of a bucket
+                // in sortb order IS the descending (size, seq) order.  Only bucket 63 (sizes
+                // >= 63, several sizes) still ranks by comparison.
                 int* hist = tmp + 32;     // [64] keys per bucket
                 int* start = tmp + 96;    // [64] first position of each bucket
-                int* fill = tmp + 160;    // [64] fill cursor
+                int* fill = tmp + 160;    // [64] fill cursor / running count
                 uint64_t* stage = (uint64_t*)sm.cpos;   // free until the node pass below
                 auto bucket = [](uint64_t k) { return min((int)(k >> 40), 63); };
                 for (int i = tid; i < 64; i += NT) { hist[i] = 0; fill[i] = 0; }
+#if OCT_BUCKET_SORT >= 2
+                constexpr int NW = NT / 64;
+                int* wc = sm.pre;         // [NW][64] keys per (wave, bucket) of one chunk
+                for (int i = tid; i < NW * 64; i += NT) wc[i] = 0;
+#endif
                 __syncthreads();
                 for (int j = tid; j < nV; j += NT) atomicAdd(&hist[bucket(sm.sortb[j])], 1);
                 __syncthreads();
@@ -1058,6 +1071,52 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     start[63 - tid] = wave_incl_scan(v) - v;
                 }
                 __syncthreads();
+#if OCT_BUCKET_SORT >= 2
+                {
+                    const int wid = tid >> 6, lane = tid & 63;
+                    for (int c0 = 0; c0 < nV; c0 += NT) {
+                        const int j = c0 + tid;
+                        const bool valid = j < nV;
+                        const uint64_t k = valid ? sm.sortb[j] : 0;
+                        const int bk = valid ? bucket(k) : -1;
+                        // rank among this wave's lanes of the same bucket, one ballot per
+                        // distinct bucket in the wave
+                        int rank = 0;
+                        uint64_t rem = __ballot(valid);
+                        while (rem) {
+                            const int b0 = __builtin_amdgcn_readlane(bk, (int)__builtin_ctzll(rem));
+                            const uint64_t m = __ballot(bk == b0);
+                            if (bk == b0) rank = lanes_below(m);
+                            if (lane == 0) wc[wid * 64 + b0] = (int)__popcll(m);
+                            rem &= ~m;
+                        }
+                        __syncthreads();
+                        if (valid) {
+                            int off = fill[bk] + rank;
+                            for (int w = 0; w < wid; ++w) off += wc[w * 64 + bk];
+                            stage[start[bk] + off] = k;
+                        }
+                        __syncthreads();
+                        if (tid < 64) {
+                            int t = 0;
+                            for (int w = 0; w < NW; ++w) { t += wc[w * 64 + tid]; wc[w * 64 + tid] = 0; }
+                            fill[tid] += t;
+                        }
+                        __syncthreads();
+                    }
+                }
+                for (int q = tid; q < nV; q += NT) {
+                    const uint64_t k = stage[q];
+                    if (bucket(k) < 63) {
+                        sm.sortb[q] = k;
+                    } else {
+                        const int s0 = start[63], s1 = s0 + hist[63];
+                        int rank = 0;
+                        for (int t = s0; t < s1; ++t) rank += stage[t] > k ? 1 : 0;
+                        sm.sortb[s0 + rank] = k;
+                    }
+                }
+#else
                 for (int j = tid; j < nV; j += NT) {
                     const uint64_t k = sm.sortb[j];
                     const int bk = bucket(k);
@@ -1071,6 +1130,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     for (int t = s0; t < s1; ++t) rank += stage[t] > k ? 1 : 0;
                     sm.sortb[s0 + rank] = k;
                 }
+#endif
             } else
 #endif
             if (nV <= 4 * NT) {
@@ -1278,12 +1338,12 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     // global fallback region of this level: [kdata u32][knode i16][kq u8]
     long long lvl_off = 0;
     for (int l = 0; l < level; ++l) lvl_off += (long long)g->lv[l].cand_cap * 8;
-    uint32_t* kdata = in_lds ? l_kdata : (uint32_t*)(gs + lvl_off);
-    int16_t* knode = in_lds ? l_knode : (int16_t*)(gs + lvl_off + (long long)L.cand_cap * 4);
-    uint8_t* kq = in_lds ? l_kq : (gs + lvl_off + (long long)L.cand_cap * 6);
     // gather candidates in cell order (cell-major, raster inside a cell)
     const uint32_t* cbase = cand + (size_t)b * g->cand_words;
     const CellDesc* lc = cells + L.cell_begin;
+    // the candidate arrays are LDS or global scratch by a runtime test; each branch passes its
+    // own pointers (a pointer selected between the two is generic: every access a flat one)
+    auto gather_and_split = [&](uint32_t* kdata, int16_t* knode, uint8_t* kq, auto keys_lds_c) {
 #if OCT_GATHER2
     // two adjacent cells per thread, their offsets from one scan of the pairs' sums, and the
     // first 8 candidates of both cells loaded at once (addresses clamped into each cell's
@@ -1334,10 +1394,13 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
         });
 #endif
     __syncthreads();
+    octree_level<NT, decltype(keys_lds_c)::value>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+    };
     if (in_lds)
-        octree_level<NT, true>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+        gather_and_split(l_kdata, l_knode, l_kq, std::true_type{});
     else
-        octree_level<NT, false>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+        gather_and_split((uint32_t*)(gs + lvl_off), (int16_t*)(gs + lvl_off + (long long)L.cand_cap * 4),
+                         gs + lvl_off + (long long)L.cand_cap * 6, std::false_type{});
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1793,7 +1856,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
         if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
         if (mode < 2) oct(dim3(G.nlevels, a.batch), oct_lds, a.ncap, oct_kcap, 0, st);
     } else {
-        err = launch_levels(a, st, 0, G.nlevels);
+        err = a.chain ? launch_pyr_chain(a, st) : launch_levels(a, st, 0, G.nlevels);
         if (err != hipSuccess) return err;
         fast(0, G.n_cells, st);
 #if OCT_MERGED

@@ -135,6 +135,23 @@ struct LevelRowTab {
     uint32_t rinf[2 * LT_HR]; // (ry0 | ry1 << 16, beta0 | beta1 << 16)
 };
 
+// k_pyr_chain: one workgroup per (tile, image) computes its tile of every level.  Per level:
+// the owned output rectangle [ox0, ox1) x [oy0, oy1) (level pixels and blurred pixels it
+// stores; the owned rectangles of a level partition it, ox0 a multiple of 4) and the
+// footprint [fx0, fx1] x [fy0, fy1] it computes into LDS: the owned rectangle + the blur's
+// 3-pixel halo, and every source pixel the next level's footprint reads (fx0 a multiple of
+// 4).  An empty footprint has fx1 < fx0.
+struct ChainRect {
+    int16_t ox0, ox1, oy0, oy1, fx0, fx1, fy0, fy1;
+};
+__host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 4; }
+#ifndef CHAIN_TW
+#define CHAIN_TW 160   // k_pyr_chain: level-0 tile width / height targets (tiles per image =
+#endif
+#ifndef CHAIN_TH
+#define CHAIN_TH 48    // ceil(w / CHAIN_TW) x ceil(h / CHAIN_TH))
+#endif
+
 // k_level_strip: a wave walks two half-strips (lanes 0-31, 32-63) down the level, one row per
 // step.  Lane q of a half-strip at X0 holds the 4-pixel group x = X0 - 4 + 4q; lanes 1..SW_OUT
 // write output.  Per lane (host-built, reflection and clamping folded in):
@@ -189,6 +206,14 @@ struct Geometry {
     int stereo_ob;          // k_stereo bucket groups: nlevels (octave, row), or 1 (row) if LDS is short
     int ltw, lth;           // k_level output tile
     int win_cap;            // k_level: largest staged source window (bytes)
+    // k_pyr_chain (small batches: every level in one launch, see orbx_pyramid.hip)
+    int chain_ok;           // 1: every level l >= 1 is INTER_LINEAR and the LDS fits
+    int chain_gx, chain_gy; // tiles per image (chain_gx * chain_gy workgroups per image)
+    int chain_tab;          // byte offset of the ChainRect table ([tile][level]) in ltab
+    int chain_toffs;        // byte offset of the per-tile table offsets ([tile][level + 1] ints)
+    int chain_buf;          // LDS bytes of one level buffer (two, ping-pong)
+    int chain_rs;           // LDS bytes of the blur row sums
+    int chain_lds;          // total dynamic LDS of the launch
     LevelGeom lv[ORBX_MAX_LEVELS];
 };
 

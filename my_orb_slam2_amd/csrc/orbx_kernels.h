@@ -141,6 +141,8 @@ struct ExtractLaunch {
     // side branch: 0 off, 1 FAST, 2 + octree, 3 + orientation / descriptors of levels
     // [0, side_lv), forked before level side_at's launch
     int side_mode = 0, side_at = 0, side_lv = 1;
+    // 1: the whole pyramid as one k_pyr_chain launch (small in-place batches, no side branch)
+    int chain = 0;
 };
 
 
@@ -170,6 +172,7 @@ struct StereoLaunch {
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
 hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, int l_end);
+hipError_t launch_pyr_chain(const ExtractLaunch& a, hipStream_t st);
 size_t level_lds_bytes(int ltw, int lth, int win_cap);
 size_t fast_lds_bytes(const Geometry& g);
 size_t octree_lds_bytes(int ncap, int kcap);

@@ -1141,6 +1141,310 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
                            wv, b);
 }
 
+// ---- k_pyr_chain: every level of a small batch in one launch ----
+// A lone frame's pyramid as per-level launches is a chain of eight kernels of a few
+// microseconds each, the GPU mostly idle.  Here one workgroup per (tile, image) computes its
+// tile of every level with no grid-wide dependency: level 0's footprint is staged from the
+// pyramid into LDS, and each level l >= 1 is computed over its footprint (host-built,
+// ChainRect: the owned rectangle + blur halo + what the next level's footprint reads) from
+// level l - 1's footprint in the other LDS buffer, so the tiles overlap (recomputed halos)
+// instead of waiting for each other.  The owned pixels of each level and their blur go to HBM.
+// Arithmetic per pixel: HResizeLinear + VResizeLinear(Vec) (vresize, as k_level's scalar
+// border path) and RowFilter<uchar,int> + SymmColumnFilter in the exact integer form of
+// tile_columns (S < 2^24, SSE2 pixels round half to even) -- src/ORBextractor.cc:1129-1154,
+// :1107-1108.
+#ifndef CHAIN_NT
+#define CHAIN_NT 1024
+#endif
+__device__ __forceinline__ int reflect101_fast(int p, int len) {
+    return (unsigned)p < (unsigned)len ? p : reflect101_i(p, len);
+}
+
+// i / d for the item loops (d >= 1, i < 2^26): one v_mul_hi_u32 by m = ceil(2^32 / d)
+struct Div {
+    uint32_t m, d;
+    // floor((2^32 - 1) / d) + 1 == ceil(2^32 / d) for every d >= 2 (a 32-bit division)
+    __device__ explicit Div(int dd) : m(dd > 1 ? 0xFFFFFFFFu / (uint32_t)dd + 1u : 0u), d((uint32_t)dd) {}
+    __device__ int operator()(int i) const { return d > 1 ? (int)__umulhi((uint32_t)i, m) : i; }
+};
+
+// Row pass of the blur of level l's owned rectangle (rows oy0 - 3 .. oy1 + 2, reflected) from
+// its footprint in LDS (src, origin (fx0, fy0), row pitch P) into rsum (int row sums, RW =
+// 4 ng per row).  Interior groups (every tap inside the row: xg >= 3, xg + 6 < W) read three
+// aligned dwords (bytes xg - 4 .. xg + 7; fx0 and ox0 are multiples of 4) and form the sums
+// as v_dot4 on shifted words, as tile_out_rows; the <= 3 border groups of a row take their
+// ten reflected bytes one by one, as separate items so that no wave of interior items runs
+// that path.
+template <int NT>
+__device__ __forceinline__ void chain_rows(const ChainRect& c, const LevelGeom& Lv, const uint8_t* src,
+                                           int P, int* rsum, const Geometry* g, int tid) {
+    const int ow = c.ox1 - c.ox0, oh = c.oy1 - c.oy0;
+    if (ow <= 0 || oh <= 0) return;
+    const int ng = (ow + 3) >> 2, RW = 4 * ng;
+    const int W = Lv.w, H = Lv.h;
+    const int t0 = g->taps[0], t1 = g->taps[1], t2 = g->taps[2], t3 = g->taps[3];
+    const int t4 = g->taps[4], t5 = g->taps[5], t6 = g->taps[6];
+    const int q_lo = c.ox0 >= 3 ? 0 : 1;
+    const int rq = W - 7 - c.ox0;
+    const int q_hi = max(q_lo, min(ng, rq >= 0 ? rq / 4 + 1 : 0));
+    const int ni = q_hi - q_lo, nb = ng - ni;
+    const uint32_t tapA = (uint32_t)t0 | (uint32_t)t1 << 8 | (uint32_t)t2 << 16 | (uint32_t)t3 << 24;
+    const uint32_t tapB = (uint32_t)t4 | (uint32_t)t5 << 8 | (uint32_t)t6 << 16;
+    const Div di(ni > 0 ? ni : 1);
+    for (int i = tid; i < (oh + 6) * ni; i += NT) {
+        const int rr = di(i), q = q_lo + (i - rr * ni);
+        const int ry = reflect101_fast(c.oy0 - 3 + rr, H) - c.fy0;
+        const int xg = c.ox0 + 4 * q;
+        const uint32_t* sw = (const uint32_t*)(src + ry * P + (xg - 4 - c.fx0));
+        const uint32_t d0 = sw[0], d1 = sw[1], d2 = sw[2];
+        int4 o;
+        o.x = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tapA,
+                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), tapB, 0u, false), false);
+        o.y = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tapA,
+                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), tapB, 0u, false), false);
+        o.z = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tapA,
+                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tapB, 0u, false), false);
+        o.w = (int)__builtin_amdgcn_udot4(d1, tapA, __builtin_amdgcn_udot4(d2, tapB, 0u, false), false);
+        *(int4*)(rsum + rr * RW + 4 * q) = o;
+    }
+    const Div db(nb > 0 ? nb : 1);
+    for (int i = tid; i < (oh + 6) * nb; i += NT) {
+        const int rr = db(i), k = i - rr * nb;
+        const int q = k < q_lo ? k : q_hi + (k - q_lo);
+        const uint8_t* sr = src + (reflect101_fast(c.oy0 - 3 + rr, H) - c.fy0) * P;
+        const int xg = c.ox0 + 4 * q;
+        int v[10];
+#pragma unroll
+        for (int k2 = 0; k2 < 10; ++k2)   // pixels past the row's last keep an in-row value
+            v[k2] = sr[reflect101_fast(min(xg - 3 + k2, W + 2), W) - c.fx0];
+        int4 o;
+        int* op = (int*)&o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            op[j] = t0 * v[j] + t1 * v[j + 1] + t2 * v[j + 2] + t3 * v[j + 3] + t4 * v[j + 4] +
+                    t5 * v[j + 5] + t6 * v[j + 6];
+        *(int4*)(rsum + rr * RW + 4 * q) = o;
+    }
+}
+
+// Column pass of the blur of level l's owned rectangle from rsum, stored to the blurred
+// pyramid: SymmColumnFilter in the exact integer form of tile_columns (S < 2^24, SSE2 pixels
+// round half to even).
+template <int NT>
+__device__ __forceinline__ void chain_cols(const ChainRect& c, const LevelGeom& Lv, const int* rsum,
+                                           uint8_t* dblur, const Geometry* g, int tid) {
+    const int ow = c.ox1 - c.ox0, oh = c.oy1 - c.oy0;
+    if (ow <= 0 || oh <= 0) return;
+    const int ng = (ow + 3) >> 2, RW = 4 * ng;
+    const uint32_t t3 = (uint32_t)g->taps[3], t4 = (uint32_t)g->taps[4];
+    const uint32_t t5 = (uint32_t)g->taps[5], t6 = (uint32_t)g->taps[6];
+    const Div dv(ng);
+    for (int i = tid; i < oh * ng; i += NT) {
+        const int rr = dv(i), q = i - rr * ng;
+        const int y = c.oy0 + rr, xg = c.ox0 + 4 * q;
+        int4 v[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v[k] = *(const int4*)(rsum + (rr + k) * RW + 4 * q);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto e = [&](int k) { return (uint32_t)((const int*)&v[k])[j]; };
+            const uint32_t S = t3 * e(3) + t4 * (e(2) + e(4)) + t5 * (e(1) + e(5)) + t6 * (e(0) + e(6));
+            const bool simd = xg + j < Lv.bsimd_end;
+            const uint32_t val = (S + (simd ? 32767u + ((S >> 16) & 1u) : 32768u)) >> 16;
+            packed |= min(val, 255u) << (8 * j);
+        }
+        uint8_t* d = dblur + blur_off(xg, y, Lv.pitch, Lv.h);
+        if (xg + 4 <= c.ox1) *(uint32_t*)d = packed;
+        else
+            for (int j = 0; xg + j < c.ox1; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+    }
+}
+
+#ifdef ORBX_CHAIN_STAMPS
+// Diagnostic build only (tools/chain_stamps.py): per-tile phase clocks of image 0.
+__device__ unsigned long long g_chain_stamps[256][40];
+#define CSTAMP(k)                                                                          \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 256 && (k) < 40)           \
+            g_chain_stamps[blockIdx.x][(k)] = __builtin_readcyclecounter();                \
+    } while (0)
+extern "C" int orbx_diag_chain_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps));
+}
+#else
+#define CSTAMP(k) do { } while (0)
+#endif
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g,
+                                                  const uint8_t* __restrict__ ltab,
+                                                  const int16_t* __restrict__ rtab,
+                                                  uint8_t* __restrict__ pyr,
+                                                  uint8_t* __restrict__ blur) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int L = g->nlevels;
+    CSTAMP(0);
+    // LDS buffers by arithmetic on smem (a pointer picked from an array loses the LDS address
+    // space: every access becomes a flat one)
+    const int cbuf = g->chain_buf;
+    int* rsum = (int*)(smem + 2 * cbuf);
+    uint32_t* tabs = (uint32_t*)(smem + 2 * cbuf + g->chain_rs);
+    uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
+    uint8_t* blr_b = blur + (size_t)b * g->pyr_bytes;
+    // the tile's rectangles, table offsets (host-built) and the level geometry in LDS: the
+    // table phase reads them per lane, and from memory each read would be a round trip
+    __shared__ ChainRect CR[ORBX_MAX_LEVELS];
+    __shared__ int toffs[ORBX_MAX_LEVELS + 1];
+    __shared__ LevelGeom LG[ORBX_MAX_LEVELS];
+    const ChainRect* gCR = (const ChainRect*)(ltab + g->chain_tab) + (size_t)tile * L;
+    if (tid < L) CR[tid] = gCR[tid];
+    if (tid <= L) toffs[tid] = ((const int*)(ltab + g->chain_toffs))[(size_t)tile * (L + 1) + tid];
+    {
+        constexpr int NDW = (int)(sizeof(LevelGeom) / 4);
+        for (int i = tid; i < L * NDW; i += NT) ((int*)LG)[i] = ((const int*)g->lv)[i];
+    }
+    // 1. level 0's footprint, in the same round trip (aligned dwords: fx0 is a multiple of 4,
+    //    rows have >= 4 bytes of slack); every load in flight before the first LDS store
+    const ChainRect c0 = gCR[0];
+    const int fw0 = c0.fx1 - c0.fx0 + 1, fh0 = c0.fy1 - c0.fy0 + 1, P0 = chain_pitch(fw0);
+    const int ndw = fw0 > 0 ? (fw0 + 3) >> 2 : 0, nst = ndw * fh0;
+    const Div dv0(ndw > 0 ? ndw : 1);
+    const uint8_t* s0 = pyr_b + g->lv[0].off + (size_t)c0.fy0 * g->lv[0].pitch + c0.fx0;
+    const int pitch0 = g->lv[0].pitch;
+    constexpr int SK = 8;
+    uint32_t sv[SK];
+#pragma unroll
+    for (int u = 0; u < SK; ++u) {
+        const int i = min(tid + u * NT, nst - 1), r = dv0(max(i, 0)), q = max(i, 0) - r * ndw;
+        sv[u] = i >= 0 ? *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q) : 0u;
+    }
+    __syncthreads();
+    CSTAMP(1);
+    // 2. every level's column / row tables, while the staged words are stored.  Per level
+    //    (8-byte units from 2 toffs[l]): [4 ng] source columns (footprint-relative) | SSE2 flag
+    //    << 16, [4 ng] alphas ((2048, 0) right of xmax: HResizeLinear's S[sx] * 2048), then
+    //    [fh, rounded up to even] row entries (the two source rows | << 16, the betas).
+    const int ntab = toffs[L];
+    for (int i = tid; i < ntab; i += NT) {
+        int l = 1;
+        while (i >= toffs[l + 1]) ++l;   // the level of entry i
+        const int base = toffs[l];
+        const ChainRect c = CR[l], cs = CR[l - 1];
+        const LevelGeom& Ld = LG[l];
+        const LevelGeom& Ls = LG[l - 1];
+        const int16_t* xofs = rtab + Ld.rtab_off;
+        const int16_t* alpha = xofs + Ld.w;
+        const int16_t* yofs = alpha + 2 * Ld.w;
+        const int16_t* beta = yofs + Ld.h;
+        const int ncol = 4 * ((c.fx1 - c.fx0 + 4) >> 2);
+        const int k = i - base;
+        uint32_t* tl = tabs + 2 * base;
+        if (k < ncol) {
+            const int x = min(c.fx0 + k, (int)c.fx1);
+            const int Ps = chain_pitch(cs.fx1 - cs.fx0 + 1);
+            const int sx = min(max((int)xofs[x] - cs.fx0, 0), Ps - 5);
+            uint32_t al = 2048u;
+            if (x < Ld.xmax) al = (uint32_t)(uint16_t)alpha[2 * x] | ((uint32_t)(uint16_t)alpha[2 * x + 1] << 16);
+            tl[k] = (uint32_t)sx | (x < Ld.rsimd_end ? 0x10000u : 0u);
+            tl[ncol + k] = al;
+        } else {
+            const int y = min(c.fy0 + (k - ncol), (int)c.fy1);
+            const int sy = yofs[y];
+            const int r0 = min(max(sy, 0), Ls.h - 1) - cs.fy0, r1 = min(max(sy + 1, 0), Ls.h - 1) - cs.fy0;
+            ((uint2*)(tl + 2 * ncol))[k - ncol] =
+                make_uint2((uint32_t)r0 | ((uint32_t)r1 << 16),
+                           (uint32_t)(uint16_t)beta[2 * y] | ((uint32_t)(uint16_t)beta[2 * y + 1] << 16));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < SK; ++u) {
+        const int i = tid + u * NT;
+        if (i < nst) {
+            const int r = dv0(i), q = i - r * ndw;
+            ((uint32_t*)(smem + r * P0))[q] = sv[u];
+        }
+    }
+    for (int i = tid + SK * NT; i < nst; i += NT) {   // footprints beyond SK * NT words
+        const int r = dv0(i), q = i - r * ndw;
+        ((uint32_t*)(smem + r * P0))[q] = *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q);
+    }
+    __syncthreads();
+    CSTAMP(2);
+    // 3. level 0's blur rows; then per level l >= 1: the previous level's blur columns beside
+    //    this level's resize (they share no LDS), then this level's blur rows
+    chain_rows<NT>(c0, LG[0], smem, P0, rsum, g, tid);
+    __syncthreads();
+    CSTAMP(3);
+    int lr = 0;   // the level whose row sums are in rsum (-1: none)
+    ChainRect cp = c0;
+    int toff = 0;
+    for (int l = 1; l < L; ++l) {
+        chain_cols<NT>(cp, LG[lr], rsum, blr_b + LG[lr].off, g, tid);
+        lr = -1;
+        const ChainRect cd = CR[l];
+        const LevelGeom& Ld = LG[l];
+        const int fw = cd.fx1 - cd.fx0 + 1, fh = cd.fy1 - cd.fy0 + 1;
+        if (fw <= 0) break;   // empty footprint: no deeper level of this tile needs anything
+        const int Ps = chain_pitch(cp.fx1 - cp.fx0 + 1), Pd = chain_pitch(fw);
+        const uint8_t* src = smem + ((l - 1) & 1) * cbuf;
+        uint8_t* dst = smem + (l & 1) * cbuf;
+        const int ng = (fw + 3) >> 2;
+        const uint32_t* colsx = tabs + 2 * toff;
+        const uint32_t* colal = colsx + 4 * ng;
+        const uint2* rowt = (const uint2*)(colal + 4 * ng);
+        toff += 4 * ng + ((fh + 1) & ~1);
+        uint8_t* dlev = pyr_b + Ld.off;
+        const Div dv(ng);
+        for (int i = tid; i < fh * ng; i += NT) {
+            const int r = dv(i), q = i - r * ng;
+            const uint2 rt = rowt[r];
+            const int b0 = (int)(rt.y & 0xFFFFu), b1 = (int)(rt.y >> 16);
+            const uint8_t* s0r = src + (int)(rt.x & 0xFFFFu) * Ps;
+            const uint8_t* s1r = src + (int)(rt.x >> 16) * Ps;
+            uint32_t out = 0;
+            const uint4 cx4 = *(const uint4*)(colsx + 4 * q), ca4 = *(const uint4*)(colal + 4 * q);
+            const uint32_t cxs[4] = {cx4.x, cx4.y, cx4.z, cx4.w}, cas[4] = {ca4.x, ca4.y, ca4.z, ca4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int sx = (int)(cxs[j] & 0xFFFFu);
+                const int a0 = (int)(cas[j] & 0xFFFFu), a1 = (int)(cas[j] >> 16);
+                const int h0 = s0r[sx] * a0 + s0r[sx + 1] * a1;
+                const int h1 = s1r[sx] * a0 + s1r[sx + 1] * a1;
+                out |= (uint32_t)vresize(h0, h1, b0, b1, (cxs[j] >> 16) != 0u) << (8 * j);
+            }
+            *(uint32_t*)(dst + r * Pd + 4 * q) = out;
+            const int y = cd.fy0 + r, xg = cd.fx0 + 4 * q;
+            if (y >= cd.oy0 && y < cd.oy1 && xg >= cd.ox0 && xg < cd.ox1) {
+                uint8_t* d = dlev + (size_t)y * Ld.pitch + xg;
+                if (xg + 4 <= cd.ox1) *(uint32_t*)d = out;
+                else
+                    for (int j = 0; xg + j < cd.ox1; ++j) d[j] = (uint8_t)(out >> (8 * j));
+            }
+        }
+        __syncthreads();
+        CSTAMP(2 + 2 * l);
+        chain_rows<NT>(cd, Ld, dst, Pd, rsum, g, tid);
+        __syncthreads();
+        CSTAMP(3 + 2 * l);
+        lr = l;
+        cp = cd;
+    }
+    if (lr >= 0) chain_cols<NT>(cp, LG[lr], rsum, blr_b + LG[lr].off, g, tid);
+    CSTAMP(18);
+}
+
+hipError_t launch_pyr_chain(const ExtractLaunch& a, hipStream_t st) {
+    const Geometry& G = *a.hg;
+    KernelTimer dummy;
+    KernelTimer& T = a.timer ? *a.timer : dummy;
+    ORBX_TIMED_LAUNCH(T, K_LEVEL, k_pyr_chain<CHAIN_NT>, dim3(G.chain_gx * G.chain_gy, a.batch),
+                      dim3(CHAIN_NT), (size_t)G.chain_lds, st, a.dg, a.ltab, a.rtab, a.pyr, a.blur);
+    return hipGetLastError();
+}
+
 size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     (void)ltw;
     (void)lth;
@@ -1210,6 +1514,9 @@ hipError_t prepare_level(size_t lds) {
     hipError_t e = hipSuccess;
     for (int m = 0; m < 4 && e == hipSuccess; ++m)
         e = hipFuncSetAttribute((const void*)level_kernel(m),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_pyr_chain<CHAIN_NT>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return e;
 }
