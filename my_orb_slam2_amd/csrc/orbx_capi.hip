@@ -475,12 +475,19 @@ static void build_chain(orbx_extractor* h) {
     G.chain_gx = G.chain_gy = 1;
     G.chain_tab = G.chain_toffs = 0;
     G.chain_buf = G.chain_rs = G.chain_lds = 0;
-    for (int l = 1; l < L; ++l)
+    for (int l = 1; l < L; ++l) {
         if (G.lv[l].copy || G.lv[l].area2) return;
+        // a 4-pixel group's taps must fit the 8 bytes one v_perm pair reads (source span <= 6,
+        // i.e. scale factors up to about 2.3; groups start at multiples of 4)
+        const int16_t* xofs = h->rtab.data() + G.lv[l].rtab_off;
+        for (int x = 0; x < G.lv[l].w; x += 4)
+            if (xofs[std::min(x + 3, G.lv[l].w - 1)] - xofs[x] > 5) return;
+    }
     const int gx = std::max(1, (G.lv[0].w + CHAIN_TW - 1) / CHAIN_TW);
     const int gy = std::max(1, (G.lv[0].h + CHAIN_TH - 1) / CHAIN_TH);
     std::vector<ChainRect> rects((size_t)gx * gy * L);
-    std::vector<int32_t> toffs((size_t)gx * gy * (L + 1), 0);   // k_pyr_chain table offsets
+    // k_pyr_chain table offsets per tile: [L + 1] entry prefix, then [L + 1] word prefix
+    std::vector<int32_t> toffs((size_t)gx * gy * 2 * (L + 1), 0);
     size_t buf = 16, rs = 16, ct = 16;
     for (int ty = 0; ty < gy; ++ty)
         for (int tx = 0; tx < gx; ++tx) {
@@ -534,14 +541,16 @@ static void build_chain(orbx_extractor* h) {
                 const int fw = fx1 - fx0 + 1;
                 buf = std::max(buf, (size_t)chain_pitch(fw) * (fy1 - fy0 + 1) + 16);
                 rs = std::max(rs, (size_t)4 * ((ox1 - ox0 + 3) & ~3) * (oy1 - oy0 + 6));
-                if (l > 0) tab += (size_t)((fw + 3) & ~3) + ((fy1 - fy0 + 2) & ~1);
+                if (l > 0) tab += chain_level_words((fw + 3) >> 2, fy1 - fy0 + 1);
             }
-            ct = std::max(ct, 8 * tab);
-            int32_t* to = &toffs[((size_t)ty * gx + tx) * (L + 1)];
+            ct = std::max(ct, 4 * tab);
+            int32_t* te = &toffs[((size_t)ty * gx + tx) * 2 * (L + 1)];
+            int32_t* tw = te + (L + 1);
             for (int l = 1; l < L; ++l) {
                 const ChainRect& c = rects[((size_t)ty * gx + tx) * L + l];
-                const int fw = c.fx1 - c.fx0 + 1;
-                to[l + 1] = to[l] + (fw > 0 ? ((fw + 3) & ~3) + ((c.fy1 - c.fy0 + 2) & ~1) : 0);
+                const int fw = c.fx1 - c.fx0 + 1, fh = c.fy1 - c.fy0 + 1;
+                te[l + 1] = te[l] + (fw > 0 ? ((fw + 3) >> 2) + ((fh + 1) & ~1) : 0);
+                tw[l + 1] = tw[l] + (fw > 0 ? chain_level_words((fw + 3) >> 2, fh) : 0);
             }
         }
     auto r16 = [](size_t v) { return (v + 15) & ~(size_t)15; };

@@ -839,18 +839,35 @@ __device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1
 
 // Chunked exclusive scan over n items (n may exceed 256).  f(i) gives the value; g(i, excl)
 // consumes the exclusive prefix.  Returns the total.  All threads must call.
+// Exclusive scan of f over [0, n), gcb(i, prefix) per element.  Up to NT elements: one block
+// scan, element i on thread i.  Beyond: each thread scans a contiguous run of ceil(n / NT)
+// elements (f evaluated twice per element, so f must not read what gcb writes), one block scan
+// of the runs' sums, and a closing barrier (a thread's gcb writes are not the elements a
+// thread-strided loop after the scan reads): 3 barriers for any n, where a scan per NT-chunk
+// took 2 per chunk (16 for a 2000-node list).
 template <int NT, class F, class G>
 __device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
-    int carry = 0;
-    for (int c0 = 0; c0 < n; c0 += NT) {
-        const int i = c0 + threadIdx.x;
+    if (n <= NT) {
+        const int i = threadIdx.x;
         const int v = (i < n) ? f(i) : 0;
         int tot;
         const int ex = block_excl_scan<NT / 64>(v, tmp, tot);
-        if (i < n) gcb(i, carry + ex);
-        carry += tot;
+        if (i < n) gcb(i, ex);
+        return tot;
     }
-    return carry;
+    const int E = (n + NT - 1) / NT;
+    const int i0 = min((int)threadIdx.x * E, n), i1 = min(i0 + E, n);
+    int s = 0;
+    for (int i = i0; i < i1; ++i) s += f(i);
+    int tot;
+    int ex = block_excl_scan<NT / 64>(s, tmp, tot);
+    for (int i = i0; i < i1; ++i) {
+        const int v = f(i);
+        gcb(i, ex);
+        ex += v;
+    }
+    __syncthreads();
+    return tot;
 }
 
 #ifdef ORBX_OCT_STAMPS

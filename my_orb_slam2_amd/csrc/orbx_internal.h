@@ -144,9 +144,15 @@ struct LevelRowTab {
 struct ChainRect {
     int16_t ox0, ox1, oy0, oy1, fx0, fx1, fy0, fy1;
 };
-__host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 4; }
+__host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 8; }
+// LDS words of a level's k_pyr_chain tables (ng column groups, fh rows): per group a base word,
+// padded to a multiple of 4, then 4 v_perm selectors and 4 alpha pairs; per row two words
+// (fh rounded up to even, so every level's tables start 16-byte aligned)
+__host__ __device__ inline int chain_level_words(int ng, int fh) {
+    return ((ng + 3) & ~3) + 8 * ng + 2 * ((fh + 1) & ~1);
+}
 #ifndef CHAIN_TW
-#define CHAIN_TW 160   // k_pyr_chain: level-0 tile width / height targets (tiles per image =
+#define CHAIN_TW 80    // k_pyr_chain: level-0 tile width / height targets (tiles per image =
 #endif
 #ifndef CHAIN_TH
 #define CHAIN_TH 48    // ceil(w / CHAIN_TW) x ceil(h / CHAIN_TH))

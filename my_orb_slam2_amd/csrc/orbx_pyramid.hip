@@ -1156,8 +1156,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
 #ifndef CHAIN_NT
 #define CHAIN_NT 1024
 #endif
+#ifndef CHAIN_DIAG
+#define CHAIN_DIAG 0   // diagnostic builds only (tools/chain_stamps.py): 1 no level stores, 2 no VResize
+#endif
 __device__ __forceinline__ int reflect101_fast(int p, int len) {
     return (unsigned)p < (unsigned)len ? p : reflect101_i(p, len);
+}
+
+// (x * y) >> 32 of two 24-bit values: one v_mul_hi_u32_u24
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t x, uint32_t y) {
+    return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * (y & 0xFFFFFFu)) >> 32);
+}
+
+// bit j: pixel x0 + j (clamped to x1) takes the SSE2 vertical form (x < rsimd_end)
+__device__ __forceinline__ uint32_t x_simd_bits(int x0, int x1, int rsimd_end) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m |= (min(x0 + j, x1) < rsimd_end ? 1u : 0u) << j;
+    return m;
 }
 
 // i / d for the item loops (d >= 1, i < 2^26): one v_mul_hi_u32 by m = ceil(2^32 / d)
@@ -1263,7 +1279,7 @@ __device__ __forceinline__ void chain_cols(const ChainRect& c, const LevelGeom& 
 
 #ifdef ORBX_CHAIN_STAMPS
 // Diagnostic build only (tools/chain_stamps.py): per-tile phase clocks of image 0.
-__device__ unsigned long long g_chain_stamps[256][40];
+__device__ unsigned long long g_chain_stamps[256][40];   // [tile][phase]
 #define CSTAMP(k)                                                                          \
     do {                                                                                   \
         if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 256 && (k) < 40)           \
@@ -1297,11 +1313,11 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
     // the tile's rectangles, table offsets (host-built) and the level geometry in LDS: the
     // table phase reads them per lane, and from memory each read would be a round trip
     __shared__ ChainRect CR[ORBX_MAX_LEVELS];
-    __shared__ int toffs[ORBX_MAX_LEVELS + 1];
+    __shared__ int toffs[2 * (ORBX_MAX_LEVELS + 1)];
     __shared__ LevelGeom LG[ORBX_MAX_LEVELS];
     const ChainRect* gCR = (const ChainRect*)(ltab + g->chain_tab) + (size_t)tile * L;
     if (tid < L) CR[tid] = gCR[tid];
-    if (tid <= L) toffs[tid] = ((const int*)(ltab + g->chain_toffs))[(size_t)tile * (L + 1) + tid];
+    if (tid < 2 * (L + 1)) toffs[tid] = ((const int*)(ltab + g->chain_toffs))[(size_t)tile * 2 * (L + 1) + tid];
     {
         constexpr int NDW = (int)(sizeof(LevelGeom) / 4);
         for (int i = tid; i < L * NDW; i += NT) ((int*)LG)[i] = ((const int*)g->lv)[i];
@@ -1324,14 +1340,18 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
     __syncthreads();
     CSTAMP(1);
     // 2. every level's column / row tables, while the staged words are stored.  Per level
-    //    (8-byte units from 2 toffs[l]): [4 ng] source columns (footprint-relative) | SSE2 flag
-    //    << 16, [4 ng] alphas ((2048, 0) right of xmax: HResizeLinear's S[sx] * 2048), then
-    //    [fh, rounded up to even] row entries (the two source rows | << 16, the betas).
-    const int ntab = toffs[L];
+    //    (chain_level_words, from word tw[l]): per column group of 4 pixels a base word
+    //    (aligned source byte | its offset o0 << 16 | 1 << 20 when all 4 pixels take the SSE2
+    //    vertical form), 4 v_perm selectors (each pixel's two taps as u16s from the 8 bytes
+    //    at base + o0) and 4 alpha pairs x 16 ((2048, 0) right of xmax: HResizeLinear's
+    //    S[sx] * 2048); per row the two source rows | << 16 and the betas.  Entries: one per
+    //    group, then one per row (te[l]).
+    const int* te = toffs;
+    const int* tw = toffs + (L + 1);
+    const int ntab = te[L];
     for (int i = tid; i < ntab; i += NT) {
         int l = 1;
-        while (i >= toffs[l + 1]) ++l;   // the level of entry i
-        const int base = toffs[l];
+        while (i >= te[l + 1]) ++l;   // the level of entry i
         const ChainRect c = CR[l], cs = CR[l - 1];
         const LevelGeom& Ld = LG[l];
         const LevelGeom& Ls = LG[l - 1];
@@ -1339,22 +1359,39 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         const int16_t* alpha = xofs + Ld.w;
         const int16_t* yofs = alpha + 2 * Ld.w;
         const int16_t* beta = yofs + Ld.h;
-        const int ncol = 4 * ((c.fx1 - c.fx0 + 4) >> 2);
-        const int k = i - base;
-        uint32_t* tl = tabs + 2 * base;
-        if (k < ncol) {
-            const int x = min(c.fx0 + k, (int)c.fx1);
-            const int Ps = chain_pitch(cs.fx1 - cs.fx0 + 1);
-            const int sx = min(max((int)xofs[x] - cs.fx0, 0), Ps - 5);
-            uint32_t al = 2048u;
-            if (x < Ld.xmax) al = (uint32_t)(uint16_t)alpha[2 * x] | ((uint32_t)(uint16_t)alpha[2 * x + 1] << 16);
-            tl[k] = (uint32_t)sx | (x < Ld.rsimd_end ? 0x10000u : 0u);
-            tl[ncol + k] = al;
+        const int ng = (c.fx1 - c.fx0 + 4) >> 2;
+        const int k = i - te[l];
+        uint32_t* tl = tabs + tw[l];
+        uint32_t* cbase = tl;
+        uint32_t* csel = tl + ((ng + 3) & ~3);
+        uint32_t* cal = csel + 4 * ng;
+        if (k < ng) {
+            int sx[4];
+            uint32_t al[4];
+            bool all_simd = true;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int x = min(c.fx0 + 4 * k + j, (int)c.fx1);
+                sx[j] = (int)xofs[x] - cs.fx0;
+                al[j] = x < Ld.xmax ? ((uint32_t)(uint16_t)alpha[2 * x] | ((uint32_t)(uint16_t)alpha[2 * x + 1] << 16))
+                                    : 2048u;
+                al[j] = ((al[j] & 0xFFFFu) << 4) | (((al[j] >> 16) << 4) << 16);
+                all_simd = all_simd && x < Ld.rsimd_end;
+            }
+            const int base = sx[0] & ~3, o0 = sx[0] & 3;
+            cbase[k] = (uint32_t)base | ((uint32_t)o0 << 16) | (all_simd ? (1u << 20) : 0u) |
+                       ((uint32_t)(((x_simd_bits(c.fx0 + 4 * k, (int)c.fx1, Ld.rsimd_end)))) << 21);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kk = min(max(sx[j] - sx[0], 0), 6);
+                csel[4 * k + j] = (uint32_t)kk | (0x0Cu << 8) | ((uint32_t)(kk + 1) << 16) | (0x0Cu << 24);
+                cal[4 * k + j] = al[j];
+            }
         } else {
-            const int y = min(c.fy0 + (k - ncol), (int)c.fy1);
+            const int y = min(c.fy0 + (k - ng), (int)c.fy1);
             const int sy = yofs[y];
             const int r0 = min(max(sy, 0), Ls.h - 1) - cs.fy0, r1 = min(max(sy + 1, 0), Ls.h - 1) - cs.fy0;
-            ((uint2*)(tl + 2 * ncol))[k - ncol] =
+            ((uint2*)(cal + 4 * ng))[k - ng] =
                 make_uint2((uint32_t)r0 | ((uint32_t)r1 << 16),
                            (uint32_t)(uint16_t)beta[2 * y] | ((uint32_t)(uint16_t)beta[2 * y + 1] << 16));
         }
@@ -1380,9 +1417,9 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
     CSTAMP(3);
     int lr = 0;   // the level whose row sums are in rsum (-1: none)
     ChainRect cp = c0;
-    int toff = 0;
     for (int l = 1; l < L; ++l) {
         chain_cols<NT>(cp, LG[lr], rsum, blr_b + LG[lr].off, g, tid);
+        CSTAMP(18 + 2 * l);
         lr = -1;
         const ChainRect cd = CR[l];
         const LevelGeom& Ld = LG[l];
@@ -1392,38 +1429,81 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         const uint8_t* src = smem + ((l - 1) & 1) * cbuf;
         uint8_t* dst = smem + (l & 1) * cbuf;
         const int ng = (fw + 3) >> 2;
-        const uint32_t* colsx = tabs + 2 * toff;
-        const uint32_t* colal = colsx + 4 * ng;
-        const uint2* rowt = (const uint2*)(colal + 4 * ng);
-        toff += 4 * ng + ((fh + 1) & ~1);
+        const uint32_t* cbase = tabs + tw[l];
+        const uint4* csel = (const uint4*)(cbase + ((ng + 3) & ~3));
+        const uint4* cal = csel + ng;
+        const uint2* rowt = (const uint2*)(cal + ng);
         uint8_t* dlev = pyr_b + Ld.off;
-        const Div dv(ng);
-        for (int i = tid; i < fh * ng; i += NT) {
-            const int r = dv(i), q = i - r * ng;
-            const uint2 rt = rowt[r];
-            const int b0 = (int)(rt.y & 0xFFFFu), b1 = (int)(rt.y >> 16);
-            const uint8_t* s0r = src + (int)(rt.x & 0xFFFFu) * Ps;
-            const uint8_t* s1r = src + (int)(rt.x >> 16) * Ps;
-            uint32_t out = 0;
-            const uint4 cx4 = *(const uint4*)(colsx + 4 * q), ca4 = *(const uint4*)(colal + 4 * q);
-            const uint32_t cxs[4] = {cx4.x, cx4.y, cx4.z, cx4.w}, cas[4] = {ca4.x, ca4.y, ca4.z, ca4.w};
+        // a thread keeps one column group q (its tables read once per level) and takes the rows
+        // r0, r0 + R, ... (R = NT / ng rows at a time), two per trip.  Per row and group: three
+        // aligned dwords of each source row realigned to the group's first tap (v_alignbyte),
+        // each pixel's two taps as u16s by one v_perm and HResizeLinear as one v_dot2 with the
+        // 16x alphas (H = 16 h, exact), as k_level's item3; VResizeLinearVec_32s8u as
+        // v_and + v_mul_hi_u32_u24 per term, or the scalar form past the SSE2 loop's end
+        const int R = NT / ng;
+        const Div dq(ng);
+        const int r0 = dq(tid), q = tid - r0 * ng;
+        if (r0 < R) {
+            const uint32_t bw = cbase[q];
+            const int base = (int)(bw & 0xFFFFu), o0 = (int)((bw >> 16) & 3u);
+            const bool all_simd = (bw >> 20) & 1u;
+            const uint32_t simd_bits = bw >> 21;
+            const uint4 sl4 = csel[q], al4 = cal[q];
+            const uint32_t sels[4] = {sl4.x, sl4.y, sl4.z, sl4.w}, als[4] = {al4.x, al4.y, al4.z, al4.w};
+            const int xg = cd.fx0 + 4 * q;
+            const bool own_x = xg >= cd.ox0 && xg < cd.ox1;
+            constexpr int RU = 2;
+            for (int rb = r0; rb < fh; rb += RU * R) {
+                uint2 rt[RU];
+                uint32_t w[RU][2][3];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int sx = (int)(cxs[j] & 0xFFFFu);
-                const int a0 = (int)(cas[j] & 0xFFFFu), a1 = (int)(cas[j] >> 16);
-                const int h0 = s0r[sx] * a0 + s0r[sx + 1] * a1;
-                const int h1 = s1r[sx] * a0 + s1r[sx + 1] * a1;
-                out |= (uint32_t)vresize(h0, h1, b0, b1, (cxs[j] >> 16) != 0u) << (8 * j);
-            }
-            *(uint32_t*)(dst + r * Pd + 4 * q) = out;
-            const int y = cd.fy0 + r, xg = cd.fx0 + 4 * q;
-            if (y >= cd.oy0 && y < cd.oy1 && xg >= cd.ox0 && xg < cd.ox1) {
-                uint8_t* d = dlev + (size_t)y * Ld.pitch + xg;
-                if (xg + 4 <= cd.ox1) *(uint32_t*)d = out;
-                else
-                    for (int j = 0; xg + j < cd.ox1; ++j) d[j] = (uint8_t)(out >> (8 * j));
+                for (int u = 0; u < RU; ++u) rt[u] = rowt[min(rb + u * R, fh - 1)];
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const uint32_t* a = (const uint32_t*)(src + (int)(rt[u].x & 0xFFFFu) * Ps + base);
+                    const uint32_t* c2 = (const uint32_t*)(src + (int)(rt[u].x >> 16) * Ps + base);
+                    w[u][0][0] = a[0]; w[u][0][1] = a[1]; w[u][0][2] = a[2];
+                    w[u][1][0] = c2[0]; w[u][1][1] = c2[1]; w[u][1][2] = c2[2];
+                }
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const int r = rb + u * R;
+                    if (r >= fh) break;
+                    const uint32_t wa0 = __builtin_amdgcn_alignbyte(w[u][0][1], w[u][0][0], o0);
+                    const uint32_t wa1 = __builtin_amdgcn_alignbyte(w[u][0][2], w[u][0][1], o0);
+                    const uint32_t wc0 = __builtin_amdgcn_alignbyte(w[u][1][1], w[u][1][0], o0);
+                    const uint32_t wc1 = __builtin_amdgcn_alignbyte(w[u][1][2], w[u][1][1], o0);
+                    const int b0 = (int)(rt[u].y & 0xFFFFu), b1 = (int)(rt[u].y >> 16);
+                    const uint32_t bs0 = (uint32_t)b0 << 8, bs1 = (uint32_t)b1 << 8;
+                    uint32_t out = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const us2 al = __builtin_bit_cast(us2, als[j]);
+                        const uint32_t H0 = __builtin_amdgcn_udot2(
+                            __builtin_bit_cast(us2, __builtin_amdgcn_perm(wa1, wa0, sels[j])), al, 0u, false);
+                        const uint32_t H1 = __builtin_amdgcn_udot2(
+                            __builtin_bit_cast(us2, __builtin_amdgcn_perm(wc1, wc0, sels[j])), al, 0u, false);
+                        // SSE2 form: ((h >> 4) * b) >> 16 = mulhi_u24((16 h) & ~0xFF, b << 8); the
+                        // two terms are <= 1020 together, so no saturation (see item3)
+                        uint32_t v = (mulhi_u24(H0 & ~0xFFu, bs0) +
+                                      mulhi_u24(H1 & ~0xFFu, bs1) + 2u) >> 2;
+                        if (!all_simd && !((simd_bits >> j) & 1u))
+                            v = min((uint32_t)((__umul24(H0 >> 4, (uint32_t)b0) + __umul24(H1 >> 4, (uint32_t)b1) +
+                                                (1u << 21)) >> 22), 255u);
+                        out |= v << (8 * j);
+                    }
+                    *(uint32_t*)(dst + r * Pd + 4 * q) = out;
+                    const int y = cd.fy0 + r;
+                    if (own_x && y >= cd.oy0 && y < cd.oy1) {
+                        uint8_t* d = dlev + (size_t)y * Ld.pitch + xg;
+                        if (xg + 4 <= cd.ox1) *(uint32_t*)d = out;
+                        else
+                            for (int j = 0; xg + j < cd.ox1; ++j) d[j] = (uint8_t)(out >> (8 * j));
+                    }
+                }
             }
         }
+        CSTAMP(19 + 2 * l);
         __syncthreads();
         CSTAMP(2 + 2 * l);
         chain_rows<NT>(cd, Ld, dst, Pd, rsum, g, tid);
