@@ -314,7 +314,8 @@ static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
 #define OCT_SMALL_BATCH 16
 #endif
 #ifndef CHAIN_MAX_BATCH
-#define CHAIN_MAX_BATCH 16     // images per call up to which the pyramid is one k_pyr_chain launch
+#define CHAIN_MAX_BATCH 8      // images per call up to which the pyramid is one k_pyr_chain launch
+                               // (r5c16: 16 images lost at K = 8 sessions, 9.5-9.9 k vs 10.2-10.7 k pairs/s)
 #endif
 #ifndef SIDE_MIN_BATCH
 #define SIDE_MIN_BATCH 16      // images per call from which the default side branch forks

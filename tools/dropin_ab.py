@@ -21,6 +21,9 @@ SETTINGS = {   # "_args": extra arguments of the bench program (facade_test: "fr
     "frame": {"_args": "frame"},
     "frame_solo": {"_args": "frame", "ORBX_FRAME_SERVER": "0"},
     "frame_nochain": {"_args": "frame", "ORBX_CHAIN_MAX_BATCH": "0"},
+    "frame_chain2": {"_args": "frame", "ORBX_CHAIN_MAX_BATCH": "2"},
+    "frame_chain4": {"_args": "frame", "ORBX_CHAIN_MAX_BATCH": "4"},
+    "frame_chain8": {"_args": "frame", "ORBX_CHAIN_MAX_BATCH": "8"},
     "frame_nostage": {"_args": "frame", "ORBX_STAGE_THREAD": "0"},
     "frame_stage2": {"_args": "frame", "ORBX_STAGE_THREAD": "2"},
     "frame_nograph": {"_args": "frame", "ORBX_EXTRACT_GRAPH": "0"},
