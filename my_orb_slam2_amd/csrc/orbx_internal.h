@@ -144,7 +144,10 @@ struct LevelRowTab {
 struct ChainRect {
     int16_t ox0, ox1, oy0, oy1, fx0, fx1, fy0, fy1;
 };
-__host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 8; }
+// LDS row of a footprint: 4 bytes of left pad (x = fx0 - 4 .. fx0 - 1: the reflected columns
+// left of the image), the footprint, and 8 bytes of slack (the reflected columns right of it,
+// the resize's third dword)
+__host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 12; }
 // LDS words of a level's k_pyr_chain tables (ng column groups, fh rows): per group a base word,
 // padded to a multiple of 4, then 4 v_perm selectors and 4 alpha pairs; per row two words
 // (fh rounded up to even, so every level's tables start 16-byte aligned)

@@ -1184,34 +1184,53 @@ struct Div {
     __device__ int operator()(int i) const { return d > 1 ? (int)__umulhi((uint32_t)i, m) : i; }
 };
 
+// Reflected columns of a footprint that touches the image's left / right edge, written into
+// its rows' pads (x = -1..-3 <- 1..3, x = W..W+2 <- W-2..W-4: BORDER_REFLECT_101), so that the
+// blur's row pass reads every group as an interior one.  Returns whether it wrote anything (the
+// caller then needs a barrier before the row pass); uniform over the workgroup.
+template <int NT>
+__device__ __forceinline__ bool chain_fill(const ChainRect& c, const LevelGeom& Lv, uint8_t* buf,
+                                           int P, int tid) {
+    const int W = Lv.w, fh = c.fy1 - c.fy0 + 1;
+    const bool left = c.fx0 == 0, right = c.fx1 == W - 1;
+    if (!left && !right) return false;
+    for (int i = tid; i < 2 * fh; i += NT) {
+        const int r = i >> 1;
+        uint8_t* row = buf + r * P + 4 - c.fx0;   // row[x] = pixel x
+        if ((i & 1) == 0 && left) {
+            row[-1] = row[min(1, W - 1)];
+            row[-2] = row[reflect101_fast(-2, W)];
+            row[-3] = row[reflect101_fast(-3, W)];
+        } else if ((i & 1) == 1 && right) {
+            row[W] = row[reflect101_fast(W, W)];
+            row[W + 1] = row[reflect101_fast(W + 1, W)];
+            row[W + 2] = row[reflect101_fast(W + 2, W)];
+        }
+    }
+    return true;
+}
+
 // Row pass of the blur of level l's owned rectangle (rows oy0 - 3 .. oy1 + 2, reflected) from
-// its footprint in LDS (src, origin (fx0, fy0), row pitch P) into rsum (int row sums, RW =
-// 4 ng per row).  Interior groups (every tap inside the row: xg >= 3, xg + 6 < W) read three
-// aligned dwords (bytes xg - 4 .. xg + 7; fx0 and ox0 are multiples of 4) and form the sums
-// as v_dot4 on shifted words, as tile_out_rows; the <= 3 border groups of a row take their
-// ten reflected bytes one by one, as separate items so that no wave of interior items runs
-// that path.
+// its footprint in LDS (src: padded rows, chain_pitch P) into rsum (int row sums, RW = 4 ng per
+// row): three aligned dwords per 4-pixel group (bytes xg - 4 .. xg + 7, the left pad and
+// chain_fill's reflected columns included), the sums as v_dot4 on shifted words, as
+// tile_out_rows.
 template <int NT>
 __device__ __forceinline__ void chain_rows(const ChainRect& c, const LevelGeom& Lv, const uint8_t* src,
                                            int P, int* rsum, const Geometry* g, int tid) {
     const int ow = c.ox1 - c.ox0, oh = c.oy1 - c.oy0;
     if (ow <= 0 || oh <= 0) return;
     const int ng = (ow + 3) >> 2, RW = 4 * ng;
-    const int W = Lv.w, H = Lv.h;
-    const int t0 = g->taps[0], t1 = g->taps[1], t2 = g->taps[2], t3 = g->taps[3];
-    const int t4 = g->taps[4], t5 = g->taps[5], t6 = g->taps[6];
-    const int q_lo = c.ox0 >= 3 ? 0 : 1;
-    const int rq = W - 7 - c.ox0;
-    const int q_hi = max(q_lo, min(ng, rq >= 0 ? rq / 4 + 1 : 0));
-    const int ni = q_hi - q_lo, nb = ng - ni;
-    const uint32_t tapA = (uint32_t)t0 | (uint32_t)t1 << 8 | (uint32_t)t2 << 16 | (uint32_t)t3 << 24;
-    const uint32_t tapB = (uint32_t)t4 | (uint32_t)t5 << 8 | (uint32_t)t6 << 16;
-    const Div di(ni > 0 ? ni : 1);
-    for (int i = tid; i < (oh + 6) * ni; i += NT) {
-        const int rr = di(i), q = q_lo + (i - rr * ni);
+    const int H = Lv.h;
+    const uint32_t tapA = (uint32_t)g->taps[0] | (uint32_t)g->taps[1] << 8 | (uint32_t)g->taps[2] << 16 |
+                          (uint32_t)g->taps[3] << 24;
+    const uint32_t tapB = (uint32_t)g->taps[4] | (uint32_t)g->taps[5] << 8 | (uint32_t)g->taps[6] << 16;
+    const Div dv(ng);
+    for (int i = tid; i < (oh + 6) * ng; i += NT) {
+        const int rr = dv(i), q = i - rr * ng;
         const int ry = reflect101_fast(c.oy0 - 3 + rr, H) - c.fy0;
         const int xg = c.ox0 + 4 * q;
-        const uint32_t* sw = (const uint32_t*)(src + ry * P + (xg - 4 - c.fx0));
+        const uint32_t* sw = (const uint32_t*)(src + ry * P + (xg - c.fx0));   // x = xg - 4 ..
         const uint32_t d0 = sw[0], d1 = sw[1], d2 = sw[2];
         int4 o;
         o.x = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tapA,
@@ -1221,24 +1240,6 @@ __device__ __forceinline__ void chain_rows(const ChainRect& c, const LevelGeom& 
         o.z = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tapA,
                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), tapB, 0u, false), false);
         o.w = (int)__builtin_amdgcn_udot4(d1, tapA, __builtin_amdgcn_udot4(d2, tapB, 0u, false), false);
-        *(int4*)(rsum + rr * RW + 4 * q) = o;
-    }
-    const Div db(nb > 0 ? nb : 1);
-    for (int i = tid; i < (oh + 6) * nb; i += NT) {
-        const int rr = db(i), k = i - rr * nb;
-        const int q = k < q_lo ? k : q_hi + (k - q_lo);
-        const uint8_t* sr = src + (reflect101_fast(c.oy0 - 3 + rr, H) - c.fy0) * P;
-        const int xg = c.ox0 + 4 * q;
-        int v[10];
-#pragma unroll
-        for (int k2 = 0; k2 < 10; ++k2)   // pixels past the row's last keep an in-row value
-            v[k2] = sr[reflect101_fast(min(xg - 3 + k2, W + 2), W) - c.fx0];
-        int4 o;
-        int* op = (int*)&o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            op[j] = t0 * v[j] + t1 * v[j + 1] + t2 * v[j + 2] + t3 * v[j + 3] + t4 * v[j + 4] +
-                    t5 * v[j + 5] + t6 * v[j + 6];
         *(int4*)(rsum + rr * RW + 4 * q) = o;
     }
 }
@@ -1401,17 +1402,18 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         const int i = tid + u * NT;
         if (i < nst) {
             const int r = dv0(i), q = i - r * ndw;
-            ((uint32_t*)(smem + r * P0))[q] = sv[u];
+            ((uint32_t*)(smem + r * P0))[q + 1] = sv[u];   // after the row's 4-byte pad
         }
     }
     for (int i = tid + SK * NT; i < nst; i += NT) {   // footprints beyond SK * NT words
         const int r = dv0(i), q = i - r * ndw;
-        ((uint32_t*)(smem + r * P0))[q] = *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q);
+        ((uint32_t*)(smem + r * P0))[q + 1] = *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q);
     }
     __syncthreads();
     CSTAMP(2);
     // 3. level 0's blur rows; then per level l >= 1: the previous level's blur columns beside
     //    this level's resize (they share no LDS), then this level's blur rows
+    if (chain_fill<NT>(c0, LG[0], smem, P0, tid)) __syncthreads();
     chain_rows<NT>(c0, LG[0], smem, P0, rsum, g, tid);
     __syncthreads();
     CSTAMP(3);
@@ -1460,8 +1462,8 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
                 for (int u = 0; u < RU; ++u) rt[u] = rowt[min(rb + u * R, fh - 1)];
 #pragma unroll
                 for (int u = 0; u < RU; ++u) {
-                    const uint32_t* a = (const uint32_t*)(src + (int)(rt[u].x & 0xFFFFu) * Ps + base);
-                    const uint32_t* c2 = (const uint32_t*)(src + (int)(rt[u].x >> 16) * Ps + base);
+                    const uint32_t* a = (const uint32_t*)(src + (int)(rt[u].x & 0xFFFFu) * Ps + 4 + base);
+                    const uint32_t* c2 = (const uint32_t*)(src + (int)(rt[u].x >> 16) * Ps + 4 + base);
                     w[u][0][0] = a[0]; w[u][0][1] = a[1]; w[u][0][2] = a[2];
                     w[u][1][0] = c2[0]; w[u][1][1] = c2[1]; w[u][1][2] = c2[2];
                 }
@@ -1492,7 +1494,7 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
                                                 (1u << 21)) >> 22), 255u);
                         out |= v << (8 * j);
                     }
-                    *(uint32_t*)(dst + r * Pd + 4 * q) = out;
+                    *(uint32_t*)(dst + r * Pd + 4 + 4 * q) = out;
                     const int y = cd.fy0 + r;
                     if (own_x && y >= cd.oy0 && y < cd.oy1) {
                         uint8_t* d = dlev + (size_t)y * Ld.pitch + xg;
@@ -1506,6 +1508,7 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         CSTAMP(19 + 2 * l);
         __syncthreads();
         CSTAMP(2 + 2 * l);
+        if (chain_fill<NT>(cd, Ld, dst, Pd, tid)) __syncthreads();
         chain_rows<NT>(cd, Ld, dst, Pd, rsum, g, tid);
         __syncthreads();
         CSTAMP(3 + 2 * l);
