@@ -802,7 +802,7 @@ def valu_from_csv(paths, kernel):
     return counter_from_csv(paths, kernel, "SQ_INSTS_VALU")
 
 
-ISA_MIX = os.path.join(HERE, "profiles", "r04_isa_mix.json")
+ISA_MIX = os.path.join(HERE, "profiles", "r05_isa_mix.json")
 
 
 def _mangled_key(demangled: str) -> str:
@@ -818,7 +818,7 @@ def _mangled_key(demangled: str) -> str:
 
 def mix_cycles_from_csv(paths, kernel, mix_path=None):
     """Mean issue cycles per VALU instruction of a kernel group: each dispatch's SQ_INSTS_VALU
-    weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r04_isa_mix.json)."""
+    weighted by its kernel's static opcode-mix cost (tools/isa_mix.py, profiles/r05_isa_mix.json)."""
     import csv
     import glob
     try:

@@ -41,9 +41,13 @@ for step in "$@"; do
         || { echo "DROPIN BENCH FAILED"; tail -20 $OUT/dropin.err; exit 1; }
       echo dropin done ;;
     counters)
-      timeout -k 10 1200 bash tools/prof_counters.sh $OUT/prof --steps 10 --warmup 3 > $OUT/counters.log 2>&1 \
+      timeout -k 10 900 bash tools/prof_counters.sh $OUT/prof --steps 10 --warmup 3 > $OUT/counters.log 2>&1 \
         || { echo "COUNTERS FAILED"; tail -20 $OUT/counters.log; exit 1; }
       echo counters done ;;
+    counters_euroc)
+      timeout -k 10 900 bash tools/prof_counters.sh $OUT/prof_euroc --workload euroc --steps 10 --warmup 3 > $OUT/counters_euroc.log 2>&1 \
+        || { echo "EUROC COUNTERS FAILED"; tail -20 $OUT/counters_euroc.log; exit 1; }
+      echo euroc counters done ;;
     workloads)
       for w in euroc reloc triangulation bf kfdb tum; do
         timeout -k 10 300 python bench.py --workload $w --cpu-seconds 5 > $OUT/$w.json 2> $OUT/$w.err \
