@@ -36,14 +36,14 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r04_pmc_fetch_b512.csv", "r04_pmc_write_b512.csv"))
+                       ("r05_pmc_fetch_b512.csv", "r05_pmc_write_b512.csv"))
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                             ("r04_pmc_fetch_euroc.csv", "r04_pmc_write_euroc.csv"))
+                             ("r05_pmc_fetch_euroc.csv", "r05_pmc_write_euroc.csv"))
 # SQ_INSTS_VALU and SQ_ACTIVE_INST_VALU passes (the VALU issue entry beside the HBM roofline)
 DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
-                         ("r04_pmc_insts_b512.csv", "r04_pmc_busy_b512.csv"))
+                         ("r05_pmc_insts_b512.csv", "r05_pmc_busy_b512.csv"))
 DEFAULT_INSTS_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                               ("r04_pmc_insts_euroc.csv", "r04_pmc_busy_euroc.csv"))
+                               ("r05_pmc_insts_euroc.csv", "r05_pmc_busy_euroc.csv"))
 # VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
 # 2 cycles per SIMD for the full-rate class (add / logic / shifts / f32 mul-add), per 4 cycles
 # for the rest (v_dot*, v_perm, v_pk_*, v_bcnt, 32-bit min / max, conversions), measured by
@@ -115,7 +115,7 @@ def parse():
                     help="euroc: projected local-map MapPoints per frame")
     ap.add_argument("--insts-csv", default=None,
                     help="rocprofv3 --pmc CSV holding SQ_INSTS_VALU for the roofline's VALU issue "
-                         "entry (default: the committed profiles/r04_pmc_insts_*.csv)")
+                         "entry (default: the committed profiles/r05_pmc_insts_*.csv)")
     ap.add_argument("--traffic-csv", default=None,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"

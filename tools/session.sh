@@ -33,7 +33,7 @@ for step in "$@"; do
         || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
       python -c "import json,sys; j=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print('bench', j['value'], j['ms_per_step'], json.dumps(j.get('roofline'))[:400])" ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/prof.log 2>&1 \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --serial-steps 0 --no-kernel-timing > $OUT/prof.log 2>&1 \
         || { echo "PROF FAILED"; tail -20 $OUT/prof.log; exit 1; }
       echo prof done ;;
     dropin)
