@@ -52,8 +52,11 @@ def test_opencv_rounding_modes(oracle_mod, orbx_lib, gpu, simd):
 
 @pytest.mark.parametrize("params", [(500, 1.2, 8, 20, 7), (3000, 1.2, 8, 20, 7),
                                     (1000, 1.3, 6, 25, 10), (1500, 1.1, 12, 20, 7),
-                                    (1000, 2.0, 3, 20, 7)])
+                                    (1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_param_sweep(oracle_mod, orbx_lib, gpu, params):
+    """One image per call: the pyramid is one k_pyr_chain launch (scale 1.1-1.3), per-level
+    launches where the chain does not apply (2.0: the exact 2:1 area path; 2.5: a 4-pixel
+    group's taps span more than one v_perm window)."""
     g, o = _pair(oracle_mod, *params)
     _check_extract(g, o, synth.frame(21, 800, 600), f"params {params}")
 
