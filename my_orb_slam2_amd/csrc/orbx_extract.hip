@@ -210,8 +210,11 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define FAST_WPE 6     // minimum waves per SIMD requested from the register allocator (80 VGPRs)
 #endif
 #ifndef OCT_NT
-#define OCT_NT 256         // k_octree threads per list (64 / 128 / 256 / 512); 512 pairs per step:
-                           // 64 0.537, 128 0.377, 256 0.323 ms
+#define OCT_NT 128         // k_octree threads per list (64 / 128 / 256 / 512) at large batches.
+                           // Round 5, 512 pairs (r5v2 / r5v3): 128 threads 0.306 ms one-stream
+                           // against 0.265 for 256, but the scheduled step is 1 % faster
+                           // (128.5-128.9 k vs 127.2-127.5 k pairs/s): the smaller workgroups
+                           // pack beside the pyramid and FAST launches; 64 threads 0.398 ms
 #endif
 #ifndef OCT_NT_SMALL
 #define OCT_NT_SMALL 256   // ... when batch * levels <= 256; one stereo pair: 128 0.112, 256 0.081,

@@ -52,7 +52,8 @@ def run(bench_args):
             print(name, "FAILED rc", r.returncode, r.stderr[-2000:], flush=True)
             raise SystemExit(1)
         j = json.loads(r.stdout.strip().splitlines()[-1])
-        ks = (j.get("roofline") or {}).get("kernel_ms_per_step", {})
+        ks = (j.get("roofline") or {}).get("one_stream_ms_per_step") or \
+            (j.get("roofline") or {}).get("kernel_ms_per_step", {})
         extra = {k: j[k] for k in ("mean_stereo_matches", "mean_keypoints_left") if k in j}
         print(f"{name:14s} {j['value']:9.0f} /s  {j['ms_per_step']:.3f} ms  {ks}  {extra}",
               flush=True)
