@@ -985,7 +985,7 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
                   h->d_blur.ensure(B * G.pyr_bytes + blur_slack) &&
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
                   h->d_cand.ensure(B * G.cand_words * 4) &&
-                  h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 4) &&
+                  h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 6) &&
                   h->d_kscr.ensure(B * h->kscratch_per_image);
         const size_t o_kps = align_up(B * 4, 256);
         const size_t o_desc = o_kps + align_up(B * G.kp_cap * sizeof(orbx_keypoint), 256);
@@ -1035,6 +1035,7 @@ ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uin
     a.cand = h->d_cand.as<uint32_t>();
     a.ocnt = h->d_ocnt.as<int>();
     a.okp = h->d_okp.as<uint32_t>();
+    a.operm = (uint16_t*)(a.okp + (size_t)batch * h->hg.out_words);
     a.kscratch = h->d_kscr.as<uint8_t>();
     a.kscratch_per_image = h->kscratch_per_image;
     a.ncap = h->ncap;

@@ -230,6 +230,17 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #define OCT_BUCKET_SORT 2   // phase-2 order by size buckets: 1 ranks inside a bucket, 2 a stable
                             // counting sort (the list order is the seq order)
 #endif
+#ifndef OD_SPATIAL
+#define OD_SPATIAL 1   // k_orient_desc takes a level's keypoints in band / column order (operm)
+#endif
+#ifndef OD_SP_XS
+#define OD_SP_XS 5     // ... columns of 32 pixels
+#endif
+#ifndef OD_SP_YS
+#define OD_SP_YS 5     // ... in bands of 32 rows.  r5d, 512 pairs: k_orient_desc 1.094 ms in
+                       // list order, 1.054 / 1.068 / 1.098 ms for bands of 32 / 64 / 128 rows
+                       // (k_octree +0.007 ms for the order)
+#endif
 #ifndef OD_WPE
 #define OD_WPE 5       // at most 96 VGPRs: five waves per SIMD (6: spills)
 #endif
@@ -915,7 +926,8 @@ extern "C" int orbx_diag_octree_stamps(unsigned long long* out) {
 template <int NT, bool KEYS_LDS>
 __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
                              int level, int ncand, uint32_t* kdata, int16_t* knode, uint8_t* kq,
-                             OctreeSmem& sm, int* __restrict__ ocnt, uint32_t* __restrict__ okp) {
+                             OctreeSmem& sm, int* __restrict__ ocnt, uint32_t* __restrict__ okp,
+                             uint16_t* __restrict__ operm) {
     const int tid = threadIdx.x;
     const int N = L.nfeat;
     int* tmp = sm.tmp;
@@ -1312,14 +1324,57 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
 
     // ---- retain the best keypoint of each node (src/ORBextractor.cc:743-762) ----
     uint32_t* best = (uint32_t*)sm.cc;
+#if OD_SPATIAL
+    // k_orient_desc's processing order (operm): the keypoints by bands of 2^OD_SP_YS rows,
+    // each band by columns of 2^OD_SP_XS pixels, so the keypoints a workgroup takes together
+    // are neighbours and their patch lines are shared in L1 / L2.  Inside a bucket the order
+    // is that of LDS atomics (not deterministic, and it needs not be: every keypoint's angle
+    // and descriptor are computed on their own and written at their list index).
+    // (taller bands while the buckets would not fit the node arrays' scratch)
+    const int sp_cols = (L.w + (1 << OD_SP_XS) - 1) >> OD_SP_XS;
+    int sp_ys = OD_SP_YS;
+    while (sp_ys < 12 && sp_cols * ((L.h + (1 << sp_ys) - 1) >> sp_ys) > sm.ncap) ++sp_ys;
+    const int sp_nb = sp_cols * ((L.h + (1 << sp_ys) - 1) >> sp_ys);
+    const bool spatial = sp_nb <= sm.ncap;
+    int* sp_hist = sm.pre;
+    if (spatial)
+        for (int i = tid; i < sp_nb; i += NT) sp_hist[i] = 0;
+#endif
     for (int i = tid; i < S; i += NT) best[i] = 0;
     __syncthreads();
     for (int k = tid; k < ncand; k += NT)
         atomicMax(&best[knode[k]], ((uint32_t)cand_s(kdata[k]) << 24) | (uint32_t)(0xFFFFFF - k));
     __syncthreads();
     uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
+#if OD_SPATIAL
+    uint16_t* perm = operm + (size_t)b * g->out_words + L.out_off;
+    for (int i = tid; i < S; i += NT) {
+        const uint32_t w = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
+        out[i] = w;
+        if (spatial) {   // bucket << 16 | rank in the bucket, over the consumed best entry
+            const int bk = (cand_y(w) >> sp_ys) * sp_cols + (cand_x(w) >> OD_SP_XS);
+            best[i] = (uint32_t)bk << 16 | (uint32_t)atomicAdd(&sp_hist[bk], 1);
+        } else {
+            perm[i] = (uint16_t)i;
+        }
+    }
+    if (tid == 0) ocnt[b * g->nlevels + level] = S;
+    if (spatial) {
+        __syncthreads();
+        int* sp_start = sm.pre2;
+        chunked_scan<NT>(sp_nb, sm.tmp, [&](int c) { return sp_hist[c]; },
+                         [&](int c, int ex) { sp_start[c] = ex; });
+        __syncthreads();
+        for (int i = tid; i < S; i += NT) {
+            const uint32_t kr = best[i];
+            perm[sp_start[kr >> 16] + (kr & 0xFFFFu)] = (uint16_t)i;
+        }
+    }
+#else
+    (void)operm;
     for (int i = tid; i < S; i += NT) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
     if (tid == 0) ocnt[b * g->nlevels + level] = S;
+#endif
     OSTAMP(61);
 }
 
@@ -1329,6 +1384,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                                                 const int* __restrict__ ccnt,
                                                 const uint32_t* __restrict__ cand,
                                                 int* __restrict__ ocnt, uint32_t* __restrict__ okp,
+                                                uint16_t* __restrict__ operm,
                                                 uint8_t* __restrict__ kscratch,
                                                 long long kscratch_per_image, int NCAP, int KCAP,
                                                 int level_base) {
@@ -1438,7 +1494,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
         });
 #endif
     __syncthreads();
-    octree_level<NT, decltype(keys_lds_c)::value>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp);
+    octree_level<NT, decltype(keys_lds_c)::value>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp, operm);
     };
     if (in_lds)
         gather_and_split(l_kdata, l_knode, l_kq, std::true_type{});
@@ -1540,8 +1596,9 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) void k_orient_desc(
     const Geometry* __restrict__ g, const uint8_t* __restrict__ pyr,
     const uint8_t* __restrict__ blur, const int* __restrict__ ocnt,
-    const uint32_t* __restrict__ okp, float* __restrict__ kps, uint8_t* __restrict__ desc,
-    int* __restrict__ nkp, int blk_base, int nkp_blk) {
+    const uint32_t* __restrict__ okp, const uint16_t* __restrict__ operm,
+    float* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ nkp, int blk_base,
+    int nkp_blk) {
     __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][OD_PATCH_DW];
     int blk, b;
     xcd_block(blk, b);
@@ -1564,8 +1621,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     for (int l = 0; l < level; ++l) off += oc[l];
     const LevelGeom& L = g->lv[level];
     const int pitch = L.pitch;
-    // every keypoint word of the wave in one load: lane k holds keypoint k
-    const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
+    // every keypoint word of the wave in one load: lane k holds keypoint k (processing
+    // position i0 + k, list index oi)
+#if OD_SPATIAL
+    const int oi = operm[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
+#else
+    const int oi = i0 + min(lane, nk - 1);
+#endif
+    const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + oi];
 
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
     const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
@@ -1625,6 +1688,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)cw, k1);
         return half ? c1 : c0;
     };
+    // the keypoint whose patch a load of pair p reads (diagnostic builds 7 / 8 only: the
+    // wave's first keypoint for every pair / the pair's first keypoint for both halves)
+    auto ld_word = [&](int p) {
+#if OD_DIAG == 7
+        (void)p;
+        return (uint32_t)__builtin_amdgcn_readlane((int)cw, 0);
+#elif OD_DIAG == 8
+        return (uint32_t)__builtin_amdgcn_readlane((int)cw, min(2 * p, nk - 1));
+#else
+        return kp_word(p);
+#endif
+    };
     uint32_t* P = patch[wid][half];
     const int npair = (nk + 1) >> 1;
     // buffer loads: one 32-bit offset add per load instead of a 64-bit address
@@ -1638,14 +1713,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     raw_t vr[OD_RL4];
     blr_t v[OD_BL4];
     auto issue_raw = [&](int p) {
-        const uint32_t c = kp_word(p);
+        const uint32_t c = ld_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
         const uint32_t vo = __umul24((uint32_t)(y - 15), (uint32_t)pitch) + (uint32_t)((x - 15) & ~3);
 #pragma unroll
         for (int j = 0; j < OD_RL4; ++j) vr[j] = od_load<OD_RAW_W>(rraw, vo + sor4[j]);
     };
     auto issue_blr = [&](int p) {
-        const uint32_t c = kp_word(p);
+        const uint32_t c = ld_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
 #if BLUR_STRIPE
         const uint32_t vo = (uint32_t)((x - 18) >> 4) * sh16 + 16u * (uint32_t)(y - 18);
@@ -1733,7 +1808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const float ca_l = glibc_cosf(ang), sb_l = glibc_sinf(ang);
 #endif
     if (lane < nk) {
-        const size_t o = (size_t)b * g->kp_cap + off + i0 + lane;
+        const size_t o = (size_t)b * g->kp_cap + off + oi;
         const int x = cand_x(cw) + ORBX_MIN_BORDER, y = cand_y(cw) + ORBX_MIN_BORDER;
         float* kp = kps + o * 7;
         const float sc = L.scale;
@@ -1816,8 +1891,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
             words[w] = half ? (uint32_t)(m >> 32) : (uint32_t)m;
         }
         const int k = 2 * p + half;
+        const int oi0 = __builtin_amdgcn_readlane(oi, k0), oi1 = __builtin_amdgcn_readlane(oi, k1);
         if (k < nk && l32 < 8) {
-            const size_t o = (size_t)b * g->kp_cap + off + i0 + k;
+            const size_t o = (size_t)b * g->kp_cap + off + (half ? oi1 : oi0);
             uint32_t wv = words[0];
 #pragma unroll
             for (int w = 1; w < 8; ++w) wv = l32 == w ? words[w] : wv;
@@ -1847,7 +1923,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
 #define ORBX_OCT_LAUNCH(N)                                                                   \
         ORBX_TIMED_LAUNCH(T, K_OCTREE, k_octree<N>, grid, dim3(N), lds, s, a.dg, a.cells,     \
                           (const int*)a.ccnt, (const uint32_t*)a.cand, a.ocnt, a.okp,         \
-                          a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
+                          a.operm, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
         if (nt == 64) ORBX_OCT_LAUNCH(64);
         else if (nt == 128) ORBX_OCT_LAUNCH(128);
         else if (nt == 512) ORBX_OCT_LAUNCH(512);
@@ -1857,7 +1933,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     auto orient = [&](int blk0, int nblk, int nkp_blk, hipStream_t s) {
         ORBX_TIMED_LAUNCH(T, K_ORIENT, k_orient_desc, dim3(nblk, a.batch), dim3(256), 0, s, a.dg,
                           (const uint8_t*)a.pyr, (const uint8_t*)a.blur, (const int*)a.ocnt,
-                          (const uint32_t*)a.okp, a.kps, a.desc, a.nkp, blk0, nkp_blk);
+                          (const uint32_t*)a.okp, (const uint16_t*)a.operm, a.kps, a.desc, a.nkp,
+                          blk0, nkp_blk);
     };
     // Side branch: the first FAST_SIDE_LV levels' FAST (FAST_SIDE 2: + their octree, 3: + their
     // orientation / descriptors) run on the handle's side stream, forked (event) before level

@@ -7,6 +7,7 @@
 //   cand  [B][Σ cells cap_c]   u32   packed candidates (x:12 | y:12 | score:8), raster order
 //   ocnt  [B][L]               i32   keypoints per level after the octree
 //   okp   [B][Σ_l out_cap_l]   u32   packed octree survivors in list order
+//   operm [B][Σ_l out_cap_l]   u16   k_orient_desc's processing order (list indices), after okp
 //   kps   [B][kp_cap]          orbx_keypoint (cv::KeyPoint layout), level-major
 //   desc  [B][kp_cap][32]      u8
 //   nkp   [B]                  i32

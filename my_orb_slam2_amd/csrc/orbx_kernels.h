@@ -116,6 +116,7 @@ struct ExtractLaunch {
     uint32_t* cand;
     int* ocnt;
     uint32_t* okp;
+    uint16_t* operm;   // [B][out_words] k_orient_desc's processing order (list indices)
     uint8_t* kscratch;
     long long kscratch_per_image;
     int ncap, kcap;          // level 0 (the largest node list)
