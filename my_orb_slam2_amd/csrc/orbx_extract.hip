@@ -233,6 +233,9 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
 #ifndef OD_SPATIAL
 #define OD_SPATIAL 1   // k_orient_desc takes a level's keypoints in band / column order (operm)
 #endif
+#ifndef OD_SPATIAL_MIN_BATCH
+#define OD_SPATIAL_MIN_BATCH 16   // ... for batches of at least this many images
+#endif
 #ifndef OD_SP_XS
 #define OD_SP_XS 5     // ... columns of 32 pixels
 #endif
@@ -1335,7 +1338,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     int sp_ys = OD_SP_YS;
     while (sp_ys < 12 && sp_cols * ((L.h + (1 << sp_ys) - 1) >> sp_ys) > sm.ncap) ++sp_ys;
     const int sp_nb = sp_cols * ((L.h + (1 << sp_ys) - 1) >> sp_ys);
-    const bool spatial = sp_nb <= sm.ncap;
+    const bool spatial = operm != nullptr && sp_nb <= sm.ncap;
     int* sp_hist = sm.pre;
     if (spatial)
         for (int i = tid; i < sp_nb; i += NT) sp_hist[i] = 0;
@@ -1347,14 +1350,14 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     __syncthreads();
     uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
 #if OD_SPATIAL
-    uint16_t* perm = operm + (size_t)b * g->out_words + L.out_off;
+    uint16_t* perm = operm != nullptr ? operm + (size_t)b * g->out_words + L.out_off : nullptr;
     for (int i = tid; i < S; i += NT) {
         const uint32_t w = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
         out[i] = w;
         if (spatial) {   // bucket << 16 | rank in the bucket, over the consumed best entry
             const int bk = (cand_y(w) >> sp_ys) * sp_cols + (cand_x(w) >> OD_SP_XS);
             best[i] = (uint32_t)bk << 16 | (uint32_t)atomicAdd(&sp_hist[bk], 1);
-        } else {
+        } else if (operm != nullptr) {
             perm[i] = (uint16_t)i;
         }
     }
@@ -1624,7 +1627,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     // every keypoint word of the wave in one load: lane k holds keypoint k (processing
     // position i0 + k, list index oi)
 #if OD_SPATIAL
-    const int oi = operm[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)];
+    const int oi = operm != nullptr ? operm[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)]
+                                    : i0 + min(lane, nk - 1);
 #else
     const int oi = i0 + min(lane, nk - 1);
 #endif
@@ -1910,6 +1914,9 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     KernelTimer dummy;
     KernelTimer& T = a.timer ? *a.timer : dummy;
     const int nt = (long long)a.batch * G.nlevels <= 256 ? OCT_NT_SMALL : OCT_NT;
+    // the spatial orientation order pays on large batches only (its L1 / L2 reuse); a lone
+    // frame keeps the list order and skips the octree's bucket pass (operm = null)
+    uint16_t* const operm = a.batch >= OD_SPATIAL_MIN_BATCH ? a.operm : nullptr;
     auto fast = [&](int c0, int c1, hipStream_t s) {
         if (c1 <= c0) return;
         const int nc = a.fast_nc;
@@ -1923,7 +1930,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
 #define ORBX_OCT_LAUNCH(N)                                                                   \
         ORBX_TIMED_LAUNCH(T, K_OCTREE, k_octree<N>, grid, dim3(N), lds, s, a.dg, a.cells,     \
                           (const int*)a.ccnt, (const uint32_t*)a.cand, a.ocnt, a.okp,         \
-                          a.operm, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
+                          operm, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
         if (nt == 64) ORBX_OCT_LAUNCH(64);
         else if (nt == 128) ORBX_OCT_LAUNCH(128);
         else if (nt == 512) ORBX_OCT_LAUNCH(512);
@@ -1933,7 +1940,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     auto orient = [&](int blk0, int nblk, int nkp_blk, hipStream_t s) {
         ORBX_TIMED_LAUNCH(T, K_ORIENT, k_orient_desc, dim3(nblk, a.batch), dim3(256), 0, s, a.dg,
                           (const uint8_t*)a.pyr, (const uint8_t*)a.blur, (const int*)a.ocnt,
-                          (const uint32_t*)a.okp, (const uint16_t*)a.operm, a.kps, a.desc, a.nkp,
+                          (const uint32_t*)a.okp, (const uint16_t*)operm, a.kps, a.desc, a.nkp,
                           blk0, nkp_blk);
     };
     // Side branch: the first FAST_SIDE_LV levels' FAST (FAST_SIDE 2: + their octree, 3: + their
