@@ -157,7 +157,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     // 2. per left keypoint: descriptor search (src/Frame.cc:542-587) + SAD (:591-667)
     const float maxD = mbf / mb;   // minZ = mb, maxD = mbf/minZ (Frame.cc:534-536)
     const float minD = 0;
-#if ST_DIAG >= 3   // diagnostic builds only: phase 1 alone
+#if ST_DIAG == 3   // diagnostic builds only: phase 1 alone
     if (NL >= 0) return;
 #endif
     const int chunk = (NL + nsplit - 1) / nsplit;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
         int best = 100, bestR = -1;   // ORBmatcher::TH_HIGH, strict '<': first minimum wins
         int bestE = -1;
-#if ST_DIAG >= 2   // diagnostic builds only: no descriptor search (and so no SAD)
+#if ST_DIAG == 2 || ST_DIAG == 3   // diagnostic builds only: no descriptor search (and so no SAD)
         if (row >= 0) continue;
 #endif
         // octaves levelL-1 .. levelL+1: a right keypoint of octave o whose band
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
         if (bestR < 0 || best >= 75) continue;   // thOrbDist = (TH_HIGH + TH_LOW) / 2
 
-#if ST_DIAG   // diagnostic builds only (tools/variants.py): descriptor search without the SAD
+#if ST_DIAG >= 1 && ST_DIAG <= 3   // diagnostic builds only (tools/variants.py): search without the SAD
         if (bestE >= 0) continue;
 #endif
         // ---- sliding-window SAD on the unblurred level of the left keypoint ----
@@ -251,7 +251,14 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         const int pitch = LV.pitch;
         const uint8_t* PL = pyrL + (size_t)b * g->pyr_bytes + LV.off;
         const uint8_t* PR = pyrR + (size_t)b * g->pyr_bytes + LV.off;
+#if ST_DIAG == 4   // timing diagnostics only (wrong SADs): every lane of a wave reads one window
+        const int yl = __builtin_amdgcn_readfirstlane((int)scaledvL), xl = __builtin_amdgcn_readfirstlane((int)scaleduL),
+                  xr = __builtin_amdgcn_readfirstlane((int)scaleduR0);
+#elif ST_DIAG == 5   // ... every lane reads its own rows, all in the wave's first lane's lines
+        const int yl = __builtin_amdgcn_readfirstlane((int)scaledvL), xl = (int)scaleduL, xr = (int)scaleduR0;
+#else
         const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
+#endif
         int acc[11];
         if constexpr (LPK == 1) {
             int accl[11];   // its own array: declared outside, `acc` made this path spill
