@@ -1237,31 +1237,41 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             // past N), and no chunk after the one that holds J
             if (tid == 0) tmp[24] = nV - 1;   // past the scan's NT / 64 partials
             __syncthreads();
+            // the same scan gives every scanned node its processing position and its
+            // children-before prefix (nonempty = delta + 1, so the prefix is the deltas' + j);
+            // the nodes of J's chunk past J are marked unprocessed again below
+            int c_last = 0;
             {
                 int carry = 0;
                 for (int c0 = 0; c0 < nV; c0 += NT) {
                     const int j = c0 + tid;
-                    const int delta = j < nV ? nonempty((int)(sm.sortb[j] & 0xFFFF)) - 1 : 0;
+                    const int n = j < nV ? (int)(sm.sortb[j] & 0xFFFF) : 0;
+                    const int delta = j < nV ? nonempty(n) - 1 : 0;
                     int tot;
                     const int ex = block_excl_scan<NT / 64>(delta, tmp, tot);
+                    if (j < nV) {
+                        sm.pre[n] = carry + ex + j;
+                        sm.pord[n] = (int16_t)j;
+                    }
                     const uint64_t past = __ballot(j < nV && S + carry + ex + delta >= N);
                     if (past && (threadIdx.x & 63) == (int)__builtin_ctzll(past)) atomicMin(&tmp[24], j);
                     carry += tot;
+                    c_last = c0;
                     if (S + carry >= N) break;   // block-uniform
                 }
             }
             __syncthreads();
             const int J = tmp[24];
-            __syncthreads();
-            const int nP = J + 1;
-            // children-before prefix in processing order, over processed nodes only
-            Ctot = chunked_scan<NT>(
-                nP, tmp, [&](int j) { return nonempty((int)(sm.sortb[j] & 0xFFFF)); },
-                [&](int j, int ex) {
-                    const int n = (int)(sm.sortb[j] & 0xFFFF);
-                    sm.pre[n] = ex;
-                    sm.pord[n] = (int16_t)j;
-                });
+            {
+                const int j = c_last + tid;
+                if (j > J && j < nV) sm.pord[(int)(sm.sortb[j] & 0xFFFF)] = (int16_t)-1;
+            }
+            if (J >= 0) {   // nV = 0: nothing expandable, J = -1
+                const int nJ = (int)(sm.sortb[J] & 0xFFFF);
+                Ctot = sm.pre[nJ] + nonempty(nJ);
+            } else {
+                Ctot = 0;
+            }
             __syncthreads();
             Stot = chunked_scan<NT>(
                 S, tmp, [&](int i) { return sm.pord[i] >= 0 ? 0 : 1; },
