@@ -39,6 +39,11 @@ DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
                        ("r05_pmc_fetch_b512.csv", "r05_pmc_write_b512.csv"))
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
                              ("r05_pmc_fetch_euroc.csv", "r05_pmc_write_euroc.csv"))
+# FETCH_SIZE / WRITE_SIZE passes of the matcher workloads (tools/session.sh counters_match)
+DEFAULT_PMC_BY_WORKLOAD = {
+    "stereo": DEFAULT_PMC,
+    **{w: ",".join(os.path.join(HERE, "profiles", f"r06_pmc_{c}_{w}.csv") for c in ("fetch", "write"))
+       for w in ("bf", "reloc", "triangulation")}}
 # SQ_INSTS_VALU and SQ_ACTIVE_INST_VALU passes (the VALU issue entry beside the HBM roofline)
 DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
                          ("r05_pmc_insts_b512.csv", "r05_pmc_busy_b512.csv"))
@@ -110,6 +115,9 @@ def parse():
     ap.add_argument("--kfs", type=int, default=10000, help="reloc: keyframes in the database")
     ap.add_argument("--db-rows", type=int, default=10_000_000,
                     help="bf: database descriptors (10k keyframes x 1000, SURVEY §8(d) C4)")
+    ap.add_argument("--bf-kernel", choices=["mfma", "valu"], default="mfma",
+                    help="bf: the distance kernel of the line (k_bf_mfma, or north_star's XOR + "
+                         "v_bcnt k_bf_top2); the other one is timed after it as alt_kernel")
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
     ap.add_argument("--queries", type=int, default=2000,
                     help="euroc: projected local-map MapPoints per frame")
@@ -252,7 +260,7 @@ def main():
     relaunch_if_needed(args)
     keep_stdout_for_result()
     if args.traffic_csv is None:
-        args.traffic_csv = DEFAULT_PMC if args.workload == "stereo" else DEFAULT_PMC_EUROC
+        args.traffic_csv = DEFAULT_PMC_BY_WORKLOAD.get(args.workload, DEFAULT_PMC_EUROC)
     if args.insts_csv is None:
         args.insts_csv = DEFAULT_INSTS if args.workload == "stereo" else DEFAULT_INSTS_EUROC
     if args.workload == "euroc":
@@ -394,6 +402,7 @@ def main():
         roof = headline_roofline(prof, args.steps, sprof, args.serial_steps, sb.ext, B,
                                  args.traffic_csv, args.insts_csv)
         roof["overlap"] = {"mode": overlap[0], "fork_level": overlap[1], "levels": overlap[2]}
+        add_valu_floor(roof, ms_per_step)
     if serial:
         serial.pop("prof", None)
         serial.pop("kernel_ms_per_step", None)
@@ -721,18 +730,43 @@ def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 1e12   # T SIMD issue cycles/s (1024 SIMDs at 2.4 GHz)
 
 
+def valu_floor_ms(per_kernel):
+    """The step's VALU issue floor: every kernel group's wave instructions per step (PMC
+    SQ_INSTS_VALU per launch x launches per step) x its mean issue cycles per instruction (the
+    opcode mix priced at the measured gfx950 rates), over 1024 SIMDs x 2.4 GHz.  None if any
+    group lacks a VALU entry."""
+    cyc = 0.0
+    for k in HEADLINE_GROUPS:
+        e = per_kernel.get(k)
+        v = (e or {}).get("valu") or {}
+        if e is None:
+            continue
+        if not v.get("wave_instr_per_launch") or not v.get("mean_issue_cycles"):
+            return None
+        cyc += v["wave_instr_per_launch"] * e["launches_per_step"] * v["mean_issue_cycles"]
+    return 1000.0 * cyc / (VALU_ISSUE_PEAK * 1e12)
+
+
+def add_valu_floor(roof, ms_per_step):
+    """roof["valu_floor_ms"] (valu_floor_ms over the one-stream per_kernel entries) and
+    roof["valu_floor_frac"] = that floor over the timed step: how close the step is to the
+    roof that binds the integer pipeline chip-wide."""
+    f = valu_floor_ms(roof.get("per_kernel") or {})
+    roof["valu_floor_ms"] = f
+    roof["valu_floor_frac"] = f / ms_per_step if f and ms_per_step > 0 else None
+
+
 def label_binding_roof(e):
-    """Name the roof the counters show for a roofline entry.  The integer kernels are bound by
-    VALU issue, not HBM: when the PMC pass shows the SIMDs issuing VALU work most of the launch
-    (the mix-aware busy fraction >= 0.7, or rocprof's 4-cycle VALUBusy >= 0.9) and that exceeds
-    the HBM fraction, `bound` is "valu" and achieved / peak / frac are VALU issue cycles per
-    second against 1024 SIMDs x 2.4 GHz; the HBM figures move to `hbm`.  `traffic` stays the
-    PMC HBM bytes per launch either way."""
+    """Name the roof the counters show for a roofline entry: the larger of its VALU issue
+    fraction (the mix-aware busy fraction from the PMC passes) and its HBM fraction.  When VALU
+    is larger, `bound` is "valu" and achieved / peak / frac are VALU issue cycles per second
+    against 1024 SIMDs x 2.4 GHz; the HBM figures move to `hbm` either way.  `traffic` stays
+    the PMC HBM bytes per launch."""
     v = e.get("valu") or {}
-    busy, b4 = v.get("busy_frac"), v.get("valubusy_4cycle")
+    busy = v.get("busy_frac")
     hbm = {"achieved": e.get("achieved"), "peak": e.get("peak"), "unit": e.get("unit"),
            "frac": e.get("frac")}
-    if busy is None or not ((b4 or 0) >= 0.9 or busy >= 0.7) or busy <= (e.get("frac") or 0):
+    if busy is None or busy <= (e.get("frac") or 0):
         e["hbm"] = hbm
         return
     ach = v["wave_instr_per_launch"] * v["mean_issue_cycles"] / (e["avg_launch_ms"] / 1000.0) / 1e12
@@ -1672,13 +1706,17 @@ def main_match(args):
                     "hbm": {"achieved": db_bytes / avg_s / 1e9, "unit": "GB/s",
                             "peak": HBM_PEAK_GBS,
                             "frac": db_bytes / avg_s / 1e9 / HBM_PEAK_GBS,
-                            "algorithmic_bytes_per_launch": db_bytes}}
+                            "algorithmic_bytes_per_launch": db_bytes,
+                            **pmc_hbm(args.traffic_csv, kern, avg_s)}}
+            roof["traffic"] = roof["hbm"]["traffic"]
         else:
             nbytes = float(sum(fs.n for fs in kfs) * (32 + 28 + 4 + 1))
             ach = nbytes / avg_s / 1e9
+            pm = pmc_hbm(args.traffic_csv, kern, avg_s)
             roof = {"kernel": kern, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                    "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": avg_s * 1000.0}
+                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": pm["traffic"],
+                    "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": avg_s * 1000.0,
+                    "pmc": pm}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = match_cpu_baseline(args, torch, keep if args.workload == "reloc" else None,
@@ -1733,6 +1771,51 @@ def bf_query(ndb: int, nq: int = 1000, seed: int = 7):
     return q, ids, rows
 
 
+BF_KERNELS = {"mfma": "k_bf_mfma", "valu": "k_bf_top2"}
+BF_KERNEL_IDS = {"mfma": 0, "valu": 1}      # ORBX_BF_MFMA / ORBX_BF_VALU (include/orbx_match.h)
+
+
+def pmc_hbm(traffic_csv, kernel, avg_s):
+    """PMC HBM traffic of one launch of `kernel` (FETCH_SIZE x 2 + WRITE_SIZE from the passes
+    in traffic_csv, MI355X_MICROARCH.md §HBM) and the rate it gives over the launch's HIP-event
+    duration, or Nones when no pass holds the kernel."""
+    tr = traffic_from_csv(traffic_csv, kernel)
+    if not tr or avg_s <= 0:
+        return {"traffic": None, "traffic_GBs": None, "traffic_frac": None}
+    return {"traffic": tr, "traffic_GBs": tr / avg_s / 1e9, "traffic_frac": tr / avg_s / 1e9 / HBM_PEAK_GBS}
+
+
+def bf_roofline(kname, prof, nq, nrows, traffic_csv):
+    """Roofline of one brute-force top-2 launch pair (the distance kernel + k_bf_merge, one
+    timer interval): k_bf_mfma against the dense i8 matrix peak (256 multiply-adds per
+    distance), k_bf_top2 against the int32 lane-op roof (8 XOR + 8 BCNT per distance); both
+    against the XOR + BCNT issue roof and HBM (the shard's rows read once per query frame:
+    algorithmic bytes; PMC traffic of the distance kernel from traffic_csv)."""
+    if not prof or not prof.get("k_bf", (0, 0))[1]:
+        return None
+    tot_ms, launches = prof["k_bf"]
+    avg_s = tot_ms / 1000.0 / launches
+    dist_n = float(nq) * nrows
+    dps = dist_n / avg_s
+    db_bytes = 32.0 * nrows + 32.0 * nq + 12.0 * nq
+    if kname == "k_bf_mfma":
+        ops = 512.0 * dist_n
+        unit, peak, bound = "TOPS (int8 MFMA)", I8_MFMA_PEAK_TOPS, "mfma"
+    else:
+        ops = 16.0 * dist_n
+        unit, peak, bound = "Tops/s (int32 lane-ops)", VALU_PEAK_TOPS, "valu"
+    hbm = {"achieved": db_bytes / avg_s / 1e9, "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "frac": db_bytes / avg_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": db_bytes}
+    pm = pmc_hbm(traffic_csv, kname, avg_s)
+    hbm.update(pm)
+    return {"kernel": kname + " + k_bf_merge", "bound": bound, "achieved": ops / avg_s / 1e12,
+            "peak": peak, "unit": unit, "frac": ops / avg_s / 1e12 / peak,
+            "traffic": pm["traffic"], "algorithmic_ops_per_launch": ops,
+            "avg_launch_ms": avg_s * 1000.0, "distances_per_s": dps,
+            "issue_peak_distances_per_s": DIST_ISSUE_PEAK, "issue_frac": dps / DIST_ISSUE_PEAK,
+            "hbm": hbm}
+
+
 def main_bf(args):
     """configs[3] as a pure brute-force top-2: one query frame (1000 descriptors) against the
     whole descriptor database (default 10^7 rows = 10k keyframes x 1000), the rows sharded
@@ -1767,6 +1850,7 @@ def main_bf(args):
     nq = len(qh)
     dq = torch.from_numpy(qh).to(dev)
     m = ORBmatcher(0.75, True, device=local)
+    m.set_bf_kernel(BF_KERNEL_IDS[args.bf_kernel])
     out = [torch.empty(nq, dtype=torch.int32, device=dev) for _ in range(3)]
 
     def step():
@@ -1798,31 +1882,37 @@ def main_bf(args):
         elapsed = float(t.item())
     prof = m.collect_profile() if not args.no_kernel_timing else {}
     bi, bd, sd = (t.cpu().numpy() for t in res)
-    roof = None
-    if prof and prof.get("k_bf", (0, 0))[1]:
-        tot_ms, launches = prof["k_bf"]
-        avg_s = tot_ms / 1000.0 / launches
-        dist_n = float(nq) * (r1 - r0)
-        dps = dist_n / avg_s
-        db_bytes = 32.0 * (r1 - r0) + 32.0 * nq + 12.0 * nq
-        kname = load().orbx_bf_kernel().decode()
-        if kname == "k_bf_mfma":
-            # +-1 int8 dot products: 256 multiply-adds (512 int8 ops) per distance, priced
-            # against the dense i8 matrix peak
-            ops = 512.0 * dist_n
-            unit, peak, bound = "TOPS (int8 MFMA)", I8_MFMA_PEAK_TOPS, "mfma"
-        else:
-            ops = 16.0 * dist_n                       # 8 XOR + 8 BCNT per 256-bit distance
-            unit, peak, bound = "Tops/s (int32 lane-ops)", VALU_PEAK_TOPS, "valu"
-        roof = {"kernel": kname + " + k_bf_merge", "bound": bound, "achieved": ops / avg_s / 1e12,
-                "peak": peak, "unit": unit,
-                "frac": ops / avg_s / 1e12 / peak, "traffic": None,
-                "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_s * 1000.0,
-                "distances_per_s": dps, "issue_peak_distances_per_s": DIST_ISSUE_PEAK,
-                "issue_frac": dps / DIST_ISSUE_PEAK,
-                "hbm": {"achieved": db_bytes / avg_s / 1e9, "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                        "frac": db_bytes / avg_s / 1e9 / HBM_PEAK_GBS,
-                        "algorithmic_bytes_per_launch": db_bytes}}
+    kname = BF_KERNELS[args.bf_kernel]
+    roof = bf_roofline(kname, prof, nq, r1 - r0, args.traffic_csv)
+    # north_star's kernel beside the default: the other distance kernel timed on the same
+    # inputs after the timed region (same steps, same collectives), its results compared
+    alt = None
+    if not args.no_kernel_timing:
+        akey = "valu" if args.bf_kernel == "mfma" else "mfma"
+        m.set_bf_kernel(BF_KERNEL_IDS[akey])
+        for _ in range(2):
+            res_a = step()
+        torch.cuda.synchronize(dev)
+        m.collect_profile()
+        if dist_on:
+            dist.barrier(device_ids=[local])
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            res_a = step()
+        torch.cuda.synchronize(dev)
+        if dist_on:
+            dist.barrier(device_ids=[local])
+        el_a = time.perf_counter() - t1
+        if dist_on:
+            t = torch.tensor([el_a], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_a = float(t.item())
+        prof_a = m.collect_profile()
+        same = all(bool(torch.equal(x, y)) for x, y in zip(res_a, res))
+        alt = {"kernel": BF_KERNELS[akey], "value": args.steps / el_a, "unit": "query frames/sec",
+               "ms_per_step": 1000.0 * el_a / args.steps, "outputs_equal_default": same,
+               "roofline": bf_roofline(BF_KERNELS[akey], prof_a, nq, r1 - r0, args.traffic_csv)}
+        m.set_bf_kernel(BF_KERNEL_IDS[args.bf_kernel])
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:
@@ -1855,7 +1945,7 @@ def main_bf(args):
                            "parallelism": f"row shards x{world}, RCCL broadcast + all-gather "
                                           "of per-query top-2, merge in rank order"},
                 "planted_found": found, "mean_best_dist": float(bd.mean()),
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "alt_kernel": alt, "cpu_baseline": cpu}
         emit(json.dumps(line))
     if dist_on:
         dist.destroy_process_group()

@@ -93,6 +93,30 @@ orbx_status orbx_extractor_prepare(orbx_extractor* h, int width, int height, int
 orbx_status orbx_pyramid_level(orbx_extractor* h, int index, int level, uint8_t* out,
                                int* width, int* height);
 
+/* ORBextractor::mvImagePyramid as the reference keeps it: filled by every operator()
+ * (src/ORBextractor.cc:1129-1154, sized in the constructor at :433).  With host_pyramid on,
+ * every orbx_extract / orbx_extract_view on the handle also copies its image's pyramid (all
+ * levels, 1.51 MB at KITTI size) into a pinned host block of the handle's own, in the same
+ * device sequence (the DMA runs beside the FAST / octree / descriptor kernels), and
+ * orbx_host_pyramid_view then points at it: level l is height[l] rows of width[l] bytes,
+ * step[l] bytes apart (the layout of a cv::Mat ROI, like the reference's levels, which are
+ * views into a bordered image).  The block stays valid until the next orbx_extract(_view) on
+ * the handle or its destruction; no other call writes it.  ORBX_ERR_STATE when the last such
+ * call ran with host_pyramid off (the default) or failed.  The drop-in facade
+ * (integration/ORBextractor.h) turns it on in its constructor. */
+orbx_status orbx_extractor_host_pyramid(orbx_extractor* h, int on);
+/* A counter that changes whenever the handle's pyramids do (every extraction or stereo frame on
+ * it, a workspace regrowth): a caller that keeps (handle, image index) as the source of a view's
+ * pyramid (the facade after ExtractStereo) detects that the source moved on. */
+uint64_t orbx_extractor_serial(const orbx_extractor* h);
+typedef struct {
+    int nlevels;
+    const uint8_t* data[16];
+    int width[16], height[16];
+    size_t step[16];
+} orbx_host_pyramid;
+orbx_status orbx_host_pyramid_view(const orbx_extractor* h, orbx_host_pyramid* out);
+
 /* The 7x7 Gaussian of level `level` that the descriptors sample (the `workingMat` clone
  * blurred at src/ORBextractor.cc:1107-1108), copied to host like orbx_pyramid_level. */
 orbx_status orbx_blur_level(orbx_extractor* h, int index, int level, uint8_t* out, int* width,

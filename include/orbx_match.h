@@ -163,7 +163,10 @@ orbx_status orbx_search_by_projection(orbx_matcher* m, int32_t mode,
  * flags: ORBX_PROJ_PREFILTER returns every accepted query's feature without the
  * rotation-consistency filter (LAST_FRAME / KEYFRAME), *nmatches = the accepted count, so the
  * caller can apply the reference's per-feature filter itself (rotHist holds feature indices,
- * :1508 / :1637: with overwritten matches a feature can sit in two bins).
+ * :1508 / :1637: with overwritten matches a feature can sit in two bins).  LAST_FRAME with
+ * check_orientation and any ORBX_QF_NO_CLAIM query requires ORBX_PROJ_PREFILTER
+ * (ORBX_ERR_INVALID otherwise): the reference clears per feature (:1516-1535), which a
+ * per-query filter cannot reproduce once a feature is matched twice.
  * Replaces the same ORBmatcher methods as orbx_search_by_projection, which equals this call
  * with qflags = NULL and flags = 0. */
 enum { ORBX_QF_NO_CLAIM = 1 };
@@ -283,8 +286,14 @@ orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int
                                         int32_t* d_best_idx, int32_t* d_best_dist,
                                         int32_t* d_second_dist, void* stream);
 
-/* The kernel the brute-force top-2 runs its distances in: "k_bf_mfma" (+-1 int8 dot products
- * on the matrix cores, the default build) or "k_bf_top2" (v_xor + v_bcnt on the vector ALUs). */
+/* The kernel the brute-force top-2 of a matcher runs its distances in (results are identical):
+ * ORBX_BF_MFMA (the default): k_bf_mfma, +-1 int8 dot products on the matrix cores;
+ * ORBX_BF_VALU: k_bf_top2, v_xor + v_bcnt on the vector ALUs (north_star's "no MFMA" form). */
+enum { ORBX_BF_MFMA = 0, ORBX_BF_VALU = 1 };
+orbx_status orbx_matcher_set_bf_kernel(orbx_matcher* m, int32_t kernel);
+/* The kernel name of that choice ("k_bf_mfma" / "k_bf_top2"); NULL for an unknown value. */
+const char* orbx_bf_kernel_name(int32_t kernel);
+/* The default's name ("k_bf_mfma"). */
 const char* orbx_bf_kernel(void);
 
 /* Waits for `stream` and returns ORBX_ERR_CAPACITY if a batched call on this matcher met a

@@ -7,17 +7,27 @@
 // ExtractORB threads at Frame.cc:89-92) compile unchanged: the constructor, operator() and the
 // getters keep the reference's signatures and results.
 //
-// One difference: mvImagePyramid is no longer filled by every operator() call.  Its only
-// reader in the reference is Frame::ComputeStereoMatches (Frame.cc:503-619), which the glue in
-// orbx_slam2_glue.h replaces with the device-resident orbx_stereo_match.  Code that still needs
-// the host pyramid calls MaterializePyramid() after operator().  After the one-call stereo Frame
-// (orbx_glue::ExtractStereo) both extractors' MaterializePyramid() return their view's levels
-// when the LEFT extractor has KeepPyramid(true), and throw otherwise, whether the frame ran
-// alone or in a frame-server batch (include/orbx.h orbx_extractor_keep_pyramid).
+// mvImagePyramid keeps the reference's contract: sized nlevels in the constructor
+// (ORBextractor.cc:433) and refilled by every operator() (:1129-1154), so the reference's own
+// Frame::ComputeStereoMatches (Frame.cc:503-619) runs unchanged on it.  Its levels are cv::Mat
+// headers over liborbx's pinned host copy of the pyramid (orbx_extractor_host_pyramid: one DMA
+// inside the extraction's device sequence, beside its FAST / octree / descriptor kernels), valid
+// until this extractor's next operator(), like the reference's, which views into a bordered
+// image that the next call replaces.
+//
+// Opt-out: the glue in orbx_slam2_glue.h replaces that only reader with the device-resident
+// orbx_stereo_match (ComputeStereoMatches) or the one-call stereo Frame (ExtractStereo), and
+// turns the copy off on the extractors it drives (SetHostPyramid(false)).  operator() then
+// leaves nlevels empty Mats, and code that still needs the host pyramid calls
+// MaterializePyramid() after the call.  After ExtractStereo both extractors'
+// MaterializePyramid() return their view's levels when the LEFT extractor has KeepPyramid(true),
+// and throw otherwise, whether the frame ran alone or in a frame-server batch (include/orbx.h
+// orbx_extractor_keep_pyramid).
 #ifndef ORBX_INTEGRATION_ORBEXTRACTOR_H
 #define ORBX_INTEGRATION_ORBEXTRACTOR_H
 
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -49,6 +59,8 @@ public:
                                     mvLevelSigma2.data(), mvInvLevelSigma2.data(),
                                     mnFeaturesPerLevel.data()),
               "orbx_extractor_tables");
+        mvImagePyramid.resize(nlevels);  // :433
+        SetHostPyramid(true);
     }
     ~ORBextractor() { orbx_extractor_destroy(h); }
     ORBextractor(const ORBextractor&) = delete;
@@ -74,9 +86,21 @@ public:
         pyramid_valid = false;
         pyr_src = h;
         pyr_index = 0;
+        pyr_owner = alive;
+        pyr_serial = orbx_extractor_serial(h);
         if (n < 0) {  // empty image inside liborbx as well
             keypoints.clear();
             return;
+        }
+        // :1129-1154: this call's levels, headers over liborbx's pinned copy
+        orbx_host_pyramid hp{};
+        if (host_pyramid && orbx_host_pyramid_view(h, &hp) == ORBX_OK) {
+            for (int l = 0; l < nlevels; ++l)
+                mvImagePyramid[l] = cv::Mat(hp.height[l], hp.width[l], CV_8U,
+                                            const_cast<uint8_t*>(hp.data[l]), hp.step[l]);
+            pyramid_valid = true;
+        } else {
+            for (int l = 0; l < nlevels; ++l) mvImagePyramid[l] = cv::Mat();
         }
         const cv::KeyPoint* k = reinterpret_cast<const cv::KeyPoint*>(kp);
         keypoints.assign(k, k + n);
@@ -100,11 +124,19 @@ public:
     std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
     std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
-    // Copies the last call's pyramid (ORBextractor.cc:1129-1155's levels, the unblurred
-    // images) into mvImagePyramid; a no-op when it is already current.  Throws when the last
-    // call left no pyramid (a stereo Frame without KeepPyramid, see the file comment).
+    // Fills mvImagePyramid with the last call's pyramid (ORBextractor.cc:1129-1155's levels,
+    // the unblurred images); a no-op when it is already current (after operator() with the
+    // host pyramid on).  Throws when the last call left no pyramid (a stereo Frame without
+    // KeepPyramid, see the file comment).
     std::vector<cv::Mat>& MaterializePyramid() {
         if (!pyramid_valid) {
+            // the source of this view's pyramid must still be the call that set it (after
+            // ExtractStereo the right view's source is the left extractor's handle)
+            if (pyr_owner.expired())
+                throw std::runtime_error("MaterializePyramid: the pyramid's extractor is gone");
+            if (orbx_extractor_serial(pyr_src) != pyr_serial)
+                throw std::runtime_error("MaterializePyramid: the pyramid's extractor ran "
+                                         "another call since this view's frame");
             mvImagePyramid.resize(nlevels);
             for (int l = 0; l < nlevels; ++l) {
                 int w = 0, hh = 0;
@@ -119,6 +151,14 @@ public:
         return mvImagePyramid;
     }
 
+    // Whether operator() refreshes mvImagePyramid (orbx_extractor_host_pyramid; on from the
+    // constructor).  The glue switches it off where it replaces the pyramid's only reader.
+    void SetHostPyramid(bool on) {
+        check(orbx_extractor_host_pyramid(h, on ? 1 : 0), "orbx_extractor_host_pyramid");
+        host_pyramid = on;
+    }
+    bool HostPyramid() const { return host_pyramid; }
+
     // orbx_extractor_keep_pyramid on this extractor's handle: a stereo Frame extracted through
     // it (orbx_glue::ExtractStereo, this being the LEFT extractor) leaves both views' pyramids.
     void KeepPyramid(bool on) { check(orbx_extractor_keep_pyramid(h, on ? 1 : 0), "orbx_extractor_keep_pyramid"); }
@@ -129,6 +169,8 @@ public:
         pyramid_valid = false;
         pyr_src = from->h;
         pyr_index = index;
+        pyr_owner = from->alive;
+        pyr_serial = orbx_extractor_serial(from->h);
     }
 
     // The liborbx handle, for orbx_stereo_match (orbx_slam2_glue.h).
@@ -155,9 +197,13 @@ protected:
     std::vector<float> mvInvLevelSigma2;
 
 private:
+    bool host_pyramid = false;
     bool pyramid_valid = false;
     orbx_extractor* pyr_src = nullptr;   // the handle and image holding this view's pyramid
     int pyr_index = 0;
+    uint64_t pyr_serial = 0;             // pyr_src's orbx_extractor_serial when it was set
+    std::shared_ptr<int> alive = std::make_shared<int>(0);   // expires with this extractor
+    std::weak_ptr<int> pyr_owner;        // ... and with pyr_src's
 };
 
 }  // namespace ORB_SLAM2

@@ -32,8 +32,12 @@ inline void check(orbx_status s, const char* what) {
 // Frame.cc:496-686 for the last extraction of both cameras.  The reference reads the member
 // mb uninitialised at Frame.cc:534 (it is set only after ComputeStereoMatches returns in the
 // stereo constructor, Frame.cc:66-120); the intended value mbf / fx is passed instead.
+// It reads the device pyramids, so it turns the extractors' host pyramid copy off for the
+// frames after this one (integration/ORBextractor.h, the opt-out).
 template <class Frame>
 int ComputeStereoMatches(Frame& F) {
+    if (F.mpORBextractorLeft->HostPyramid()) F.mpORBextractorLeft->SetHostPyramid(false);
+    if (F.mpORBextractorRight->HostPyramid()) F.mpORBextractorRight->SetHostPyramid(false);
     F.mvuRight = std::vector<float>(F.N, -1.0f);
     F.mvDepth = std::vector<float>(F.N, -1.0f);
     int nvalid = 0;
@@ -67,6 +71,10 @@ int ExtractStereo(Frame& F, const cv::Mat& imLeft, const cv::Mat& imRight) {
     }
     if (imLeft.rows != imRight.rows || imLeft.cols != imRight.cols)
         throw std::invalid_argument("ExtractStereo: left and right sizes differ");
+    // the match reads the device pyramids: no host copy from the extractors' operator()
+    // (empty images above) either
+    if (F.mpORBextractorLeft->HostPyramid()) F.mpORBextractorLeft->SetHostPyramid(false);
+    if (F.mpORBextractorRight->HostPyramid()) F.mpORBextractorRight->SetHostPyramid(false);
     orbx_stereo_frame_out o{};
     check(orbx_stereo_frame_view(F.mpORBextractorLeft->handle(), imLeft.data,
                                  (size_t)imLeft.step, imRight.data, (size_t)imRight.step,

@@ -110,6 +110,8 @@ SIGNATURES = {
     "orbx_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
     "orbx_hamming_bf_top2": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, _vp, _vp, _vp]),
     "orbx_bf_kernel": (ctypes.c_char_p, []),
+    "orbx_bf_kernel_name": (ctypes.c_char_p, [_i]),
+    "orbx_matcher_set_bf_kernel": (_i, [_vp, _i]),
     "orbx_hamming_bf_top2_device": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, ctypes.c_int64,
                                          _vp, _vp, _vp, _vp]),
     "orbx_matcher_profile_enable": (_i, [_vp, _i]),

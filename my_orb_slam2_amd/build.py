@@ -79,6 +79,9 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(),
     """Compile the library (if stale, or always with force).  `extra_flags` / `out` build a
     tuning variant (tools/variants.py) next to the product library."""
     target = pathlib.Path(out) if out else LIB
+    if extra_flags and target.resolve() == LIB.resolve():
+        # the product library is the sources as they are: no variant or diagnostic switches
+        raise ValueError(f"refusing to build {LIB.name} with extra flags {list(extra_flags)}")
     digest = source_hash(extra_flags)
     if not force and embedded_hash(target) == digest:
         return target

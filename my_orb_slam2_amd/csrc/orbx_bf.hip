@@ -33,16 +33,7 @@ namespace orbx {
 
 namespace {
 
-#ifndef BF_PIPE
-#define BF_PIPE 1      // k_bf_top2: ping-pong row groups (0: 8-row groups, one wait each)
-#endif
-#ifndef BF_PACKED
-#define BF_PACKED 1    // k_bf_top2: packed 16-bit top-2 keys over blocks of BF_BLK rows
-#endif
 #define BF_BLK 256     // rows per packed block (128 pairs: the pair index fits 7 bits)
-#ifndef BF_MFMA
-#define BF_MFMA 1      // the distances on the matrix cores (k_bf_mfma) instead of k_bf_top2
-#endif
 
 constexpr uint32_t BF_NONE = 256u << 23;       // (distance 256, row 0): the loop's initial value
 constexpr int BF_ROW_BITS = 23;                 // rows per chunk < 2^23
@@ -98,7 +89,6 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
 #pragma unroll
             for (int k = 0; k < 8; ++k) g[j][k] = p[(size_t)(e0 + j) * 8 + k];
     };
-#if BF_PACKED
     // Blocks of BF_BLK rows with the top-2 kept as packed 16-bit keys: rows e0 + 2i (low half)
     // and e0 + 2i + 1 (high half) get the key (distance << 7 | i), built by two v_lshl_or per
     // row pair; the top-2 update is three v_pk_min/max_u16 per pair (second = max(best,
@@ -156,37 +146,6 @@ __global__ __launch_bounds__(256) void k_bf_top2(const uint32_t* __restrict__ q,
         pair(B[2], B[3], (uint32_t)(o / 2 + 3) * 0x10001u, h1, h2);
         fold(h1, h2, e);
     }
-#else
-    auto group = [&](const uint32_t (&g)[BF_G][8], int e0) {
-#pragma unroll
-        for (int j = 0; j < BF_G; ++j) row(g[j], e0 + j);
-    };
-#if BF_PIPE == 0
-    // plain groups of 8 rows: all 8 rows' loads, one wait, then the 8 rows
-    for (; e + 8 <= n; e += 8) {
-        uint32_t A[BF_G][8], B[BF_G][8];
-        load(A, e);
-        load(B, e + BF_G);
-        group(A, e);
-        group(B, e + BF_G);
-    }
-#else
-    if (n >= 2 * BF_G) {
-        uint32_t A[BF_G][8], B[BF_G][8];
-        load(A, 0);
-        for (; e + 4 * BF_G <= n; e += 2 * BF_G) {
-            load(B, e + BF_G);
-            group(A, e);
-            load(A, e + 2 * BF_G);
-            group(B, e + BF_G);
-        }
-        load(B, e + BF_G);
-        group(A, e);
-        group(B, e + BF_G);
-        e += 2 * BF_G;
-    }
-#endif
-#endif
     for (; e < n; ++e) row(p + (size_t)e * 8, e);
     if (qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1, b2);
 }
@@ -418,7 +377,9 @@ size_t bf_partial_bytes(long long ndb, int nq, int chunk) {
     return (size_t)nchunks * (size_t)nqpad * sizeof(uint2);
 }
 
-const char* bf_kernel_name() { return BF_MFMA ? "k_bf_mfma" : "k_bf_top2"; }
+const char* bf_kernel_name(int kernel) {
+    return kernel == ORBX_BF_MFMA ? "k_bf_mfma" : kernel == ORBX_BF_VALU ? "k_bf_top2" : nullptr;
+}
 
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer) {
     if (a.nq <= 0) return hipSuccess;
@@ -427,7 +388,7 @@ hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer)
     if (nchunks > INT32_MAX / 2) return hipErrorInvalidValue;
     hipEvent_t e = timer ? timer->start(st) : nullptr;
     if (nchunks > 0)
-        hipLaunchKernelGGL(BF_MFMA ? k_bf_mfma : k_bf_top2, dim3(nqpad / 256, (unsigned)nchunks),
+        hipLaunchKernelGGL(a.kernel == ORBX_BF_VALU ? k_bf_top2 : k_bf_mfma, dim3(nqpad / 256, (unsigned)nchunks),
                            dim3(256), 0, st, (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db,
                            a.ndb, a.chunk, nqpad, (uint2*)a.part);
     hipLaunchKernelGGL(k_bf_merge, dim3((a.nq + 31) / 32), dim3(256), 0, st, (const uint2*)a.part,

@@ -123,6 +123,12 @@ struct orbx_extractor {
     size_t h_in_n = 0;
     uint8_t* h_out = nullptr;
     size_t h_out_n = 0;
+    // mvImagePyramid on the host (orbx_extractor_host_pyramid): every orbx_extract(_view) also
+    // copies its image's pyramid block here (a pinned block of its own: no other call writes it)
+    bool host_pyr = false;
+    bool host_pyr_ok = false;   // h_pyr holds the last orbx_extract(_view)'s pyramid
+    uint8_t* h_pyr = nullptr;
+    size_t h_pyr_n = 0;
     // ORBextractor tables
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> nfeat;
@@ -155,6 +161,7 @@ struct orbx_extractor {
     // orbx_pyramid_level).  A stereo frame (orbx_stereo_frame_view) leaves them only when
     // keep_pyr is set, solo or served alike (orbx_extractor_keep_pyramid)
     int pyr_images = 0;
+    uint64_t serial = 0;     // +1 whenever the pyramids change (orbx_extractor_serial)
     bool keep_pyr = false;
     bool fs_user = false;    // counted as a user of its frame server (released with the last)
     std::unique_ptr<OrbxStager> stager;   // created by the first stereo-frame call
@@ -254,29 +261,6 @@ int vresize_simd_end(int width) {
     return x;
 }
 
-#ifndef LEVEL_STRIP
-#define LEVEL_STRIP 1  // 0: every level on the tiled k_level
-#endif
-// Output rows per strip of level l: `def`; tuning builds (-DORBX_TUNING, tools/strip_sweep.py)
-// also read ORBX_STRIP_TH="h0,h1,..." (0 or a missing entry keeps the default).  The product
-// library never reads the environment.
-static int strip_height(int l, int def) {
-    int th = def;
-#ifdef ORBX_TUNING
-    if (const char* e = getenv("ORBX_STRIP_TH")) {
-        for (int i = 0; i <= l && e; ++i) {
-            const int v = atoi(e);
-            if (i == l && v > 0) th = std::min(v, 4096);
-            e = strchr(e, ',');
-            if (e) ++e;
-        }
-    }
-#else
-    (void)l;
-#endif
-    return th;
-}
-
 // Strip height of a level for a batch of nimg images: STRIP_TH rows while the level's strip
 // walks give every SIMD of the device (ncu CUs x 4) two waves, else the tallest of 32 / 16 / 8
 // rows that does (8 at most).  A strip walk is a serial chain of rows, so a small batch (one
@@ -296,46 +280,27 @@ static void strip_heights(const orbx_extractor* h, int nimg, int* sth) {
     for (int l = 0; l < ORBX_MAX_LEVELS; ++l) sth[l] = STRIP_TH;
     for (int l = 0; l < h->hg.nlevels; ++l) {
         const LevelGeom& lv = h->hg.lv[l];
-        if (lv.strip) sth[l] = strip_height(l, strip_default(lv, nimg, h->ncu));
+        if (lv.strip) sth[l] = strip_default(lv, nimg, h->ncu);
     }
 }
 
 static int stereo_split_of(int pairs) { return orbx::stereo_split(pairs); }
 
-// Small-batch launch policies.  Tuning builds (-DORBX_TUNING) read an environment override
-// (tools/variants.py A/B runs); the product library never reads the environment.
-#ifndef OCT_LDS_SMALL_KB
+// Small-batch launch policies.
 #define OCT_LDS_SMALL_KB 152   // octree LDS budget for small batches (one workgroup per list)
-#endif
-#ifndef OCT_SMALL_BATCH
+#define OCT_SMALL_BATCH 16
 // images per call up to which the octree takes that budget (one workgroup per CU is still
 // every list at once up to 32 images; a frame-server batch of 2-16 images: 46.4 -> 42.0 us
 // with 16 instead of 4, r4aa)
-#define OCT_SMALL_BATCH 16
-#endif
-#ifndef CHAIN_MAX_BATCH
 #define CHAIN_MAX_BATCH 8      // images per call up to which the pyramid is one k_pyr_chain launch
                                // (r5c16: 16 images lost at K = 8 sessions, 9.5-9.9 k vs 10.2-10.7 k pairs/s)
-#endif
-#ifndef SIDE_MIN_BATCH
 #define SIDE_MIN_BATCH 16      // images per call from which the default side branch forks
-#endif
-static int tuned(const char* name, int def) {
-#ifdef ORBX_TUNING
-    if (const char* e = getenv(name)) return atoi(e);
-#else
-    (void)name;
-#endif
-    return def;
-}
 
 // k_fast cells per wave: FAST_NC (the next cell's ROI loads overlap the current cell) while the
 // launch gives every CU two workgroups, fewer for small batches (a wave's cells run in series,
 // so one image's FAST is a chain of FAST_NC cells otherwise).
 static int fast_cells_per_wave(int ncells, int batch, int ncu) {
-    int nc = tuned("ORBX_FAST_NC", 0);
-    if (nc > 0) return nc;
-    nc = FAST_NC;
+    int nc = FAST_NC;
     while (nc > 1 && (long long)ncells * batch / (4 * nc) < 2LL * ncu) nc >>= 1;
     return nc;
 }
@@ -363,11 +328,9 @@ static bool wait_idle(orbx_extractor* h) {
 // last event for up to WAIT_SPIN_US (yielding the core between polls) before a blocking wait.
 // A blocking wait returns tens of microseconds after the work ends (the thread sleeps); the
 // drop-in path waits twice per stereo frame on its critical path.
-#ifndef WAIT_SPIN_US
 #define WAIT_SPIN_US 400
-#endif
 static bool wait_done(orbx_extractor* h) {
-    const int spin_us = tuned("ORBX_WAIT_SPIN_US", WAIT_SPIN_US);
+    const int spin_us = WAIT_SPIN_US;
     if (spin_us > 0) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
@@ -400,7 +363,7 @@ void build_strip_tables(orbx_extractor* h, int l, int mode, const int16_t* xofs,
     Geometry& G = h->hg;
     LevelGeom& lv = G.lv[l];
     lv.strip = 0;
-    if (!LEVEL_STRIP || (mode != 0 && mode != 3)) return;
+    if (mode != 0 && mode != 3) return;
     const LevelGeom& S = G.lv[l > 0 ? l - 1 : 0];
     lv.snh = (lv.w + SW_PX - 1) / SW_PX;
     lv.snw = (lv.snh + 1) / 2;
@@ -646,8 +609,8 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
                     // k_fast stages the ROI as aligned dwords: <= cols + 6 bytes per row
                     {
                         const int lpc = std::max((c.cols + 6 + 3) / 4, fast_lpitch((3 + c.cols + 3) / 4, dw));
-                        // FAST_PFU: a prefetched ROI writes all 4 * FAST_PF2D rows
-                        const int rows_w = (FAST_PFU && FAST_STAGE2D) ? std::max((int)c.rows, 4 * FAST_PF2D) : (int)c.rows;
+                        // a prefetched ROI writes all 4 * FAST_PF2D rows
+                        const int rows_w = std::max((int)c.rows, 4 * FAST_PF2D);
                         G.max_roi_bytes = std::max(G.max_roi_bytes, rows_w * lpc * 4);
                     }
                     if (dh > 0 && dw > 0) {
@@ -880,37 +843,17 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     h->kscratch_per_image = 0;
     for (int l = 0; l < L; ++l) h->kscratch_per_image += (long long)G.lv[l].cand_cap * 8;
     h->kscratch_per_image = (long long)align_up((size_t)std::max(h->kscratch_per_image, 16LL), 256);
-    // octree LDS: node arrays for the largest list, candidate arrays up to kcap in LDS (a
-    // level with more candidates keeps them in global scratch).  Level 0 gets up to OCT_LDS0_KB (two per CU);
-    // levels 1.. run as a second launch sized to fit four workgroups per CU (OCT_LDS1_KB).
-    int ncand0 = 0, ncand1 = 0, oc1 = 16;
-    {
-        int c = 0;
-        for (int l = 0; l < L; ++l) {
-            int n = 0;
-            for (int k = 0; k < G.lv[l].ncells; ++k) n += h->cells[G.lv[l].cell_begin + k].cap;
-            if (l == 0) ncand0 = n; else ncand1 = std::max(ncand1, n);
-            if (l > 0) oc1 = std::max(oc1, G.lv[l].out_cap);
-            c += n;
-        }
-        (void)c;
+    // octree LDS (all levels in one launch): node arrays for the largest level's list, the
+    // candidate arrays in LDS up to the OCT_LDS_KB budget (a level with more candidates keeps
+    // them in global scratch)
+    int ncand0 = 0, ncand1 = 0, ocmax = 16;
+    for (int l = 0; l < L; ++l) {
+        int n = 0;
+        for (int k = 0; k < G.lv[l].ncells; ++k) n += h->cells[G.lv[l].cell_begin + k].cap;
+        if (l == 0) ncand0 = n; else ncand1 = std::max(ncand1, n);
+        ocmax = std::max(ocmax, G.lv[l].out_cap);
     }
-    h->ncap = (int)align_up((size_t)G.lv[0].out_cap, 16);
-    int kcap = std::min(std::max(ncand0, 64), 8192);
-    while (kcap > 64 && octree_lds_bytes(h->ncap, kcap) > OCT_LDS0_KB * 1024) kcap -= 64;
-    h->kcap = kcap;
-    h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
-    h->ncap1 = (int)align_up((size_t)oc1, 16);
-    int kcap1 = std::min(std::max(ncand1, 64), 8192);
-    while (kcap1 > 64 && octree_lds_bytes(h->ncap1, kcap1) > OCT_LDS1_KB * 1024) kcap1 -= 64;
-    h->kcap1 = kcap1;
-    h->octree_lds1 = octree_lds_bytes(h->ncap1, h->kcap1);
-#if OCT_MERGED
     {
-        // all levels in one launch: node arrays for the largest level, candidates in LDS up to
-        // the budget (the synthetic and KITTI-like frames stay far below it at every level)
-        int ocmax = 16;
-        for (int l = 0; l < L; ++l) ocmax = std::max(ocmax, G.lv[l].out_cap);
         h->ncap = (int)align_up((size_t)ocmax, 16);
         int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
         while (kc > 64 && octree_lds_bytes(h->ncap, kc) > OCT_LDS_KB * 1024) kc -= 64;
@@ -920,7 +863,6 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         h->kcap1 = h->kcap;
         h->octree_lds1 = h->octree_lds;
     }
-#endif
     {
         // small batches: the same node arrays, candidates in LDS up to OCT_LDS_SMALL_KB
         int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
@@ -974,15 +916,14 @@ orbx_status ensure_workspace(orbx_extractor* h, int W, int H, int batch) {
     if (batch > h->cap_batch) {
         // growing frees the old buffers: the handle's work in flight must be done
         if (!wait_idle(h)) return ORBX_ERR_DEVICE;
+        h->pyr_images = 0;   // the pyramids go with them
+        ++h->serial;
         const Geometry& G = h->hg;
         const size_t B = (size_t)batch;
-        // k_fast (FAST_PFU) reads up to 4 * FAST_PF2D rows past a cell's ROI
+        // k_fast reads up to 4 * FAST_PF2D rows past a cell's ROI
         const size_t pyr_slack = (size_t)4 * FAST_PF2D * G.lv[0].pitch + 256;
-        // BLUR_STRIPE: k_orient_desc reads whole 16-byte stripes, up to one stripe past a
-        // level's last
-        const size_t blur_slack = BLUR_STRIPE ? (size_t)16 * (G.lv[0].h + 64) : 0;
         bool ok = h->d_pyr.ensure(B * G.pyr_bytes + pyr_slack) &&
-                  h->d_blur.ensure(B * G.pyr_bytes + blur_slack) &&
+                  h->d_blur.ensure(B * G.pyr_bytes) &&
                   h->d_ccnt.ensure(B * std::max(G.n_cells, 1) * 4) &&
                   h->d_cand.ensure(B * G.cand_words * 4) &&
                   h->d_ocnt.ensure(B * G.nlevels * 4) && h->d_okp.ensure(B * G.out_words * 6) &&
@@ -1046,7 +987,7 @@ ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uin
     a.octree_lds1 = h->octree_lds1;
     a.kcap_small = h->kcap_small;
     a.octree_lds_small = h->octree_lds_small;
-    a.oct_small = batch <= tuned("ORBX_OCT_SMALL_BATCH", OCT_SMALL_BATCH) ? 1 : 0;
+    a.oct_small = batch <= OCT_SMALL_BATCH ? 1 : 0;
     a.fast_nc = fast_cells_per_wave(h->hg.n_cells, batch, h->ncu);
     a.kps = h->d_kps.as<float>();
     a.desc = h->d_desc.as<uint8_t>();
@@ -1059,12 +1000,12 @@ ExtractLaunch extract_launch(orbx_extractor* h, const uint8_t* d_imgs, const uin
     // small batch's kernels are latency chains, and the fork / join events between the two
     // streams cost more than the overlap gives (an explicit orbx_extractor_set_overlap applies
     // at every batch size)
-    a.side_mode = (h->side_auto && batch < tuned("ORBX_SIDE_MIN_BATCH", SIDE_MIN_BATCH)) ? 0
+    a.side_mode = (h->side_auto && batch < SIDE_MIN_BATCH) ? 0
                                                                                      : h->side_mode;
     a.side_at = h->side_at;
     a.side_lv = h->side_lv;
     a.chain = (h->hg.chain_ok && a.in_place && a.side_mode == 0 &&
-               batch <= tuned("ORBX_CHAIN_MAX_BATCH", CHAIN_MAX_BATCH)) ? 1 : 0;
+               batch <= CHAIN_MAX_BATCH) ? 1 : 0;
     strip_heights(h, batch, a.sth);
     return a;
 }
@@ -1077,6 +1018,7 @@ orbx_status run_extract(orbx_extractor* h, const uint8_t* d_imgs, const uint8_t*
     h->last_batch = batch;
     h->last_valid = true;
     h->pyr_images = h->last_batch;
+    ++h->serial;
     h->last_n = -1;   // on the device only (orbx_extract records it once copied back)
     return ORBX_OK;
 }
@@ -1116,7 +1058,7 @@ orbx_status stereo_launch_args(orbx_extractor* L, orbx_extractor* R, int batch, 
     a.ssad = nullptr;
     a.sidx = nullptr;
     if (stereo_split(batch) > 1) {
-        // split path scratch: counters (zeroed when allocated; k_stereo_cut leaves them zero),
+        // split path scratch: counters (zeroed when allocated; the median cut leaves them zero),
         // then per pair kp_cap SADs and left indices
         // (a fixed counter block: one slot per pair of the largest split batch, so a later
         // call with another batch finds its counters zero)
@@ -1172,28 +1114,18 @@ orbx_status run_stereo(orbx_extractor* L, orbx_extractor* R, int batch, int offL
 // each with its own server handle: a batch forms in one while the other's runs, and up to
 // FS_INFLIGHT batches run at once.  With several sessions the runtime's submission path,
 // not the GPU, bounded the rate of one-call frames (14 submissions each).
-#ifndef STAGE_THREAD
+#define STAGE_THREAD 1
 // orbx_stereo_frame_view: the right image staged by a helper thread (0 never, 1 for frames that
 // queue for the frame server, 2 always).  Measured (r04_ab_runs.txt, r4i): the helper's wake-up
 // costs a lone caller with cache-hot images more (0.239 -> 0.257 ms) than it saves on cold ones
 // (0.268 -> 0.259 ms); with 8 sessions it raised 9.4-9.6k to 9.6-9.9k pairs/s.
-#define STAGE_THREAD 1
-#endif
-#ifndef EXTRACT_GRAPH
 #define EXTRACT_GRAPH 1   // orbx_extract replays its device sequence from a per-handle graph
-#endif
 // Batches on the device at once (each on its block pair's own server handle): a batch of a
 // few frames is a latency-bound chain that leaves most of the GPU idle, so the next one runs
 // beside it.
-#ifndef FS_INFLIGHT
 #define FS_INFLIGHT 2
-#endif
-#ifndef FS_MAX_FRAMES
 #define FS_MAX_FRAMES 8
-#endif
-#ifndef FRAME_SERVER
 #define FRAME_SERVER 1
-#endif
 struct FsReq {
     orbx_extractor* h;            // the caller's handle (its stager)
     int slot = -1, blk = -1;      // its frame in the batch, the block pair of that batch
@@ -1245,6 +1177,16 @@ struct FrameServer {
     // valid.  Only when idle: nothing forming, running or being copied out.
     bool idle() const { return n == 0 && inflight == 0 && readers[0] == 0 && readers[1] == 0; }
     void release_resources() {
+        // first drain every copy that may still read or write the pinned / staging blocks: a
+        // batch whose event record failed returns without run_served, and its staging copies
+        // on cst can still be pending; the server handles' graphs DMA into hout
+        if (cst) (void)hipStreamSynchronize(cst);
+        for (int b = 0; b < 2; ++b)
+            if (sh[b]) {
+                (void)wait_idle(sh[b]);
+                if (sh[b]->stream) (void)hipStreamSynchronize(sh[b]->stream);
+                if (sh[b]->side) (void)hipStreamSynchronize(sh[b]->side);
+            }
         for (int b = 0; b < 2; ++b) {
             for (FsGraph& G : graphs[b]) {
                 if (G.gx) (void)hipGraphExecDestroy(G.gx);
@@ -1271,27 +1213,6 @@ struct FrameServer {
         blk = n = staged = 0;
         stats.resident = 0;
     }
-#ifdef ORBX_TUNING
-    // ORBX_FS_STATS=1: batch sizes and where the device time goes, printed at exit
-    using clk = std::chrono::steady_clock;
-    long st_solo = 0, st_hist[FS_MAX_FRAMES + 1] = {};
-    double st_run_us = 0, st_solo_us = 0, st_idle_us = 0, st_readers_us = 0;
-    clk::time_point st_free = clk::now();
-    static double us(clk::time_point a, clk::time_point b) {
-        return std::chrono::duration<double, std::micro>(b - a).count();
-    }
-    ~FrameServer() {
-        if (!getenv("ORBX_FS_STATS")) return;
-        long nb = 0, nf = 0;
-        for (int m = 1; m <= FS_MAX_FRAMES; ++m) nb += st_hist[m], nf += m * st_hist[m];
-        fprintf(stderr, "frame server: %ld solo calls (%.1f us each), %ld batches of %ld frames "
-                "(%.1f us each), device idle %.0f us, readers wait %.0f us; sizes",
-                st_solo, st_solo ? st_solo_us / st_solo : 0.0, nb, nf, nb ? st_run_us / nb : 0.0,
-                st_idle_us, st_readers_us);
-        for (int m = 1; m <= FS_MAX_FRAMES; ++m) fprintf(stderr, " %ld", st_hist[m]);
-        fprintf(stderr, "\n");
-    }
-#endif
 };
 
 // One server per (device, extractor parameters).  The registry owns them for the life of the
@@ -1395,7 +1316,7 @@ static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, 
     std::memcpy(&mb_bits, &g.mb, 4);
     FsGraph& G = fs.graphs[blk][m];
     const bool graph =
-        tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !S->timer.on &&
+        EXTRACT_GRAPH && !S->timer.on &&
         extract1_graph(S, a, st, g.width, g.height, enqueue, G.gx, G.key,
                        {dsg, hout, S->d_sscr.p, dso, (const void*)(uintptr_t)mbf_bits,
                         (const void*)(uintptr_t)mb_bits, (const void*)(intptr_t)m,
@@ -1407,6 +1328,7 @@ static orbx_status run_served(FrameServer& fs, const orbx_extractor* h0, int m, 
     S->last_batch = 2 * m;
     S->last_valid = true;
     S->pyr_images = 2 * m;
+    ++S->serial;
     S->last_n = -1;
     fs.lay[blk] = FsLayout{o_kps, o_desc, o_st, KC, m};
     return ORBX_OK;
@@ -1452,6 +1374,7 @@ static orbx_status copy_served(FrameServer& fs, const FsReq& r, const FsBatch& g
     // this handle's own workspace does not hold the frame's keypoints ...
     h->last_valid = false;
     h->pyr_images = 0;
+    ++h->serial;
     if (!h->keep_pyr) return ORBX_OK;
     // ... but its pyramids when asked for (orbx_extractor_keep_pyramid): both views' blocks,
     // device to device from the server handle, whose workspace this block pair's next batch
@@ -1472,6 +1395,7 @@ static orbx_status copy_served(FrameServer& fs, const FsReq& r, const FsBatch& g
         return ORBX_ERR_DEVICE;
     h->last_batch = 2;
     h->pyr_images = 2;
+    ++h->serial;
     return ORBX_OK;
 }
 
@@ -1561,18 +1485,8 @@ int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return d;
 }
 
-#ifndef FAST_SIDE_PRIO
-#define FAST_SIDE_PRIO 0   // 1: the side stream at the lowest priority (the level chain first)
-#endif
 static hipError_t create_side_stream(hipStream_t* s) {
-#if FAST_SIDE_PRIO
-    int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e != hipSuccess) return e;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
-#else
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-#endif
 }
 
 orbx_status orbx_extractor_create(const orbx_extractor_params* p, orbx_extractor** out) {
@@ -1616,6 +1530,7 @@ orbx_status orbx_extractor_destroy(orbx_extractor* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->h_in) (void)hipHostFree(h->h_in);
     if (h->h_out) (void)hipHostFree(h->h_out);
+    if (h->h_pyr) (void)hipHostFree(h->h_pyr);
     DevBuf* bufs[] = {&h->d_geom, &h->d_cells, &h->d_rtab, &h->d_ltab, &h->d_pyr, &h->d_blur,
                       &h->d_ccnt, &h->d_cand, &h->d_ocnt, &h->d_okp, &h->d_kscr, &h->d_kps,
                       &h->d_desc, &h->d_nkp, &h->d_uR, &h->d_dep, &h->d_nv, &h->d_sscr,
@@ -1704,8 +1619,10 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
     const size_t o_kps = (size_t)((uint8_t*)h->d_kps.p - (uint8_t*)h->d_outs.p);
     const size_t o_desc = (size_t)((uint8_t*)h->d_desc.p - (uint8_t*)h->d_outs.p);
     const size_t o_end = o_desc + KC * 32;
+    h->host_pyr_ok = false;
     if (!ensure_pinned(h->h_in, h->h_in_n, img_bytes) ||
-        !ensure_pinned(h->h_out, h->h_out_n, o_end))
+        !ensure_pinned(h->h_out, h->h_out_n, o_end) ||
+        (h->host_pyr && !ensure_pinned(h->h_pyr, h->h_pyr_n, (size_t)h->hg.pyr_bytes)))
         return ORBX_ERR_DEVICE;
     for (int y = 0; y < height; ++y)
         std::memcpy(h->h_in + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
@@ -1717,17 +1634,24 @@ static orbx_status extract_host(orbx_extractor* h, const uint8_t* img, int width
                HIPOK(launch_extract(a, st)) &&
                HIPOK(hipMemcpyAsync(h->h_out, h->d_outs.p, o_end, hipMemcpyDeviceToHost, st));
     };
-    const ExtractLaunch a = extract_launch(h, nullptr, nullptr, 1, 1, 0, 0);
+    ExtractLaunch a = extract_launch(h, nullptr, nullptr, 1, 1, 0, 0);
+    if (h->host_pyr) {
+        a.pyr_host = h->h_pyr;
+        a.pyr_host_bytes = (size_t)h->hg.pyr_bytes;
+    }
     // replayed from a graph (one launch instead of ~15 enqueues: several tracking sessions
     // on one GPU contend for the runtime's per-call work), eagerly when kernels are timed
-    const bool graph = tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
-                       extract1_graph(h, a, st, width, height, enqueue, h->g1, h->g1key, {});
+    const bool graph = EXTRACT_GRAPH && !h->timer.on &&
+                       extract1_graph(h, a, st, width, height, enqueue, h->g1, h->g1key,
+                                      {(const void*)a.pyr_host});
     if (!(graph ? HIPOK(hipGraphLaunch(h->g1, st)) : enqueue(a)) || !mark_done(h, st) ||
         !wait_done(h))
         return ORBX_ERR_DEVICE;
     h->last_batch = 1;
     h->last_valid = true;
     h->pyr_images = h->last_batch;
+    ++h->serial;
+    h->host_pyr_ok = h->host_pyr;
     std::memcpy(&h->last_n, h->h_out, 4);
     *o_kps_out = o_kps;
     *o_desc_out = o_desc;
@@ -1790,7 +1714,7 @@ static void stage_frame(orbx_extractor* h, uint8_t* dst, size_t pitch0, size_t i
         for (int y = 0; y < height; ++y)
             std::memcpy(d + (size_t)y * pitch0, img + (size_t)y * stride, (size_t)width);
     };
-    const int stage_thread = tuned("ORBX_STAGE_THREAD", STAGE_THREAD);
+    const int stage_thread = STAGE_THREAD;
     if (stage_thread == 2 || (stage_thread == 1 && queued)) {
         if (!h->stager) h->stager.reset(new OrbxStager());
         h->stager->post([=] { copy(1); });
@@ -1855,7 +1779,7 @@ static orbx_status stereo_frame_solo(orbx_extractor* h, const uint8_t* left, siz
     std::memcpy(&mbf_bits, &mbf, 4);
     std::memcpy(&mb_bits, &mb, 4);
     const bool graph =
-        tuned("ORBX_EXTRACT_GRAPH", EXTRACT_GRAPH) && !h->timer.on &&
+        EXTRACT_GRAPH && !h->timer.on &&
         extract1_graph(h, a, st, width, height, enqueue, h->g2, h->g2key,
                        {h->d_sscr.p, (const void*)(uintptr_t)mbf_bits,
                         (const void*)(uintptr_t)mb_bits, (const void*)(uintptr_t)one_dma});
@@ -1864,7 +1788,8 @@ static orbx_status stereo_frame_solo(orbx_extractor* h, const uint8_t* left, siz
         return ORBX_ERR_DEVICE;
     h->last_batch = 2;
     h->last_valid = true;
-    h->pyr_images = h->keep_pyr ? 2 : 0;   // the stereo-frame pyramid contract (keep_pyr)
+    h->pyr_images = h->keep_pyr ? 2 : 0;
+    ++h->serial;   // the stereo-frame pyramid contract (keep_pyr)
     h->last_n = -1;   // not the single-image state orbx_stereo_match expects
     const uint8_t* ho = h->h_out;
     std::memcpy(out->n, ho, 8);
@@ -1884,29 +1809,20 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
     if (!h || !out || !left || !right || width <= 0 || height <= 0 ||
         stride_left < (size_t)width || stride_right < (size_t)width)
         return ORBX_ERR_INVALID;
-    if (!tuned("ORBX_FRAME_SERVER", FRAME_SERVER))
+    if (!FRAME_SERVER)
         return stereo_frame_solo(h, left, stride_left, right, stride_right, width, height, mbf,
                                  mb, out);
     FrameServer& fs = frame_server(h);
     frame_server_use(h, fs);
-    const int inflight_max = tuned("ORBX_FS_INFLIGHT", FS_INFLIGHT);
+    const int inflight_max = FS_INFLIGHT;
     std::unique_lock<std::mutex> lk(fs.mu);
     if (fs.inflight == 0 && fs.n == 0) {   // alone on the device: on this handle
         ++fs.inflight;
         fs.stats.solo_calls++;
-#ifdef ORBX_TUNING
-        const auto t0 = FrameServer::clk::now();
-        fs.st_idle_us += FrameServer::us(fs.st_free, t0);
-#endif
         lk.unlock();
         const orbx_status s = stereo_frame_solo(h, left, stride_left, right, stride_right, width,
                                                 height, mbf, mb, out);
         lk.lock();
-#ifdef ORBX_TUNING
-        fs.st_free = FrameServer::clk::now();
-        fs.st_solo++;
-        fs.st_solo_us += FrameServer::us(t0, fs.st_free);
-#endif
         --fs.inflight;
         fs.cv.notify_all();
         return s;
@@ -1988,25 +1904,12 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         fs.stats.peak_inflight = std::max(fs.stats.peak_inflight, fs.inflight);
         fs.stats.resident = 1;
         fs.cv.notify_all();
-#ifdef ORBX_TUNING
-        const auto t0 = FrameServer::clk::now();
-        fs.st_idle_us += FrameServer::us(fs.st_free, t0);
-#endif
         fs.cv.wait(lk, [&] { return fs.readers[blk] == 0; });   // two batches ago: copied out
-#ifdef ORBX_TUNING
-        const auto t1 = FrameServer::clk::now();
-#endif
         lk.unlock();
         orbx_status bs = recorded ? run_served(fs, take[0]->h, m, blk, bg) : ORBX_ERR_DEVICE;
         for (int i = 0; i < m; ++i)
             if (take[i]->st != ORBX_OK) bs = take[i]->st;   // a frame's copy failed
         lk.lock();
-#ifdef ORBX_TUNING
-        fs.st_free = FrameServer::clk::now();
-        fs.st_readers_us += FrameServer::us(t0, t1);
-        fs.st_run_us += FrameServer::us(t1, fs.st_free);
-        fs.st_hist[m]++;
-#endif
         for (int i = 0; i < m; ++i) {
             take[i]->st = bs;
             take[i]->done = true;
@@ -2024,6 +1927,36 @@ orbx_status orbx_stereo_frame_view(orbx_extractor* h, const uint8_t* left, size_
         fs.cv.notify_all();
     }
     return s;
+}
+
+uint64_t orbx_extractor_serial(const orbx_extractor* h) {
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return h->serial;
+}
+
+orbx_status orbx_extractor_host_pyramid(orbx_extractor* h, int on) {
+    if (!h) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->host_pyr = on != 0;
+    if (!h->host_pyr) h->host_pyr_ok = false;
+    return ORBX_OK;
+}
+
+orbx_status orbx_host_pyramid_view(const orbx_extractor* h, orbx_host_pyramid* out) {
+    if (!h || !out) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->host_pyr_ok || !h->have_geom || !h->h_pyr) return ORBX_ERR_STATE;
+    std::memset(out, 0, sizeof(*out));
+    out->nlevels = h->hg.nlevels;
+    for (int l = 0; l < h->hg.nlevels && l < 16; ++l) {
+        const LevelGeom& L = h->hg.lv[l];
+        out->data[l] = h->h_pyr + L.off;
+        out->width[l] = L.w;
+        out->height[l] = L.h;
+        out->step[l] = (size_t)L.pitch;
+    }
+    return ORBX_OK;
 }
 
 orbx_status orbx_extractor_keep_pyramid(orbx_extractor* h, int on) {
@@ -2071,20 +2004,7 @@ static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, i
     if (!out) return ORBX_OK;
     (void)hipSetDevice(h->device);
     const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
-#if BLUR_STRIPE
-    if (blurred) {   // column stripes (blur_off): the whole level, re-laid row-major here
-        std::vector<uint8_t> tmp((size_t)lv.pitch * lv.h);
-        if (!order_after_last(h, h->stream) ||
-            !HIPOK(hipMemcpyAsync(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost, h->stream)) ||
-            !HIPOK(hipStreamSynchronize(h->stream)))
-            return ORBX_ERR_DEVICE;
-        for (int y = 0; y < lv.h; ++y)
-            for (int x = 0; x < lv.w; ++x) out[(size_t)y * lv.w + x] = tmp[blur_off(x, y, lv.pitch, lv.h)];
-        return ORBX_OK;
-    }
-#else
     (void)blurred;
-#endif
     if (!order_after_last(h, h->stream) ||
         !HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
         !HIPOK(hipStreamSynchronize(h->stream)))

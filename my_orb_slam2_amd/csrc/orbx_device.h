@@ -4,9 +4,7 @@
 #include <stdint.h>
 
 namespace orbx {
-#ifndef ORBX_XCD_REMAP
 #define ORBX_XCD_REMAP 1
-#endif
 // Logical (x, y) block of a 2-D grid.  Consecutive linear blocks are dealt round-robin over
 // the 8 XCDs (MI355X_MICROARCH.md §Workgroup dispatch: blocks b and b + 8 share an XCD), so
 // linear block L runs logical block (L mod 8) * n/8 + L / 8: every XCD walks a contiguous
@@ -27,18 +25,6 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -160,41 +146,6 @@ __device__ __forceinline__ bool stage_dwords_cols(const uint8_t* __restrict__ gs
     }
     vmem_drained();
     return true;
-}
-
-// Same for an arbitrary byte window (no alignment), 16 loads in flight per thread.
-template <int NT>
-__device__ __forceinline__ void stage_bytes(const uint8_t* __restrict__ gsrc, size_t gpitch,
-                                            int rows, int cols, uint8_t* lds, int lpitch,
-                                            int tid) {
-    const int n = rows * cols;
-    if (n <= 0) return;
-    const uint32_t gp = (uint32_t)gpitch;
-    const int dr = NT / cols, dc = NT - dr * cols;
-    int r = tid / cols, c = tid - r * cols;
-    uint32_t go = (uint32_t)r * gp + (uint32_t)c;
-    int lo = r * lpitch + c;
-    const uint32_t gstep = (uint32_t)dr * gp + (uint32_t)dc, gwrap = gp - (uint32_t)cols;
-    const int lstep = dr * lpitch + dc, lwrap = lpitch - cols;
-    const uint32_t glast = (uint32_t)(rows - 1) * gp + (uint32_t)(cols - 1);
-    for (int base = 0; base < n; base += NT * 16) {
-        uint8_t v[16];
-        int at[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const bool in = base + k * NT + tid < n;
-            v[k] = gsrc[in ? go : glast];
-            at[k] = in ? lo : -1;
-            c += dc;
-            go += gstep;
-            lo += lstep;
-            if (c >= cols) { c -= cols; go += gwrap; lo += lwrap; }
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (at[k] >= 0) lds[at[k]] = v[k];
-    }
-    vmem_drained();
 }
 
 }  // namespace orbx

@@ -25,60 +25,6 @@ __constant__ int8_t c_pattern[1024] = {
 #include "orbx_pattern.inc"
 };
 
-// ----------------------------------------------------------------------------------------
-// FAST-9 per cell: one wave per 30px cell.  The reference calls cv::FAST on every cell ROI
-// with iniThFAST and, if the cell yields nothing, again with minThFAST; NMS is local to the
-// ROI.  Here the ROI is staged in LDS once, the threshold-free arc score M (max over the 16
-// 9-pixel arcs of the min |difference|, signed per polarity) is computed once per pixel,
-// and both thresholds are derived from it: corner at t <=> M > t, cornerScore = M - 1.
-// ----------------------------------------------------------------------------------------
-__device__ __forceinline__ int fast_arc_score(const uint8_t* roi, int cols, int r, int c) {
-    const int v = roi[r * cols + c];
-    int d[16];
-    // Bresenham circle of radius 3 in cv::FAST order (makeOffsets, patternSize 16): (dx, dy)
-    d[0] = v - roi[(r + 3) * cols + c];
-    d[1] = v - roi[(r + 3) * cols + c + 1];
-    d[2] = v - roi[(r + 2) * cols + c + 2];
-    d[3] = v - roi[(r + 1) * cols + c + 3];
-    d[4] = v - roi[(r)*cols + c + 3];
-    d[5] = v - roi[(r - 1) * cols + c + 3];
-    d[6] = v - roi[(r - 2) * cols + c + 2];
-    d[7] = v - roi[(r - 3) * cols + c + 1];
-    d[8] = v - roi[(r - 3) * cols + c];
-    d[9] = v - roi[(r - 3) * cols + c - 1];
-    d[10] = v - roi[(r - 2) * cols + c - 2];
-    d[11] = v - roi[(r - 1) * cols + c - 3];
-    d[12] = v - roi[(r)*cols + c - 3];
-    d[13] = v - roi[(r + 1) * cols + c - 3];
-    d[14] = v - roi[(r + 2) * cols + c - 2];
-    d[15] = v - roi[(r + 3) * cols + c - 1];
-    // min / max over the 16 cyclic 9-runs as three 3-runs each: every step is one
-    // v_min3 / v_max3 (a 2-input v_min costs the same issue slot on gfx950)
-    int mn3[16], mx3[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        mn3[i] = min(min(d[i], d[(i + 1) & 15]), d[(i + 2) & 15]);
-        mx3[i] = max(max(d[i], d[(i + 1) & 15]), d[(i + 2) & 15]);
-    }
-    int mn9[16], mx9[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        mn9[i] = min(min(mn3[i], mn3[(i + 3) & 15]), mn3[(i + 6) & 15]);
-        mx9[i] = max(max(mx3[i], mx3[(i + 3) & 15]), mx3[(i + 6) & 15]);
-    }
-    // 9 pixels all darker than v by > t: max_i mn9; all brighter: -min_i mx9
-    int best_dark = max(max(mn9[0], mn9[1]), mn9[2]);
-    int best_min_max = min(min(mx9[0], mx9[1]), mx9[2]);
-#pragma unroll
-    for (int i = 3; i < 15; i += 2) {
-        best_dark = max(max(best_dark, mn9[i]), mn9[i + 1]);
-        best_min_max = min(min(best_min_max, mx9[i]), mx9[i + 1]);
-    }
-    best_dark = max(best_dark, mn9[15]);
-    best_min_max = min(best_min_max, mx9[15]);
-    return max(best_dark, -best_min_max);
-}
-
 // The same score with both polarities in the halves of one packed-f16 register, so every
 // run min / max is one v_pk_minimum3 / v_pk_maximum3 for dark and bright together (40 of
 // them instead of 80).  A circle pixel n enters as the f16 whose bits are n (a subnormal:
@@ -120,47 +66,6 @@ __device__ __forceinline__ int fast_arc_score_pk(const uint8_t* roi, int cols, i
     return max(v - (int)(bits & 0x3FFu), (int)((bits >> 16) & 0x3FFu) - v);
 }
 
-// Exact necessary condition for M > t: the 9 circle indices of any arc include 4 or 5
-// consecutive even indices, so a corner at t has 4 cyclically consecutive even-index pixels
-// (0, 2, .., 14) all darker than v - t or all brighter than v + t.  8 reads instead of 16.
-__device__ __forceinline__ bool fast_even8(const uint8_t* roi, int cols, int r, int c, int t) {
-    const int v = roi[r * cols + c];
-    int e[8];
-    e[0] = v - roi[(r + 3) * cols + c];
-    e[1] = v - roi[(r + 2) * cols + c + 2];
-    e[2] = v - roi[(r)*cols + c + 3];
-    e[3] = v - roi[(r - 2) * cols + c + 2];
-    e[4] = v - roi[(r - 3) * cols + c];
-    e[5] = v - roi[(r - 2) * cols + c - 2];
-    e[6] = v - roi[(r)*cols + c - 3];
-    e[7] = v - roi[(r + 2) * cols + c - 2];
-    int dark = -256, bmax = 256;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int mn = min(min(min(e[k], e[(k + 1) & 7]), e[(k + 2) & 7]), e[(k + 3) & 7]);
-        const int mx = max(max(max(e[k], e[(k + 1) & 7]), e[(k + 2) & 7]), e[(k + 3) & 7]);
-        dark = max(dark, mn);
-        bmax = min(bmax, mx);
-    }
-    return max(dark, -bmax) > t;
-}
-
-// Keypoint test at threshold t on the M map (mb: (dh+2) x (dw+2), zero ring).
-__device__ __forceinline__ bool fast_nms_kp(const uint8_t* mb, int mw, int rr, int cc, int t,
-                                            int& score) {
-    const uint8_t* p = mb + (rr + 1) * mw + (cc + 1);
-    const int m = p[0];
-    if (m <= t) return false;
-    const int s = m - 1;
-    if (s <= 0) return false;   // every neighbour score is >= 0
-    score = s;
-#define ORBX_NB(o) { const int q = p[o]; if (q > t && q - 1 >= s) return false; }
-    ORBX_NB(-mw - 1) ORBX_NB(-mw) ORBX_NB(-mw + 1) ORBX_NB(-1) ORBX_NB(1)
-    ORBX_NB(mw - 1) ORBX_NB(mw) ORBX_NB(mw + 1)
-#undef ORBX_NB
-    return true;
-}
-
 // Keypoint tests at both thresholds on the M map in one read of the 3x3 neighbourhood.
 __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, int cc, int t_hi,
                                              int t_lo, bool& k_hi, bool& k_lo, int& score) {
@@ -181,74 +86,23 @@ __device__ __forceinline__ void fast_nms_kp2(const uint8_t* mb, int mw, int rr, 
     k_lo = base && m > t_lo && supp <= t_lo;
 }
 
-#ifndef FAST_LIST
-#define FAST_LIST 512    // compass survivors listed per row block (a multiple of 256)
-#endif
-#ifndef FAST_PF
 #define FAST_PF 6      // prefetched ROI dwords per lane (larger ROIs are staged directly)
-#endif
-#ifndef FAST_XCD
-#define FAST_XCD 1   // XCD block order for k_fast: HBM traffic 3.03 -> 1.56 GB per step, time
                      // 2.304 -> 2.288 ms per step one-stream (r4e A/B, B=512)
-#endif
-#ifndef FAST_CMPONLY
-#define FAST_CMPONLY 0
-#endif
-#ifndef FAST_NOLDS
-#define FAST_NOLDS 0
-#endif
-#ifndef FAST_2PASS
-#define FAST_2PASS 1   // detect at iniThFAST first, minThFAST only for cells without a keypoint
-#endif
-#ifndef FAST_ARC_PK
-#define FAST_ARC_PK 1   // arc score with both polarities in one packed-f16 register
-#endif
-#ifndef FAST_PRE8
-#define FAST_PRE8 0    // even-point segment test before the arc score (measured slower: off)
-#endif
-#ifndef FAST_WPE
 #define FAST_WPE 6     // minimum waves per SIMD requested from the register allocator (80 VGPRs)
-#endif
-#ifndef OCT_NT
 #define OCT_NT 128         // k_octree threads per list (64 / 128 / 256 / 512) at large batches.
                            // Round 5, 512 pairs (r5v2 / r5v3): 128 threads 0.306 ms one-stream
                            // against 0.265 for 256, but the scheduled step is 1 % faster
                            // (128.5-128.9 k vs 127.2-127.5 k pairs/s): the smaller workgroups
                            // pack beside the pyramid and FAST launches; 64 threads 0.398 ms
-#endif
-#ifndef OCT_NT_SMALL
 #define OCT_NT_SMALL 256   // ... when batch * levels <= 256; one stereo pair: 128 0.112, 256 0.081,
                            // 1024 0.101 ms
-#endif
-#ifndef OCTREE_PACKED
-#define OCTREE_PACKED 1   // phase-1 rounds: one packed scan instead of two scans and a sum
-#endif
-#ifndef OCT_GATHER2
-#define OCT_GATHER2 1       // candidate gather: two cells per thread, one scan per 2 NT cells
-#endif
-#ifndef OCT_BUCKET_SORT
-#define OCT_BUCKET_SORT 2   // phase-2 order by size buckets: 1 ranks inside a bucket, 2 a stable
-                            // counting sort (the list order is the seq order)
-#endif
-#ifndef OD_SPATIAL
-#define OD_SPATIAL 1   // k_orient_desc takes a level's keypoints in band / column order (operm)
-#endif
-#ifndef OD_SPATIAL_MIN_BATCH
 #define OD_SPATIAL_MIN_BATCH 16   // ... for batches of at least this many images
-#endif
-#ifndef OD_SP_XS
 #define OD_SP_XS 5     // ... columns of 32 pixels
-#endif
-#ifndef OD_SP_YS
 #define OD_SP_YS 5     // ... in bands of 32 rows.  r5d, 512 pairs: k_orient_desc 1.094 ms in
                        // list order, 1.054 / 1.068 / 1.098 ms for bands of 32 / 64 / 128 rows
                        // (k_octree +0.007 ms for the order)
-#endif
-#ifndef OD_WPE
 #define OD_WPE 5       // at most 96 VGPRs: five waves per SIMD (6: spills)
-#endif
 __device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -290,21 +144,12 @@ __device__ __forceinline__ uint32_t compass4_fr(const uint8_t* roi0, int rp, int
     constexpr int KC = (XO + 9) >> 2;
     constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
     uint32_t C[5], D[5], U[5];
-#if FAST_NOLDS   // diagnostic builds only: compass operands without LDS reads
-    const uint32_t z = (uint32_t)(uintptr_t)rc ^ (uint32_t)(uintptr_t)rd ^ (uint32_t)(uintptr_t)ru;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        C[k] = z * (k + 3); D[k] = z * (k + 5); U[k] = z * (k + 7);
-        asm volatile("" : "+v"(C[k]), "+v"(D[k]), "+v"(U[k]));
-    }
-#else
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         C[k] = k <= KC ? rc[k] : 0u;
         D[k] = (k >= K0 && k <= K1) ? rd[k] : 0u;
         U[k] = (k >= K0 && k <= K1) ? ru[k] : 0u;
     }
-#endif
     uint32_t F[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -320,60 +165,11 @@ __device__ __forceinline__ uint32_t compass4_fr(const uint8_t* roi0, int rp, int
     return F[0] | (F[1] << 1);
 }
 
-// FAST compass pre-test of 4 adjacent pixels (detection columns 4gx..4gx+3 of ROI row R):
-// a 9-pixel arc beyond the threshold contains two neighbouring compass pixels (circle
-// indices i, i+4) beyond it on the same side.  Packed 16-bit saturating arithmetic, two
-// pixels per instruction: a pixel passes when, over the four neighbouring compass pairs,
-// max(min(n_i, n_j)) > v + t (both brighter) or min(max(n_i, n_j)) < (v - t)+ (both darker),
-// tested as non-zero saturating differences.  XO = the ROI's byte offset in its first LDS
-// dword (ROI rows are aligned dwords).
-// Returns 4 flag bits, bit j = pixel 4gx+j.
-template <int XO>
-__device__ __forceinline__ uint32_t compass4(const uint8_t* roi0, int rp, int R, int gx, u16x2 T) {
-    const uint32_t* rc = (const uint32_t*)(roi0 + R * rp) + gx;
-    const uint32_t* rd = (const uint32_t*)(roi0 + (R + 3) * rp) + gx;
-    const uint32_t* ru = (const uint32_t*)(roi0 + (R - 3) * rp) + gx;
-    constexpr int KC = (XO + 9) >> 2;               // last centre-row dword used
-    constexpr int K0 = (XO + 3) >> 2, K1 = (XO + 6) >> 2;
-    uint32_t C[5], D[5], U[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        C[k] = k <= KC ? rc[k] : 0u;
-        D[k] = (k >= K0 && k <= K1) ? rd[k] : 0u;
-        U[k] = (k >= K0 && k <= K1) ? ru[k] : 0u;
-    }
-    uint32_t w[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int o = XO + 3 + 2 * h;               // byte of pixel 2h (centre row)
-        const u16x2 V = pair_u16(C, o), N12 = pair_u16(C, o - 3), N4 = pair_u16(C, o + 3);
-        const u16x2 N0 = pair_u16(D, o), N8 = pair_u16(U, o);
-        const u16x2 HI = V + T, LO = __builtin_elementwise_sub_sat(V, T);
-#define MN(a, b) __builtin_elementwise_min(a, b)
-#define MX(a, b) __builtin_elementwise_max(a, b)
-        // a neighbouring pair is all brighter iff its min exceeds v + t, all darker iff its max
-        // is below v - t: compare the best pair of each kind once
-        const u16x2 bmin = MX(MX(MN(N0, N4), MN(N4, N8)), MX(MN(N8, N12), MN(N12, N0)));
-        const u16x2 dmax = MN(MN(MX(N0, N4), MX(N4, N8)), MN(MX(N8, N12), MX(N12, N0)));
-        const u16x2 pb = __builtin_elementwise_sub_sat(bmin, HI);
-        const u16x2 pd = __builtin_elementwise_sub_sat(LO, dmax);
-        const u16x2 one = {1, 1};
-        w[h] = __builtin_bit_cast(uint32_t, MN(MX(pb, pd), one));   // 0/1 per pixel
-#undef MN
-#undef MX
-    }
-    const uint32_t f = w[0] | (w[1] << 2);          // bits 0, 16 (pixels 0, 1), 2, 18 (2, 3)
-    return (f & 5u) | ((f >> 15) & 10u);
-}
-
 // One pixel pair of the compass test (u16 halves as in compass4_fr) with the pairs folded
 // first: (b0 | b8) & (b4 | b12) for "brighter than v + t" is min(max(n0, n8), max(n4, n12))
 // > v + t, and the darker side is max(min(n0, n8), min(n4, n12)) < v - t, so six packed u16
 // min / max and one add or subtract per side replace eight adds and six logic ops (r5c,
 // 512 pairs: k_fast 1.218 -> 1.165 ms one-stream, 128.8 k -> 130.2 k pairs/s).
-#ifndef FAST_COMPASS_MM
-#define FAST_COMPASS_MM 1
-#endif
 __device__ __forceinline__ uint32_t compass_pair_mm(uint32_t V, uint32_t N0, uint32_t N4,
                                                     uint32_t N8, uint32_t N12, uint32_t K) {
     const u16x2 a0 = __builtin_bit_cast(u16x2, N0), a4 = __builtin_bit_cast(u16x2, N4);
@@ -387,7 +183,7 @@ __device__ __forceinline__ uint32_t compass_pair_mm(uint32_t V, uint32_t N0, uin
 
 // The compass pre-test of 16 adjacent pixels (detection columns 16g .. 16g+15 of ROI row R),
 // the arithmetic of compass4_fr on four 4-pixel groups.  The centre row's 8 dwords and the
-// +-3 rows' 6 are read with 16-byte LDS loads (FAST_W16 rows are 16-byte aligned).  Returns
+// +-3 rows' 6 are read with 16-byte LDS loads (the ROI rows are 16-byte aligned).  Returns
 // bit i = pixel 16g + i passes.
 template <int XO>
 __device__ __forceinline__ uint32_t compass16_fr(const uint8_t* roi0, int rp, int R, int g, uint32_t K) {
@@ -410,14 +206,7 @@ __device__ __forceinline__ uint32_t compass16_fr(const uint8_t* roi0, int rp, in
             const uint32_t V = pair_u16_stride2(C, o);
             const uint32_t N12 = pair_u16_stride2(C, o - 3), N4 = pair_u16_stride2(C, o + 3);
             const uint32_t N0 = pair_u16_stride2(D, o), N8 = pair_u16_stride2(U, o);
-#if FAST_COMPASS_MM
             F[h] = compass_pair_mm(V, N0, N4, N8, N12, K);
-#else
-            const uint32_t A = K - V, B = K + V;
-            const uint32_t bright = ((N0 + A) | (N8 + A)) & ((N4 + A) | (N12 + A));
-            const uint32_t dark = ((B - N0) | (B - N8)) & ((B - N4) | (B - N12));
-            F[h] = (bright | dark) & 0x40004000u;    // bits 14 (pixel h), 30 (pixel h + 2)
-#endif
         }
         const uint32_t f = F[0] | (F[1] << 1);       // bits 14, 15, 30, 31: pixels 0..3
         mask |= (((f >> 14) & 3u) | ((f >> 28) & 12u)) << (4 * h4);
@@ -444,14 +233,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                                               int c_begin, int c_end, int nc) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#if FAST_XCD
     // XCD block order: an XCD walks a contiguous range of (image, cell block), so the ROI
     // borders shared with the neighbouring cells (left / right and the next cell row) hit its L2
     int bx, b;
     xcd_block(bx, b);
-#else
-    const int bx = blockIdx.x, b = blockIdx.y;
-#endif
     // one wave owns nc (FAST_NC, or fewer for a small batch: fast_cells_per_wave) consecutive
     // cells; no block-level barriers: waves are independent.  Cells [c_begin, c_end) of every
     // image (a launch may cover a range of levels)
@@ -460,23 +245,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     const int ncw = min(nc, c_end - c_first);
     const int roi_cap = (g->max_roi_bytes + 15) & ~15, mb_cap = (g->max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (g->max_cell_px * 2 + 15) & ~15;
-#if FAST_W16
     // one buffer: the corners found so far, then the current pass's survivor list (scored in
     // place: a corner is written at or below the entry it was read from)
     uint8_t* roi0 = smem + wid * (roi_cap + mb_cap + 64 * 2 + cl_cap);
     uint8_t* mb = roi0 + roi_cap;
     int16_t* list = (int16_t*)(mb + mb_cap);
     int16_t* corners = list;
-#else
-    uint8_t* roi0 = smem + wid * (roi_cap + mb_cap + (FAST_LIST + 64) * 2 + cl_cap);
-    uint8_t* mb = roi0 + roi_cap;
-    int16_t* list = (int16_t*)(mb + mb_cap);
-    int16_t* corners = list + FAST_LIST + 64;   // pixels with M > min threshold, raster order
-#endif
     const uint8_t* pyr_b = pyr + (size_t)b * g->pyr_bytes;
 
     // ROI of a cell as aligned dwords, dense rows of ndw dwords: LDS dword t = lane + 64j
-#if FAST_STAGE2D
     // ROI of a cell as a 2-D lane grid: lane (r = lane / 16, col = lane % 16) holds ROI dword
     // col of rows r, r + 4, .., so an element costs one 24-bit multiply-add of address and no
     // divisions (columns >= ndw idle)
@@ -486,7 +263,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
         if (ndw > 16 || c.rows > 4 * FAST_PF2D || c.rows <= 6 || c.cols <= 6) return false;
         const LevelGeom& L = g->lv[c.level];
-#if FAST_PFU
         // every lane reads its 10 rows unclamped (rows past the ROI land in the LDS buffer's
         // spare rows; the pyramid buffer has FAST_PF2D * 4 rows of slack after the last
         // image): a wave-uniform row base per load plus one lane offset, no per-load VALU
@@ -495,41 +271,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 #pragma unroll
         for (int j = 0; j < FAST_PF2D; ++j)
             pf[j] = *(const uint32_t*)(src + (size_t)(4 * j) * L.pitch + lane_off);
-#else
-        const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3) +
-                             4 * min(lc2, ndw - 1);
-        const uint32_t gp = (uint32_t)L.pitch;
-#pragma unroll
-        for (int j = 0; j < FAST_PF2D; ++j)
-            pf[j] = *(const uint32_t*)(src + __umul24((uint32_t)min(lr2 + 4 * j, c.rows - 1), gp));
-#endif
         return true;
     };
-#else
-    uint32_t pf[FAST_PF];
-    auto prefetch = [&](const CellDesc& c) -> bool {
-        const int ndw = ((c.ini_x & 3) + c.cols + 3) >> 2;
-        const int n = c.rows * ndw;
-        if (n > 64 * FAST_PF || c.rows <= 6 || c.cols <= 6) return false;
-        const LevelGeom& L = g->lv[c.level];
-        const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3);
-        const uint32_t gp = (uint32_t)L.pitch;
-        const int dr = 64 / ndw, dc = 64 - dr * ndw;
-        int r = lane / ndw, col = lane - r * ndw;
-        uint32_t go = (uint32_t)r * gp + 4u * (uint32_t)col;
-        const uint32_t gstep = (uint32_t)dr * gp + 4u * (uint32_t)dc, gwrap = gp - 4u * (uint32_t)ndw;
-        const uint32_t glast = (uint32_t)(c.rows - 1) * gp + 4u * (uint32_t)(ndw - 1);
-#pragma unroll
-        for (int j = 0; j < FAST_PF; ++j) {
-            pf[j] = *(const uint32_t*)(src + (lane + 64 * j < n ? go : glast));
-            col += dc;
-            go += gstep;
-            if (col >= ndw) { col -= ndw; go += gwrap; }
-        }
-        return true;
-    };
-
-#endif
     CellDesc cn = cells[c_first];
     bool have = prefetch(cn);
     for (int k = 0; k < ncw; ++k) {
@@ -543,16 +286,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const int lp = fast_lpitch(ndw, dw);   // LDS row pitch of the ROI, dwords
         const int rp = lp * 4;
         if (dh > 0 && dw > 0) {
-#if FAST_STAGE2D
             if (pre) {
                 if (lc2 < ndw) {
                     uint32_t* l = (uint32_t*)roi0 + lr2 * lp + lc2;
 #pragma unroll
                     for (int j = 0; j < FAST_PF2D; ++j)
-                        if (FAST_PFU || lr2 + 4 * j < rows) l[4 * j * lp] = pf[j];
+                        l[4 * j * lp] = pf[j];
                 }
             } else
-#endif
             if (pre) {
                 if (lp == ndw) {
 #pragma unroll
@@ -594,14 +335,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         [[maybe_unused]] const int rpp = 64 >> gsh;
         const int sub = lane >> gsh, gx = lane & ((1 << gsh) - 1);
         const uint32_t colmask4 = (1u << min(max(dw - 4 * gx, 0), 4)) - 1u;
-#if FAST_COMPASS_PK
-        const uint32_t colmask = colmask4;
-        [[maybe_unused]] constexpr int PB[4] = {0, 1, 2, 3};
-#else
         const uint32_t colmask = ((colmask4 & 3u) << CMP_B0) | ((colmask4 & 12u) << (CMP_B2 - 2));
         [[maybe_unused]] constexpr int PB[4] = {CMP_B0, CMP_B1, CMP_B2, CMP_B3};
-#endif
-#if FAST_W16
         // 16 pixels per lane: lpr lanes per detection row, 64 / lpr rows per pass; one pass
         // is one block of the survivor list
         const int lsh = dw > 32 ? 2 : 1;
@@ -611,33 +346,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const uint32_t colmask16 = rem16 >= 16 ? 0xFFFFu : (rem16 > 0 ? (1u << rem16) - 1u : 0u);
         const int rows_blk = rpp16;
         (void)colmask; (void)sub; (void)gx;
-#else
-        const int rows_blk = FAST_LIST / 256 * rpp;   // <= FAST_LIST pixels per block
-#endif
         uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
         const int t_ini = g->ini_th, t_min = g->min_th;
         int base = 0;
-        // FAST_2PASS: the cell is first detected at iniThFAST alone (compass test, arc scores
+        // Two passes: the cell is first detected at iniThFAST alone (compass test, arc scores
         // and NMS at that threshold); only a cell with no keypoint there is detected again at
-        // minThFAST (:830-837).  Otherwise one pass at the lower threshold serves both.
-        for (int pass = 0; pass < (FAST_2PASS ? 2 : 1); ++pass) {
-        const int tq = FAST_2PASS ? (pass == 0 ? t_ini : t_min) : min(t_ini, t_min);
-#if FAST_COMPASS_PK
-        const u16x2 T = {(unsigned short)tq, (unsigned short)tq};
-#else
+        // minThFAST (:830-837).
+        for (int pass = 0; pass < 2; ++pass) {
+        const int tq = pass == 0 ? t_ini : t_min;
         const uint32_t KT = (uint32_t)(0x4000 - tq - 1) * 0x10001u;
-#endif
         // 1. compass pre-test at tq, 4 pixels per lane: 2^gsh lanes per detection row (groups
         //    of 4 columns), 64 >> gsh rows per pass, so lane order then pixel order within a
         //    lane is raster order.
         int ncorner = 0;
-#if FAST_DIAG >= 3   // diagnostic builds only: no detection work at all
-        for (int rb = 0; rb < 0; rb += rows_blk) {
-#else
         for (int rb = 0; rb < dh; rb += rows_blk) {
-#endif
             int nlist = 0;
-#if FAST_W16
             {
                 const int rr = rb + sub16;
                 const int R = min(rr, dh - 1) + 3;
@@ -648,13 +371,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                     case 2: f = compass16_fr<2>(roi0, rp, R, g16, KT); break;
                     default: f = compass16_fr<3>(roi0, rp, R, g16, KT); break;
                 }
-#if FAST_DIAG >= 2
-                f = 0u;
-#endif
-#if FAST_CMPONLY
-                asm volatile("" ::"v"(f));
-                f = 0u;
-#endif
                 f &= rr < dh ? colmask16 : 0u;
                 // ordered compaction: lanes are in raster order, bits within a lane too
                 const int cnt = __builtin_popcount(f);
@@ -668,96 +384,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
                 }
                 nlist = __builtin_amdgcn_readlane(incl, 63);
             }
-#else
-            for (int r0 = rb; r0 < min(dh, rb + rows_blk); r0 += rpp) {
-                const int rr = r0 + sub;
-                const int R = min(rr, dh - 1) + 3;
-                uint32_t f;
-#if FAST_COMPASS_PK
-                switch (xo) {
-                    case 0: f = compass4<0>(roi0, rp, R, gx, T); break;
-                    case 1: f = compass4<1>(roi0, rp, R, gx, T); break;
-                    case 2: f = compass4<2>(roi0, rp, R, gx, T); break;
-                    default: f = compass4<3>(roi0, rp, R, gx, T); break;
-                }
-#else
-                switch (xo) {
-                    case 0: f = compass4_fr<0>(roi0, rp, R, gx, KT); break;
-                    case 1: f = compass4_fr<1>(roi0, rp, R, gx, KT); break;
-                    case 2: f = compass4_fr<2>(roi0, rp, R, gx, KT); break;
-                    default: f = compass4_fr<3>(roi0, rp, R, gx, KT); break;
-                }
-#endif
-#if FAST_DIAG >= 2   // diagnostic builds only (tools/variants.py): no compass survivors
-                f = 0u;
-#endif
-#if FAST_CMPONLY   // diagnostic builds only: the compass test kept, no survivor list
-                asm volatile("" ::"v"(f));
-                f = 0u;
-#endif
-                f &= rr < dh ? colmask : 0u;
-                const uint64_t m0 = __ballot(f & (1u << PB[0])), m1 = __ballot(f & (1u << PB[1]));
-                const uint64_t m2 = __ballot(f & (1u << PB[2])), m3 = __ballot(f & (1u << PB[3]));
-                uint32_t below = __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u);
-                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), below);
-                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m1, below);
-                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), below);
-                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m2, below);
-                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), below);
-                below = __builtin_amdgcn_mbcnt_lo((uint32_t)m3, below);
-                below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), below);
-                int pos = nlist + (int)below;
-                const int e0 = (rr << 6) | (4 * gx);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {   // unset bits write this lane's spare slot
-                    const int on = (f >> PB[j]) & 1u;
-                    list[on ? pos : FAST_LIST + lane] = (int16_t)(e0 + j);
-                    pos += on;
-                }
-                nlist += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
-            }
-#endif
             lds_order();
-#if FAST_DIAG >= 1   // diagnostic builds only: skip the arc score
-            nlist = 0;
-#endif
-#if FAST_PRE8
-            // 1b. even-point segment test (exact filter, fast_even8), compacted in place: a
-            //     lane writes at or below the entry it read, so no unread entry is overwritten.
-            //     Survivors dropped here have M <= tq and keep 0 in the M map, which no NMS
-            //     test at a threshold >= tq distinguishes from their true M.
-            {
-                int n2 = 0;
-                for (int j0 = 0; j0 < nlist; j0 += 64) {
-                    const int j = j0 + lane;
-                    int pe = 0;
-                    bool pass = false;
-                    if (j < nlist) {
-                        pe = list[j];
-                        pass = fast_even8(roi, rp, (pe >> 6) + 3, (pe & 63) + 3, tq);
-                    }
-                    const uint64_t pm = __ballot(pass);
-                    if (pass) list[n2 + lanes_below(pm)] = (int16_t)pe;
-                    n2 += __popcll(pm);
-                }
-                nlist = n2;
-                lds_order();
-            }
-#endif
             // 2. full arc score for the survivors only (dense across lanes); those above the
             //    lower threshold are appended to the corner list, keeping raster order
-            const int lb = FAST_W16 ? ncorner : 0;
+            const int lb = ncorner;
             for (int j0 = 0; j0 < nlist; j0 += 64) {
                 const int j = j0 + lane;
                 int pe = 0, m = 0;
                 if (j < nlist) {
                     pe = list[lb + j];
                     const int rr = pe >> 6, cc = pe & 63;
-#if FAST_ARC_PK
                     m = fast_arc_score_pk(roi, rp, rr + 3, cc + 3);
-#else
-                    m = fast_arc_score(roi, rp, rr + 3, cc + 3);
-#endif
                     mb[(rr + 1) * mw + cc + 1] = (uint8_t)max(m, 0);
                 }
                 const bool corner = j < nlist && m > tq;
@@ -769,8 +406,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         }
         // 3. cell-local NMS at iniThFAST, or at minThFAST when the cell has no keypoint at
         //    iniThFAST (:833-837); 4. ordered compaction (raster order, as cv::FAST emits).
-        //    One pass tests both thresholds (FAST_2PASS = 0) or the pass's own.
-        const int th_hi = FAST_2PASS ? tq : t_ini, th_lo = FAST_2PASS ? tq : t_min;
+        const int th_hi = tq, th_lo = tq;
         if (ncorner <= 64) {
             int sc = 0, pe = 0;
             bool k_hi = false, k_lo = false;
@@ -830,7 +466,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 size_t fast_lds_bytes(const Geometry& G) {
     const int roi_cap = (G.max_roi_bytes + 15) & ~15, mb_cap = (G.max_mbuf_bytes + 15) & ~15;
     const int cl_cap = (G.max_cell_px * 2 + 15) & ~15;
-    return (size_t)4 * (roi_cap + mb_cap + (FAST_W16 ? 64 : FAST_LIST + 64) * 2 + cl_cap);
+    return (size_t)4 * (roi_cap + mb_cap + 64 * 2 + cl_cap);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -911,20 +547,6 @@ __device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
     return tot;
 }
 
-#ifdef ORBX_OCT_STAMPS
-// Diagnostic build only (tools/octree_stamps.py): round clocks of one image's octrees.
-__device__ unsigned long long g_oct_stamps[16][64];
-#define OSTAMP(k)                                                                          \
-    do {                                                                                   \
-        if (threadIdx.x == 0 && blockIdx.y == ORBX_OCT_STAMPS && (k) < 64)                   \
-            g_oct_stamps[level][(k)] = __builtin_readcyclecounter();                        \
-    } while (0)
-extern "C" int orbx_diag_octree_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_stamps), sizeof(g_oct_stamps));
-}
-#else
-#define OSTAMP(k) do { } while (0)
-#endif
 
 template <int NT, bool KEYS_LDS>
 __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
@@ -939,7 +561,6 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     const int Hh = L.h - 2 * ORBX_MIN_BORDER;
 
     // ---- roots (src/ORBextractor.cc:552-587) ----
-    OSTAMP(1);
     for (int i = tid; i < nIni; i += NT) sm.cc[i * 4] = 0;
     __syncthreads();
     for (int k = tid; k < ncand; k += NT) {
@@ -971,10 +592,8 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     int seq_base = 1;
     bool phase2 = false;
     NodeArrays cur = sm.A, nxt = sm.B;
-    OSTAMP(2);
     for (int guard = 0; guard < 100000; ++guard) {
         const int prevS = S;
-        OSTAMP(3 + 2 * guard);
         // ---- split every multi-key node: quadrant of each of its keys ----
         for (int i = tid; i < S; i += NT) {
             sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
@@ -1026,7 +645,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         int Ctot, Stot, nToExpand = 0;
         if (!phase2) {
             // ---- phase 1 (src/ORBextractor.cc:608-667): expand every multi-key node ----
-            if (OCTREE_PACKED && S < 512) {
+            if (S < 512) {
                 // one scan of packed (children | survivor << 11 | multi-key children << 20):
                 // every field's total stays below its width while S < 512 (children and
                 // multi-key children <= 4 S < 2048 < 4096, survivors < 512).  The thread that
@@ -1099,12 +718,9 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                                        ((uint64_t)(uint32_t)cur.seq[i] << 16) | (uint64_t)i;
                 });
             __syncthreads();
-#if OCT_BUCKET_SORT
-            if (nV <= sm.ncap && (OCT_BUCKET_SORT < 2 || sm.ncap >= NT)) {
+            if (nV <= sm.ncap && sm.ncap >= NT) {
                 // bucket sort, descending: keys go to buckets by size (min(cnt, 63), larger
-                // sizes first).  OCT_BUCKET_SORT 1: a key's place inside its bucket is the
-                // number of larger keys there (keys are unique: they end in the node index).
-                // 2: a stable counting sort.  In phase 2 no root is expandable (phase 1's first
+                // sizes first), a stable counting sort.  In phase 2 no root is expandable (phase 1's first
                 // round split them all), and every other node's seq falls strictly with its
                 // position in the list (children go to the front with the highest seqs, and the
                 // survivors keep their order), so sortb, built in list order, is already in
@@ -1117,11 +733,9 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                 uint64_t* stage = (uint64_t*)sm.cpos;   // free until the node pass below
                 auto bucket = [](uint64_t k) { return min((int)(k >> 40), 63); };
                 for (int i = tid; i < 64; i += NT) { hist[i] = 0; fill[i] = 0; }
-#if OCT_BUCKET_SORT >= 2
                 constexpr int NW = NT / 64;
                 int* wc = sm.pre;         // [NW][64] keys per (wave, bucket) of one chunk
                 for (int i = tid; i < NW * 64; i += NT) wc[i] = 0;
-#endif
                 __syncthreads();
                 for (int j = tid; j < nV; j += NT) atomicAdd(&hist[bucket(sm.sortb[j])], 1);
                 __syncthreads();
@@ -1130,7 +744,6 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     start[63 - tid] = wave_incl_scan(v) - v;
                 }
                 __syncthreads();
-#if OCT_BUCKET_SORT >= 2
                 {
                     const int wid = tid >> 6, lane = tid & 63;
                     for (int c0 = 0; c0 < nV; c0 += NT) {
@@ -1175,23 +788,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                         sm.sortb[s0 + rank] = k;
                     }
                 }
-#else
-                for (int j = tid; j < nV; j += NT) {
-                    const uint64_t k = sm.sortb[j];
-                    const int bk = bucket(k);
-                    stage[start[bk] + atomicAdd(&fill[bk], 1)] = k;
-                }
-                __syncthreads();
-                for (int q = tid; q < nV; q += NT) {
-                    const uint64_t k = stage[q];
-                    const int bk = bucket(k), s0 = start[bk], s1 = s0 + hist[bk];
-                    int rank = 0;
-                    for (int t = s0; t < s1; ++t) rank += stage[t] > k ? 1 : 0;
-                    sm.sortb[s0 + rank] = k;
-                }
-#endif
             } else
-#endif
             if (nV <= 4 * NT) {
                 // rank sort, descending: a key's position is the number of larger keys (keys
                 // are unique: they end in the node index); two barriers instead of bitonic's
@@ -1329,15 +926,12 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         NodeArrays t2 = cur; cur = nxt; nxt = t2;
         S = Ctot + Stot;
         seq_base += Ctot;
-        OSTAMP(4 + 2 * guard);
         if (S >= N || S == prevS) break;
         if (!phase2 && S + nToExpand * 3 > N) phase2 = true;
     }
-    OSTAMP(60);
 
     // ---- retain the best keypoint of each node (src/ORBextractor.cc:743-762) ----
     uint32_t* best = (uint32_t*)sm.cc;
-#if OD_SPATIAL
     // k_orient_desc's processing order (operm): the keypoints by bands of 2^OD_SP_YS rows,
     // each band by columns of 2^OD_SP_XS pixels, so the keypoints a workgroup takes together
     // are neighbours and their patch lines are shared in L1 / L2.  Inside a bucket the order
@@ -1352,14 +946,12 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     int* sp_hist = sm.pre;
     if (spatial)
         for (int i = tid; i < sp_nb; i += NT) sp_hist[i] = 0;
-#endif
     for (int i = tid; i < S; i += NT) best[i] = 0;
     __syncthreads();
     for (int k = tid; k < ncand; k += NT)
         atomicMax(&best[knode[k]], ((uint32_t)cand_s(kdata[k]) << 24) | (uint32_t)(0xFFFFFF - k));
     __syncthreads();
     uint32_t* out = okp + (size_t)b * g->out_words + L.out_off;
-#if OD_SPATIAL
     uint16_t* perm = operm != nullptr ? operm + (size_t)b * g->out_words + L.out_off : nullptr;
     for (int i = tid; i < S; i += NT) {
         const uint32_t w = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
@@ -1383,12 +975,6 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
             perm[sp_start[kr >> 16] + (kr & 0xFFFFu)] = (uint16_t)i;
         }
     }
-#else
-    (void)operm;
-    for (int i = tid; i < S; i += NT) out[i] = kdata[0xFFFFFF - (best[i] & 0xFFFFFF)];
-    if (tid == 0) ocnt[b * g->nlevels + level] = S;
-#endif
-    OSTAMP(61);
 }
 
 template <int NT>
@@ -1402,16 +988,11 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                                                 long long kscratch_per_image, int NCAP, int KCAP,
                                                 int level_base) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-#if OCT_MERGED && OCT_LEVEL_MAJOR
     // one launch for all levels, the (long) level-0 lists dispatched first
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
     const int lrel = lin / gridDim.y, b = lin - lrel * gridDim.y, tid = threadIdx.x;
     const int level = level_base + lrel;
-#else
-    const int level = level_base + blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-#endif
     const LevelGeom& L = g->lv[level];
-    OSTAMP(0);
     // carve LDS
     uint8_t* p = smem;
     auto take = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
@@ -1457,7 +1038,6 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     // the candidate arrays are LDS or global scratch by a runtime test; each branch passes its
     // own pointers (a pointer selected between the two is generic: every access a flat one)
     auto gather_and_split = [&](uint32_t* kdata, int16_t* knode, uint8_t* kq, auto keys_lds_c) {
-#if OCT_GATHER2
     // two adjacent cells per thread, their offsets from one scan of the pairs' sums, and the
     // first 8 candidates of both cells loaded at once (addresses clamped into each cell's
     // slot, so no load is guarded): a level of up to 2 NT cells costs one memory round trip
@@ -1488,24 +1068,6 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
             }
         }
     }
-#else
-    chunked_scan<NT>(
-        L.ncells, sm.tmp, [&](int c) { return cc[c]; },
-        [&](int c, int ex) {
-            // 8 loads in flight per batch (addresses clamped into the cell's slot, so no load
-            // is guarded), then the stores: one memory round trip per 8 candidates of a cell
-            const int n = cc[c];
-            const uint32_t* s = cbase + lc[c].slot;
-            for (int e0 = 0; e0 < n; e0 += 8) {
-                uint32_t v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = s[min(e0 + j, n - 1)];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (e0 + j < n) kdata[ex + e0 + j] = v[j];
-            }
-        });
-#endif
     __syncthreads();
     octree_level<NT, decltype(keys_lds_c)::value>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp, operm);
     };
@@ -1535,41 +1097,20 @@ static_assert(OD_RAW_DW == 9 && OD_BLR_DW == 10, "k_orient_desc row divisions ar
 #define OD_RL ((OD_RAW_N + 31) / 32)               // 9 dword loads per lane per raw patch
 #define OD_BL ((OD_BLR_N + 31) / 32)               // 12 per blurred patch
 static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
-#ifndef OD_X4
-#define OD_X4 1        // patches staged by 16-byte loads, three lanes per 48-byte LDS row: the
                        // dword form kept the texture addresser 85 % busy (TA_BUSY_avr)
-#endif
-#if OD_X4
-#ifndef OD_RAW_W
 #define OD_RAW_W 12    // bytes per lane chunk of a raw-patch row (12 or 16; 3 chunks per row)
-#endif
-#ifndef OD_BLR_W
 #define OD_BLR_W 16    // ... of a blurred-patch row (8: 5 chunks per row, 16: 3)
-#endif
 static_assert((OD_RAW_W == 12 || OD_RAW_W == 16) && (OD_BLR_W == 8 || OD_BLR_W == 16), "chunk widths");
 #define OD_RAW_CH 3                                // chunks per raw row (36 / 48 bytes >= 34)
 #define OD_BLR_CH (OD_BLR_W == 8 ? 5 : 3)          // chunks per blurred row (40 / 48 >= 40)
 #define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per patch row
 #define OD_RL4 ((31 * OD_RAW_CH + 31) / 32)        // loads per lane per raw patch (3)
-#if BLUR_STRIPE
-// blurred patch: 4 column stripes x 37 rows of 16 bytes (148 contiguous-per-stripe chunks),
-// restaged row-major in LDS (rows of 64 bytes: the 4 stripes side by side)
-#define OD_BLR_NCH 148
-#define OD_BLR_RP 64
-#else
 #define OD_BLR_NCH (37 * OD_BLR_CH)
 #define OD_BLR_RP (OD_BLR_CH * OD_BLR_W)
-#endif
 #define OD_BL4 ((OD_BLR_NCH + 31) / 32)            // loads per lane per blurred patch (4, 5 or 6)
 #define OD_PATCH_B (37 * OD_BLR_RP > 31 * OD_RAW_RP ? 37 * OD_BLR_RP : 31 * OD_RAW_RP)
 #define OD_PATCH_DW ((OD_PATCH_B + 15) / 16 * 4)   // dwords per half-wave, 16-byte multiple
-#else
-#define OD_RAW_RP (OD_RAW_DW * 4)
-#define OD_BLR_RP (OD_BLR_DW * 4)
-#define OD_PATCH_DW OD_BLR_N
-#endif
 
-#if OD_X4
 // Patch staging chunks of W bytes: buffer load and the store of chunk t at byte W t of the
 // half-wave's LDS patch (rows are OD_*_CH chunks apart, so chunk t = row * CH + c).
 template <int W> struct od_chunk;
@@ -1590,7 +1131,6 @@ __device__ __forceinline__ void od_store(uint32_t* P, int t, typename od_chunk<W
     else if constexpr (W == 12) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
     else { typedef uint32_t T4 __attribute__((ext_vector_type(4))); *(T4*)d = v; }
 }
-#endif
 
 // Sums over each half-wave (lanes 0-31 / 32-63) as two scalars.
 __device__ __forceinline__ void half_sums_dpp(int v, int& lo, int& hi) {
@@ -1636,17 +1176,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const int pitch = L.pitch;
     // every keypoint word of the wave in one load: lane k holds keypoint k (processing
     // position i0 + k, list index oi)
-#if OD_SPATIAL
     const int oi = operm != nullptr ? operm[(size_t)b * g->out_words + L.out_off + i0 + min(lane, nk - 1)]
                                     : i0 + min(lane, nk - 1);
-#else
-    const int oi = i0 + min(lane, nk - 1);
-#endif
     const uint32_t cw = okp[(size_t)b * g->out_words + L.out_off + oi];
 
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
     const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
-#if OD_X4
     // per-lane offsets of the 16-byte chunks relative to the patch bases: chunk t = l32 + 32 j
     // is row t / 3, bytes 16 (t % 3) .. +16 of it; in LDS it lands at 16 t (rows 48 bytes apart)
     uint32_t sor4[OD_RL4], sob4[OD_BL4];
@@ -1654,46 +1189,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     for (int k = 0; k < OD_RL4; ++k) {
         const int t = min(l32 + 32 * k, 31 * OD_RAW_CH - 1), row = t / OD_RAW_CH;
         sor4[k] = __umul24(row, pitch) + OD_RAW_W * (t - OD_RAW_CH * row);
-#if OD_DIAG == 6
-        sor4[k] = OD_RAW_W * t;
-#endif
     }
-#if BLUR_STRIPE
-    // chunk t: stripe t / 37, row t % 37; LDS 16-byte slot row * 4 + stripe
-    static_assert(OD_BLR_W == 16, "stripe chunks are 16 bytes");
-    const uint32_t sh16 = 16u * (uint32_t)L.h;   // bytes per stripe of this level
-    uint32_t sdst[OD_BL4];
-#endif
 #pragma unroll
     for (int k = 0; k < OD_BL4; ++k) {
-#if BLUR_STRIPE
-        const int t = min(l32 + 32 * k, OD_BLR_NCH - 1), st = t / 37, row = t - 37 * st;
-        sob4[k] = (uint32_t)st * sh16 + 16u * (uint32_t)row;
-        sdst[k] = (uint32_t)(row * 4 + st);
-#else
         const int t = min(l32 + 32 * k, 37 * OD_BLR_CH - 1), row = t / OD_BLR_CH;
         sob4[k] = __umul24(row, pitch) + OD_BLR_W * (t - OD_BLR_CH * row);
-#endif
-#if OD_DIAG == 5 || OD_DIAG == 6   // timing diagnostics only (wrong descriptors): contiguous chunks
-        sob4[k] = OD_BLR_W * t;
-#endif
     }
-#else
-    // per-lane patch offsets relative to the patch bases
-    uint32_t sor[OD_RL], sob[OD_BL];
-#pragma unroll
-    for (int k = 0; k < OD_RL; ++k) {
-        const int t = min(l32 + 32 * k, OD_RAW_N - 1);
-        const int row = (int)(__umul24((uint32_t)t, 7282u) >> 16);   // t / 9 for t < 1000 (24-bit multiply)
-        sor[k] = __umul24(row, pitch) + 4 * (t - row * OD_RAW_DW);
-    }
-#pragma unroll
-    for (int k = 0; k < OD_BL; ++k) {
-        const int t = min(l32 + 32 * k, OD_BLR_N - 1);
-        const int row = (int)(__umul24((uint32_t)t, 6554u) >> 16);   // t / 10 for t < 1000
-        sob[k] = __umul24(row, pitch) + 4 * (t - row * OD_BLR_DW);
-    }
-#endif
     // keypoint of this half-wave in pair p: k = 2p + half (clamped: a lone last keypoint is
     // computed by both halves, the upper half's results are not used)
     auto kp_word = [&](int p) {
@@ -1705,20 +1206,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     // the keypoint whose patch a load of pair p reads (diagnostic builds 7 / 8 only: the
     // wave's first keypoint for every pair / the pair's first keypoint for both halves)
     auto ld_word = [&](int p) {
-#if OD_DIAG == 7
-        (void)p;
-        return (uint32_t)__builtin_amdgcn_readlane((int)cw, 0);
-#elif OD_DIAG == 8
-        return (uint32_t)__builtin_amdgcn_readlane((int)cw, min(2 * p, nk - 1));
-#else
         return kp_word(p);
-#endif
     };
     uint32_t* P = patch[wid][half];
     const int npair = (nk + 1) >> 1;
     // buffer loads: one 32-bit offset add per load instead of a 64-bit address
     const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc((void*)blr_l, 0, 0x7FFFFFFF, 0x00020000);
-#if OD_X4
     // a chunk reads up to 14 bytes past the patch row: the row's padding or the next row of
     // the same buffer (patch rows end at least one row before the level's last)
     const __amdgpu_buffer_rsrc_t rraw = __builtin_amdgcn_make_buffer_rsrc((void*)pyr_l, 0, 0x7FFFFFFF, 0x00020000);
@@ -1736,31 +1229,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     auto issue_blr = [&](int p) {
         const uint32_t c = ld_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
-#if BLUR_STRIPE
-        const uint32_t vo = (uint32_t)((x - 18) >> 4) * sh16 + 16u * (uint32_t)(y - 18);
-#else
         const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
-#endif
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo + sob4[j]);
     };
-#else
-    uint32_t v[OD_BL];
-    auto issue_raw = [&](int p) {
-        const uint32_t c = kp_word(p);
-        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
-        const uint8_t* pr = pyr_l + __umul24(y - 15, pitch) + ((x - 15) & ~3);
-#pragma unroll
-        for (int j = 0; j < OD_RL; ++j) v[j] = *(const uint32_t*)(pr + sor[j]);
-    };
-    auto issue_blr = [&](int p) {
-        const uint32_t c = kp_word(p);
-        const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
-        const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
-#pragma unroll
-        for (int j = 0; j < OD_BL; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rblr, vo + sob[j], 0, 0);
-    };
-#endif
 
     // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
     //      u = l32 - 15 of its half's keypoint, rows v = 1..15; umax decreases with v, so the
@@ -1772,25 +1244,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const uint8_t* raw = (const uint8_t*)P;   // [31][OD_RAW_RP]
     int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
     issue_raw(0);
-#if OD_DIAG == 2   // diagnostic builds only: no moment phase (angle from zero moments)
-    for (int p = 0; p < 0; ++p) {
-#else
     for (int p = 0; p < npair; ++p) {
-#endif
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
-#if OD_X4
 #pragma unroll
         for (int j = 0; j < OD_RL4; ++j) {
             const int t = l32 + 32 * j;
             if (t < 31 * OD_RAW_CH) od_store<OD_RAW_W>(P, t, vr[j]);
         }
-#else
-#pragma unroll
-        for (int j = 0; j < OD_RL; ++j) {
-            const int t = l32 + 32 * j;
-            if (t < OD_RAW_N) P[t] = v[j];
-        }
-#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_raw(p + 1);   // next pair's patches in flight
         else issue_blr(0);                     // phase 3's first patches in flight
@@ -1813,14 +1273,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     }
 
     // ---- 2. angle, cos / sin (src/ORBextractor.cc:103, 113) and the keypoint record ----
-#if OD_DIAG == 3   // diagnostic builds only: no angle / sincos work
-    const float angle = (float)(mk01 ^ mk10), ca_l = angle, sb_l = -angle;
-#else
     const float angle = cv_fast_atan2((float)mk01, (float)mk10);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float ca_l = glibc_cosf(ang), sb_l = glibc_sinf(ang);
-#endif
     if (lane < nk) {
         const size_t o = (size_t)b * g->kp_cap + off + oi;
         const int x = cand_x(cw) + ORBX_MIN_BORDER, y = cand_y(cw) + ORBX_MIN_BORDER;
@@ -1847,39 +1303,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         py2[w] = (float)c_pattern[4 * q + 3];
     }
     const uint8_t* blr = (const uint8_t*)P;   // [37][OD_BLR_RP]
-#if OD_DIAG == 1   // diagnostic builds only (tools/variants.py): no descriptor phase
-    if (npair > 0) return;
-#endif
     for (int p = 0; p < npair; ++p) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
         const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
         const float ca0 = readlane_f(ca_l, k0), ca1 = readlane_f(ca_l, k1);
         const float sb0 = readlane_f(sb_l, k0), sb1 = readlane_f(sb_l, k1);
         const float ca = half ? ca1 : ca0, sb = half ? sb1 : sb0;
-#if OD_X4
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) {
             const int t = l32 + 32 * j;
-#if BLUR_STRIPE
-            if (t < OD_BLR_NCH) od_store<OD_BLR_W>(P, (int)sdst[j], v[j]);
-#else
             if (t < 37 * OD_BLR_CH) od_store<OD_BLR_W>(P, t, v[j]);
-#endif
         }
-#else
-#pragma unroll
-        for (int j = 0; j < OD_BL; ++j) {
-            const int t = l32 + 32 * j;
-            if (t < OD_BLR_N) P[t] = v[j];
-        }
-#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_blr(p + 1);
-#if BLUR_STRIPE
-        const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~15));
-#else
         const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~3));
-#endif
         // cvRound (:118-120) by the round-to-nearest-even of a float add: for |v| < 2^22,
         // v + 1.5*2^23 holds rint(v) in its low mantissa bits, so its bit pattern is
         // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
@@ -1976,6 +1413,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     const bool side_l0 = side_od && mode >= 4 && a.in_place;
     const int main0 = side_l0 ? 1 : 0;
     const int fork_main = fork_at > main0 ? fork_at : main0;
+    // the host pyramid copy takes the side stream when the side branch does not
+    const bool pyr_fork = a.pyr_host && !side && a.side && a.ev_fork && a.ev_join;
     hipError_t err = hipSuccess;
     if (side) {
         err = launch_levels(a, st, main0, fork_main);
@@ -1996,15 +1435,25 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     } else {
         err = a.chain ? launch_pyr_chain(a, st) : launch_levels(a, st, 0, G.nlevels);
         if (err != hipSuccess) return err;
+        if (pyr_fork) {   // the pyramid's DMA to the host beside the kernels below
+            if ((err = hipEventRecord(a.ev_fork, st)) != hipSuccess ||
+                (err = hipStreamWaitEvent(a.side, a.ev_fork, 0)) != hipSuccess ||
+                (err = hipMemcpyAsync(a.pyr_host, a.pyr, a.pyr_host_bytes, hipMemcpyDeviceToHost,
+                                      a.side)) != hipSuccess ||
+                (err = hipEventRecord(a.ev_join, a.side)) != hipSuccess)
+                return err;
+        }
         fast(0, G.n_cells, st);
-#if OCT_MERGED
         oct(dim3(G.nlevels, a.batch), oct_lds, a.ncap, oct_kcap, 0, st);
-#else
-        oct(dim3(1, a.batch), a.octree_lds, a.ncap, a.kcap, 0, st);
-        if (G.nlevels > 1) oct(dim3(G.nlevels - 1, a.batch), a.octree_lds1, a.ncap1, a.kcap1, 1, st);
-#endif
     }
     orient(ob0, G.orient_blocks - ob0, ob0, st);
+    if (pyr_fork) {
+        if ((err = hipStreamWaitEvent(st, a.ev_join, 0)) != hipSuccess) return err;
+    } else if (a.pyr_host &&
+               (err = hipMemcpyAsync(a.pyr_host, a.pyr, a.pyr_host_bytes, hipMemcpyDeviceToHost,
+                                     st)) != hipSuccess) {
+        return err;
+    }
     return hipGetLastError();
 }
 

@@ -4,9 +4,7 @@
 
 #include <cstddef>
 
-#ifndef ORBX_MAX_DEVICES
 #define ORBX_MAX_DEVICES 64  // per-device kernel attribute caches (prepare_kernels, kfdb)
-#endif
 
 namespace orbx {
 

@@ -19,9 +19,7 @@
 #define ORBX_MAX_LEVELS 16
 #define ORBX_EDGE 19
 #define ORBX_MIN_BORDER 16   // EDGE_THRESHOLD - 3, src/ORBextractor.cc:785
-#ifndef ORBX_MAX_DEVICES
 #define ORBX_MAX_DEVICES 64  // per-device kernel attribute caches (prepare_kernels, kfdb)
-#endif
 
 namespace orbx {
 
@@ -57,65 +55,30 @@ struct LevelGeom {
 };
 
 // k_level tiling (orbx_pyramid.hip): 128 x 32 output tile, staged with a 4-byte / 3-row halo.
-#ifndef OD_NK
 #define OD_NK 8               // keypoints per wave in k_orient_desc (<= 64)
-#endif
-// k_octree: one launch over all levels (OCT_MERGED) under one LDS budget per workgroup, the
+// k_octree: one launch over all levels under one LDS budget per workgroup, the
 // blocks in level-major order so the long level-0 lists start first and the shorter lists of
 // levels 1.. fill the CUs behind them; a level whose candidates exceed the budget's kcap keeps
 // them in global scratch.  B = 512, two runs each (profiles/r03_ab_octree_merged.txt): merged
 // level-major at 40 KB 0.322-0.323 ms, two launches (level 0, then levels 1..) at 40 KB
 // 0.335-0.339, merged in (image, level) order 0.536-0.542, merged level-major at 52 KB 0.358-0.361
-#ifndef OCT_MERGED
-#define OCT_MERGED 1
-#endif
-#ifndef OCT_LDS0_KB
-#define OCT_LDS0_KB 40  // level 0 launch (OCT_MERGED = 0): four workgroups per CU, all 1024 images in
-                        // one round (76 KB, two per CU: 0.341 vs 0.327 ms)
-#endif
-#ifndef OCT_LDS1_KB
-#define OCT_LDS1_KB 40  // levels 1.. launch (OCT_MERGED = 0): four workgroups per CU
-#endif
-#ifndef OCT_LEVEL_MAJOR
-#define OCT_LEVEL_MAJOR 1   // OCT_MERGED: blocks in level-major order (level 0's lists first)
-#endif
-#ifndef OCT_LDS_KB
-#define OCT_LDS_KB 40       // OCT_MERGED: four workgroups per CU
-#endif
+#define OCT_LDS_KB 40       // four workgroups per CU
 // Default side branch of an extraction (orbx_extractor_set_overlap): the first FAST_SIDE_LV
 // levels' FAST (FAST_SIDE 1), + octree (2), + orientation / descriptors (3) on the handle's
 // second stream, forked before level FAST_SIDE_AT's launch; 0 = every kernel on one stream.
 // B = 512 (profiles/r03_ab_side_*.txt): one stream 4.66-4.68 ms per step; mode 3 forked at
 // level 3, 4.47 ms
-#ifndef FAST_SIDE
 #define FAST_SIDE 3
-#endif
-#ifndef FAST_SIDE_AT
 #define FAST_SIDE_AT 3
-#endif
-#ifndef FAST_SIDE_LV
 #define FAST_SIDE_LV 1
-#endif
-// Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches).  BLUR_STRIPE:
-// each level is stored as 16-byte-wide column stripes of all its rows (byte (x, y) at
-// (x / 16) * 16 h + 16 y + x % 16, the same pitch * h bytes as row-major), so a 37-row
-// patch is 4 contiguous runs of 592 bytes instead of 37 rows on 37+ cache lines.
-#ifndef BLUR_STRIPE
-#define BLUR_STRIPE 0
-#endif
+// Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches): row-major, the
+// pyramid's own pitch (16-byte column stripes were measured in round 3: profiles/r04_ab_design_history.txt)
 __host__ __device__ inline uint32_t blur_off(int x, int y, int pitch, int h) {
-#if BLUR_STRIPE
-    (void)pitch;
-    return (uint32_t)(x >> 4) * (uint32_t)(16 * h) + 16u * (uint32_t)y + (uint32_t)(x & 15);
-#else
     (void)h;
     return (uint32_t)y * (uint32_t)pitch + (uint32_t)x;
-#endif
 }
 #define LT_W 128              // output tile width  (32 groups of 4)
-#ifndef LT_H
 #define LT_H 32               // output tile height
-#endif
 #define LT_G 34               // halo groups per row: x = X0-4 .. X0+131
 #define LT_HR (LT_H + 6)      // halo rows: y = Y0-3 .. Y0+LT_H+2
 
@@ -155,12 +118,8 @@ __host__ __device__ inline int chain_pitch(int fw) { return ((fw + 3) & ~3) + 12
 __host__ __device__ inline int chain_level_words(int ng, int fh) {
     return ((ng + 3) & ~3) + 8 * ng + 2 * ((fh + 1) & ~1);
 }
-#ifndef CHAIN_TW
 #define CHAIN_TW 80    // k_pyr_chain: level-0 tile width / height targets (tiles per image =
-#endif
-#ifndef CHAIN_TH
 #define CHAIN_TH 48    // ceil(w / CHAIN_TW) x ceil(h / CHAIN_TH))
-#endif
 
 // k_level_strip: a wave walks two half-strips (lanes 0-31, 32-63) down the level, one row per
 // step.  Lane q of a half-strip at X0 holds the 4-pixel group x = X0 - 4 + 4q; lanes 1..SW_OUT
@@ -172,9 +131,7 @@ __host__ __device__ inline int chain_level_words(int ng, int fh) {
 //     2 bits per pixel (right tap in range, SSE2 vertical form).
 // Row table per level: rows y = -3 .. h + 2, 4 dwords each: mode 3 the byte offsets of the
 // two source rows in level l-1 and (beta0 | beta1 << 16); mode 0 the reflected input row.
-#ifndef STRIP_TH
 #define STRIP_TH 64   // output rows per strip (<= 122: the row table sits in two registers)
-#endif
 #define SW_OUT 30
 #define SW_PX (4 * SW_OUT)
 struct StripLane {
@@ -227,35 +184,17 @@ struct Geometry {
     LevelGeom lv[ORBX_MAX_LEVELS];
 };
 
-// k_fast ROI row pitch in dwords (FAST_W16): a multiple of 4 (16-byte aligned rows for the
+// k_fast ROI row pitch in dwords: a multiple of 4 (16-byte aligned rows for the
 // compass's b128 reads) with room for the widest lane's reads (16 pixels per lane, 2 lanes
 // per detection row up to 32 columns, else 4).  A bank-conflict-free pitch (24 / 48 dwords)
 // was measured slower: the larger ROI costs a workgroup per CU.
-#ifndef FAST_NC
 #define FAST_NC 4        // k_fast cells per wave at large batches (the next cell's ROI loads
                          // overlap this cell's work); small batches take fewer
-#endif
-#ifndef FAST_STAGE2D
-#define FAST_STAGE2D 1   // k_fast ROI prefetch on a 16-lanes-per-row grid (no index divisions)
-#endif
-#ifndef FAST_PF2D
 #define FAST_PF2D 10     // its rows per lane: ROIs up to 40 rows are prefetched
-#endif
-#ifndef FAST_PFU
-#define FAST_PFU 1       // prefetch all 4 * FAST_PF2D rows unclamped (LDS and pyramid slack)
-#endif
-#ifndef FAST_W16
-#define FAST_W16 1
-#endif
 __host__ __device__ inline int fast_lpitch(int ndw, int dw) {
-#if FAST_W16
     const int lpr = dw > 32 ? 4 : 2;
     const int need = ndw > 4 * lpr + 4 ? ndw : 4 * lpr + 4;
     return (need + 3) & ~3;
-#else
-    (void)dw;
-    return ndw;
-#endif
 }
 
 // Packed candidate / octree survivor: x, y relative to (minBorderX, minBorderY).

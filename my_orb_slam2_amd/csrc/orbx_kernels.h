@@ -139,6 +139,11 @@ struct ExtractLaunch {
     // the handle's side stream and fork / join events (level-0 branch, launch_extract)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the host copy of image 0's pyramid block (mvImagePyramid, orbx_extractor_host_pyramid):
+    // pyr_host_bytes from the pyramid into pinned pyr_host, on the side stream beside the
+    // FAST / octree / orientation launches (after them when the side branch is in use)
+    uint8_t* pyr_host = nullptr;
+    size_t pyr_host_bytes = 0;
     // side branch: 0 off, 1 FAST, 2 + octree, 3 + orientation / descriptors of levels
     // [0, side_lv), forked before level side_at's launch
     int side_mode = 0, side_at = 0, side_lv = 1;

@@ -142,12 +142,8 @@ __device__ __forceinline__ int x86_int(float f) {
 //      claim is re-scanned (all 64 lanes, against the claim bitmap).  Within a chunk, the
 //      lanes before the first one that claims or conflicts are decided together.
 // BLDS = false reads the B descriptors from global memory (nodes too large for LDS).
-#ifndef BOW_R
 #define BOW_R 4   // A features per thread in the static pass
-#endif
-#ifndef BOW_T
 #define BOW_T 256 // threads per job
-#endif
 template <bool BLDS>
 __global__ __launch_bounds__(BOW_T) void k_bow(BowLaunch g) {
     extern __shared__ __attribute__((aligned(16))) int lds[];

@@ -36,6 +36,7 @@ struct orbx_matcher {
     hipEvent_t bf_done = nullptr;
     hipStream_t bf_stream = nullptr;
     bool have_bf = false;
+    int bf_kernel = ORBX_BF_MFMA;
 };
 
 namespace {
@@ -504,8 +505,15 @@ orbx_status orbx_search_by_projection_ex(orbx_matcher* m, int32_t mode,
                                          const float* inv_sigma2, int32_t nlevels,
                                          int32_t orb_dist, int32_t flags, int32_t* match_q,
                                          int32_t* nmatches) {
-    if (mode < 0 || mode >= ORBX_PROJ_MODE_COUNT || (flags & ~ORBX_PROJ_PREFILTER))
+    if (mode < 0 || mode >= ORBX_PROJ_MODE_COUNT || (flags & ~ORBX_PROJ_PREFILTER) || !m)
         return ORBX_ERR_INVALID;
+    // LAST_FRAME's rotation filter runs per feature in the reference (:1516-1535): with
+    // no-claim queries a feature can be matched twice and sit in two bins, which a per-query
+    // filter cannot reproduce, so that combination needs the caller's own filter (PREFILTER)
+    if (mode == ORBX_PROJ_LAST_FRAME && m->prm.check_orientation && !(flags & ORBX_PROJ_PREFILTER) &&
+        qflags && nq > 0)
+        for (int32_t i = 0; i < nq; ++i)
+            if (qflags[i] & ORBX_QF_NO_CLAIM) return ORBX_ERR_INVALID;
     return proj_common(m, mode, target, claimed, qdesc, q, nq, inv_sigma2, nlevels, orb_dist,
                        match_q, nmatches, qflags, flags);
 }
@@ -798,6 +806,7 @@ orbx_status bf_run(orbx_matcher* m, const uint8_t* d_q, int nq, const uint8_t* d
     a.best_idx = bi;
     a.best_dist = bd;
     a.second_dist = sd;
+    a.kernel = m->bf_kernel;
     if (!HIPOK(launch_bf_top2(a, st, &m->timer)) || !HIPOK(hipEventRecord(m->bf_done, st)))
         return ORBX_ERR_DEVICE;
     m->bf_stream = st;
@@ -835,7 +844,16 @@ orbx_status orbx_hamming_bf_top2(orbx_matcher* m, const uint8_t* q, int32_t nq,
     return ORBX_OK;
 }
 
-const char* orbx_bf_kernel(void) { return orbx::bf_kernel_name(); }
+const char* orbx_bf_kernel(void) { return orbx::bf_kernel_name(ORBX_BF_MFMA); }
+
+const char* orbx_bf_kernel_name(int32_t kernel) { return orbx::bf_kernel_name(kernel); }
+
+orbx_status orbx_matcher_set_bf_kernel(orbx_matcher* m, int32_t kernel) {
+    if (!m || !orbx::bf_kernel_name(kernel)) return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->bf_kernel = kernel;
+    return ORBX_OK;
+}
 
 orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int32_t nq,
                                         const uint8_t* d_db, int64_t ndb, int64_t idx_base,

@@ -100,12 +100,13 @@ struct BfLaunch {
     int32_t* best_idx;
     int32_t* best_dist;
     int32_t* second_dist;
+    int kernel;            // ORBX_BF_MFMA / ORBX_BF_VALU
 };
 int bf_chunk_rows(long long ndb, int nq, int ncu);
 size_t bf_partial_bytes(long long ndb, int nq, int chunk);
 struct KernelTimer;
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer);
-const char* bf_kernel_name();
+const char* bf_kernel_name(int kernel);
 hipError_t launch_distinctive(const uint8_t* desc, const int32_t* off, int np, int32_t* best,
                               int* err, hipStream_t st);
 size_t distinctive_lds_bytes();

@@ -27,9 +27,7 @@
 #define ORBX_HD static inline
 #endif
 
-#ifndef ORBX_GLIBC_FMA
 #define ORBX_GLIBC_FMA 1
-#endif
 
 namespace orbx {
 
@@ -39,12 +37,7 @@ ORBX_HD float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 // a*b+c with the rounding the glibc FMA ifunc variant uses (one rounding), or the SSE2
 // variant (two roundings).
 ORBX_HD double glibc_madd(double a, double b, double c) {
-#if ORBX_GLIBC_FMA
     return fma(a, b, c);
-#else
-    double t = a * b;
-    return c + t;
-#endif
 }
 
 // Polynomial coefficients, __sincosf_table[0] of glibc sincosf_data.c (!TOINT_INTRINSICS).
@@ -97,11 +90,7 @@ ORBX_HD double glibc_reduce_fast(double x, const SinCosTab& p, int* np) {
     double r = x * p.hpi_inv;
     int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
-#if ORBX_GLIBC_FMA
     return fma(-(double)n, p.hpi, x);
-#else
-    return x - n * p.hpi;
-#endif
 }
 
 ORBX_HD double sign_of(const SinCosTab& p, int q) {

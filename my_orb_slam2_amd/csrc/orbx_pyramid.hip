@@ -22,20 +22,6 @@
 
 namespace orbx {
 
-#ifdef ORBX_STAMPS
-// Diagnostic build only (tools/level_stamps.py): per-workgroup phase clocks of k_level.
-__device__ unsigned long long g_level_stamps[8][4096][6];
-#define STAMP(k)                                                                         \
-    do {                                                                                 \
-        __builtin_amdgcn_sched_barrier(0);                                               \
-        unsigned long long t_;                                                           \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
-        __builtin_amdgcn_sched_barrier(0);                                               \
-        if (tid == 0 && blockIdx.y == 0 && blockIdx.x < 4096) g_level_stamps[level][blockIdx.x][k] = t_; \
-    } while (0)
-#else
-#define STAMP(k) do { } while (0)
-#endif
 
 #define LT_GW (LT_W / 4)      // output groups per row
 
@@ -53,28 +39,6 @@ __device__ __forceinline__ int sat8(int v) { return min(max(v, 0), 255); }
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef float f2v __attribute__((ext_vector_type(2)));
-
-// min / max of reflect101(p) over p in [lo, hi].
-__device__ __forceinline__ void reflected_range(int lo, int hi, int len, int& mn, int& mx) {
-    mn = 1 << 30;
-    mx = -1;
-    const int a = max(lo, 0), b = min(hi, len - 1);
-    if (a <= b) { mn = a; mx = b; }
-    for (int p = lo; p < min(0, hi + 1); ++p) {
-        const int r = reflect101_i(p, len);
-        mn = min(mn, r); mx = max(mx, r);
-    }
-    for (int p = max(len, lo); p <= hi; ++p) {
-        const int r = reflect101_i(p, len);
-        mn = min(mn, r); mx = max(mx, r);
-    }
-}
-
-// byte k (runtime, 0..11) of the 12-byte little-endian sequence d0 d1 d2
-__device__ __forceinline__ int byte12(uint32_t d0, uint32_t d1, uint32_t d2, int k) {
-    const uint32_t v = k < 4 ? d0 : (k < 8 ? d1 : d2);
-    return (int)((v >> ((k & 3) * 8)) & 255u);
-}
 
 // OpenCV INTER_LINEAR 8U value from the two horizontal sums (VResizeLinear + cast).
 __device__ __forceinline__ int vresize(int h0, int h1, int b0, int b1, bool simd) {
@@ -200,17 +164,9 @@ __device__ __forceinline__ void tile_columns(const uint16_t* rows, int tid, int 
     }
 }
 
-#ifndef BLUR_F32
-#define BLUR_F32 1     // row sums kept as floats, column pass in float (exact, see below)
-#endif
-#ifndef BLUR_SLIDE
 #define BLUR_SLIDE 4   // full tiles: output rows per thread in the column pass (0: one row per item)
-#endif
-#ifndef BLUR_CVTPK
-#define BLUR_CVTPK 1   // round + saturate + pack with v_cvt_pk_u8_f32 (else magic-add rounding)
-#endif
 
-// ---- 4'. blur row pass with float row sums (BLUR_F32) ----
+// ---- 4'. blur row pass with float row sums ----
 // Same v_dot4 sums as tile_out_rows; each sum (<= 257 * 255) is stored as an exact float.
 template <bool FULL>
 __device__ __forceinline__ void tile_out_rows_f(const uint32_t* lvl, float* rows, int tid, int vw,
@@ -259,7 +215,7 @@ __device__ __forceinline__ void tile_out_rows_f(const uint32_t* lvl, float* rows
     }
 }
 
-// ---- 5'. blur column pass in float (BLUR_F32) ----
+// ---- 5'. blur column pass in float ----
 // S = k3*c + k4*(r2+r4) + k5*(r1+r5) + k6*(r0+r6) with integer taps and integer row sums:
 // every pairwise sum (< 2^17), product (< 2^23) and partial sum (< 2^24, see tile_columns)
 // is exact in float, so Sf == S.  SSE2 pixels take rint(S / 65536) saturated to u8
@@ -293,16 +249,8 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
         const int xg = X0 + 4 * gq;
         uint32_t packed = 0;
         if (tile_simd || xg + 4 <= bsimd_end) {
-#if BLUR_CVTPK
 #pragma unroll
             for (int j = 0; j < 4; ++j) packed = __builtin_amdgcn_cvt_pk_u8_f32(S[j], j, packed);
-#else
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t t = __builtin_bit_cast(uint32_t, S[j] + 12582912.0f) - 0x4B400000u;
-                packed |= min(t, 255u) << (8 * j);
-            }
-#endif
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -327,7 +275,6 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
         col_sums(v, S);
         col_store(r, gq, S);
     };
-#if BLUR_SLIDE
     if constexpr (FULL) {
         // a thread owns one group and BLUR_SLIDE consecutive output rows: it reads their
         // BLUR_SLIDE + 6 row sums once (7 per output row in the item form)
@@ -344,7 +291,6 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
             col_store(r0 + o, gq, S);
         }
     } else
-#endif
     if constexpr (FULL) {
 #pragma unroll
         for (int k = 0; k < LT_H * LT_GW / 256; ++k) col_item(tid + 256 * k);
@@ -353,22 +299,8 @@ __device__ __forceinline__ void tile_columns_f(const float* rows, int tid, int v
     }
 }
 
-#ifndef LEVEL_DIAG
-#define LEVEL_DIAG 0   // diagnostic builds only: 1 no resize math, 2 no mode-3 staging, 4 no column pass, 8 no row pass,
-                       // 16 no level-0 loads, 32 no table loads
-#endif
-#ifndef LEVEL_FORCE_GENERIC
-#define LEVEL_FORCE_GENERIC 0   // diagnostic builds only: every tile on the partial-tile paths
-#endif
-#ifndef LEVEL_COLQ
-#define LEVEL_COLQ 1   // mode-3 full tiles: a thread keeps one column group (tables read once)
-#endif
-#ifndef STAGE_MAXK
 #define STAGE_MAXK 12  // column-owner window staging: up to 48 rows (0: always the generic form)
-#endif
-#ifndef LEVEL_WPE
 #define LEVEL_WPE 1
-#endif
 // MODE (host-chosen per level, one instantiation each): 0 level 0 (copy of the input), 1 scale
 // 1 copy, 2 exact 2:1 area, 3 INTER_LINEAR
 template <int MODE>
@@ -383,7 +315,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     int bx, b;
     xcd_block(bx, b);
     const int tid = threadIdx.x;
-    STAMP(0);
     const LevelGeom& L = g->lv[level];
     const int tx = bx % L.ntx, ty = bx / L.ntx;
     const int X0 = tx * LT_W, Y0 = ty * LT_H;
@@ -414,9 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     const int wx0 = CT->x0, WWb = CT->ww, wy0 = RT->y0, WH = RT->wh;
     // table loads issued before the window loads, so both land in one round trip
     uint4 tc = make_uint4(0, 0, 0, 0), ta = make_uint4(0, 0, 0, 0), ts = ta;
-    if (LEVEL_DIAG & 32) {
-        tc = make_uint4(tid, 0, 0, 0);
-    } else if (mode == 0) {
+    if (mode == 0) {
         // level 0 reads no tables
     } else if (tid < LT_G) {
         tc = make_uint4(CT->cgrp[2 * tid], CT->cgrp[2 * tid + 1], CT->cinf[tid], 0);
@@ -432,9 +361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
     // aligned dwords + v_alignbyte per 4-pixel group, or on border tiles four byte loads per
     // group (rows and columns reflected per item)
     constexpr bool direct = mode == 0;
-    if (direct && (LEVEL_DIAG & 16)) {
-        for (int i = tid; i < LT_HR * LT_G; i += 256) lvl[i] = (uint32_t)i;
-    } else if (direct) {
+    if (direct) {
         const uint8_t* src = (b < split ? in0 + (size_t)b * bstride : in1 + (size_t)(b - split) * bstride);
         const int W = L.w, H = L.h;
         constexpr int NI = (LT_HR * LT_G + 255) / 256;
@@ -494,7 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                                            (WWb + 3) >> 2, (uint32_t*)(win + wcol0), WP / 4, tid))
             stage_dwords<256>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, (WWb + 3) >> 2,
                               (uint32_t*)(win + wcol0), WP / 4, tid);
-    } else if (mode == 3 && !(LEVEL_DIAG & 2)) {
+    } else if (mode == 3) {
         const uint8_t* src = pyr + (size_t)b * g->pyr_bytes + S.off;
         if (!stage_dwords_cols<STAGE_MAXK>(src + (size_t)wy0 * S.pitch + wx0, S.pitch, WH, WP / 4,
                                            (uint32_t*)win, WP / 4, tid))
@@ -511,18 +438,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         rinf[tid - 64] = make_uint2(tc.x, tc.y);
     }
     __syncthreads();
-    STAMP(2);
 
     // ---- 2. level l on tile + halo, 4 pixels per item ----
     const uint8_t* src2 = pyr + (size_t)b * g->pyr_bytes + S.off;   // mode 2 only
     // item i = (halo row hr, group q); 256 = 7 * LT_G + 18, advanced without divisions
-    const bool full_tile = !LEVEL_FORCE_GENERIC && vw == LT_W && vh == LT_H;   // every halo item is needed
+    const bool full_tile = vw == LT_W && vh == LT_H;   // every halo item is needed
     // mode 3 (generic INTER_LINEAR) on one 4-pixel group: halo row hr, the group's column
     // tables (cg: source columns, ci: flags, al: alphas, sl: v_perm selectors)
     auto item3 = [&](int hr, uint2 cg, uint32_t ci, uint4 al, uint4 sl, auto fast_c) -> uint32_t {
         constexpr bool FASTP = decltype(fast_c)::value;   // simple group, all four pixels SSE2
         uint32_t out = 0;
-        if (LEVEL_DIAG & 1) return cg.x ^ ci ^ al.x ^ sl.y ^ (uint32_t)hr;
         const uint2 ri = rinf[hr];
         const int xs[4] = {(int)(cg.x & 0xFFFF), (int)(cg.x >> 16), (int)(cg.y & 0xFFFF),
                            (int)(cg.y >> 16)};
@@ -637,7 +562,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         }
         lvl[hr * LT_G + q] = out;
     };
-#if LEVEL_COLQ
     if (!direct && mode == 3 && full_tile) {
         // thread t < 7 LT_G keeps column group q = t % LT_G for halo rows t / LT_G + 7k: the
         // group's tables are read once, not once per item
@@ -665,7 +589,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
             }
         }
     } else
-#endif
     if (!direct) {
         int hr = tid / LT_G, q = tid - hr * LT_G;
         if (full_tile) {
@@ -685,7 +608,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
         }
     }
     __syncthreads();
-    STAMP(3);
 
     uint8_t* dlev = pyr + (size_t)b * g->pyr_bytes + L.off;
     uint8_t* dblur = blur + (size_t)b * g->pyr_bytes + L.off;
@@ -696,26 +618,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
                          (uint32_t)k4 * 0x10001u, (uint32_t)k5 * 0x10001u, (uint32_t)k6 * 0x10001u,
                          (uint32_t)k3};
     // full tiles (all but the right / bottom edge) run the fixed-trip-count form
-    const bool full = !LEVEL_FORCE_GENERIC && vw == LT_W && vh == LT_H;
-#if BLUR_F32
+    const bool full = vw == LT_W && vh == LT_H;
     float* rowsf = (float*)rows;
-    if (LEVEL_DIAG & 8) {} else
     if (full) tile_out_rows_f<true>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     else tile_out_rows_f<false>(lvl, rowsf, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
     __syncthreads();
-    STAMP(4);
-    if (LEVEL_DIAG & 4) {} else
     if (full) tile_columns_f<true>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
     else tile_columns_f<false>(rowsf, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
-#else
-    if (full) tile_out_rows<true>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
-    else tile_out_rows<false>(lvl, rows, tid, vw, vh, dlev, X0, Y0, L.pitch, tp);
-    __syncthreads();
-    STAMP(4);
-    if (full) tile_columns<true>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
-    else tile_columns<false>(rows, tid, vw, vh, dblur, X0, Y0, L.pitch, L.h, L.bsimd_end, tp);
-#endif
-    STAMP(5);
 }
 
 // ---- k_level_strip: level l and its blur by column strips, one row per step ----
@@ -727,77 +636,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 // symmetric column sum.  No LDS, no barriers: the loads of later rows are in flight while
 // the wave computes.  The arithmetic is item3's (resize, mode 3) and tile_out_rows_f /
 // tile_columns_f's (blur), bit for bit.
-#ifndef STRIP_PF
 #define STRIP_PF 2   // mode 3: rows of source loads in flight ahead of the row being computed
-#endif
-#ifndef STRIP_ST_POLICY
 #define STRIP_ST_POLICY 0   // cache-policy bits of the strip walk stores: nt (2) 1.99 ms, sc1 (16) 1.88 ms vs 1.71 ms
-#endif
-#ifndef STRIP_BUFST
-#define STRIP_BUFST 1
-#endif
-#ifndef STRIP_DIAG
-#define STRIP_DIAG 0   // diagnostic builds only: 1 no stores (every store dropped)
-#endif
-#if STRIP_BUFST
 #define STRIP_LEV rlev
 #define STRIP_BLR rblr
-#else
-#define STRIP_LEV lev0
-#define STRIP_BLR blr0
-#endif
-#ifndef STRIP_PRO_STORES
-#define STRIP_PRO_STORES 1
-#endif
-#ifndef STRIP_ROWDOT
-#define STRIP_ROWDOT 1   // row pass as 10 v_dot4 with shifted tap words (no v_alignbyte)
-#endif
-#ifndef STRIP_SCHEDB
-#define STRIP_SCHEDB 1
-#endif
-#ifndef STRIP_HREUSE
 #define STRIP_HREUSE 1   // mode 3: reuse the previous step's HResize of a shared source row
-#endif
-#ifndef STRIP_HMASK
 #define STRIP_HMASK 1   // mode 3, SSE2 waves: horizontal sums masked once per source row
-#endif
 // One workgroup per strip row (its snw <= 8 waves side by side) with an s_barrier every
 // STRIP_SYNC* blocks of 7 steps (0: 4-wave workgroups, no barrier): the waves of a strip row
 // then store each row within a few steps of each other, so the 128-byte lines split between
 // two waves' 120-pixel runs are merged in L2 before they are written back (without it one
 // write-back per part: level 0 wrote 1.24x its bytes, levels 1-7 1.10x).
-#ifndef STRIP_SYNC0
 #define STRIP_SYNC0 0  // level 0
-#endif
-#ifndef STRIP_SYNC3
 #define STRIP_SYNC3 2  // INTER_LINEAR levels
-#endif
-#ifndef STRIP_SYNC_LEVELS
 #define STRIP_SYNC_LEVELS 0xFFFF  // bit l: level l may take strip-row workgroups
-#endif
-#ifndef STRIP_PEEL
-#define STRIP_PEEL 1   // interior blocks of a walk without store predicates
-#endif
-#ifndef STRIP_NS3
 #define STRIP_NS3 2  // mode 3: load slots (1, 2 or 3; PF <= NS)
-#endif
-#ifndef STRIP_NS0
 #define STRIP_NS0 7  // mode 0: load slots (1, 2 or 7)
-#endif
-#ifndef STRIP_PF0
 #define STRIP_PF0 6  // mode 0: rows in flight (<= STRIP_NS0)
-#endif
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 template <typename F, int... K>
 __device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, K...>) {
     (f(std::integral_constant<int, K>{}), ...);
 }
-#ifndef STRIP_WPE0
 #define STRIP_WPE0 6
-#endif
-#ifndef STRIP_WPE3
 #define STRIP_WPE3 5
-#endif
 // One wave's strip of level `level` of image b (wave wv of the image's snw x sns strip waves).
 // MODE 0: level 0 from the caller's images (copied into the pyramid as it is blurred);
 // MODE 4: level 0 already in the pyramid (written there by the H2D copy or the caller, see
@@ -945,7 +807,7 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
             }
         };
         uint32_t hA[4], hC[4];
-        if (STRIP_HREUSE && RAo[slot] == prevRC) {   // wave-uniform
+        if (RAo[slot] == prevRC) {   // wave-uniform
 #pragma unroll
             for (int j = 0; j < 4; ++j) hA[j] = HCp[j];
         } else {
@@ -981,7 +843,6 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
     // store into the padding dword of the level's row 0.
     uint8_t* const lev0 = pyr + (size_t)b * g->pyr_bytes + L.off;
     uint8_t* const blr0 = blur + (size_t)b * g->pyr_bytes + L.off;
-#if STRIP_BUFST
     // buffer stores: a lane or step with nothing to write gets an offset past num_records,
     // which the hardware drops (no branch, no write)
     const int nrec = pitch * H;
@@ -989,40 +850,20 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
     const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc(blr0, 0, nrec, 0x00020000);
     // the row's byte offset rides in soffset (scalar), the lane's column in voffset: in range
     // or not whether or not the hardware adds soffset into its range check
-    const uint32_t lane_off = (out_lane && !(STRIP_DIAG & 1)) ? (uint32_t)x : 0x80000000u;
+    const uint32_t lane_off = out_lane ? (uint32_t)x : 0x80000000u;
     auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, int r, bool ok, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, STRIP_ST_POLICY);
     };
-#if BLUR_STRIPE
-    // the blurred rows go to the column-stripe layout (blur_off): a lane's 4-pixel group sits
-    // in one 16-byte stripe, rows 16 bytes apart
-    const uint32_t blane_off = (out_lane && !(STRIP_DIAG & 1)) ? blur_off(x, 0, pitch, H) : 0x80000000u;
-    auto store_blr = [&](int r, bool ok, uint32_t v) {
-        __builtin_amdgcn_raw_buffer_store_b32(v, rblr, ok ? blane_off : 0x80000000u, ok ? r * 16 : 0, STRIP_ST_POLICY);
-    };
-#else
     auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(rblr, r, ok, v); };
-#endif
-#else
-    const uint32_t pad_off = (uint32_t)(pitch - 4);
-    const uint32_t lane_off = out_lane ? (uint32_t)x : pad_off;
-    auto store_row = [&](uint8_t* base, int r, bool ok, uint32_t v) {
-        *(uint32_t*)(base + (size_t)(ok ? r : 0) * pitch + (ok ? lane_off : pad_off)) = v;
-    };
-    static_assert(!BLUR_STRIPE, "BLUR_STRIPE needs the buffer-store strip walk");
-    auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(blr0, r, ok, v); };
-#endif
     // step i (k = i mod U: the load slot k mod NS, the row-sum register k mod 7)
     // ALL: every step of this block stores both rows (no per-step store predicates)
     auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c, auto all_c) {
         constexpr int k = decltype(k_c)::value;
         constexpr bool ALL = decltype(all_c)::value;
         constexpr bool BSIMD = decltype(bsimd_c)::value;
-#if STRIP_SCHEDB
         // keep each step's memory operations in its step: the scheduler would otherwise sink
         // the prefetch loads toward their use (shorter live ranges), shortening the prefetch
         __builtin_amdgcn_sched_barrier(0);
-#endif
         const uint32_t v = level_group(k % NS, rsimd_c);
         issue((k + PF) % NS, i + PF);
         if constexpr (MODE != 4) store_row(STRIP_LEV, Y0 + i - 3, ALL || (i >= 3 && i < vh + 3), v);
@@ -1030,22 +871,12 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
         const uint32_t d0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);  // wave_shr:1 (bound_ctrl: lane 0 reads 0)
         const uint32_t d2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);  // wave_shl:1
         float4 o;
-#if STRIP_ROWDOT
         // taps shifted onto the three dwords (10 v_dot4, no v_alignbyte)
         auto dot4 = [](uint32_t a, uint32_t w, uint32_t c) { return __builtin_amdgcn_udot4(a, w, c, false); };
         o.x = (float)dot4(d0, W00, dot4(v, W01, 0u));
         o.y = (float)dot4(d0, W10, dot4(v, W11, dot4(d2, W12, 0u)));
         o.z = (float)dot4(d0, W20, dot4(v, W21, dot4(d2, W22, 0u)));
         o.w = (float)dot4(v, tp.tapA, dot4(d2, tp.tapB, 0u));
-#else
-        o.x = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 1), tp.tapA,
-                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 1), tp.tapB, 0u, false), false);
-        o.y = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 2), tp.tapA,
-                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 2), tp.tapB, 0u, false), false);
-        o.z = (float)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(v, d0, 3), tp.tapA,
-                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, v, 3), tp.tapB, 0u, false), false);
-        o.w = (float)__builtin_amdgcn_udot4(v, tp.tapA, __builtin_amdgcn_udot4(d2, tp.tapB, 0u, false), false);
-#endif
         R[k % 7] = o;
         {
             // blurred row y - 3 from the row sums of steps i-6 .. i (every lane computes it;
@@ -1089,12 +920,10 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             issue(i % NS, i);
-#if STRIP_PRO_STORES
             // the same memory-op sequence as a block's last steps (two stores after each
             // issue), so the loop header sees one pending-load state from both edges
             if constexpr (MODE != 4) store_row(STRIP_LEV, 0, false, 0u);
             store_blr(0, false, 0u);
-#endif
         }
         // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
         // store nothing)
@@ -1109,13 +938,11 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
                        std::make_integer_sequence<int, U>{});
         };
         int i0 = 0;
-#if STRIP_PEEL
         // the first block (the 6 halo steps), then the blocks that store every step (a copy
         // without the store predicates), then the rest
         static_assert(U >= 6, "the first block holds the halo steps");
         block(0, std::false_type{});
         for (i0 = U; i0 + U <= vh + 3; i0 += U) block(i0, std::true_type{});
-#endif
         for (; i0 < n; i0 += U) block(i0, std::false_type{});
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
@@ -1153,12 +980,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
 // border path) and RowFilter<uchar,int> + SymmColumnFilter in the exact integer form of
 // tile_columns (S < 2^24, SSE2 pixels round half to even) -- src/ORBextractor.cc:1129-1154,
 // :1107-1108.
-#ifndef CHAIN_NT
 #define CHAIN_NT 1024
-#endif
-#ifndef CHAIN_DIAG
-#define CHAIN_DIAG 0   // diagnostic builds only (tools/chain_stamps.py): 1 no level stores, 2 no VResize
-#endif
 __device__ __forceinline__ int reflect101_fast(int p, int len) {
     return (unsigned)p < (unsigned)len ? p : reflect101_i(p, len);
 }
@@ -1278,20 +1100,6 @@ __device__ __forceinline__ void chain_cols(const ChainRect& c, const LevelGeom& 
     }
 }
 
-#ifdef ORBX_CHAIN_STAMPS
-// Diagnostic build only (tools/chain_stamps.py): per-tile phase clocks of image 0.
-__device__ unsigned long long g_chain_stamps[256][40];   // [tile][phase]
-#define CSTAMP(k)                                                                          \
-    do {                                                                                   \
-        if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 256 && (k) < 40)           \
-            g_chain_stamps[blockIdx.x][(k)] = __builtin_readcyclecounter();                \
-    } while (0)
-extern "C" int orbx_diag_chain_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps));
-}
-#else
-#define CSTAMP(k) do { } while (0)
-#endif
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g,
@@ -1303,7 +1111,6 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
     const int tile = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x;
     const int L = g->nlevels;
-    CSTAMP(0);
     // LDS buffers by arithmetic on smem (a pointer picked from an array loses the LDS address
     // space: every access becomes a flat one)
     const int cbuf = g->chain_buf;
@@ -1339,7 +1146,6 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         sv[u] = i >= 0 ? *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q) : 0u;
     }
     __syncthreads();
-    CSTAMP(1);
     // 2. every level's column / row tables, while the staged words are stored.  Per level
     //    (chain_level_words, from word tw[l]): per column group of 4 pixels a base word
     //    (aligned source byte | its offset o0 << 16 | 1 << 20 when all 4 pixels take the SSE2
@@ -1410,18 +1216,15 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
         ((uint32_t*)(smem + r * P0))[q + 1] = *(const uint32_t*)(s0 + (size_t)r * pitch0 + 4 * q);
     }
     __syncthreads();
-    CSTAMP(2);
     // 3. level 0's blur rows; then per level l >= 1: the previous level's blur columns beside
     //    this level's resize (they share no LDS), then this level's blur rows
     if (chain_fill<NT>(c0, LG[0], smem, P0, tid)) __syncthreads();
     chain_rows<NT>(c0, LG[0], smem, P0, rsum, g, tid);
     __syncthreads();
-    CSTAMP(3);
     int lr = 0;   // the level whose row sums are in rsum (-1: none)
     ChainRect cp = c0;
     for (int l = 1; l < L; ++l) {
         chain_cols<NT>(cp, LG[lr], rsum, blr_b + LG[lr].off, g, tid);
-        CSTAMP(18 + 2 * l);
         lr = -1;
         const ChainRect cd = CR[l];
         const LevelGeom& Ld = LG[l];
@@ -1505,18 +1308,14 @@ __global__ __launch_bounds__(NT) void k_pyr_chain(const Geometry* __restrict__ g
                 }
             }
         }
-        CSTAMP(19 + 2 * l);
         __syncthreads();
-        CSTAMP(2 + 2 * l);
         if (chain_fill<NT>(cd, Ld, dst, Pd, tid)) __syncthreads();
         chain_rows<NT>(cd, Ld, dst, Pd, rsum, g, tid);
         __syncthreads();
-        CSTAMP(3 + 2 * l);
         lr = l;
         cp = cd;
     }
     if (lr >= 0) chain_cols<NT>(cp, LG[lr], rsum, blr_b + LG[lr].off, g, tid);
-    CSTAMP(18);
 }
 
 hipError_t launch_pyr_chain(const ExtractLaunch& a, hipStream_t st) {
@@ -1534,7 +1333,7 @@ size_t level_lds_bytes(int ltw, int lth, int win_cap) {
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
     const size_t tables = r(LT_G * 8) + r(LT_G * 4) + r(LT_G * 16) + r(LT_G * 16) + r(LT_HR * 8);
     const size_t phase12 = tables + r((size_t)win_cap + 16);
-    const size_t phase34 = r((size_t)LT_HR * LT_W * (BLUR_F32 ? 4 : 2));
+    const size_t phase34 = r((size_t)LT_HR * LT_W * 4);
     return r((size_t)LT_HR * LT_G * 4) + (phase12 > phase34 ? phase12 : phase34) + r(64);
 }
 
@@ -1587,11 +1386,6 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, in
     return hipGetLastError();
 }
 
-#ifdef ORBX_STAMPS
-extern "C" int orbx_diag_level_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_level_stamps), sizeof(g_level_stamps));
-}
-#endif
 
 hipError_t prepare_level(size_t lds) {
     hipError_t e = hipSuccess;

@@ -21,37 +21,14 @@
 
 namespace orbx {
 
-#ifndef ST_THREADS
 #define ST_THREADS 1024
-#endif
 #define ST_WAVES (ST_THREADS / 64)
-#ifndef ST_FUSED_CUT
-// split path: the last workgroup of a pair runs the cut (no k_stereo_cut); 1: its hand-off by
-// an agent-scope fence on both sides, 2: by write-through stores and loads (no fence)
-#define ST_FUSED_CUT 2
-#endif
-// the split path's stores of uRight / depth / SADs: write-through (sc1) under ST_FUSED_CUT 2,
-// so the last workgroup reads them from memory and overwrites them with no fence between
+// split path: the last workgroup of a pair to finish runs the median cut; the split path's
+// stores of uRight / depth / SADs are write-through (sc1), so that workgroup reads them from
+// memory and overwrites them with no fence between
 template <class T>
 __device__ __forceinline__ void split_store(T* p, T v) {
-#if ST_FUSED_CUT == 2
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *p = v;
-#endif
-}
-
-// N bytes of a pyramid row starting at x, as ceil(N/4) dwords realigned to x (bytes of
-// dword i = row[x + 4i .. x + 4i + 3]).  Rows are 64-byte aligned with >= 4 bytes of slack.
-template <int ND>
-__device__ __forceinline__ void load_row(const uint8_t* row, int x, uint32_t out[ND]) {
-    const uint32_t* p = (const uint32_t*)(row + (x & ~3));
-    const int sh = x & 3;
-    uint32_t raw[ND + 1];
-#pragma unroll
-    for (int i = 0; i <= ND; ++i) raw[i] = p[i];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) out[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
 }
 
 __device__ __forceinline__ int byte_of(const uint32_t* w, int k) {   // k compile-time
@@ -157,9 +134,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
     // 2. per left keypoint: descriptor search (src/Frame.cc:542-587) + SAD (:591-667)
     const float maxD = mbf / mb;   // minZ = mb, maxD = mbf/minZ (Frame.cc:534-536)
     const float minD = 0;
-#if ST_DIAG == 3   // diagnostic builds only: phase 1 alone
-    if (NL >= 0) return;
-#endif
     const int chunk = (NL + nsplit - 1) / nsplit;
     const int iL0 = slice * chunk, iL1 = min(NL, iL0 + chunk);
     const int sub = tid % LPK;   // this lane's share of its keypoint (control flow is per group)
@@ -186,9 +160,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
         int best = 100, bestR = -1;   // ORBmatcher::TH_HIGH, strict '<': first minimum wins
         int bestE = -1;
-#if ST_DIAG == 2 || ST_DIAG == 3   // diagnostic builds only: no descriptor search (and so no SAD)
-        if (row >= 0) continue;
-#endif
         // octaves levelL-1 .. levelL+1: a right keypoint of octave o whose band
         // [floor(y - 2s), ceil(y + 2s)] holds `row` has int(y) within ceil(2s) + 1 rows of it
         // (one group of every octave when OB = 1: the window of the largest scale, octaves
@@ -234,9 +205,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
         if (bestR < 0 || best >= 75) continue;   // thOrbDist = (TH_HIGH + TH_LOW) / 2
 
-#if ST_DIAG >= 1 && ST_DIAG <= 3   // diagnostic builds only (tools/variants.py): search without the SAD
-        if (bestE >= 0) continue;
-#endif
         // ---- sliding-window SAD on the unblurred level of the left keypoint ----
         const LevelGeom& LV = g->lv[levelL];
         const float uR0 = __uint_as_float(rrec[bestE].x);
@@ -251,14 +219,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         const int pitch = LV.pitch;
         const uint8_t* PL = pyrL + (size_t)b * g->pyr_bytes + LV.off;
         const uint8_t* PR = pyrR + (size_t)b * g->pyr_bytes + LV.off;
-#if ST_DIAG == 4   // timing diagnostics only (wrong SADs): every lane of a wave reads one window
-        const int yl = __builtin_amdgcn_readfirstlane((int)scaledvL), xl = __builtin_amdgcn_readfirstlane((int)scaleduL),
-                  xr = __builtin_amdgcn_readfirstlane((int)scaleduR0);
-#elif ST_DIAG == 5   // ... every lane reads its own rows, all in the wave's first lane's lines
-        const int yl = __builtin_amdgcn_readfirstlane((int)scaledvL), xl = (int)scaleduL, xr = (int)scaleduR0;
-#else
         const int yl = (int)scaledvL, xl = (int)scaleduL, xr = (int)scaleduR0;
-#endif
         int acc[11];
         if constexpr (LPK == 1) {
             int accl[11];   // its own array: declared outside, `acc` made this path spill
@@ -470,7 +431,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
         }
     }
     if (nsplit > 1) {
-#if ST_FUSED_CUT == 2
         // the pair's last workgroup to finish takes the median: every wave's write-through
         // stores complete, then the workgroup's arrival is one agent-scope acq_rel add (its
         // release orders this workgroup's stores, ordered before it by the barrier, ahead of
@@ -495,26 +455,6 @@ __global__ __launch_bounds__(ST_THREADS) void k_stereo(const Geometry* __restric
             scnt[256 + b] = 0;
         }
         median_cut(nv, vsad, vidx, hist, tmp, uR, dep, nvalid, b);
-#elif ST_FUSED_CUT
-        // the pair's last workgroup to finish takes the median over the global scratch (the
-        // others' SADs are visible after their release fence and this one's acquire): no
-        // second launch for the cut
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            tmp[17] = atomicAdd(&scnt[256 + b], 1) == nsplit - 1;
-        }
-        __syncthreads();
-        if (!tmp[17]) return;
-        __threadfence();
-        const int nv = min(__hip_atomic_load(&scnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), KC);
-        __syncthreads();
-        if (tid == 0) {
-            scnt[b] = 0;
-            scnt[256 + b] = 0;
-        }
-        median_cut(nv, ssad + (size_t)b * KC, sidx + (size_t)b * KC, hist, tmp, uR, dep, nvalid, b);
-#endif
         return;
     }
     __syncthreads();
@@ -575,26 +515,6 @@ __device__ void median_cut(int nv, const int* vsad, const int16_t* vidx, int* hi
     if (tid == 0 && nvalid) nvalid[b] = nv - dropped;
 }
 
-// The split path's cut: one workgroup per pair over the global scratch of k_stereo, which it
-// leaves zeroed for the next call.
-__global__ __launch_bounds__(ST_THREADS) void k_stereo_cut(const Geometry* __restrict__ g,
-                                                           float* __restrict__ uRight,
-                                                           float* __restrict__ depth,
-                                                           int* __restrict__ nvalid,
-                                                           int* __restrict__ scnt,
-                                                           const int* __restrict__ ssad,
-                                                           const int16_t* __restrict__ sidx) {
-    __shared__ int hist[256];
-    __shared__ int tmp[32];
-    const int b = blockIdx.x;
-    const size_t KC = (size_t)g->kp_cap;
-    const int nv = min(scnt[b], (int)KC);
-    __syncthreads();
-    if (threadIdx.x == 0) scnt[b] = 0;
-    median_cut(nv, ssad + b * KC, sidx + b * KC, hist, tmp, uRight + b * KC, depth + b * KC,
-               nvalid, b);
-}
-
 size_t stereo_lds_bytes(int kp_cap, int height, int ob) {
     auto r = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t s = r(32 * 4) + r((size_t)kp_cap * 32) + r((size_t)ob * height * 4);
@@ -606,15 +526,9 @@ size_t stereo_lds_bytes(int kp_cap, int height, int ob) {
 // Small batches (at most ST_LPK_BATCH pairs): ST_LPK lanes per left keypoint, ST_LPK_SPLIT
 // workgroups per pair (every keypoint of a 2000-keypoint image in flight at once).  One pair
 // (r4p, r4w): 1 lane 47.8 us, 2 x 8 workgroups 37.3, 4 x 8 33.9, 4 x 16 30.7, 8 x 16 30.5.
-#ifndef ST_LPK
 #define ST_LPK 8
-#endif
-#ifndef ST_LPK_SPLIT
 #define ST_LPK_SPLIT 16
-#endif
-#ifndef ST_LPK_BATCH
 #define ST_LPK_BATCH 32
-#endif
 
 hipError_t prepare_stereo(size_t lds) {
     hipError_t e = hipFuncSetAttribute((const void*)k_stereo<1>,
@@ -629,9 +543,7 @@ hipError_t prepare_stereo(size_t lds) {
 // pair would leave most CUs idle and run two left keypoints per thread in series).  One
 // stereo pair: k_stereo 0.089 ms unsplit, 0.058 split in 2, 0.050 in 4; 64 pairs: 0.107 /
 // 0.080 / 0.070 ms; 512 pairs are not split.
-#ifndef ST_SPLIT
 #define ST_SPLIT 4
-#endif
 static bool stereo_lpk(int batch) { return ST_LPK > 1 && batch <= ST_LPK_BATCH; }
 int stereo_split(int batch) {
     int ns = stereo_lpk(batch) ? ST_LPK_SPLIT : ST_SPLIT;
@@ -640,21 +552,16 @@ int stereo_split(int batch) {
 }
 
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {
-    // timed by the kernels' own dispatches (ORBX_TIMED_LAUNCH): from k_stereo's start to the
-    // end of the last kernel (k_stereo_cut on the split path)
+    // timed by the kernel's own dispatch (ORBX_TIMED_LAUNCH)
     KernelTimer* T = a.timer && a.timer->on ? a.timer : nullptr;
     hipEvent_t e0 = T ? T->get() : nullptr, e1 = T ? T->get() : nullptr;
     if (!e0 || !e1) e0 = e1 = nullptr;
     const int ns = stereo_split(a.batch);
     hipExtLaunchKernelGGL(stereo_lpk(a.batch) ? k_stereo<ST_LPK> : k_stereo<1>,
                           dim3(a.batch * ns), dim3(ST_THREADS), (uint32_t)a.lds, st, e0,
-                          (ns > 1 && !ST_FUSED_CUT) ? nullptr : e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
+                          e1, 0u, a.dg, a.kpsL, a.descL, a.nkpL, a.pyrL,
                           a.kpsR, a.descR, a.nkpR, a.pyrR, a.mbf, a.mb, a.uR, a.depth, a.nvalid,
                           ns, a.scnt, a.ssad, a.sidx);
-    if (ns > 1 && !ST_FUSED_CUT)
-        hipExtLaunchKernelGGL(k_stereo_cut, dim3(a.batch), dim3(ST_THREADS), 0u, st, nullptr, e1, 0u,
-                              a.dg, a.uR, a.depth, a.nvalid, a.scnt, (const int*)a.ssad,
-                              (const int16_t*)a.sidx);
     if (e0 && e1) T->pending.push_back(KernelTimer::Rec{K_STEREO, e0, e1});
     return hipGetLastError();
 }

@@ -236,6 +236,13 @@ class ORBmatcher:
                                                               ptr(best)))
         return best[:len(o) - 1]
 
+    BF_MFMA, BF_VALU = 0, 1
+
+    def set_bf_kernel(self, kernel):
+        """The brute-force top-2's distance kernel: BF_MFMA (k_bf_mfma, the default) or BF_VALU
+        (k_bf_top2: v_xor + v_bcnt); the results are identical."""
+        check("orbx_matcher_set_bf_kernel", self._lib.orbx_matcher_set_bf_kernel(self._h, int(kernel)))
+
     def hamming_bf_top2(self, q, db):
         """Brute-force Hamming top-2 of every query row against every database row, with the
         best / second loop of the ORBmatcher searches (src/ORBmatcher.cc:232-256): returns

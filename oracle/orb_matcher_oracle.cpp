@@ -356,6 +356,12 @@ int oracle_search_by_projection_ex(int mode, const orbx_featureset* T, const uin
                                    const uint8_t* qflags, int nq, const float* inv_sigma2,
                                    int orb_dist, float nnratio, int checkOri, int prefilter,
                                    int32_t* match_q) {
+    // the per-query filter below equals the reference's per-feature loop (:1516-1535) only
+    // while every feature has at most one match: LAST_FRAME with no-claim queries (a feature
+    // matched twice) needs the caller's own filter (prefilter), as the C ABI requires
+    if (mode == ORBX_PROJ_LAST_FRAME && checkOri && !prefilter && qflags)
+        for (int iq = 0; iq < nq; iq++)
+            if (qflags[iq] & ORBX_QF_NO_CLAIM) return -1;
     std::vector<char> claimed(T->n, 0);
     const bool greedy = mode <= ORBX_PROJ_KEYFRAME;
     if (claimed_in && greedy)

@@ -16,6 +16,8 @@
 //   A.t()          transpose (then convertTo when scaled)
 //   A + B, A - B   element-wise float add / subtract
 //   norm(A)        sqrt of the squares summed in double;  A.dot(B): (double)a*b summed in double
+//   norm(A, B, NORM_L1)  |a - b| in float, summed in double (normDiffL1_<float, double>)
+//   A.convertTo(D, CV_32F)  8U -> 32F element by element (a new buffer, so D may be A)
 #ifndef ORBX_CV_STANDIN_CORE_HPP
 #define ORBX_CV_STANDIN_CORE_HPP
 
@@ -151,6 +153,29 @@ public:
         Mat m(r, c, type);
         for (int i = 0; i < r; ++i) std::memset(m.ptr(i), 0, (size_t)c * m.elemSize());
         return m;
+    }
+    static Mat ones(int r, int c, int type) {
+        Mat m(r, c, type);
+        for (int i = 0; i < r; ++i)
+            for (int k = 0; k < c; ++k) {
+                if (type == CV_32F) m.at<float>(i, k) = 1.f;
+                else m.at<uchar>(i, k) = 1;
+            }
+        return m;
+    }
+    // convertTo(m, rtype) with alpha 1, beta 0: CV_8U -> CV_32F, or a copy of the same type
+    void convertTo(Mat& dst, int rtype) const {
+        if (rtype == type_) {
+            Mat c = clone();
+            dst = c;
+            return;
+        }
+        if (type_ != CV_8U || rtype != CV_32F)
+            throw std::invalid_argument("cv stand-in: convertTo CV_8U -> CV_32F only");
+        Mat d(rows, cols, CV_32F);
+        for (int r = 0; r < rows; ++r)
+            for (int k = 0; k < cols; ++k) d.at<float>(r, k) = (float)at<uchar>(r, k);
+        dst = d;
     }
     static Mat eye(int r, int c, int type) {
         Mat m = zeros(r, c, type);
@@ -328,6 +353,18 @@ inline double norm(const Mat& a) {
         s += v * v;
     }
     return std::sqrt(s);
+}
+
+enum { NORM_L1 = 2 };
+// cv::norm(a, b, NORM_L1) for CV_32F: normDiffL1_<float, double>, |a - b| accumulated in double
+inline double norm(const Mat& a, const Mat& b, int type) {
+    if (type != NORM_L1 || a.type() != CV_32F || b.type() != CV_32F || a.rows != b.rows ||
+        a.cols != b.cols)
+        throw std::invalid_argument("cv stand-in: norm(a, b, NORM_L1) of CV_32F arrays of one size");
+    double s = 0;
+    for (int r = 0; r < a.rows; ++r)
+        for (int k = 0; k < a.cols; ++k) s += std::fabs(a.at<float>(r, k) - b.at<float>(r, k));
+    return s;
 }
 
 class _InputArray {

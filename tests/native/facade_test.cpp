@@ -17,8 +17,19 @@
 //                         boundary_test `bench` (pair_<i>_left/right.raw, params.txt
 //                         "W H nfeatures mbf mb P").  Prints boundary_test bench's JSON line.
 //   a trailing "frame" on run / bench: each stereo frame through orbx_glue::ExtractStereo
-//   (both views as one two-image submission with the stereo match appended)
+//   (both views as one two-image submission with the stereo match appended); a trailing "pyr"
+//   on bench: the two ExtractORB threads keep refreshing mvImagePyramid (the host pyramid copy
+//   on, as for an unchanged Frame::ComputeStereoMatches) and the stereo match runs through the
+//   C ABI directly, so the line prices operator()'s pyramid copy
+//
+// `run` (threads) also checks the mvImagePyramid contract (ORBextractor.h:85, ORBextractor.cc:433,
+// 1129-1154): both extractors' levels after operator() go to pyr_left.bin / pyr_right.bin (every
+// level, rows tightly packed) for the oracle comparison, and the reference's own stereo body
+// (Frame.cc:496-686, restated below over those cv::Mat levels) must give the same uRight / depth
+// as orbx_glue::ComputeStereoMatches.
+#include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <condition_variable>
 #include <cstdint>
@@ -67,7 +78,121 @@ struct Frame {
         else
             (*mpORBextractorRight)(im, cv::Mat(), mvKeysRight, mDescriptorsRight);
     }
+
+    // Frame::ComputeStereoMatches as the reference has it (Frame.cc:496-686), restated over the
+    // extractors' mvImagePyramid (the drop-in must keep that member valid for exactly this
+    // body).  mb is passed (the reference reads it before it is set, Frame.cc:534 / :127).  An
+    // empty vDistIdx skips the cut (the reference takes the median of an empty vector, UB).
+    int ComputeStereoMatchesReference(float mb) {
+        mvuRight = std::vector<float>(N, -1.0f);
+        mvDepth = std::vector<float>(N, -1.0f);
+        const std::vector<float> sf = mpORBextractorLeft->GetScaleFactors();
+        const std::vector<float> isf = mpORBextractorLeft->GetInverseScaleFactors();
+        const int TH_HIGH = 100, TH_LOW = 50;
+        const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+        const int nRows = mpORBextractorLeft->mvImagePyramid[0].rows;
+        std::vector<std::vector<size_t>> rows((size_t)nRows);
+        const int Nr = (int)mvKeysRight.size();
+        for (int iR = 0; iR < Nr; iR++) {
+            const cv::KeyPoint& kp = mvKeysRight[(size_t)iR];
+            const float r = 2.0f * sf[(size_t)kp.octave];
+            const int maxr = (int)std::ceil(kp.pt.y + r), minr = (int)std::floor(kp.pt.y - r);
+            for (int yi = minr; yi <= maxr; yi++) rows[(size_t)yi].push_back((size_t)iR);
+        }
+        const float minZ = mb, minD = 0, maxD = mbf / minZ;
+        std::vector<std::pair<int, int>> vDistIdx;
+        for (int iL = 0; iL < N; iL++) {
+            const cv::KeyPoint& kpL = mvKeys[(size_t)iL];
+            const int levelL = kpL.octave;
+            const float vL = kpL.pt.y, uL = kpL.pt.x;
+            const std::vector<size_t>& cand = rows[(size_t)vL];
+            if (cand.empty()) continue;
+            const float minU = uL - maxD, maxU = uL - minD;
+            if (maxU < 0) continue;
+            int bestDist = TH_HIGH;
+            size_t bestIdxR = 0;
+            for (size_t iR : cand) {
+                const cv::KeyPoint& kpR = mvKeysRight[iR];
+                if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+                const float uR = kpR.pt.x;
+                if (uR >= minU && uR <= maxU) {
+                    const uint32_t* a = (const uint32_t*)mDescriptors.ptr(iL);
+                    const uint32_t* b = (const uint32_t*)mDescriptorsRight.ptr((int)iR);
+                    int dist = 0;   // ORBmatcher::DescriptorDistance (:1715-1731)
+                    for (int k = 0; k < 8; ++k) dist += __builtin_popcount(a[k] ^ b[k]);
+                    if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+                }
+            }
+            if (bestDist >= thOrbDist) continue;
+            const float uR0 = mvKeysRight[bestIdxR].pt.x;
+            const float scaleFactor = isf[(size_t)kpL.octave];
+            const float scaleduL = std::round(kpL.pt.x * scaleFactor);
+            const float scaledvL = std::round(kpL.pt.y * scaleFactor);
+            const float scaleduR0 = std::round(uR0 * scaleFactor);
+            const int w = 5;
+            const cv::Mat& PL = mpORBextractorLeft->mvImagePyramid[(size_t)kpL.octave];
+            const cv::Mat& PR = mpORBextractorRight->mvImagePyramid[(size_t)kpL.octave];
+            cv::Mat IL = PL.rowRange((int)scaledvL - w, (int)scaledvL + w + 1)
+                             .colRange((int)scaleduL - w, (int)scaleduL + w + 1);
+            IL.convertTo(IL, CV_32F);
+            IL = IL - IL.at<float>(w, w) * cv::Mat::ones(IL.rows, IL.cols, CV_32F);
+            int bestSad = INT_MAX, bestincR = 0;
+            const int L = 5;
+            std::vector<float> vDists(2 * L + 1);
+            const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
+            if (iniu < 0 || endu >= PR.cols) continue;
+            for (int incR = -L; incR <= +L; incR++) {
+                cv::Mat IR = PR.rowRange((int)scaledvL - w, (int)scaledvL + w + 1)
+                                 .colRange((int)scaleduR0 + incR - w, (int)scaleduR0 + incR + w + 1);
+                IR.convertTo(IR, CV_32F);
+                IR = IR - IR.at<float>(w, w) * cv::Mat::ones(IR.rows, IR.cols, CV_32F);
+                const float dist = (float)cv::norm(IL, IR, cv::NORM_L1);
+                if (dist < bestSad) { bestSad = (int)dist; bestincR = incR; }
+                vDists[(size_t)(L + incR)] = dist;
+            }
+            if (bestincR == -L || bestincR == L) continue;
+            const float dist1 = vDists[(size_t)(L + bestincR - 1)];
+            const float dist2 = vDists[(size_t)(L + bestincR)];
+            const float dist3 = vDists[(size_t)(L + bestincR + 1)];
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (deltaR < -1 || deltaR > 1) continue;
+            float bestuR = sf[(size_t)kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) {
+                    disparity = 0.01f;
+                    bestuR = uL - 0.01f;
+                }
+                mvDepth[(size_t)iL] = mbf / disparity;
+                mvuRight[(size_t)iL] = bestuR;
+                vDistIdx.push_back(std::pair<int, int>(bestSad, iL));
+            }
+        }
+        std::sort(vDistIdx.begin(), vDistIdx.end());
+        int nvalid = (int)vDistIdx.size();
+        if (vDistIdx.empty()) return 0;
+        const float median = (float)vDistIdx[vDistIdx.size() / 2].first;
+        const float thDist = 1.5f * 1.4f * median;
+        for (int i = (int)vDistIdx.size() - 1; i >= 0; i--) {
+            if (vDistIdx[(size_t)i].first < thDist) break;
+            mvuRight[(size_t)vDistIdx[(size_t)i].second] = -1;
+            mvDepth[(size_t)vDistIdx[(size_t)i].second] = -1;
+            --nvalid;
+        }
+        return nvalid;
+    }
 };
+
+// Every level of an extractor's mvImagePyramid, rows tightly packed, level after level.
+bool dump_pyramid(const ORB_SLAM2::ORBextractor& ex, std::vector<uint8_t>& out) {
+    out.clear();
+    if (ex.mvImagePyramid.size() != 8) return false;
+    for (const cv::Mat& m : ex.mvImagePyramid) {
+        if (m.empty() || m.type() != CV_8U) return false;
+        for (int y = 0; y < m.rows; ++y) out.insert(out.end(), m.ptr(y), m.ptr(y) + m.cols);
+    }
+    return true;
+}
 
 // The members of ORB_SLAM2::KeyFrame SearchByBoW reads.
 struct KeyFrame {
@@ -174,7 +299,31 @@ int run(const std::string& dir, bool frame_call) {
             return 4;
         }
         nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+        {   // the right view's pyramid source is the left handle: another call on it first
+            // makes MaterializePyramid throw instead of returning another frame's levels
+            Frame G;
+            G.mpORBextractorLeft = &left;
+            G.mpORBextractorRight = &right;
+            G.mbf = F.mbf;
+            G.fx = F.fx;
+            orbx_glue::ExtractStereo(G, imL, imR);
+            std::vector<cv::KeyPoint> k2;
+            cv::Mat d2;
+            left(imR, cv::Mat(), k2, d2);   // the left handle moves on
+            try {
+                right.MaterializePyramid();
+                std::printf("facade_test: a stale pyramid source was not detected\n");
+                return 4;
+            } catch (const std::runtime_error&) {
+            }
+        }
+        nvalid = orbx_glue::ExtractStereo(F, imL, imR);
     } else {   // Frame.cc:89-92
+        // the constructor sized mvImagePyramid (ORBextractor.cc:433)
+        if (left.mvImagePyramid.size() != 8 || !left.HostPyramid()) {
+            std::printf("facade_test: mvImagePyramid not sized / host pyramid off after the constructor\n");
+            return 4;
+        }
         std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
         std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
         tl.join();
@@ -198,7 +347,54 @@ int run(const std::string& dir, bool frame_call) {
                 return 4;
             }
     }
-    if (!frame_call) nvalid = orbx_glue::ComputeStereoMatches(F);
+    if (!frame_call) {
+        // every level of both views straight after operator() (the oracle compares them) ...
+        std::vector<uint8_t> pl, pr;
+        if (!dump_pyramid(left, pl) || !dump_pyramid(right, pr) ||
+            !write_file(dir + "/pyr_left.bin", pl.data(), pl.size()) ||
+            !write_file(dir + "/pyr_right.bin", pr.data(), pr.size())) {
+            std::printf("facade_test: mvImagePyramid incomplete after operator()\n");
+            return 4;
+        }
+        // ... and the reference's own stereo body over them equals the glue's device match
+        const int nref = F.ComputeStereoMatchesReference(F.mbf / F.fx);
+        const std::vector<float> uref = F.mvuRight, dref = F.mvDepth;
+        nvalid = orbx_glue::ComputeStereoMatches(F);
+        if (nref != nvalid || uref.size() != F.mvuRight.size() ||
+            std::memcmp(uref.data(), F.mvuRight.data(), uref.size() * 4) != 0 ||
+            std::memcmp(dref.data(), F.mvDepth.data(), dref.size() * 4) != 0) {
+            std::printf("facade_test: Frame.cc's stereo body over mvImagePyramid (%d) differs "
+                        "from orbx_glue::ComputeStereoMatches (%d)\n", nref, nvalid);
+            return 4;
+        }
+        if (!write_file(dir + "/nvalid_ref.bin", &nref, 4)) return 3;
+        // the glue turned the host copy off (it reads the device pyramids): the next
+        // operator() leaves empty levels, MaterializePyramid() fills them on request
+        if (left.HostPyramid() || right.HostPyramid()) {
+            std::printf("facade_test: host pyramid still on after the glue's stereo match\n");
+            return 4;
+        }
+        std::vector<cv::KeyPoint> k2;
+        cv::Mat d2;
+        left(imL, cv::Mat(), k2, d2);
+        if (left.mvImagePyramid.size() != 8 || !left.mvImagePyramid[0].empty()) {
+            std::printf("facade_test: stale mvImagePyramid after the opt-out\n");
+            return 4;
+        }
+        std::vector<uint8_t> pl2;
+        left.MaterializePyramid();
+        if (!dump_pyramid(left, pl2) || pl2 != pl) {
+            std::printf("facade_test: MaterializePyramid after the opt-out differs\n");
+            return 4;
+        }
+        // the source check: the right extractor's view does not outlive its handle's next call
+        left.SetHostPyramid(true);
+        left(imL, cv::Mat(), k2, d2);
+        if (!dump_pyramid(left, pl2) || pl2 != pl) {
+            std::printf("facade_test: mvImagePyramid after re-enabling differs\n");
+            return 4;
+        }
+    }
 
     // SearchByBoW(KF = right view, F = left view), one vocabulary node holding every feature
     F.mvKeysUn = F.mvKeys;
@@ -248,7 +444,8 @@ uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     return h;
 }
 
-int bench(const std::string& dir, int nframes, int warmup, int trackers, bool frame_call) {
+int bench(const std::string& dir, int nframes, int warmup, int trackers, bool frame_call,
+          bool host_pyr) {
     int W = 0, H = 0, nfeat = 0, P = 0;
     float mbf = 0.f, mb = 0.f;
     {
@@ -308,6 +505,21 @@ int bench(const std::string& dir, int nframes, int warmup, int trackers, bool fr
                 int nvalid = 0;
                 if (frame_call) {   // Frame.cc:89-102 as one two-image submission
                     nvalid = orbx_glue::ExtractStereo(F, imL, imR);
+                } else if (host_pyr) {   // mvImagePyramid refreshed by every operator()
+                    std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
+                    std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
+                    tl.join();
+                    tr.join();
+                    F.N = (int)F.mvKeys.size();
+                    if (F.mpORBextractorLeft->mvImagePyramid[0].empty())
+                        throw std::runtime_error("bench pyr: no mvImagePyramid");
+                    F.mvuRight.assign((size_t)F.N, -1.f);
+                    F.mvDepth.assign((size_t)F.N, -1.f);
+                    orbx_glue::check(orbx_stereo_match(F.mpORBextractorLeft->handle(),
+                                                       F.mpORBextractorRight->handle(), F.mbf,
+                                                       F.mbf / F.fx, F.mvuRight.data(),
+                                                       F.mvDepth.data(), F.N, &nvalid),
+                                     "orbx_stereo_match");
                 } else {
                     std::thread tl(&Frame::ExtractORB, &F, 0, std::cref(imL));
                     std::thread tr(&Frame::ExtractORB, &F, 1, std::cref(imR));
@@ -385,14 +597,15 @@ int main(int argc, char** argv) {
         // a trailing "frame": the stereo Frame's extraction and matching as one call
         // (orbx_glue::ExtractStereo) instead of two ExtractORB threads + ComputeStereoMatches
         const bool frame_call = std::string(argv[argc - 1]) == "frame";
+        const bool host_pyr = std::string(argv[argc - 1]) == "pyr";
         if (mode == "run" && argc > 2) return run(argv[2], frame_call);
         if (mode == "bench" && argc > 5)
             return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
-                         frame_call);
+                         frame_call, host_pyr);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "facade_test: %s\n", e.what());
         return 1;
     }
-    std::fprintf(stderr, "usage: facade_test nogpu | run DIR [frame] | bench DIR FRAMES WARMUP K [frame]\n");
+    std::fprintf(stderr, "usage: facade_test nogpu | run DIR [frame] | bench DIR FRAMES WARMUP K [frame|pyr]\n");
     return 2;
 }

@@ -119,7 +119,7 @@ orbx_status orbx_search_by_projection_ex(orbx_matcher* m, int32_t mode,
                                                inv_sigma2, orb_dist, m->prm.nnratio,
                                                m->prm.check_orientation,
                                                (flags & ORBX_PROJ_PREFILTER) != 0, match_q);
-    return ORBX_OK;
+    return *nmatches < 0 ? ORBX_ERR_INVALID : ORBX_OK;
 }
 
 orbx_status orbx_search_by_sim3(orbx_matcher* /*m*/, const orbx_featureset* kf1,

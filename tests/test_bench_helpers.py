@@ -56,11 +56,56 @@ def test_binding_roof_label():
     b.label_binding_roof(e)
     assert e["bound"] == "valu" and e["frac"] == pytest.approx(0.75) and e["hbm"]["frac"] == hbm_frac
     assert e["frac"] == pytest.approx(e["achieved"] / e["peak"], rel=1e-9)
+    # k_level1_7 in r05: VALU 0.60 busy against HBM 0.34-0.43 -> valu (round 5 said hbm)
     e = b.roofline_entry("k_level1_7", 10.0, 70, 10, 3.4e9, None)
+    hbm_frac = e["frac"]
     e["valu"] = {"busy_frac": 0.60, "valubusy_4cycle": 0.64, "wave_instr_per_launch": 7e7,
                  "mean_issue_cycles": 3.66}
     b.label_binding_roof(e)
-    assert e["bound"] == "hbm" and e["hbm"]["frac"] == e["frac"]
+    assert hbm_frac < 0.6 and e["bound"] == "valu" and e["hbm"]["frac"] == hbm_frac
+    # an entry whose HBM fraction exceeds its VALU busy fraction stays hbm
+    e = b.roofline_entry("k_level0", 10.0, 10, 10, 7.0e9, None)
+    e["valu"] = {"busy_frac": 0.30, "wave_instr_per_launch": 1e8, "mean_issue_cycles": 3.0}
+    b.label_binding_roof(e)
+    assert e["frac"] > 0.3 and e["bound"] == "hbm" and e["hbm"]["frac"] == e["frac"]
+    # no VALU entry: hbm
+    e = b.roofline_entry("k_octree", 1.0, 10, 10, 1e6, None)
+    b.label_binding_roof(e)
+    assert e["bound"] == "hbm"
+
+
+def test_valu_floor_on_committed_r05_line():
+    """the step's VALU issue floor = sum over the kernel groups of wave
+    instructions per launch x launches per step x mean issue cycles, over 1024 SIMDs x 2.4 GHz.
+    On the committed r05 line (its per_kernel entries come from the r05 PMC CSVs) that is
+    2.61 ms, 0.67 of the 3.90 ms timed step."""
+    b = _bench()
+    line = json.load(open(os.path.join(ROOT, "profiles", "r05_v5_bench.json")))
+    pk = line["roofline"]["per_kernel"]
+    want = sum(pk[k]["valu"]["wave_instr_per_launch"] * pk[k]["launches_per_step"] *
+               pk[k]["valu"]["mean_issue_cycles"] for k in b.HEADLINE_GROUPS) / (1024 * 2.4e9) * 1e3
+    assert b.valu_floor_ms(pk) == pytest.approx(want, rel=1e-12)
+    assert b.valu_floor_ms(pk) == pytest.approx(2.61, abs=0.01)
+    roof = {"per_kernel": pk}
+    b.add_valu_floor(roof, line["ms_per_step"])
+    assert roof["valu_floor_frac"] == pytest.approx(0.67, abs=0.01)
+    # the k_level union entry is not counted twice
+    assert "k_level" in pk and "k_level" not in b.HEADLINE_GROUPS
+    # an entry without PMC counts makes the floor unknown, not smaller
+    pk2 = dict(pk, k_fast=dict(pk["k_fast"], valu=None))
+    assert b.valu_floor_ms(pk2) is None
+
+
+def test_latest_line_carries_valu_floor():
+    b = _bench()
+    roof = json.load(open(_latest("r[0-9][0-9]_v*_bench.json")))["roofline"]
+    if "valu_floor_ms" not in roof:
+        pytest.skip("headline line predates the VALU floor (round 6)")
+    assert roof["valu_floor_ms"] == pytest.approx(b.valu_floor_ms(roof["per_kernel"]), rel=1e-9)
+    for e in roof["per_kernel"].values():
+        v = (e.get("valu") or {}).get("busy_frac")
+        if v is not None:
+            assert e["bound"] == ("valu" if v > e["hbm"]["frac"] else "hbm")
 
 
 def test_roofline_entries_per_launch():

@@ -119,24 +119,32 @@ def test_gloo_gather_top2():
 # ---- GPU ----------------------------------------------------------------------------------
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [0, 1], ids=["k_bf_mfma", "k_bf_top2"])
 @pytest.mark.parametrize("seed,nq,ndb", [(10, 1000, 100003), (11, 37, 1), (12, 300, 0),
                                          (13, 64, 2), (14, 257, 4099), (15, 1, 65536)])
-def test_gpu_bf_top2_parity(orbx_lib, seed, nq, ndb):
+def test_gpu_bf_top2_parity(orbx_lib, seed, nq, ndb, kernel):
+    """Both distance kernels (ORBX_BF_MFMA: +-1 int8 MFMA dot products; ORBX_BF_VALU: XOR +
+    v_bcnt, north_star's "no MFMA" form) against the oracle's best / second loop
+    (src/ORBmatcher.cc:232-256 over every row; DescriptorDistance :1715-1731)."""
     from my_orb_slam2_amd import ORBmatcher
     q, db = bf_database(seed, nq, ndb)
-    got = ORBmatcher(0.75, True).hamming_bf_top2(q, db)
+    m = ORBmatcher(0.75, True)
+    m.set_bf_kernel(kernel)
+    got = m.hamming_bf_top2(q, db)
     want = om.bf_top2(q, db)
     for g, w in zip(got, want):
         np.testing.assert_array_equal(g, w)
 
 
 @pytest.mark.gpu
-def test_gpu_bf_top2_device_shards(orbx_lib, gpu):
+@pytest.mark.parametrize("kernel", [0, 1], ids=["k_bf_mfma", "k_bf_top2"])
+def test_gpu_bf_top2_device_shards(orbx_lib, gpu, kernel):
     """The device entry point on shards of one database (idx_base = the shard's first row),
     folded by merge_top2 in shard order, equals the whole database's result."""
     from my_orb_slam2_amd import ORBmatcher
     q, db = bf_database(16, 500, 300007)
     m = ORBmatcher(0.75, True)
+    m.set_bf_kernel(kernel)
     dq = torch.from_numpy(q).to(gpu)
     ddb = torch.from_numpy(db).to(gpu)
     whole = om.bf_top2(q, db)

@@ -10,7 +10,8 @@ semantics, so this proves the facade's marshalling, not OpenCV itself).
 * GPU: Frame's two ExtractORB threads (Frame.cc:89-92) on the KITTI fixture pair, the left image
   behind a padded row stride, the stereo glue and SearchByBoW: keypoints, descriptors, uRight and
   depth equal the committed golden digests (tests/golden/fixtures.json), the matches equal the
-  restated matcher's.
+  restated matcher's.  mvImagePyramid after operator() equals the oracle's levels bytewise, and
+  the reference's stereo body (Frame.cc:496-686) run over it equals the glue's device match.
 """
 import hashlib
 import json
@@ -81,6 +82,20 @@ def test_facade_dropin_sequence(facade_bin, oracle_mod, gpu, tmp_path, seed, mod
     n_o, m_o = om.search_by_bow_kf_frame(KF, np.ones(nr, bool), F, 0.75, True)
     assert bow[0] == n_o and n_o > 0
     np.testing.assert_array_equal(bow[1:], m_o)
+    if mode == "threads":
+        # mvImagePyramid straight after operator() (ORBextractor.h:85; refilled at
+        # ORBextractor.cc:1129-1154): every level of both views bytewise against the oracle's;
+        # the program also checked that Frame.cc:496-686 over these cv::Mat levels gives the
+        # glue's uRight / depth (nvalid_ref == nvalid)
+        from oracle import OracleExtractor
+        for view, img in (("left", L), ("right", R)):
+            ox = OracleExtractor(g["params"][0])
+            ox(img)
+            want = b"".join(ox.level(l).tobytes() for l in range(8))
+            got = rd(f"pyr_{view}.bin")
+            assert len(got) == len(want), view
+            assert got == want, f"mvImagePyramid of the {view} view differs from the oracle's levels"
+        assert int(np.frombuffer(rd("nvalid_ref.bin"), np.int32)[0]) == g["n_valid"]
 
 
 @pytest.mark.gpu

@@ -106,8 +106,7 @@ def test_projection_large_target(oracle_mod, orbx_lib, gpu, mode):
 
 @pytest.mark.parametrize("mode,seed,th,prefilter", [
     (PROJ_FRAME_MAPPOINTS, 11, 15.0, False), (PROJ_LAST_FRAME, 12, 7.0, True),
-    (PROJ_LAST_FRAME, 13, 25.0, True), (PROJ_LAST_FRAME, 14, 25.0, False),
-    (PROJ_KEYFRAME, 15, 10.0, True)])
+    (PROJ_LAST_FRAME, 13, 25.0, True), (PROJ_KEYFRAME, 15, 10.0, True)])
 def test_projection_no_claim_queries(oracle_mod, orbx_lib, gpu, mode, seed, th, prefilter):
     """orbx_search_by_projection_ex: a third of the queries are MapPoints without
     observations (ORBX_QF_NO_CLAIM), whose matches later queries may take over (ORBmatcher.cc
@@ -133,6 +132,30 @@ def test_projection_no_claim_queries(oracle_mod, orbx_lib, gpu, mode, seed, th, 
     if mode != PROJ_KEYFRAME:   # some feature is matched by two queries
         hit = m_o[m_o >= 0]
         assert len(np.unique(hit)) < len(hit) - 50
+
+
+def test_projection_no_claim_last_frame_needs_prefilter(oracle_mod, orbx_lib, gpu):
+    """LAST_FRAME + rotation check + no-claim queries without ORBX_PROJ_PREFILTER is refused
+    by the library and the oracle alike: the reference's rotation filter clears per feature
+    (ORBmatcher.cc:1516-1535) and a feature matched by two queries sits in two bins."""
+    from my_orb_slam2_amd import OrbxError
+    from oracle import matcher as om
+    f1, f2, t = synth.feature_pair(54, n1=600, n2=500, dup_frac=0.1)
+    q, d = synth.projection_queries(14, f1, f2, t, th=25.0, mode_levels="frame")
+    qflags = np.zeros(len(q), np.uint8)
+    qflags[3] = 1
+    m = _matcher(0.8, True)
+    with pytest.raises(OrbxError):
+        m.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, qflags, orb_dist=64)
+    n_o, _ = om.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, qflags, orb_dist=64, nnratio=0.8)
+    assert n_o == -1
+    # without no-claim queries, or with the prefilter, the call runs
+    n_g, m_g = m.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, np.zeros(len(q), np.uint8),
+                                         orb_dist=64)
+    n_o, m_o = om.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, np.zeros(len(q), np.uint8),
+                                          orb_dist=64, nnratio=0.8)
+    assert n_g == n_o and n_o > 0
+    np.testing.assert_array_equal(m_g, m_o)
 
 
 def test_sim3(oracle_mod, orbx_lib, gpu):

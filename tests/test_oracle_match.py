@@ -328,8 +328,7 @@ def test_projection_crosscheck(mode):
 
 
 @pytest.mark.parametrize("mode,prefilter", [(PROJ_FRAME_MAPPOINTS, False),
-                                            (PROJ_LAST_FRAME, False), (PROJ_LAST_FRAME, True),
-                                            (PROJ_KEYFRAME, True)])
+                                            (PROJ_LAST_FRAME, True), (PROJ_KEYFRAME, True)])
 def test_projection_ex_crosscheck(mode, prefilter):
     """orbx_search_by_projection_ex's per-query no-claim flag and the prefilter call flag."""
     f1, f2, t = synth.feature_pair(31 + mode, n1=150, n2=160, dup_frac=0.15)
@@ -349,6 +348,22 @@ def test_projection_ex_crosscheck(mode, prefilter):
     if mode != PROJ_KEYFRAME:
         hit = m_o[m_o >= 0]
         assert len(np.unique(hit)) < len(hit)
+
+
+def test_projection_ex_last_frame_no_claim_needs_prefilter():
+    """LAST_FRAME + rotation check + a no-claim query without the prefilter: the oracle refuses
+    (-1), as the C ABI does (ORBX_ERR_INVALID): the reference clears per feature
+    (ORBmatcher.cc:1516-1535), which a per-query filter cannot reproduce."""
+    f1, f2, t = synth.feature_pair(34, n1=150, n2=160, dup_frac=0.15)
+    q, d = synth.projection_queries(12, f1, f2, t, th=12.0, mode_levels="frame")
+    qflags = np.zeros(len(q), np.uint8)
+    qflags[0] = 1
+    n_o, _ = om.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, qflags, orb_dist=64,
+                                        nnratio=0.8, prefilter=False)
+    assert n_o == -1
+    n_o, _ = om.search_by_projection_ex(PROJ_LAST_FRAME, f2, q, d, qflags, orb_dist=64,
+                                        nnratio=0.8, prefilter=False, check_ori=False)
+    assert n_o >= 0
 
 
 def _distinctive_case(seed, npts=60, maxn=40):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Drop-in host path: where a stereo frame's time goes (kernel + HIP API + copy traces at K=1 and
-# K=8) and the split-8 stereo A/B.  usage: tools/dropin_trace.sh TAG
+# K=8).  usage: tools/dropin_trace.sh TAG
 set -o pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
@@ -8,11 +8,10 @@ export TMPDIR=/tmp
 python tools/dropin_data.py /tmp/dd 8 > /dev/null || exit 1
 B=tests/native/boundary_test
 timeout -k 10 120 $B bench /tmp/dd 300 30 1 > $OUT/k1.json || exit 1
-LD_LIBRARY_PATH=$PWD/tools/_var/st8:$LD_LIBRARY_PATH timeout -k 10 120 $B bench /tmp/dd 300 30 1 > $OUT/k1_st8.json || exit 1
 timeout -k 10 120 $B bench /tmp/dd 100 20 8 > $OUT/k8.json || exit 1
 python - $OUT <<'PY'
 import json, sys
-for n in ("k1", "k1_st8", "k8"):
+for n in ("k1", "k8"):
     j = json.load(open(f"{sys.argv[1]}/{n}.json")); v = sorted(j["latency_ms"])
     print(n, "median", v[len(v)//2], "mean", sum(v)/len(v), "pairs/s", j["trackers"]*j["frames"]/(j["wall_ms"]/1e3))
 PY

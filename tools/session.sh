@@ -6,7 +6,7 @@
 #          stats of a short headline run), dropin (drop-in line), pmc (HBM fetch/write passes),
 #          k=<pytest -k expr> (a subset of the GPU tests), counters (kernel trace + PMC passes,
 #          tools/prof_counters.sh), workloads (the side-row benches: euroc, reloc, tri, bf, kfdb,
-#          tum, host-io), dropin_ab (the one-call Frame with / without the pyramid chain),
+#          tum, host-io), ab (tools/variants.py run: the headline per built variant),
 #          frame_trace (kernel + API trace of the one-call Frame, K = 1 and 8)
 # Copy what is kept into profiles/ with tools/collect_profiles.sh.
 set -o pipefail
@@ -48,6 +48,17 @@ for step in "$@"; do
       timeout -k 10 900 bash tools/prof_counters.sh $OUT/prof_euroc --workload euroc --steps 10 --warmup 3 > $OUT/counters_euroc.log 2>&1 \
         || { echo "EUROC COUNTERS FAILED"; tail -20 $OUT/counters_euroc.log; exit 1; }
       echo euroc counters done ;;
+    counters_match)
+      # FETCH_SIZE and WRITE_SIZE passes (one counter per run) of the matcher workloads; the bf
+      # run times both distance kernels (k_bf_mfma, then k_bf_top2 as alt_kernel)
+      for w in bf reloc triangulation; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 240 rocprofv3 --pmc $c -d $OUT/pmc_${w}_${c}dir -o run --output-format csv -- python3 bench.py --workload $w --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/pmc_${w}_$c.log 2>&1 \
+            || { echo "PMC $w $c FAILED"; tail -20 $OUT/pmc_${w}_$c.log; exit 1; }
+          cp $OUT/pmc_${w}_${c}dir/run_counter_collection.csv $OUT/pmc_${w}_$c.csv
+        done
+      done
+      echo match counters done ;;
     workloads)
       for w in euroc reloc triangulation bf kfdb tum; do
         timeout -k 10 300 python bench.py --workload $w --cpu-seconds 5 > $OUT/$w.json 2> $OUT/$w.err \
@@ -56,11 +67,10 @@ for step in "$@"; do
       timeout -k 10 300 python bench.py --host-io --cpu-seconds 0 > $OUT/hostio.json 2> $OUT/hostio.err \
         || { echo "HOST-IO FAILED"; tail -20 $OUT/hostio.err; exit 1; }
       echo workloads done ;;
-    dropin_ab)
-      python tools/dropin_data.py /tmp/dd 32 > /dev/null || exit 1
-      ORBX_AB_SETTINGS=frame,frame_nochain timeout -k 10 400 python tools/dropin_ab.py run /tmp/dd 1,8 > $OUT/dropin_ab.txt 2>&1 \
-        || { echo "DROPIN AB FAILED"; tail -5 $OUT/dropin_ab.txt; exit 1; }
-      cat $OUT/dropin_ab.txt ;;
+    ab)
+      timeout -k 10 900 python tools/variants.py run --rounds 2 > $OUT/ab.txt 2>&1 \
+        || { echo "AB FAILED"; tail -5 $OUT/ab.txt; exit 1; }
+      cat $OUT/ab.txt ;;
     frame_trace)
       bash tools/frame_trace.sh ${OUT#gpurun_out/}/tr || exit 1 ;;
     *)
