@@ -1114,7 +1114,7 @@ def main_dropin(args):
     def loop(d, via):
         binp = os.path.join(ROOT, "tests", "native",
                             "boundary_test" if via == "cabi" else "facade_test")
-        extra = ["frame"] if via == "frame" else []
+        extra = ["frame"] if via == "frame" else (["pyr"] if via == "pyr" else [])
         per_k, digests = {}, {}
         for K in ks:
             r = subprocess.run([binp, "bench", d, str(args.frames), str(warm), str(K)] + extra,
@@ -1144,6 +1144,17 @@ def main_dropin(args):
             alt = {"via": "facade (two ExtractORB threads + ComputeStereoMatches)",
                    "per_trackers": [alt_k[k] for k in ks],
                    "digests_equal_one_call": alt_dig == dig}
+            # the same two-thread facade with mvImagePyramid refreshed by every operator()
+            # (the host pyramid copy on, as for an unchanged Frame::ComputeStereoMatches):
+            # operator()'s added cost
+            pyr_k, pyr_dig = loop(d, "pyr")
+            alt["host_pyramid"] = {
+                "via": "facade, every operator() refreshing mvImagePyramid (pinned host copy of "
+                       "the pyramid, ORBextractor.cc:1129-1154), stereo through orbx_stereo_match",
+                "per_trackers": [pyr_k[k] for k in ks], "digests_equal_one_call": pyr_dig == dig,
+                "added_ms_median_per_frame": {
+                    k: pyr_k[k]["latency"]["median_ms"] - alt_k[k]["latency"]["median_ms"]
+                    for k in ks}}
     cpu = None
     if args.cpu_seconds > 0:
         cpu = cpu_baseline(pairs, mb, min(args.cpu_seconds, 6.0))

@@ -1379,12 +1379,16 @@ static orbx_status copy_served(FrameServer& fs, const FsReq& r, const FsBatch& g
     // ... but its pyramids when asked for (orbx_extractor_keep_pyramid): both views' blocks,
     // device to device from the server handle, whose workspace this block pair's next batch
     // does not touch while this thread holds its reader count
+    // The frame's keypoints, descriptors and stereo outputs are complete at this point: a
+    // failure below leaves the handle in the "no pyramid" state (orbx_pyramid_level returns
+    // ORBX_ERR_STATE) and the frame still succeeds.  The handle's workspace is the two-image
+    // one its own solo frames run in (the server serves only handles that run solo when it is
+    // idle), so sizing it here allocates nothing those would not.
     const orbx_extractor* S = fs.sh[r.blk];
-    orbx_status s = ensure_workspace(h, g.width, g.height, 2);
-    if (s != ORBX_OK) return s;
+    if (ensure_workspace(h, g.width, g.height, 2) != ORBX_OK) return ORBX_OK;
     const size_t pyrb = (size_t)h->hg.pyr_bytes;
     if (!S || (size_t)S->hg.pyr_bytes != pyrb || S->hg.lv[0].pitch != h->hg.lv[0].pitch)
-        return ORBX_ERR_STATE;
+        return ORBX_OK;
     const uint8_t* src = S->d_pyr.as<uint8_t>();
     uint8_t* dst = h->d_pyr.as<uint8_t>();
     if (!HIPOK(hipSetDevice(h->device)) || !order_after_last(h, h->stream) ||
@@ -1392,7 +1396,7 @@ static orbx_status copy_served(FrameServer& fs, const FsReq& r, const FsBatch& g
         !HIPOK(hipMemcpyAsync(dst + pyrb, src + img[1] * pyrb, pyrb, hipMemcpyDeviceToDevice,
                               h->stream)) ||
         !mark_done(h, h->stream) || !wait_done(h))
-        return ORBX_ERR_DEVICE;
+        return ORBX_OK;
     h->last_batch = 2;
     h->pyr_images = 2;
     ++h->serial;

@@ -30,4 +30,9 @@ cp $V/prof/pmc5/run_counter_collection.csv profiles/${R}_pmc_busy_b512.csv
 [ -d $V/prof_euroc ] && cp $V/prof_euroc/pmc5/run_counter_collection.csv profiles/${R}_pmc_busy_euroc.csv
 [ -f $V/prof_reloc/run_kernel_stats.csv ] && cp $V/prof_reloc/run_kernel_stats.csv profiles/${R}_c4_reloc_kernel_stats.csv
 [ -f $V/prof_tri/run_kernel_stats.csv ] && cp $V/prof_tri/run_kernel_stats.csv profiles/${R}_c5_triangulation_kernel_stats.csv
+for w in bf reloc triangulation; do
+  [ -f $V/pmc_${w}_FETCH_SIZE.csv ] && cp $V/pmc_${w}_FETCH_SIZE.csv profiles/${R}_pmc_fetch_${w}.csv
+  [ -f $V/pmc_${w}_WRITE_SIZE.csv ] && cp $V/pmc_${w}_WRITE_SIZE.csv profiles/${R}_pmc_write_${w}.csv
+  [ -f $V/trace_${w}/run_kernel_stats.csv ] && cp $V/trace_${w}/run_kernel_stats.csv profiles/${R}_${w}_kernel_stats.csv
+done
 echo copied

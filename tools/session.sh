@@ -57,6 +57,8 @@ for step in "$@"; do
             || { echo "PMC $w $c FAILED"; tail -20 $OUT/pmc_${w}_$c.log; exit 1; }
           cp $OUT/pmc_${w}_${c}dir/run_counter_collection.csv $OUT/pmc_${w}_$c.csv
         done
+        timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python3 bench.py --workload $w --steps 10 --warmup 2 --cpu-seconds 0 > $OUT/trace_$w.log 2>&1 \
+          || { echo "TRACE $w FAILED"; tail -20 $OUT/trace_$w.log; exit 1; }
       done
       echo match counters done ;;
     workloads)
