@@ -64,9 +64,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="stereo pairs (default 512) or EuRoC frames (default 256) per step per GPU")
-    ap.add_argument("--distinct", type=int, default=32,
-                    help="synthetic base pairs / frames generated per rank (stereo: the batch "
-                         "slots are row-rolled copies of them, all distinct)")
+    ap.add_argument("--distinct", type=int, default=None,
+                    help="synthetic base pairs / frames generated per rank (stereo default: one "
+                         "per batch slot, 512 independent scenes; fewer: the batch slots are "
+                         "row-rolled copies of them, all distinct; other workloads default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -134,14 +135,35 @@ def parse():
 # ---- the timed workloads' inputs (also built by tests/test_gpu_bench_geometry.py, which checks
 # parity at exactly the sizes and geometries timed here) ----------------------------------------
 
+def _gen_pair(seed):
+    from my_orb_slam2_amd import synth
+    return synth.stereo_pair(seed, W, H)
+
+
 def stereo_inputs(rank: int, B: int, P: int):
     """configs[1] inputs of one rank: B host stereo pairs (left [B,H,W], right [B,H,W]) built
-    from P generated base pairs; slot i is base pair i % P with both views rolled down by
-    37 * (i // P) rows (still rectified; generating B pairs from scratch would cost ~60 ms
-    each on the host).  Returns (Lh, Rh, base_pairs, distinct_slots)."""
-    from my_orb_slam2_amd import synth
+    from P generated base pairs (the headline: P = B, every slot its own scene); with P < B
+    slot i is base pair i % P with both views rolled down by 37 * (i // P) rows (still
+    rectified).  A pair costs ~40 ms on one host core, so more than 8 are generated by a
+    process pool over this process's CPUs, forked only while the process has not touched the
+    GPU.  Returns (Lh, Rh, base_pairs, distinct_slots)."""
     P = max(1, min(P, B))
-    pairs = [synth.stereo_pair(1000 * rank + i, W, H) for i in range(P)]
+    seeds = [1000 * rank + i for i in range(P)]
+    pairs = None
+    # not under a profiler: its preloaded library would start a GPU session in every worker
+    profiled = "rocprof" in os.environ.get("LD_PRELOAD", "") or any(
+        k.startswith("ROCPROF") for k in os.environ)
+    if P > 8 and not profiled:
+        try:
+            import multiprocessing as mp
+            import torch
+            if not torch.cuda.is_initialized():
+                with mp.get_context("fork").Pool(max(1, min(cpu_quota()[0], 8))) as pool:
+                    pairs = pool.map(_gen_pair, seeds, chunksize=4)
+        except Exception:
+            pairs = None
+    if pairs is None:
+        pairs = [_gen_pair(s) for s in seeds]
 
     def slot(i, view):
         return np.roll(pairs[i % P][view], 37 * (i // P), axis=0)
@@ -257,6 +279,8 @@ def relaunch_if_needed(args) -> None:
 
 def main():
     args = parse()
+    if args.distinct is None:   # the headline: every slot its own scene
+        args.distinct = (args.batch or 512) if args.workload == "stereo" else 32
     relaunch_if_needed(args)
     keep_stdout_for_result()
     if args.traffic_csv is None:
@@ -281,6 +305,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    B = args.batch or 512
+    P = max(1, min(args.distinct, B))
+    # every slot of the batch holds a different pair (stereo_inputs); generated before the
+    # process touches the GPU (the generator pool forks)
+    Lh, Rh, pairs, n_distinct = stereo_inputs(rank, B, P)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # ORBX_FORCE_DIST=1 takes the process-group path at world size 1 (torchrun
@@ -291,10 +320,6 @@ def main():
 
     import my_orb_slam2_amd as orbx
 
-    B = args.batch or 512
-    P = max(1, min(args.distinct, B))
-    # every slot of the batch holds a different pair (stereo_inputs)
-    Lh, Rh, pairs, n_distinct = stereo_inputs(rank, B, P)
     Ls = torch.from_numpy(Lh).to(dev)
     Rs = torch.from_numpy(Rh).to(dev)
     torch.cuda.synchronize(dev)
@@ -1105,8 +1130,8 @@ def main_dropin(args):
     one-call loop's.  Beside it the CPU restatement run the same way on the same pairs."""
     import subprocess
     import tempfile
-    B = max(1, args.distinct)
-    Lh, Rh, pairs, _ = stereo_inputs(0, B, args.distinct)
+    B = max(1, min(args.distinct, 32))
+    Lh, Rh, pairs, _ = stereo_inputs(0, B, B)
     mb = float(np.float32(MBF) / np.float32(FX))
     warm = max(20, args.warmup)
     ks = [max(1, int(k)) for k in str(args.trackers).split(",")]

@@ -856,9 +856,9 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     {
         h->ncap = (int)align_up((size_t)ocmax, 16);
         int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
-        while (kc > 64 && octree_lds_bytes(h->ncap, kc) > OCT_LDS_KB * 1024) kc -= 64;
+        while (kc > 64 && octree_lds_bytes(h->ncap, kc, true) > OCT_LDS_KB * 1024) kc -= 64;
         h->kcap = kc;
-        h->octree_lds = octree_lds_bytes(h->ncap, h->kcap);
+        h->octree_lds = octree_lds_bytes(h->ncap, h->kcap, true);
         h->ncap1 = h->ncap;
         h->kcap1 = h->kcap;
         h->octree_lds1 = h->octree_lds;
@@ -866,9 +866,9 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
     {
         // small batches: the same node arrays, candidates in LDS up to OCT_LDS_SMALL_KB
         int kc = std::min(std::max(std::max(ncand0, ncand1), 64), 8192);
-        while (kc > 64 && octree_lds_bytes(h->ncap, kc) > OCT_LDS_SMALL_KB * 1024) kc -= 64;
+        while (kc > 64 && octree_lds_bytes(h->ncap, kc, false) > OCT_LDS_SMALL_KB * 1024) kc -= 64;
         h->kcap_small = std::max(kc, h->kcap);
-        h->octree_lds_small = std::max(octree_lds_bytes(h->ncap, h->kcap_small), h->octree_lds);
+        h->octree_lds_small = std::max(octree_lds_bytes(h->ncap, h->kcap_small, false), h->octree_lds);
     }
     G.stereo_ob = G.nlevels;
     h->stereo_lds = stereo_lds_bytes(G.kp_cap, G.lv[0].h, G.stereo_ob);

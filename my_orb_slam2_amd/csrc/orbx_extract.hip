@@ -275,6 +275,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
     };
     CellDesc cn = cells[c_first];
     bool have = prefetch(cn);
+    // The wave's cells' candidates are written back to back from its first cell's slot (the
+    // slots of consecutive cells are contiguous, and a cell writes at most its capacity), so
+    // the octree reads about one cache line per wave instead of one per cell: a cell's run
+    // starts `delta` words before its own slot, ccnt = count | delta << 16
+    const uint32_t wslot = (uint32_t)cn.slot;
+    uint32_t wpos = 0;
     for (int k = 0; k < ncw; ++k) {
         const int ci = c_first + k;
         const CellDesc c = cn;
@@ -292,25 +298,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
 #pragma unroll
                     for (int j = 0; j < FAST_PF2D; ++j)
                         l[4 * j * lp] = pf[j];
-                }
-            } else
-            if (pre) {
-                if (lp == ndw) {
-#pragma unroll
-                    for (int j = 0; j < FAST_PF; ++j)
-                        if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lane + 64 * j] = pf[j];
-                } else {   // dense element t = lane + 64 j -> row t / ndw, column t % ndw
-                    const int dr = 64 / ndw, dc = 64 - dr * ndw;
-                    int r = lane / ndw, col = lane - r * ndw;
-                    int lo = r * lp + col;
-                    const int lstep = dr * lp + dc, lwrap = lp - ndw;
-#pragma unroll
-                    for (int j = 0; j < FAST_PF; ++j) {
-                        if (lane + 64 * j < rows * ndw) ((uint32_t*)roi0)[lo] = pf[j];
-                        col += dc;
-                        lo += lstep;
-                        if (col >= ndw) { col -= ndw; lo += lwrap; }
-                    }
                 }
             } else {
                 const LevelGeom& L = g->lv[c.level];
@@ -346,7 +333,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         const uint32_t colmask16 = rem16 >= 16 ? 0xFFFFu : (rem16 > 0 ? (1u << rem16) - 1u : 0u);
         const int rows_blk = rpp16;
         (void)colmask; (void)sub; (void)gx;
-        uint32_t* slot = cand + (size_t)b * g->cand_words + c.slot;
+        uint32_t* slot = cand + (size_t)b * g->cand_words + wslot + wpos;
         const int t_ini = g->ini_th, t_min = g->min_th;
         int base = 0;
         // Two passes: the cell is first detected at iniThFAST alone (compass test, arc scores
@@ -458,7 +445,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         if (base > 0) break;   // wave-uniform: keypoints at this pass's threshold
         lds_order();
         }
-        if (lane == 0) *cnt_out = min(base, c.cap);
+        const int nout = min(base, c.cap);
+        if (lane == 0) *cnt_out = nout | (int)(((uint32_t)c.slot - (wslot + wpos)) << 16);
+        wpos += (uint32_t)nout;
         lds_order();
     }
 }
@@ -488,7 +477,7 @@ struct NodeArrays {
 
 struct OctreeSmem {
     NodeArrays A, B;
-    int32_t* cc;      // [NCAP][4] child counts
+    int32_t* cc;      // child counts: [NCAP][4] u32, or [NCAP][2] u16 pairs (see octree_level)
     int16_t* cpos;    // [NCAP][4] new position of each child
     int16_t* npos;    // [NCAP] new position of a surviving node
     int16_t* pord;    // [NCAP] processing order in a phase-2 round (-1: not processed)
@@ -548,12 +537,36 @@ __device__ __forceinline__ int chunked_scan(int n, int* tmp, F f, G gcb) {
 }
 
 
-template <int NT, bool KEYS_LDS>
+// knode[k]: candidate k's node (< NCAP <= 8192: 13 bits); between a round's quadrant pass and
+// its remap pass bits 13-14 also hold the candidate's quadrant in a node being split.
+template <int NT, bool KEYS_LDS, bool PACKED>
 __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L, int b,
-                             int level, int ncand, uint32_t* kdata, int16_t* knode, uint8_t* kq,
+                             int level, int ncand, uint32_t* kdata, int16_t* knode,
                              OctreeSmem& sm, int* __restrict__ ocnt, uint32_t* __restrict__ okp,
                              uint16_t* __restrict__ operm) {
     const int tid = threadIdx.x;
+    // child counts per node: PACKED (large batches, candidates in LDS: ncand <= KCAP <= 8192)
+    // two 16-bit counts per dword ([NCAP][2]: half the LDS, so a 1500-candidate level-0 list
+    // fits the 40 KB budget); else [NCAP][4] dwords (small batches, whose budget is large and
+    // whose lone lists are a serial chain the unpacking would lengthen; and the global-scratch
+    // path, where a node may hold more than 65535 keys)
+    static_assert(KEYS_LDS || !PACKED, "packed counts need ncand <= KCAP");
+    uint32_t* const ccw = (uint32_t*)sm.cc;
+    auto cc_zero = [&](int n) {
+        if (PACKED) {
+            ccw[n * 2] = 0u; ccw[n * 2 + 1] = 0u;
+        } else {
+            ccw[n * 4] = 0u; ccw[n * 4 + 1] = 0u; ccw[n * 4 + 2] = 0u; ccw[n * 4 + 3] = 0u;
+        }
+    };
+    auto cc_add = [&](int n, int q) {
+        if (PACKED) atomicAdd(&ccw[n * 2 + (q >> 1)], 1u << (16 * (q & 1)));
+        else atomicAdd(&ccw[n * 4 + q], 1u);
+    };
+    auto cc_get = [&](int n, int q) -> int {
+        if (PACKED) return (int)((ccw[n * 2 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
+        return (int)ccw[n * 4 + q];
+    };
     const int N = L.nfeat;
     int* tmp = sm.tmp;
     const int nIni = L.n_ini;
@@ -561,20 +574,20 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
     const int Hh = L.h - 2 * ORBX_MIN_BORDER;
 
     // ---- roots (src/ORBextractor.cc:552-587) ----
-    for (int i = tid; i < nIni; i += NT) sm.cc[i * 4] = 0;
+    for (int i = tid; i < nIni; i += NT) cc_zero(i);
     __syncthreads();
     for (int k = tid; k < ncand; k += NT) {
         const int x = cand_x(kdata[k]);
         int r = (int)((float)x / hX);
         r = min(r, nIni - 1);
         knode[k] = (int16_t)r;
-        atomicAdd(&sm.cc[r * 4], 1);
+        cc_add(r, 0);
     }
     __syncthreads();
     int S = chunked_scan<NT>(
-        nIni, tmp, [&](int i) { return sm.cc[i * 4] > 0 ? 1 : 0; },
+        nIni, tmp, [&](int i) { return cc_get(i, 0) > 0 ? 1 : 0; },
         [&](int i, int ex) {
-            const int c = sm.cc[i * 4];
+            const int c = cc_get(i, 0);
             if (c > 0) {
                 sm.A.x0[ex] = (int16_t)(int)(hX * (float)i);
                 sm.A.x1[ex] = (int16_t)(int)(hX * (float)(i + 1));
@@ -596,8 +609,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
         const int prevS = S;
         // ---- split every multi-key node: quadrant of each of its keys ----
         for (int i = tid; i < S; i += NT) {
-            sm.cc[i * 4 + 0] = 0; sm.cc[i * 4 + 1] = 0;
-            sm.cc[i * 4 + 2] = 0; sm.cc[i * 4 + 3] = 0;
+            cc_zero(i);
             sm.pord[i] = -1;
             // a multi-key node's split lines, once per node (cpos is free until the node pass)
             if (cur.cnt[i] > 1) {
@@ -628,19 +640,17 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     const int sx = sm.cpos[n[u] * 4], sy = sm.cpos[n[u] * 4 + 1];
                     const int x = cand_x(kd[u]), y = cand_y(kd[u]);
                     const int q = (x < sx) ? (y < sy ? 0 : 2) : (y < sy ? 1 : 3);
-                    kq[k] = (uint8_t)q;
-                    atomicAdd(&sm.cc[n[u] * 4 + q], 1);
+                    knode[k] = (int16_t)(n[u] | q << 13);
+                    cc_add(n[u], q);
                 }
             }
         }
         __syncthreads();
         auto nonempty = [&](int n) {
-            return (sm.cc[n * 4] > 0) + (sm.cc[n * 4 + 1] > 0) + (sm.cc[n * 4 + 2] > 0) +
-                   (sm.cc[n * 4 + 3] > 0);
+            return (cc_get(n, 0) > 0) + (cc_get(n, 1) > 0) + (cc_get(n, 2) > 0) + (cc_get(n, 3) > 0);
         };
         auto multi = [&](int n) {
-            return (sm.cc[n * 4] > 1) + (sm.cc[n * 4 + 1] > 1) + (sm.cc[n * 4 + 2] > 1) +
-                   (sm.cc[n * 4 + 3] > 1);
+            return (cc_get(n, 0) > 1) + (cc_get(n, 1) > 1) + (cc_get(n, 2) > 1) + (cc_get(n, 3) > 1);
         };
         int Ctot, Stot, nToExpand = 0;
         if (!phase2) {
@@ -687,7 +697,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     split_lines(x0, y0, x1, y1, sx, sy);
                     int rank_asc = 0;
                     for (int q = 0; q < 4; ++q) {
-                        const int cq = sm.cc[i * 4 + q];
+                        const int cq = cc_get(i, q);
                         if (cq > 0) {
                             const int pos = start + (c - 1 - rank_asc);   // n4..n1 from the front
                             int cx0, cy0, cx1, cy1;
@@ -882,7 +892,7 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
                     split_lines(x0, y0, x1, y1, sx, sy);
                     int rank_asc = 0;
                     for (int q = 0; q < 4; ++q) {
-                        const int cq = sm.cc[i * 4 + q];
+                        const int cq = cc_get(i, q);
                         if (cq > 0) {
                             const int pos = start + (c - 1 - rank_asc);
                             int cx0, cy0, cx1, cy1;
@@ -910,8 +920,9 @@ __device__ void octree_level(const Geometry* __restrict__ g, const LevelGeom& L,
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int k = min(k0 + u * NT, ncand - 1);
-                n[u] = knode[k];
-                q[u] = kq[k];
+                const int kn = knode[k];
+                n[u] = kn & 0x1FFF;
+                q[u] = (kn >> 13) & 3;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) o[u] = sm.pord[n[u]];
@@ -986,7 +997,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
                                                 uint16_t* __restrict__ operm,
                                                 uint8_t* __restrict__ kscratch,
                                                 long long kscratch_per_image, int NCAP, int KCAP,
-                                                int level_base) {
+                                                int level_base, int packed) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // one launch for all levels, the (long) level-0 lists dispatched first
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1008,20 +1019,22 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     sm.B.x0 = (int16_t*)take(NCAP * 2); sm.B.y0 = (int16_t*)take(NCAP * 2);
     sm.B.x1 = (int16_t*)take(NCAP * 2); sm.B.y1 = (int16_t*)take(NCAP * 2);
     sm.B.cnt = (int32_t*)take(NCAP * 4); sm.B.seq = (int32_t*)take(NCAP * 4);
-    sm.cc = (int32_t*)take((size_t)NCAP * 16);
     sm.cpos = (int16_t*)take((size_t)NCAP * 8);
     sm.npos = (int16_t*)take(NCAP * 2);
     sm.pord = (int16_t*)take(NCAP * 2);
     sm.pre = (int32_t*)take(NCAP * 4);
     sm.pre2 = (int32_t*)take(NCAP * 4);
+    // the child counts last but the candidate arrays: the LDS path's counts ([NCAP][2] packed
+    // or [NCAP][4]), then its candidates; the global-scratch path's [NCAP][4] counts run on
+    // over the (unused) candidate arrays (octree_lds_bytes sizes both)
+    sm.cc = (int32_t*)take((size_t)NCAP * (packed ? 8 : 16));
     uint32_t* l_kdata = (uint32_t*)take((size_t)KCAP * 4);
     int16_t* l_knode = (int16_t*)take((size_t)KCAP * 2);
-    uint8_t* l_kq = (uint8_t*)take((size_t)KCAP);
 
     // count the level's candidates
     const int* cc = ccnt + (size_t)b * g->n_cells + L.cell_begin;
     int part = 0;
-    for (int c = tid; c < L.ncells; c += NT) part += cc[c];
+    for (int c = tid; c < L.ncells; c += NT) part += cc[c] & 0xFFFF;
     const int ncand = block_sum<NT / 64>(part, sm.tmp);
     if (ncand == 0 || L.n_ini < 1 || L.nfeat <= 0) {
         if (tid == 0) ocnt[b * g->nlevels + level] = 0;
@@ -1029,7 +1042,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     }
     const bool in_lds = ncand <= KCAP;
     uint8_t* gs = kscratch + (size_t)b * kscratch_per_image;
-    // global fallback region of this level: [kdata u32][knode i16][kq u8]
+    // global fallback region of this level: [kdata u32][knode i16]
     long long lvl_off = 0;
     for (int l = 0; l < level; ++l) lvl_off += (long long)g->lv[l].cand_cap * 8;
     // gather candidates in cell order (cell-major, raster inside a cell)
@@ -1037,7 +1050,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
     const CellDesc* lc = cells + L.cell_begin;
     // the candidate arrays are LDS or global scratch by a runtime test; each branch passes its
     // own pointers (a pointer selected between the two is generic: every access a flat one)
-    auto gather_and_split = [&](uint32_t* kdata, int16_t* knode, uint8_t* kq, auto keys_lds_c) {
+    auto gather_and_split = [&](uint32_t* kdata, int16_t* knode, auto keys_lds_c, auto packed_c) {
     // two adjacent cells per thread, their offsets from one scan of the pairs' sums, and the
     // first 8 candidates of both cells loaded at once (addresses clamped into each cell's
     // slot, so no load is guarded): a level of up to 2 NT cells costs one memory round trip
@@ -1046,13 +1059,15 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
         int carry = 0;
         for (int c0 = 0; c0 < L.ncells; c0 += 2 * NT) {
             const int ca = c0 + 2 * tid, cb = ca + 1;
-            const int na = ca < L.ncells ? cc[ca] : 0, nb = cb < L.ncells ? cc[cb] : 0;
+            // ccnt = count | (words the cell's run starts before its slot) << 16 (k_fast)
+            const int wa = ca < L.ncells ? cc[ca] : 0, wb = cb < L.ncells ? cc[cb] : 0;
+            const int na = wa & 0xFFFF, nb = wb & 0xFFFF;
             int tot;
             const int exa = carry + block_excl_scan<NT / 64>(na + nb, sm.tmp, tot);
             const int exb = exa + na;
             carry += tot;
-            const uint32_t* sa = cbase + (na > 0 ? lc[ca].slot : 0);
-            const uint32_t* sb = cbase + (nb > 0 ? lc[cb].slot : 0);
+            const uint32_t* sa = cbase + (na > 0 ? lc[ca].slot - (wa >> 16) : 0);
+            const uint32_t* sb = cbase + (nb > 0 ? lc[cb].slot - (wb >> 16) : 0);
             for (int e0 = 0; e0 < max(na, nb); e0 += 8) {
                 uint32_t va[8], vb[8];
 #pragma unroll
@@ -1069,13 +1084,15 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
         }
     }
     __syncthreads();
-    octree_level<NT, decltype(keys_lds_c)::value>(g, L, b, level, ncand, kdata, knode, kq, sm, ocnt, okp, operm);
+    octree_level<NT, decltype(keys_lds_c)::value, decltype(packed_c)::value>(g, L, b, level, ncand, kdata, knode, sm, ocnt, okp, operm);
     };
-    if (in_lds)
-        gather_and_split(l_kdata, l_knode, l_kq, std::true_type{});
+    if (in_lds && packed)
+        gather_and_split(l_kdata, l_knode, std::true_type{}, std::true_type{});
+    else if (in_lds)
+        gather_and_split(l_kdata, l_knode, std::true_type{}, std::false_type{});
     else
         gather_and_split((uint32_t*)(gs + lvl_off), (int16_t*)(gs + lvl_off + (long long)L.cand_cap * 4),
-                         gs + lvl_off + (long long)L.cand_cap * 6, std::false_type{});
+                         std::false_type{}, std::false_type{});
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1377,7 +1394,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
 #define ORBX_OCT_LAUNCH(N)                                                                   \
         ORBX_TIMED_LAUNCH(T, K_OCTREE, k_octree<N>, grid, dim3(N), lds, s, a.dg, a.cells,     \
                           (const int*)a.ccnt, (const uint32_t*)a.cand, a.ocnt, a.okp,         \
-                          operm, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base)
+                          operm, a.kscratch, a.kscratch_per_image, ncap, kcap, level_base,   \
+                          a.oct_small ? 0 : 1)
         if (nt == 64) ORBX_OCT_LAUNCH(64);
         else if (nt == 128) ORBX_OCT_LAUNCH(128);
         else if (nt == 512) ORBX_OCT_LAUNCH(512);
@@ -1457,15 +1475,17 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-size_t octree_lds_bytes(int ncap, int kcap) {
+size_t octree_lds_bytes(int ncap, int kcap, bool packed) {
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
     int np2 = 1;
     while (np2 < ncap) np2 <<= 1;
     size_t s = r(224 * 4) + r((size_t)np2 * 8);
     s += 2 * (4 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4));
-    s += r((size_t)ncap * 16) + r((size_t)ncap * 8) + 2 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4);
-    s += r((size_t)kcap * 4) + r((size_t)kcap * 2) + r((size_t)kcap);
-    return s;
+    s += r((size_t)ncap * 8) + 2 * r((size_t)ncap * 2) + 2 * r((size_t)ncap * 4);
+    // the LDS path's packed counts + candidates, or the global path's wide counts
+    const size_t lds_path = r((size_t)ncap * (packed ? 8 : 16)) + r((size_t)kcap * 4) + r((size_t)kcap * 2);
+    const size_t glb_path = r((size_t)ncap * 16);
+    return s + (lds_path > glb_path ? lds_path : glb_path);
 }
 
 }  // namespace orbx

@@ -181,7 +181,7 @@ hipError_t launch_levels(const ExtractLaunch& a, hipStream_t st, int l_begin, in
 hipError_t launch_pyr_chain(const ExtractLaunch& a, hipStream_t st);
 size_t level_lds_bytes(int ltw, int lth, int win_cap);
 size_t fast_lds_bytes(const Geometry& g);
-size_t octree_lds_bytes(int ncap, int kcap);
+size_t octree_lds_bytes(int ncap, int kcap, bool packed);
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st);
 int stereo_split(int batch);   // workgroups per pair of a launch_stereo over `batch` pairs
 size_t stereo_lds_bytes(int kp_cap, int height, int ob);  // ob: octave bucket groups

@@ -89,11 +89,13 @@ def test_c2_timed_schedule_b512(oracle_mod, orbx_lib, gpu):
     it): two StereoBatch handles of 512 pairs alternating steps on two torch streams, each
     extraction with the side branch 3,3,1, six steps.  Every slot of both handles equals the
     single-handle one-stream run (overlap 0) of the same pairs, and 16 slots equal the CPU
-    restatement (ORBextractor.cc:1065-1154, Frame.cc:496-686)."""
+    restatement (ORBextractor.cc:1065-1154, Frame.cc:496-686).  The inputs are the headline's:
+    512 independent generated scenes (bench.py's default --distinct)."""
     import torch
     import my_orb_slam2_amd as m
     B = 512
-    Lh, Rh, pairs, _ = bench.stereo_inputs(0, B, 32)
+    Lh, Rh, pairs, n_distinct = bench.stereo_inputs(0, B, B)
+    assert len(pairs) == B and n_distinct == B
     Ls, Rs = torch.from_numpy(Lh).to(gpu), torch.from_numpy(Rh).to(gpu)
     mb = float(np.float32(bench.MBF) / np.float32(bench.FX))
     sbs, sts, run_on, run_step, overlap = bench.headline_handles(
