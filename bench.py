@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0                  # MI355X_MICROARCH.md: 8 TB/s spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_PMC = ",".join(os.path.join(HERE, "profiles", f) for f in
-                       ("r05_pmc_fetch_b512.csv", "r05_pmc_write_b512.csv"))
+                       ("r06_pmc_fetch_b512.csv", "r06_pmc_write_b512.csv"))
 DEFAULT_PMC_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
                              ("r05_pmc_fetch_euroc.csv", "r05_pmc_write_euroc.csv"))
 # FETCH_SIZE / WRITE_SIZE passes of the matcher workloads (tools/session.sh counters_match)
@@ -46,7 +46,7 @@ DEFAULT_PMC_BY_WORKLOAD = {
        for w in ("bf", "reloc", "triangulation")}}
 # SQ_INSTS_VALU and SQ_ACTIVE_INST_VALU passes (the VALU issue entry beside the HBM roofline)
 DEFAULT_INSTS = ",".join(os.path.join(HERE, "profiles", f) for f in
-                         ("r05_pmc_insts_b512.csv", "r05_pmc_busy_b512.csv"))
+                         ("r06_pmc_insts_b512.csv", "r06_pmc_busy_b512.csv"))
 DEFAULT_INSTS_EUROC = ",".join(os.path.join(HERE, "profiles", f) for f in
                                ("r05_pmc_insts_euroc.csv", "r05_pmc_busy_euroc.csv"))
 # VALU issue peaks of the chip (256 CUs x 4 SIMDs at 2.4 GHz): one wave64 instruction per
@@ -124,7 +124,7 @@ def parse():
                     help="euroc: projected local-map MapPoints per frame")
     ap.add_argument("--insts-csv", default=None,
                     help="rocprofv3 --pmc CSV holding SQ_INSTS_VALU for the roofline's VALU issue "
-                         "entry (default: the committed profiles/r05_pmc_insts_*.csv)")
+                         "entry (default: the committed profiles/r06_pmc_insts_*.csv)")
     ap.add_argument("--traffic-csv", default=None,
                     help="comma-separated rocprofv3 --pmc counter CSVs (globs) holding FETCH_SIZE"
                          " and WRITE_SIZE for the roofline traffic field (default: the"
@@ -861,7 +861,7 @@ def valu_from_csv(paths, kernel):
     return counter_from_csv(paths, kernel, "SQ_INSTS_VALU")
 
 
-ISA_MIX = os.path.join(HERE, "profiles", "r05_isa_mix.json")
+ISA_MIX = os.path.join(HERE, "profiles", "r06_isa_mix.json")
 
 
 def _mangled_key(demangled: str) -> str:

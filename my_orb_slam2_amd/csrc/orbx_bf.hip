@@ -205,13 +205,19 @@ __device__ __forceinline__ uint32_t max_u16(uint32_t a, uint32_t b) {
     return r;
 }
 
-__global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q, int nq,
+// BF_MFMA_WAVES waves x 64 queries per workgroup: 1024 queries, so a 1000-descriptor query
+// frame reads each database row once (4 workgroups of 256 queries read it 4 times: PMC traffic
+// 4.0x the rows' bytes, profiles/r06_pmc_fetch_bf.csv); the first 256 threads stage a block
+constexpr int BF_MFMA_WAVES = 16;
+constexpr int BF_MFMA_Q = 64 * BF_MFMA_WAVES;
+__global__ __launch_bounds__(64 * BF_MFMA_WAVES) void k_bf_mfma(const uint32_t* __restrict__ q, int nq,
                                                   const uint32_t* __restrict__ db, long long ndb,
                                                   int chunk, int nqpad, uint2* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) v4i frag[2][8 * 64];   // [buffer][step * 64 + lane]
     int bx, c;
     xcd_block(bx, c);
     const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const bool stager = tid < 256;
     const long long r0 = (long long)c * chunk;
     const int n = (int)min((long long)chunk, ndb - r0);
     const uint32_t* __restrict__ p = db + r0 * 8;
@@ -221,12 +227,12 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
     v4i bq[2][8];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-        const int qi = min(bx * 256 + w * 64 + t * 32 + r, nq - 1);
+        const int qi = min(bx * BF_MFMA_Q + w * 64 + t * 32 + r, nq - 1);
 #pragma unroll
         for (int s = 0; s < 8; ++s) bq[t][s] = expand16<true>(q[(size_t)qi * 8 + s] >> (16 * h), fe);
     }
-    // this thread's share of a block: dword (tid & 7) of row (tid >> 3)
-    const int lr = tid >> 3, ls = tid & 7;
+    // a stager's share of a block: dword (tid & 7) of row (tid >> 3)
+    const int lr = (tid >> 3) & 31, ls = tid & 7;
     auto stage = [&](int buf, uint32_t v) {
         frag[buf][ls * 64 + lr] = expand16<false>(v & 0xFFFFu, fe);
         frag[buf][ls * 64 + 32 + lr] = expand16<false>(v >> 16, fe);
@@ -252,11 +258,11 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
             l1[t] = l2[t] = 0xFFFFu;
         }
     };
-    if (nblk > 0) stage(0, fetch(0));
+    if (nblk > 0 && stager) stage(0, fetch(0));
     __syncthreads();
     for (int blk = 0; blk < nblk; ++blk) {
         const int buf = blk & 1, e0 = blk * 32, j = blk & 3;
-        const uint32_t nxt = blk + 1 < nblk ? fetch(e0 + 32) : 0u;   // in flight meanwhile
+        const uint32_t nxt = (stager && blk + 1 < nblk) ? fetch(e0 + 32) : 0u;   // in flight meanwhile
         v16i acc[2];
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[0][i] = acc[1][i] = (int)(kinit[i] + 32u * (uint32_t)j);
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
                 }
         }
         if (j == 3 || blk + 1 == nblk) fold(e0 - 32 * j);
-        if (blk + 1 < nblk) stage(buf ^ 1, nxt);
+        if (stager && blk + 1 < nblk) stage(buf ^ 1, nxt);
         __syncthreads();
     }
     // the two half-waves hold the same queries' other 16 rows of every block: fold them
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint32_t* __restrict__ q,
         const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[t], 32), o2 = (uint32_t)__shfl_xor((int)b2[t], 32);
         b2[t] = min(max(b1[t], o1), min(b2[t], o2));
         b1[t] = min(b1[t], o1);
-        const int qi = bx * 256 + w * 64 + t * 32 + r;
+        const int qi = bx * BF_MFMA_Q + w * 64 + t * 32 + r;
         if (h == 0 && qi < nq) part[(size_t)c * nqpad + qi] = make_uint2(b1[t], b2[t]);
     }
 }
@@ -360,8 +366,8 @@ __global__ __launch_bounds__(256) void k_bf_merge(const uint2* __restrict__ part
 
 // Rows per chunk: enough chunks that the (query block, chunk) grid gives every CU several
 // workgroups, rounded so the grid fills the 8 XCDs evenly.
-int bf_chunk_rows(long long ndb, int nq, int ncu) {
-    const int qb = (nq + 255) / 256;
+int bf_chunk_rows(long long ndb, int nq, int ncu, int kernel) {
+    const int qb = kernel == ORBX_BF_VALU ? (nq + 255) / 256 : (nq + BF_MFMA_Q - 1) / BF_MFMA_Q;
     long long target = (long long)std::max(ncu, 1) * 8 / qb;          // chunks wanted
     if (target < 8) target = 8;
     long long rows = (ndb + target - 1) / target;
@@ -373,7 +379,7 @@ int bf_chunk_rows(long long ndb, int nq, int ncu) {
 
 size_t bf_partial_bytes(long long ndb, int nq, int chunk) {
     const long long nchunks = (ndb + chunk - 1) / chunk;
-    const int nqpad = ((nq + 255) / 256) * 256;
+    const int nqpad = ((nq + BF_MFMA_Q - 1) / BF_MFMA_Q) * BF_MFMA_Q;
     return (size_t)nchunks * (size_t)nqpad * sizeof(uint2);
 }
 
@@ -383,14 +389,19 @@ const char* bf_kernel_name(int kernel) {
 
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer) {
     if (a.nq <= 0) return hipSuccess;
-    const int nqpad = ((a.nq + 255) / 256) * 256;
+    // the partials' query stride: a multiple of both kernels' queries per workgroup
+    const int nqpad = ((a.nq + BF_MFMA_Q - 1) / BF_MFMA_Q) * BF_MFMA_Q;
     const long long nchunks = a.ndb > 0 ? (a.ndb + a.chunk - 1) / a.chunk : 0;
     if (nchunks > INT32_MAX / 2) return hipErrorInvalidValue;
     hipEvent_t e = timer ? timer->start(st) : nullptr;
-    if (nchunks > 0)
-        hipLaunchKernelGGL(a.kernel == ORBX_BF_VALU ? k_bf_top2 : k_bf_mfma, dim3(nqpad / 256, (unsigned)nchunks),
-                           dim3(256), 0, st, (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db,
-                           a.ndb, a.chunk, nqpad, (uint2*)a.part);
+    if (nchunks > 0 && a.kernel == ORBX_BF_VALU)
+        hipLaunchKernelGGL(k_bf_top2, dim3(nqpad / 256, (unsigned)nchunks), dim3(256), 0, st,
+                           (const uint32_t*)a.q, a.nq, (const uint32_t*)a.db, a.ndb, a.chunk,
+                           nqpad, (uint2*)a.part);
+    else if (nchunks > 0)
+        hipLaunchKernelGGL(k_bf_mfma, dim3(nqpad / BF_MFMA_Q, (unsigned)nchunks),
+                           dim3(BF_MFMA_Q), 0, st, (const uint32_t*)a.q, a.nq,
+                           (const uint32_t*)a.db, a.ndb, a.chunk, nqpad, (uint2*)a.part);
     hipLaunchKernelGGL(k_bf_merge, dim3((a.nq + 31) / 32), dim3(256), 0, st, (const uint2*)a.part,
                        a.nq, nqpad, (int)nchunks, a.chunk, a.idx_base, a.best_idx, a.best_dist,
                        a.second_dist);

@@ -793,7 +793,7 @@ orbx_status bf_run(orbx_matcher* m, const uint8_t* d_q, int nq, const uint8_t* d
     a.db = d_db;
     a.ndb = ndb;
     a.idx_base = idx_base;
-    a.chunk = bf_chunk_rows(ndb, nq, m->ncu);
+    a.chunk = bf_chunk_rows(ndb, nq, m->ncu, m->bf_kernel);
     const size_t need = bf_partial_bytes(ndb, nq, a.chunk);
     // growing frees the scratch an earlier launch (any stream) may still use
     if (need > m->d_bf.n && m->have_bf && !HIPOK(hipEventSynchronize(m->bf_done)))

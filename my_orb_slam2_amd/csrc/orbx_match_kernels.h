@@ -102,7 +102,7 @@ struct BfLaunch {
     int32_t* second_dist;
     int kernel;            // ORBX_BF_MFMA / ORBX_BF_VALU
 };
-int bf_chunk_rows(long long ndb, int nq, int ncu);
+int bf_chunk_rows(long long ndb, int nq, int ncu, int kernel);
 size_t bf_partial_bytes(long long ndb, int nq, int chunk);
 struct KernelTimer;
 hipError_t launch_bf_top2(const BfLaunch& a, hipStream_t st, KernelTimer* timer);
