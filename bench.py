@@ -120,6 +120,9 @@ def parse():
                     help="bf: the distance kernel of the line (k_bf_mfma, or north_star's XOR + "
                          "v_bcnt k_bf_top2); the other one is timed after it as alt_kernel")
     ap.add_argument("--jobs", type=int, default=512, help="triangulation: keyframe-pair jobs")
+    ap.add_argument("--tri-gather", action="store_true",
+                    help="triangulation: the database without its node-order copies (every "
+                         "feature gathered by index, round 5's layout)")
     ap.add_argument("--queries", type=int, default=2000,
                     help="euroc: projected local-map MapPoints per frame")
     ap.add_argument("--insts-csv", default=None,
@@ -1669,6 +1672,11 @@ def main_match(args):
         dF, dE = T(np.array(F12, np.float32)), T(np.array(epi, np.float32))
         s, s2, _ = synth.scale_tables()
         m = ORBmatcher(0.6, False, device=local)      # LocalMapping.cc:276
+        # the resident database in node order (built with it, like the upload; not timed):
+        # the kernel reads each vocabulary node's features as contiguous runs
+        if not args.tri_gather:
+            db.node_order(m, st)
+            torch.cuda.synchronize(dev)
         out = torch.empty(int(n1.sum()), dtype=torch.int32, device=dev)
         cnt = torch.empty(max(nj, 1), dtype=torch.int32, device=dev)
 
@@ -1695,7 +1703,7 @@ def main_match(args):
         kern = "k_triangulate"
         cfg = {"workload": "batched_search_for_triangulation", "jobs": args.jobs,
                "features_per_keyframe": 2000, "vocabulary_nodes": 100, "only_stereo": False,
-               "check_orientation": False,
+               "check_orientation": False, "db_layout": "gather" if args.tri_gather else "node order",
                "parallelism": f"job shards x{world}, RCCL all-gather of counts and match arrays"}
         metric = "SearchForTriangulation keyframe-pair jobs/sec (512 jobs, 2000 features/KF)"
 

@@ -106,6 +106,7 @@ SIGNATURES = {
     "orbx_search_by_projection_batch_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _i, _vp, _vp,
                                                     _vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp]),
     "orbx_matcher_sync": (_i, [_vp, _vp]),
+    "orbx_kf_db_node_order": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "orbx_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp]),
     "orbx_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
     "orbx_hamming_bf_top2": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, _vp, _vp, _vp]),

@@ -398,6 +398,9 @@ __global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
     __shared__ int sBf[4][64];   // octave | stereo << 8 | valid << 9 | idx2 << 10
     const int na0 = db.node_off[k1], na1 = db.node_off[k1 + 1];
     const int nb0 = db.node_off[k2], nb1 = db.node_off[k2 + 1];
+    // features by node-entry position (contiguous per node) when the database carries the
+    // node-order copies, else gathered by feature index
+    const bool nord = db.node_keys != nullptr;
     for (int ga = na0 + w; ga < na1; ga += 4) {
         const uint32_t id = db.node_id[ga];
         int lo = nb0, hi = nb1;   // lower_bound
@@ -413,16 +416,19 @@ __global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
             const int idx1 = ia < a1 ? db.node_feat[ia] : -1;
             bool validA = (unsigned)idx1 < (unsigned)n1;
             const int i1 = validA ? idx1 : 0;
-            validA = validA && !db.flag[f10 + i1];   // :749
-            const bool bStereo1 = (db.u_right ? db.u_right[f10 + i1] : -1.0f) >= 0;
+            const long long pa = nord ? (long long)(ia < a1 ? ia : a0) : (long long)f10 + i1;
+            validA = validA && !(nord ? db.node_flag[pa] : db.flag[pa]);   // :749
+            const float ur1 = nord ? (db.node_u_right ? db.node_u_right[pa] : -1.0f)
+                                   : (db.u_right ? db.u_right[pa] : -1.0f);
+            const bool bStereo1 = ur1 >= 0;
             if (g.only_stereo && !bStereo1) validA = false;
-            const orbx_keypoint kp1 = db.keys[f10 + i1];
+            const orbx_keypoint kp1 = nord ? db.node_keys[pa] : db.keys[pa];
             // CheckDistEpipolarLine's line coefficients depend on kp1 only.
             const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
             const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
             const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
             const float den = a * a + b * b;
-            const Desc d1 = load_desc(db.desc, (long long)f10 + i1);
+            const Desc d1 = load_desc(nord ? db.node_desc : db.desc, pa);
             int bestDist = TH_LOW, bestIdx2 = -1;
             float bestAng = 0.f;
             for (int bc = 0; bc < nB; bc += 64) {
@@ -431,11 +437,14 @@ __global__ __launch_bounds__(256) void k_triangulate(TriLaunch g) {
                     const int idx2 = db.node_feat[b0 + bc + lane];
                     bool ok = (unsigned)idx2 < (unsigned)n2;
                     const int i2 = ok ? idx2 : 0;
-                    ok = ok && !db.flag[f20 + i2];   // :773
-                    const bool st2 = (db.u_right ? db.u_right[f20 + i2] : -1.0f) >= 0;
+                    const long long pb = nord ? (long long)(b0 + bc + lane) : (long long)f20 + i2;
+                    ok = ok && !(nord ? db.node_flag[pb] : db.flag[pb]);   // :773
+                    const float ur2 = nord ? (db.node_u_right ? db.node_u_right[pb] : -1.0f)
+                                           : (db.u_right ? db.u_right[pb] : -1.0f);
+                    const bool st2 = ur2 >= 0;
                     if (g.only_stereo && !st2) ok = false;
-                    const orbx_keypoint kp2 = db.keys[f20 + i2];
-                    const uint4* q = (const uint4*)(db.desc + 32 * ((long long)f20 + i2));
+                    const orbx_keypoint kp2 = nord ? db.node_keys[pb] : db.keys[pb];
+                    const uint4* q = (const uint4*)((nord ? db.node_desc : db.desc) + 32 * pb);
                     sBd[w][lane][0] = q[0];
                     sBd[w][lane][1] = q[1];
                     sBx[w][lane] = kp2.x;
@@ -1111,6 +1120,38 @@ hipError_t launch_bow(const BowLaunch& a, hipStream_t st) {
 }
 
 size_t tri_lds_bytes(int max_feat) { return 4 * ((size_t)max_feat + 32); }
+
+// orbx_kf_db_node_order: one workgroup per keyframe, one thread per node entry of it
+__global__ __launch_bounds__(256) void k_node_order(orbx_kf_db db, int n, orbx_keypoint* keys,
+                                                     uint8_t* desc, float* ur, uint8_t* flag) {
+    const int k = blockIdx.x;
+    const int f0 = db.feat_off[k], nf = db.feat_off[k + 1] - f0;
+    const int p0 = db.node_feat_off[db.node_off[k]], p1 = min(db.node_feat_off[db.node_off[k + 1]], n);
+    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+        const int i = db.node_feat[p];
+        const bool ok = (unsigned)i < (unsigned)nf;
+        const long long f = (long long)f0 + (ok ? i : 0);
+        orbx_keypoint kp = db.keys[f];
+        const uint4* s = (const uint4*)(db.desc + 32 * f);
+        uint4 d0 = s[0], d1 = s[1];
+        if (!ok) {
+            kp = orbx_keypoint{};
+            d0 = d1 = make_uint4(0u, 0u, 0u, 0u);
+        }
+        keys[p] = kp;
+        ((uint4*)(desc + 32 * (long long)p))[0] = d0;
+        ((uint4*)(desc + 32 * (long long)p))[1] = d1;
+        if (ur) ur[p] = ok && db.u_right ? db.u_right[f] : -1.0f;
+        flag[p] = ok ? db.flag[f] : (uint8_t)1;
+    }
+}
+
+hipError_t launch_node_order(const orbx_kf_db& db, int n, orbx_keypoint* keys, uint8_t* desc,
+                             float* ur, uint8_t* flag, hipStream_t st) {
+    if (db.nkf <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_node_order, dim3(db.nkf), dim3(256), 0, st, db, n, keys, desc, ur, flag);
+    return hipGetLastError();
+}
 
 hipError_t launch_triangulate(const TriLaunch& a, hipStream_t st) {
     if (a.njobs <= 0) return hipSuccess;

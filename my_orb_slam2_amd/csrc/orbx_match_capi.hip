@@ -156,7 +156,7 @@ DbOffsets pack_db(Packer& P, const orbx_featureset* const* fs, const uint8_t* co
 }
 
 orbx_kf_db dev_db(const DbOffsets& o, uint8_t* base) {
-    orbx_kf_db d;
+    orbx_kf_db d{};
     d.nkf = o.nkf;
     d.max_feat = o.max_feat;
     d.feat_off = (const int32_t*)(base + o.feat_off);
@@ -641,6 +641,11 @@ orbx_status orbx_search_for_triangulation_batch_device(
         !db->node_feat_off || !db->node_feat)
         return ORBX_ERR_INVALID;
     if ((uintptr_t)db->desc & 15) return ORBX_ERR_INVALID;
+    const bool nord = db->node_keys || db->node_desc || db->node_flag || db->node_u_right;
+    if (nord && (!db->node_keys || !db->node_desc || !db->node_flag ||
+                 (db->u_right != nullptr) != (db->node_u_right != nullptr) ||
+                 ((uintptr_t)db->node_desc & 15)))
+        return ORBX_ERR_INVALID;
     std::lock_guard<std::mutex> lk(m->mu);
     if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
     TriLaunch L{};
@@ -868,6 +873,28 @@ orbx_status orbx_hamming_bf_top2_device(orbx_matcher* m, const uint8_t* d_q, int
     if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
     return bf_run(m, d_q, nq, d_db, ndb, idx_base, d_best_idx, d_best_dist, d_second_dist,
                   (hipStream_t)stream);
+}
+
+orbx_status orbx_kf_db_node_order(orbx_matcher* m, const orbx_kf_db* db, int32_t n,
+                                  orbx_keypoint* d_keys, uint8_t* d_desc, float* d_u_right,
+                                  uint8_t* d_flag, void* stream) {
+    if (!m || !db || n < 0 || db->nkf < 0) return ORBX_ERR_INVALID;
+    if (db->nkf == 0 || n == 0) return ORBX_OK;
+    if (!db->feat_off || !db->keys || !db->desc || !db->flag || !db->node_off ||
+        !db->node_feat_off || !db->node_feat || !d_keys || !d_desc || !d_flag ||
+        (db->u_right && !d_u_right) || ((uintptr_t)d_desc & 15) || ((uintptr_t)db->desc & 15))
+        return ORBX_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!HIPOK(hipSetDevice(m->prm.device))) return ORBX_ERR_DEVICE;
+    orbx_kf_db d = *db;
+    d.node_keys = nullptr;
+    d.node_desc = nullptr;
+    d.node_u_right = nullptr;
+    d.node_flag = nullptr;
+    if (!HIPOK(launch_node_order(d, n, d_keys, d_desc, db->u_right ? d_u_right : nullptr, d_flag,
+                                 (hipStream_t)stream)))
+        return ORBX_ERR_DEVICE;
+    return ORBX_OK;
 }
 
 orbx_status orbx_matcher_sync(orbx_matcher* m, void* stream) {

@@ -27,6 +27,9 @@ struct BowLaunch {
     int* err;
 };
 
+hipError_t launch_node_order(const orbx_kf_db& db, int n, orbx_keypoint* keys, uint8_t* desc,
+                             float* ur, uint8_t* flag, hipStream_t st);
+
 struct TriLaunch {
     orbx_kf_db db;
     int njobs;

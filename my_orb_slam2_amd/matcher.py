@@ -47,7 +47,9 @@ class KfDbC(ctypes.Structure):
                 ("desc", ctypes.c_void_p), ("u_right", ctypes.c_void_p),
                 ("flag", ctypes.c_void_p), ("node_off", ctypes.c_void_p),
                 ("node_id", ctypes.c_void_p), ("node_feat_off", ctypes.c_void_p),
-                ("node_feat", ctypes.c_void_p)]
+                ("node_feat", ctypes.c_void_p), ("node_keys", ctypes.c_void_p),
+                ("node_desc", ctypes.c_void_p), ("node_u_right", ctypes.c_void_p),
+                ("node_flag", ctypes.c_void_p)]
 
 
 def _u8(mask, n):
@@ -437,3 +439,22 @@ class DeviceKfDb:
         p = [x.data_ptr() for x in self.tensors]
         self.c = KfDbC(len(fss), int(n.max()) if len(fss) else 0, *p)
         self.feat_off = feat_off
+        self.n_entries = int(base)
+        self._device = device
+
+    def node_order(self, matcher, stream=0):
+        """Give the database its node-order copies (orbx_kf_db_node_order): the per-node
+        matchers (SearchForTriangulation) then read contiguous runs instead of gathering each
+        feature.  Returns self."""
+        import torch
+        n = max(self.n_entries, 1)
+        self.node_tensors = [torch.empty(n * 28, dtype=torch.uint8, device=self._device),
+                             torch.empty(n * 32, dtype=torch.uint8, device=self._device),
+                             torch.empty(n, dtype=torch.float32, device=self._device),
+                             torch.empty(n, dtype=torch.uint8, device=self._device)]
+        k, d, u, f = (x.data_ptr() for x in self.node_tensors)
+        check("orbx_kf_db_node_order", matcher._lib.orbx_kf_db_node_order(
+            matcher._h, ctypes.byref(self.c), self.n_entries, ctypes.c_void_p(k),
+            ctypes.c_void_p(d), ctypes.c_void_p(u), ctypes.c_void_p(f), ctypes.c_void_p(stream)))
+        self.c.node_keys, self.c.node_desc, self.c.node_u_right, self.c.node_flag = k, d, u, f
+        return self

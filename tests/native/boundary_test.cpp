@@ -91,7 +91,9 @@ static int layout() {
     STRUCT(orbx_kf_db, FIELD(orbx_kf_db, nkf); FIELD(orbx_kf_db, max_feat); FIELD(orbx_kf_db, feat_off);
            FIELD(orbx_kf_db, keys); FIELD(orbx_kf_db, desc); FIELD(orbx_kf_db, u_right);
            FIELD(orbx_kf_db, flag); FIELD(orbx_kf_db, node_off); FIELD(orbx_kf_db, node_id);
-           FIELD(orbx_kf_db, node_feat_off); FIELD(orbx_kf_db, node_feat));
+           FIELD(orbx_kf_db, node_feat_off); FIELD(orbx_kf_db, node_feat);
+           FIELD(orbx_kf_db, node_keys); FIELD(orbx_kf_db, node_desc);
+           FIELD(orbx_kf_db, node_u_right); FIELD(orbx_kf_db, node_flag));
     STRUCT(orbx_proj_query, FIELD(orbx_proj_query, u); FIELD(orbx_proj_query, v);
            FIELD(orbx_proj_query, ur); FIELD(orbx_proj_query, radius);
            FIELD(orbx_proj_query, min_level); FIELD(orbx_proj_query, max_level);

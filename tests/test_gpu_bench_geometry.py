@@ -261,7 +261,10 @@ def test_c4_bf_10m(orbx_lib, gpu):
         np.testing.assert_array_equal(g, w)
 
 
-def test_c5_triangulation_512(oracle_mod, orbx_lib, gpu):
+@pytest.mark.parametrize("node_order", [False, True], ids=["gather", "node_order"])
+def test_c5_triangulation_512(oracle_mod, orbx_lib, gpu, node_order):
+    """All 512 C5 jobs vs the restatement, with the database's features gathered by index and
+    with its node-order copies (orbx_kf_db_node_order: the bench's layout)."""
     import torch
     from oracle import matcher as om
     from my_orb_slam2_amd import ORBmatcher, synth
@@ -274,6 +277,9 @@ def test_c5_triangulation_512(oracle_mod, orbx_lib, gpu):
     job_off = np.concatenate([[0], np.cumsum(n1)]).astype(np.int32)
     s, s2, _ = synth.scale_tables()
     mt = ORBmatcher(0.6, False)
+    if node_order:
+        db.node_order(mt)
+        torch.cuda.synchronize()
     out = torch.full((int(job_off[-1]),), -7, dtype=torch.int32, device=gpu)
     cnt = torch.full((J,), -7, dtype=torch.int32, device=gpu)
     mt.search_for_triangulation_batch_device(db.c, T(np.arange(J, dtype=np.int32) * 2),
