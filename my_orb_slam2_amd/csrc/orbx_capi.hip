@@ -564,7 +564,8 @@ orbx_status build_geometry(orbx_extractor* h, int W, int H) {
         if (lv.w > 4096 + 32 || lv.h > 4096 + 32) return ORBX_ERR_UNSUPPORTED;   // 12-bit packing
         lv.pitch = (int)align_up(lv.w + 4, 64);   // >= 4 bytes of slack for dword staging
         lv.off = off;
-        off += (long long)align_up((size_t)lv.pitch * lv.h, 256);
+        // whole bands of 4 rows: the blurred pyramid (same offsets) is stored in 16x4 tiles
+        off += (long long)align_up((size_t)lv.pitch * align_up((size_t)lv.h, 4), 256);
         lv.scale = h->scale[l];
         lv.inv_scale = h->inv_scale[l];
         lv.nfeat = h->nfeat[l];
@@ -2008,7 +2009,20 @@ static orbx_status copy_level(orbx_extractor* h, const DevBuf& buf, int index, i
     if (!out) return ORBX_OK;
     (void)hipSetDevice(h->device);
     const uint8_t* src = buf.as<uint8_t>() + (size_t)index * h->hg.pyr_bytes + lv.off;
-    (void)blurred;
+    if (blurred) {
+        // 16x4 tiles (blur_off): the level's whole bands to the host, then de-tiled
+        const size_t bytes = (size_t)lv.pitch * align_up((size_t)lv.h, 4);
+        std::vector<uint8_t> tiles(bytes);
+        if (!order_after_last(h, h->stream) ||
+            !HIPOK(hipMemcpyAsync(tiles.data(), src, bytes, hipMemcpyDeviceToHost, h->stream)) ||
+            !HIPOK(hipStreamSynchronize(h->stream)))
+            return ORBX_ERR_DEVICE;
+        for (int y = 0; y < lv.h; ++y)
+            for (int x = 0; x < lv.w; x += 16)
+                std::memcpy(out + (size_t)y * lv.w + x, tiles.data() + blur_off(x, y, lv.pitch, lv.h),
+                            (size_t)std::min(16, lv.w - x));
+        return ORBX_OK;
+    }
     if (!order_after_last(h, h->stream) ||
         !HIPOK(hipMemcpy2DAsync(out, lv.w, src, lv.pitch, lv.w, lv.h, hipMemcpyDeviceToHost, h->stream)) ||
         !HIPOK(hipStreamSynchronize(h->stream)))

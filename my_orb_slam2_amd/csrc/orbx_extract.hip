@@ -21,7 +21,7 @@
 
 namespace orbx {
 
-__constant__ int8_t c_pattern[1024] = {
+__constant__ __attribute__((aligned(4))) int8_t c_pattern[1024] = {
 #include "orbx_pattern.inc"
 };
 
@@ -1106,26 +1106,23 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
 //   3. rBRIEF, two keypoints at a time from the 37x37 blurred patch, same pipelining.
 // The per-lane patch offsets are the same for every keypoint of the level, computed once.
 // ----------------------------------------------------------------------------------------
-#define OD_RAW_DW 9    // dwords per raw-patch row: x-15..x+15 from an aligned base (<= 34 B)
-#define OD_BLR_DW 10   // dwords per blurred-patch row: x-18..x+18 (<= 40 B)
-#define OD_RAW_N (31 * OD_RAW_DW)                  // 279
-static_assert(OD_RAW_DW == 9 && OD_BLR_DW == 10, "k_orient_desc row divisions are hard-coded");
-#define OD_BLR_N (37 * OD_BLR_DW)                  // 370
-#define OD_RL ((OD_RAW_N + 31) / 32)               // 9 dword loads per lane per raw patch
-#define OD_BL ((OD_BLR_N + 31) / 32)               // 12 per blurred patch
 static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
-                       // dword form kept the texture addresser 85 % busy (TA_BUSY_avr)
-#define OD_RAW_W 12    // bytes per lane chunk of a raw-patch row (12 or 16; 3 chunks per row)
-#define OD_BLR_W 16    // ... of a blurred-patch row (8: 5 chunks per row, 16: 3)
-static_assert((OD_RAW_W == 12 || OD_RAW_W == 16) && (OD_BLR_W == 8 || OD_BLR_W == 16), "chunk widths");
-#define OD_RAW_CH 3                                // chunks per raw row (36 / 48 bytes >= 34)
-#define OD_BLR_CH (OD_BLR_W == 8 ? 5 : 3)          // chunks per blurred row (40 / 48 >= 40)
-#define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per patch row
+// Raw patch (row-major pyramid): 12-byte chunks, three per 36-byte LDS row (x-15..x+15 from a
+// dword-aligned base is <= 34 bytes).
+#define OD_RAW_W 12
+#define OD_RAW_CH 3                                // chunks per raw row
+#define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per raw patch row
 #define OD_RL4 ((31 * OD_RAW_CH + 31) / 32)        // loads per lane per raw patch (3)
-#define OD_BLR_NCH (37 * OD_BLR_CH)
-#define OD_BLR_RP (OD_BLR_CH * OD_BLR_W)
-#define OD_BL4 ((OD_BLR_NCH + 31) / 32)            // loads per lane per blurred patch (4, 5 or 6)
-#define OD_PATCH_B (37 * OD_BLR_RP > 31 * OD_RAW_RP ? 37 * OD_BLR_RP : 31 * OD_RAW_RP)
+// Blurred patch (16x4-pixel tiled pyramid, blur_off): x-18..x+18 spans 3 or 4 tile columns,
+// y-18..y+18 10 tile bands; staged as 10 bands x 4 tile columns x 4 rows of 16-byte chunks
+// (one tile row each) into a row-major 40 x 64-byte LDS patch.  A 32-lane load covers two
+// bands' 4 tiles (8 whole 64-byte sectors); with 3 tile columns the 4th column's lanes read
+// the 3rd's addresses again (no extra sectors).  Row-major, the 37 rows touched ~55 sectors.
+#define OD_BLR_W 16
+#define OD_BLR_RP 64                               // LDS bytes per blurred patch row
+#define OD_BLR_ROWS 40
+#define OD_BL4 (OD_BLR_ROWS * 4 / 32)              // loads per lane per blurred patch (5)
+#define OD_PATCH_B (OD_BLR_ROWS * OD_BLR_RP > 31 * OD_RAW_RP ? OD_BLR_ROWS * OD_BLR_RP : 31 * OD_RAW_RP)
 #define OD_PATCH_DW ((OD_PATCH_B + 15) / 16 * 4)   // dwords per half-wave, 16-byte multiple
 
 // Patch staging chunks of W bytes: buffer load and the store of chunk t at byte W t of the
@@ -1135,11 +1132,12 @@ template <> struct od_chunk<8> { typedef uint32_t type __attribute__((ext_vector
 template <> struct od_chunk<12> { typedef uint32_t type __attribute__((ext_vector_type(3))); };
 template <> struct od_chunk<16> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
 template <int W>
-__device__ __forceinline__ typename od_chunk<W>::type od_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+__device__ __forceinline__ typename od_chunk<W>::type od_load(__amdgpu_buffer_rsrc_t r, uint32_t off,
+                                                             uint32_t soff = 0) {
     typedef typename od_chunk<W>::type T;
-    if constexpr (W == 8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-    else if constexpr (W == 12) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0));
-    else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    if constexpr (W == 8) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0));
+    else if constexpr (W == 12) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b96(r, off, soff, 0));
+    else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
 }
 template <int W>
 __device__ __forceinline__ void od_store(uint32_t* P, int t, typename od_chunk<W>::type v) {
@@ -1199,19 +1197,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 
     const uint8_t* pyr_l = pyr + b * g->pyr_bytes + L.off;
     const uint8_t* blr_l = blur + b * g->pyr_bytes + L.off;
-    // per-lane offsets of the 16-byte chunks relative to the patch bases: chunk t = l32 + 32 j
-    // is row t / 3, bytes 16 (t % 3) .. +16 of it; in LDS it lands at 16 t (rows 48 bytes apart)
-    uint32_t sor4[OD_RL4], sob4[OD_BL4];
+    // per-lane offsets of the raw patch's 12-byte chunks relative to the patch base: chunk
+    // t = l32 + 32 j is row t / 3, bytes 12 (t % 3) .. +12 of it; in LDS it lands at 12 t
+    uint32_t sor4[OD_RL4];
 #pragma unroll
     for (int k = 0; k < OD_RL4; ++k) {
         const int t = min(l32 + 32 * k, 31 * OD_RAW_CH - 1), row = t / OD_RAW_CH;
         sor4[k] = __umul24(row, pitch) + OD_RAW_W * (t - OD_RAW_CH * row);
     }
-#pragma unroll
-    for (int k = 0; k < OD_BL4; ++k) {
-        const int t = min(l32 + 32 * k, 37 * OD_BLR_CH - 1), row = t / OD_BLR_CH;
-        sob4[k] = __umul24(row, pitch) + OD_BLR_W * (t - OD_BLR_CH * row);
-    }
+    // blurred patch: chunk c = l32 + 32 j is tile band c / 16, tile column (c / 4) % 4 (the
+    // same for every j), tile row c % 4; relative to the patch's first tile it sits at
+    // band * 4 pitch + column * 64 + row * 16, in LDS at patch row 4 band + row, byte 16 column
+    const int btc = (l32 >> 2) & 3;
+    const uint32_t sob0 = (uint32_t)(__umul24(l32 >> 4, 4 * pitch) + 64 * btc + 16 * (l32 & 3));
+    const int bls0 = ((l32 >> 4) * 16 + (l32 & 3) * 4 + btc);   // LDS chunk index, j = 0
     // keypoint of this half-wave in pair p: k = 2p + half (clamped: a lone last keypoint is
     // computed by both halves, the upper half's results are not used)
     auto kp_word = [&](int p) {
@@ -1229,7 +1228,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const int npair = (nk + 1) >> 1;
     // buffer loads: one 32-bit offset add per load instead of a 64-bit address
     const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc((void*)blr_l, 0, 0x7FFFFFFF, 0x00020000);
-    // a chunk reads up to 14 bytes past the patch row: the row's padding or the next row of
+    // a raw chunk reads up to 14 bytes past the patch row: the row's padding or the next row of
     // the same buffer (patch rows end at least one row before the level's last)
     const __amdgpu_buffer_rsrc_t rraw = __builtin_amdgcn_make_buffer_rsrc((void*)pyr_l, 0, 0x7FFFFFFF, 0x00020000);
     typedef od_chunk<OD_RAW_W>::type raw_t;
@@ -1246,9 +1245,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     auto issue_blr = [&](int p) {
         const uint32_t c = ld_word(p);
         const int x = cand_x(c) + ORBX_MIN_BORDER, y = cand_y(c) + ORBX_MIN_BORDER;
-        const uint32_t vo = __umul24((uint32_t)(y - 18), (uint32_t)pitch) + (uint32_t)((x - 18) & ~3);
+        // first tile: band (y - 18) / 4, column (x - 18) / 16; the 4th column only when
+        // x + 18 reaches it
+        const int tx0 = (x - 18) >> 4;
+        const bool c4 = ((x + 18) >> 4) - tx0 == 3;
+        uint32_t vo = __umul24((uint32_t)(y - 18) & ~3u, (uint32_t)pitch) + 64u * (uint32_t)tx0 + sob0;
+        vo -= (!c4 && btc == 3) ? 64u : 0u;
 #pragma unroll
-        for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo + sob4[j]);
+        for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo, (uint32_t)j * 8u * (uint32_t)pitch);
     };
 
     // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
@@ -1309,52 +1313,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     }
 
     // ---- 3. computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level ----
-    // this lane's 8 rBRIEF pairs (q = 32w + l32), converted once
-    float px1[8], py1[8], px2[8], py2[8];
+    // this lane's 8 rBRIEF pairs (q = 32w + l32), converted once; a pair's two points side by
+    // side, so each product / sum below is one packed-f32 op for both (per element the same
+    // IEEE operations as the scalar form)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 PX[8], PY[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
         const int q = 32 * w + l32;
-        px1[w] = (float)c_pattern[4 * q];
-        py1[w] = (float)c_pattern[4 * q + 1];
-        px2[w] = (float)c_pattern[4 * q + 2];
-        py2[w] = (float)c_pattern[4 * q + 3];
+        const int pw = ((const int*)c_pattern)[q];   // x1, y1, x2, y2 as int8
+        PX[w] = f2{(float)(int8_t)pw, (float)(int8_t)(pw >> 16)};
+        PY[w] = f2{(float)(int8_t)(pw >> 8), (float)(pw >> 24)};
     }
-    const uint8_t* blr = (const uint8_t*)P;   // [37][OD_BLR_RP]
+    const uint8_t* blr = (const uint8_t*)P;   // [OD_BLR_ROWS][OD_BLR_RP]
     for (int p = 0; p < npair; ++p) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
         const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
         const float ca0 = readlane_f(ca_l, k0), ca1 = readlane_f(ca_l, k1);
         const float sb0 = readlane_f(sb_l, k0), sb1 = readlane_f(sb_l, k1);
         const float ca = half ? ca1 : ca0, sb = half ? sb1 : sb0;
+        const int y = cand_y(kp_word(p)) + ORBX_MIN_BORDER;
 #pragma unroll
-        for (int j = 0; j < OD_BL4; ++j) {
-            const int t = l32 + 32 * j;
-            if (t < 37 * OD_BLR_CH) od_store<OD_BLR_W>(P, t, v[j]);
-        }
+        for (int j = 0; j < OD_BL4; ++j) od_store<OD_BLR_W>(P, bls0 + 32 * j, v[j]);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_blr(p + 1);
-        const uint8_t* bc = blr + 18 * OD_BLR_RP + (x - ((x - 18) & ~3));
+        // the keypoint in the staged patch: its first tile starts at ((x - 18) & ~15,
+        // (y - 18) & ~3)
+        const uint8_t* bc = blr + (18 + ((y - 18) & 3)) * OD_BLR_RP + (x - ((x - 18) & ~15));
         // cvRound (:118-120) by the round-to-nearest-even of a float add: for |v| < 2^22,
         // v + 1.5*2^23 holds rint(v) in its low mantissa bits, so its bit pattern is
-        // 0x4B400000 + rint(v).  v_mad_u32_u24 reads the low 24 bits (0x400000 + rint(row)),
-        // so one mad gives the patch offset up to a constant folded into the base.
-        const float MAGIC = 12582912.0f;
+        // 0x4B400000 + rint(v).  Shifted by log2(OD_BLR_RP) in 32 bits that is a constant +
+        // rint(row) * OD_BLR_RP, so one v_lshl_add gives the patch offset up to a constant
+        // folded into the base.
+        static_assert(OD_BLR_RP == 64, "row offset as a shift by 6");
+        const f2 MAGIC = {12582912.0f, 12582912.0f};
         // (the constant is folded into a wrapping u32 offset from the patch start, not into
         // the pointer: a pointer that far outside the LDS object is undefined behaviour, which
         // the compiler may turn into a constant descriptor)
-        const uint32_t bko = (uint32_t)(bc - blr) - (0x400000u * OD_BLR_RP + 0x4B400000u);
-        auto sample = [&](float ra, float rb, float cA, float cB) {
-            const uint32_t ro = __builtin_bit_cast(uint32_t, (ra + rb) + MAGIC);
-            const uint32_t co = __builtin_bit_cast(uint32_t, (cA - cB) + MAGIC);
-            return (int)blr[__umul24(ro, OD_BLR_RP) + co + bko];
-        };
+        const uint32_t bko = (uint32_t)(bc - blr) - ((0x4B400000u << 6) + 0x4B400000u);
+        const f2 CA = {ca, ca}, SB = {sb, sb};
         uint32_t words[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
-            const float r1a = px1[w] * sb, r1b = py1[w] * ca, c1a = px1[w] * ca, c1b = py1[w] * sb;
-            const float r2a = px2[w] * sb, r2b = py2[w] * ca, c2a = px2[w] * ca, c2b = py2[w] * sb;
-            const int t0 = sample(r1a, r1b, c1a, c1b);
-            const int t1 = sample(r2a, r2b, c2a, c2b);
+            // row x*b + y*a and column x*a - y*b of both points (:118-120)
+            const f2 R = (PX[w] * SB + PY[w] * CA) + MAGIC;
+            const f2 C = (PX[w] * CA - PY[w] * SB) + MAGIC;
+            const float rx = R.x, ry = R.y, cx = C.x, cy = C.y;
+            const uint32_t i0 = (__builtin_bit_cast(uint32_t, rx) << 6) + __builtin_bit_cast(uint32_t, cx) + bko;
+            const uint32_t i1 = (__builtin_bit_cast(uint32_t, ry) << 6) + __builtin_bit_cast(uint32_t, cy) + bko;
+            const int t0 = blr[i0];
+            const int t1 = blr[i1];
             const uint64_t m = __ballot(t0 < t1);
             words[w] = half ? (uint32_t)(m >> 32) : (uint32_t)m;
         }

@@ -71,11 +71,15 @@ struct LevelGeom {
 #define FAST_SIDE 3
 #define FAST_SIDE_AT 3
 #define FAST_SIDE_LV 1
-// Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches): row-major, the
-// pyramid's own pitch (16-byte column stripes were measured in round 3: profiles/r04_ab_design_history.txt)
+// Layout of the blurred pyramid (read only by k_orient_desc's rBRIEF patches and the
+// orbx_blur_level readback): 16x4-pixel tiles of 64 bytes (one sector), row-major inside the
+// tile, tiles row-major over the level (pitch / 16 tiles per band of 4 rows: the level keeps
+// the raw pyramid's pitch, a multiple of 64, and its offset; levels are allocated in whole
+// bands).  A 37x37 rBRIEF patch touches 30-40 sectors instead of ~55 row-major.
 __host__ __device__ inline uint32_t blur_off(int x, int y, int pitch, int h) {
     (void)h;
-    return (uint32_t)y * (uint32_t)pitch + (uint32_t)x;
+    return (uint32_t)(y >> 2) * (uint32_t)(4 * pitch) + ((uint32_t)(x >> 4) << 6) +
+           ((uint32_t)(y & 3) << 4) + (uint32_t)(x & 15);
 }
 #define LT_W 128              // output tile width  (32 groups of 4)
 #define LT_H 32               // output tile height

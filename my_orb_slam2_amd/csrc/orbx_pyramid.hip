@@ -639,7 +639,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #define STRIP_PF 2   // mode 3: rows of source loads in flight ahead of the row being computed
 #define STRIP_ST_POLICY 0   // cache-policy bits of the strip walk stores: nt (2) 1.99 ms, sc1 (16) 1.88 ms vs 1.71 ms
 #define STRIP_LEV rlev
-#define STRIP_BLR rblr
 #define STRIP_HREUSE 1   // mode 3: reuse the previous step's HResize of a shared source row
 #define STRIP_HMASK 1   // mode 3, SSE2 waves: horizontal sums masked once per source row
 // One workgroup per strip row (its snw <= 8 waves side by side) with an s_barrier every
@@ -673,7 +672,7 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
                                                  size_t stride, size_t bstride,
                                                  uint8_t* __restrict__ pyr,
                                                  uint8_t* __restrict__ blur, int level, int sth,
-                                                 int sync, int wv, int b) {
+                                                 int sync, int wv, int b, uint32_t* sbl) {
     static_assert(MODE == 0 || MODE == 3 || MODE == 4, "strip kernel: level 0 or INTER_LINEAR levels");
     constexpr bool L0 = MODE != 3;         // level 0: an 8-bit image in, no resize
     const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -847,17 +846,26 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
     // which the hardware drops (no branch, no write)
     const int nrec = pitch * H;
     const __amdgpu_buffer_rsrc_t rlev = __builtin_amdgcn_make_buffer_rsrc(lev0, 0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc(blr0, 0, nrec, 0x00020000);
+    // the blurred level in 16x4 tiles (blur_off), whole bands
+    const __amdgpu_buffer_rsrc_t rblr = __builtin_amdgcn_make_buffer_rsrc(blr0, 0, pitch * ((H + 3) & ~3), 0x00020000);
     // the row's byte offset rides in soffset (scalar), the lane's column in voffset: in range
     // or not whether or not the hardware adds soffset into its range check
     const uint32_t lane_off = out_lane ? (uint32_t)x : 0x80000000u;
     auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, int r, bool ok, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs, ok ? lane_off : 0x80000000u, ok ? r * pitch : 0, STRIP_ST_POLICY);
     };
-    auto store_blr = [&](int r, bool ok, uint32_t v) { store_row(rblr, r, ok, v); };
+    // Blurred rows go through the wave's 4 LDS rows (64 dwords each: the wave's 240 output
+    // pixels, halo lanes into dwords 60-63); after every 4th row the band leaves as whole
+    // tiles: lane t + 15 j (< 60) stores tile t's row j, 16 bytes, so one store instruction
+    // writes the wave's 15 tiles (15 whole sectors; row by row, a half-wave's 120 bytes
+    // touched 2-3 sectors per row).  Wave strips are 240 pixels = 15 tiles wide.
+    const int sbl_dw = (l32 >= 1 && l32 <= SW_OUT) ? SW_OUT * half + l32 - 1 : 60;
+    const int ft = lane % 15, fj = lane / 15;
+    const int ftx = 15 * (wv % L.snw) + ft;
+    const uint32_t fl_off = (lane < 60 && 16 * ftx < W) ? (uint32_t)(64 * ftx + 16 * fj) : 0x80000000u;
     // step i (k = i mod U: the load slot k mod NS, the row-sum register k mod 7)
     // ALL: every step of this block stores both rows (no per-step store predicates)
-    auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c, auto all_c) {
+    auto step = [&](auto k_c, int i, auto rsimd_c, auto bsimd_c, auto all_c) __attribute__((always_inline)) {
         constexpr int k = decltype(k_c)::value;
         constexpr bool ALL = decltype(all_c)::value;
         constexpr bool BSIMD = decltype(bsimd_c)::value;
@@ -912,24 +920,43 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
                     packed |= min(val, 255u) << (8 * j);
                 }
             }
-            store_blr(Y0 + i - 6, ALL || (i >= 6 && i < n), packed);
+            const int slot = (i + 2) & 3;                // row Y0 + i - 6 (Y0 % 4 == 0)
+            sbl[slot * 64 + sbl_dw] = packed;
+            // other lanes read this row: a fence on every path (the compiler would otherwise
+            // treat a row store overwritten 4 steps later as dead)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (slot == 3) {   // wave-uniform
+                // rows Y0 + i - 9 .. Y0 + i - 6 complete (LDS operations of a wave run in order)
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                // read as the u32 it was written as (a vector-typed read would let the
+                // compiler treat the row stores as dead under type-based alias analysis)
+                const uint32_t* fp = (const uint32_t*)__builtin_assume_aligned(sbl + 64 * fj + 4 * ft, 16);
+                const v4u q = {fp[0], fp[1], fp[2], fp[3]};
+                const bool ok = ALL || (i >= 9 && i - 9 < vh);
+                __builtin_amdgcn_raw_buffer_store_b128(q, rblr, ok ? fl_off : 0x80000000u,
+                                                       ok ? (Y0 + i - 9) * pitch : 0, STRIP_ST_POLICY);
+                // wait states before a VALU may overwrite the store's data VGPRs: the 16-byte
+                // store reads them after issue, and the compiler inserts none when soffset is
+                // an SGPR (measured: lanes 12-15 of each 16 stored the next step's v_perm)
+                __asm__ volatile("s_nop 4");
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
         }
     };
     constexpr int U = NS == 7 ? 7 : 7 * NS;   // steps per block: a multiple of NS and of 7
-    auto walk = [&](auto rsimd_c, auto bsimd_c) {
+    auto walk = [&](auto rsimd_c, auto bsimd_c) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             issue(i % NS, i);
             // the same memory-op sequence as a block's last steps (two stores after each
             // issue), so the loop header sees one pending-load state from both edges
             if constexpr (MODE != 4) store_row(STRIP_LEV, 0, false, 0u);
-            store_blr(0, false, 0u);
         }
         // whole blocks of U steps (no per-step exits: steps past n load clamped rows and
-        // store nothing)
+        // store nothing but the last band's rows past the level, into its padding band)
         // sync > 0 only when a workgroup is one strip row (every wave takes the same steps)
         int nblk = 0;
-        auto block = [&](int i0, auto all_c) {
+        auto block = [&](int i0, auto all_c) __attribute__((always_inline)) {
             if (sync > 0) {
                 if (nblk % sync == 0) __builtin_amdgcn_s_barrier();
                 ++nblk;
@@ -943,7 +970,8 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
         static_assert(U >= 6, "the first block holds the halo steps");
         block(0, std::false_type{});
         for (i0 = U; i0 + U <= vh + 3; i0 += U) block(i0, std::true_type{});
-        for (; i0 < n; i0 += U) block(i0, std::false_type{});
+        const int nend = ((vh + 3) & ~3) + 6;   // >= n: the last band's flush step < nend
+        for (; i0 < nend; i0 += U) block(i0, std::false_type{});
     };
     // two forms only (code size): interior waves, and right-edge waves with per-pixel forms
     if ((L0 || wave_rsimd) && wave_bsimd) walk(std::true_type{}, std::true_type{});
@@ -964,8 +992,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MODE != 3 ?
     // wave of this image; readfirstlane makes it (and the strip row, the row counters and the
     // row addresses derived from it) scalar for the compiler, not per-lane VALU work
     const int wv = bx * (int)(blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    __shared__ __attribute__((aligned(16))) uint32_t sbl[8][4 * 64];   // per wave: 4 blurred rows
     level_strip_wave<MODE>(g, ltab, in0, in1, split, stride, bstride, pyr, blur, level, sth, sync,
-                           wv, b);
+                           wv, b, sbl[threadIdx.x >> 6]);
 }
 
 // ---- k_pyr_chain: every level of a small batch in one launch ----

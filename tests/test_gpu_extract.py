@@ -193,6 +193,33 @@ def test_blurred_levels_bitwise(oracle_mod, orbx_lib, gpu, simd):
             assert_bytes_equal(g.blur_level(l), want, f"{name} simd={simd} blur L{l}")
 
 
+def test_batch_blurred_levels_bitwise(oracle_mod, orbx_lib, gpu):
+    """The blurred levels of a bench-like batch (96 images: the strip walk's 64 / 32 / 16 /
+    8-row strips and its tiled band stores, every wave position of a level) vs
+    GaussianBlur(7x7, sigma 2) restated on each image's own level (ORBextractor.cc:1107-1108),
+    read back through the de-tiling orbx_blur_level."""
+    import torch
+    import my_orb_slam2_amd as m
+    B = 96
+    imgs = np.stack([np.roll(synth.frame(40 + i % 12), 31 * (i // 12), axis=0) for i in range(B)])
+    g = m.ORBextractor(2000, 1.2, 8, 20, 7, max_batch=B)
+    g.extract_batch_device(torch.from_numpy(imgs).to(gpu))
+    torch.cuda.synchronize()
+    for i in (0, 1, 37, 95):
+        for l in range(8):
+            lvl = g.pyramid_level(l, i)
+            want = oracle_mod.gaussian7(lvl, True)
+            got = g.blur_level(l, i)
+            bad = np.argwhere(got != want)
+            if bad.size:
+                y, x = bad[0]
+                y0, x0 = y & ~3, x & ~15
+                print("bad", bad.tolist())
+                print("got\n", got[y0 - 4:y0 + 8, x0:x0 + 16])
+                print("want\n", want[y0 - 4:y0 + 8, x0:x0 + 16])
+            assert bad.size == 0, f"image {i} blur L{l} ({lvl.shape}): {len(bad)} pixels differ, first (y, x) {bad[:6].tolist()}"
+
+
 def test_large_batch_equals_single_images(oracle_mod, orbx_lib, gpu):
     """Batch invariance at a bench-like batch: 48 stereo pairs (96 images: every kernel runs
     its XCD-ordered grid) give, image by image, exactly the single-image outputs; two of them
