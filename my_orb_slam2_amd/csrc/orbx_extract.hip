@@ -1168,6 +1168,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     float* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ nkp, int blk_base,
     int nkp_blk) {
     __shared__ __attribute__((aligned(16))) uint32_t patch[4][2][OD_PATCH_DW];
+    // the rBRIEF pattern as floats, pair q = (x1, x2, y1, y2): one 16-byte LDS read per pair
+    // and lane instead of a global load and four conversions (which the register budget
+    // re-issued for every keypoint pair)
+    __shared__ __attribute__((aligned(16))) float spat[256][4];
+    {
+        const int pw = ((const int*)c_pattern)[threadIdx.x];   // x1, y1, x2, y2 as int8
+        *(float4*)spat[threadIdx.x] = float4{(float)(int8_t)pw, (float)(int8_t)(pw >> 16),
+                                             (float)(int8_t)(pw >> 8), (float)(pw >> 24)};
+        __syncthreads();
+    }
     int blk, b;
     xcd_block(blk, b);
     blk += blk_base;   // a launch may cover a range of the blocks (launch_extract's side branch)
@@ -1313,18 +1323,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     }
 
     // ---- 3. computeOrbDescriptor (src/ORBextractor.cc:108-147) on the blurred level ----
-    // this lane's 8 rBRIEF pairs (q = 32w + l32), converted once; a pair's two points side by
-    // side, so each product / sum below is one packed-f32 op for both (per element the same
-    // IEEE operations as the scalar form)
+    // this lane's 8 rBRIEF pairs are q = 32w + l32 (spat); a pair's two points side by side,
+    // so each product / sum below is one packed-f32 op for both (per element the same IEEE
+    // operations as the scalar form)
     typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 PX[8], PY[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        const int q = 32 * w + l32;
-        const int pw = ((const int*)c_pattern)[q];   // x1, y1, x2, y2 as int8
-        PX[w] = f2{(float)(int8_t)pw, (float)(int8_t)(pw >> 16)};
-        PY[w] = f2{(float)(int8_t)(pw >> 8), (float)(pw >> 24)};
-    }
     const uint8_t* blr = (const uint8_t*)P;   // [OD_BLR_ROWS][OD_BLR_RP]
     for (int p = 0; p < npair; ++p) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
@@ -1356,8 +1358,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             // row x*b + y*a and column x*a - y*b of both points (:118-120)
-            const f2 R = (PX[w] * SB + PY[w] * CA) + MAGIC;
-            const f2 C = (PX[w] * CA - PY[w] * SB) + MAGIC;
+            const float4 pq = *(const float4*)spat[32 * w + l32];
+            const f2 PX = {pq.x, pq.y}, PY = {pq.z, pq.w};
+            const f2 R = (PX * SB + PY * CA) + MAGIC;
+            const f2 C = (PX * CA - PY * SB) + MAGIC;
             const float rx = R.x, ry = R.y, cx = C.x, cy = C.y;
             const uint32_t i0 = (__builtin_bit_cast(uint32_t, rx) << 6) + __builtin_bit_cast(uint32_t, cx) + bko;
             const uint32_t i1 = (__builtin_bit_cast(uint32_t, ry) << 6) + __builtin_bit_cast(uint32_t, cy) + bko;
