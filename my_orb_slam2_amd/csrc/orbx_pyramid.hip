@@ -922,9 +922,6 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
             }
             const int slot = (i + 2) & 3;                // row Y0 + i - 6 (Y0 % 4 == 0)
             sbl[slot * 64 + sbl_dw] = packed;
-            // other lanes read this row: a fence on every path (the compiler would otherwise
-            // treat a row store overwritten 4 steps later as dead)
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             if (slot == 3) {   // wave-uniform
                 // rows Y0 + i - 9 .. Y0 + i - 6 complete (LDS operations of a wave run in order)
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
