@@ -1107,11 +1107,12 @@ __global__ __launch_bounds__(NT) void k_octree(const Geometry* __restrict__ g,
 // The per-lane patch offsets are the same for every keypoint of the level, computed once.
 // ----------------------------------------------------------------------------------------
 static_assert(OD_NK >= 2 && OD_NK <= 64, "keypoints per wave");
-// Raw patch (row-major pyramid): 12-byte chunks, three per 36-byte LDS row (x-15..x+15 from a
-// dword-aligned base is <= 34 bytes).
+// Raw patch (row-major pyramid): 12-byte chunks, three per row (x-15..x+15 from a dword-aligned
+// base is <= 34 bytes), into 48-byte LDS rows (16-byte aligned: a lane reads its row's 9
+// dwords as two 16-byte reads and one dword).
 #define OD_RAW_W 12
 #define OD_RAW_CH 3                                // chunks per raw row
-#define OD_RAW_RP (OD_RAW_CH * OD_RAW_W)           // LDS bytes per raw patch row
+#define OD_RAW_RP 48                               // LDS bytes per raw patch row
 #define OD_RL4 ((31 * OD_RAW_CH + 31) / 32)        // loads per lane per raw patch (3)
 // Blurred patch (16x4-pixel tiled pyramid, blur_off): x-18..x+18 spans 3 or 4 tile columns,
 // y-18..y+18 10 tile bands; staged as 10 bands x 4 tile columns x 4 rows of 16-byte chunks
@@ -1265,14 +1266,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
         for (int j = 0; j < OD_BL4; ++j) v[j] = od_load<OD_BLR_W>(rblr, vo, (uint32_t)j * 8u * (uint32_t)pitch);
     };
 
-    // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104): lane l32 < 31 is column
-    //      u = l32 - 15 of its half's keypoint, rows v = 1..15; umax decreases with v, so the
-    //      rows with |u| <= umax[v] are a prefix [1, vend).
-    const int u = l32 - 15, au = u < 0 ? -u : u;
-    const int uw = l32 < 31 ? u : 0;
-    int vend = 1;
-    for (int vv = 1; vv < 16; ++vv) vend += (l32 < 31 && au <= g->umax[vv]) ? 1 : 0;
-    const uint8_t* raw = (const uint8_t*)P;   // [31][OD_RAW_RP]
+    // ---- 1. IC_Angle moments (src/ORBextractor.cc:77-104), exact integers in any order: lane
+    //      l32 < 31 takes patch row v = l32 - 15 of its half's keypoint.  With the row's pixels
+    //      realigned so that byte k of dword d is column u = 4d + k - 15, the circle's columns
+    //      |u| <= umax[|v|] are byte masks per dword, fixed per lane: with the pixels masked,
+    //      the row sum S is Σ_d dot4(pixels, 1) and Σ (u + 15) I is Σ_d dot4(pixels, 4d + k),
+    //      so m_10 = that - 15 S and m_01 = v S.
+    const int vrow = l32 - 15;
+    uint32_t wM[8];   // the circle's bytes of dword d as 0xFF
+    {
+        // bit c of cm: column c = u + 15 inside the circle on this row (lane 31: none)
+        const int um = l32 < 31 ? g->umax[vrow < 0 ? -vrow : vrow] : -1;
+        const uint32_t cm = um < 0 ? 0u : ((2u << (15 + um)) - 1u) & ~((1u << (15 - um)) - 1u);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            // the 4 bits of dword d as bytes 0 / 1 (bit k lands at bit 8k: no carries)
+            const uint32_t m = (((cm >> (4 * d)) & 0xFu) * 0x204081u) & 0x01010101u;
+            wM[d] = (m << 8) - m;
+        }
+    }
+    // raw chunk j of this lane: patch row t / 3, bytes 12 (t % 3) of it, at that place in the
+    // LDS row
+    int lds_raw[OD_RL4];
+#pragma unroll
+    for (int j = 0; j < OD_RL4; ++j) {
+        const int t = l32 + 32 * j, row = t / OD_RAW_CH;
+        lds_raw[j] = row * (OD_RAW_RP / 4) + 3 * (t - OD_RAW_CH * row);
+    }
+    const uint32_t* rrow = P + min(l32, 30) * (OD_RAW_RP / 4);   // this lane's patch row
     int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
     issue_raw(0);
     for (int p = 0; p < npair; ++p) {
@@ -1280,22 +1301,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_RL4; ++j) {
             const int t = l32 + 32 * j;
-            if (t < 31 * OD_RAW_CH) od_store<OD_RAW_W>(P, t, vr[j]);
+            if (t < 31 * OD_RAW_CH) {
+                uint32_t* d = P + lds_raw[j];
+                d[0] = vr[j].x;
+                d[1] = vr[j].y;
+                d[2] = vr[j].z;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (p + 1 < npair) issue_raw(p + 1);   // next pair's patches in flight
         else issue_blr(0);                     // phase 3's first patches in flight
-        const uint8_t* center = raw + 15 * OD_RAW_RP + (x - ((x - 15) & ~3));
-        // fixed trip count (all 30 reads in flight at once); rows v >= vend contribute 0.  The
-        // reads stay inside the staged patch for every lane (lane 31: u = 16, weight 0).
-        int m10 = __mul24(uw, (int)center[u]), m01 = 0;
+        // the row's 9 dwords; the keypoint sits at byte 15 + a of the staged row
+        const uint4 q0 = *(const uint4*)rrow, q1 = *(const uint4*)(rrow + 4);
+        const uint32_t D[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, rrow[8]};
+        const uint32_t a = (uint32_t)(x - 15) & 3u;
+        uint32_t S = 0, A = 0;
 #pragma unroll
-        for (int vv = 1; vv < 16; ++vv) {
-            const int vp = center[u + vv * OD_RAW_RP], vm = center[u - vv * OD_RAW_RP];
-            const bool on = vv < vend;
-            m10 += __mul24(uw, on ? vp + vm : 0);
-            m01 += __mul24(vv, on ? vp - vm : 0);
+        for (int d = 0; d < 8; ++d) {
+            const uint32_t px = __builtin_amdgcn_alignbyte(D[d + 1], D[d], a) & wM[d];
+            S = __builtin_amdgcn_udot4(px, 0x01010101u, S, false);
+            A = __builtin_amdgcn_udot4(px, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
         }
+        const int m10 = (int)A - 15 * (int)S, m01 = __mul24(vrow, (int)S);
         int a10, b10, a01, b01;
         half_sums_dpp(m10, a10, b10);
         half_sums_dpp(m01, a01, b01);
