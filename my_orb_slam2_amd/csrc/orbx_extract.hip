@@ -1182,7 +1182,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     int blk, b;
     xcd_block(blk, b);
     blk += blk_base;   // a launch may cover a range of the blocks (launch_extract's side branch)
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index as a scalar: the keypoint range, trip counts and pair loop below are then
+    // wave-uniform to the compiler (scalar loop control, no exec-mask loop)
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int half = lane >> 5, l32 = lane & 31;
     int level = 0;
     while (level + 1 < g->nlevels && blk >= g->orient_block_begin[level + 1]) ++level;
@@ -1296,7 +1298,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     const uint32_t* rrow = P + min(l32, 30) * (OD_RAW_RP / 4);   // this lane's patch row
     int mk10 = 0, mk01 = 0;                   // lane k: keypoint k's moments
     issue_raw(0);
-    for (int p = 0; p < npair; ++p) {
+    // one pair; the last pair (peeled: its loads are the blurred patch's, so no loop-carried
+    // load registers are copied, and no wait for them, at the loop's back edge)
+    auto moments_pair = [&](int p, auto last_c) __attribute__((always_inline)) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
 #pragma unroll
         for (int j = 0; j < OD_RL4; ++j) {
@@ -1309,7 +1313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (p + 1 < npair) issue_raw(p + 1);   // next pair's patches in flight
+        if constexpr (!decltype(last_c)::value) issue_raw(p + 1);   // next pair's patches in flight
         else issue_blr(0);                     // phase 3's first patches in flight
         // the row's 9 dwords; the keypoint sits at byte 15 + a of the staged row
         const uint4 q0 = *(const uint4*)rrow, q1 = *(const uint4*)(rrow + 4);
@@ -1322,13 +1326,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
             S = __builtin_amdgcn_udot4(px, 0x01010101u, S, false);
             A = __builtin_amdgcn_udot4(px, 0x03020100u + 0x04040404u * (uint32_t)d, A, false);
         }
-        const int m10 = (int)A - 15 * (int)S, m01 = __mul24(vrow, (int)S);
+        const int m10 = __mul24(-15, (int)S) + (int)A, m01 = __mul24(vrow, (int)S);
         int a10, b10, a01, b01;
         half_sums_dpp(m10, a10, b10);
         half_sums_dpp(m01, a01, b01);
         mk10 = lane == 2 * p ? a10 : (lane == 2 * p + 1 ? b10 : mk10);
         mk01 = lane == 2 * p ? a01 : (lane == 2 * p + 1 ? b01 : mk01);
-    }
+    };
+    for (int p = 0; p + 1 < npair; ++p) moments_pair(p, std::false_type{});
+    moments_pair(npair - 1, std::true_type{});
 
     // ---- 2. angle, cos / sin (src/ORBextractor.cc:103, 113) and the keypoint record ----
     const float angle = cv_fast_atan2((float)mk01, (float)mk10);
@@ -1355,7 +1361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
     // operations as the scalar form)
     typedef float f2 __attribute__((ext_vector_type(2)));
     const uint8_t* blr = (const uint8_t*)P;   // [OD_BLR_ROWS][OD_BLR_RP]
-    for (int p = 0; p < npair; ++p) {
+    auto brief_pair = [&](int p, auto last_c) __attribute__((always_inline)) {
         const int x = cand_x(kp_word(p)) + ORBX_MIN_BORDER;
         const int k0 = min(2 * p, nk - 1), k1 = min(2 * p + 1, nk - 1);
         const float ca0 = readlane_f(ca_l, k0), ca1 = readlane_f(ca_l, k1);
@@ -1365,7 +1371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
 #pragma unroll
         for (int j = 0; j < OD_BL4; ++j) od_store<OD_BLR_W>(P, bls0 + 32 * j, v[j]);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (p + 1 < npair) issue_blr(p + 1);
+        if constexpr (!decltype(last_c)::value) issue_blr(p + 1);
         // the keypoint in the staged patch: its first tile starts at ((x - 18) & ~15,
         // (y - 18) & ~3)
         const uint8_t* bc = blr + (18 + ((y - 18) & 3)) * OD_BLR_RP + (x - ((x - 18) & ~15));
@@ -1406,7 +1412,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) v
             for (int w = 1; w < 8; ++w) wv = l32 == w ? words[w] : wv;
             *(uint32_t*)(desc + o * 32 + l32 * 4) = wv;
         }
-    }
+    };
+    for (int p = 0; p + 1 < npair; ++p) brief_pair(p, std::false_type{});
+    brief_pair(npair - 1, std::true_type{});
 }
 
 // ----------------------------------------------------------------------------------------
