@@ -18,6 +18,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -305,9 +306,21 @@ static int fast_cells_per_wave(int ncells, int batch, int ncu) {
     return nc;
 }
 
+// Stream captures (extract1_graph) against waits on an event recorded on another stream: the
+// runtime refuses hipStreamWaitEvent (hipErrorStreamCaptureIsolation) while the stream the event
+// was last recorded on is being captured, even when the record came before the capture began.
+// A handle's done event can sit on another handle's stream (orbx_stereo_match records the right
+// handle's on the left's), whose thread may be capturing a graph just then (a handle re-captures
+// when its pinned blocks grow), so such waits and the captures exclude each other.  Captures
+// happen on a handle's first calls and after a regrowth; the waits take the lock shared.
+static std::shared_mutex g_capture_mu;
+
 // Orders stream st after all work issued so far for this handle (on whatever stream).
 static bool order_after_last(orbx_extractor* h, hipStream_t st) {
-    if (h->have_done && h->done_stream != st) return HIPOK(hipStreamWaitEvent(st, h->done, 0));
+    if (h->have_done && h->done_stream != st) {
+        std::shared_lock<std::shared_mutex> lk(g_capture_mu);
+        return HIPOK(hipStreamWaitEvent(st, h->done, 0));
+    }
     return true;
 }
 
@@ -1593,9 +1606,13 @@ static bool extract1_graph(orbx_extractor* h, const ExtractLaunch& a, hipStream_
         gx = nullptr;
     }
     hipGraph_t g = nullptr;
-    if (!HIPOK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal))) return false;
-    const bool ok = enqueue(a);
-    const bool ended = HIPOK(hipStreamEndCapture(st, &g));
+    bool ok = false, ended = false;
+    {
+        std::unique_lock<std::shared_mutex> lk(g_capture_mu);   // see order_after_last
+        if (!HIPOK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal))) return false;
+        ok = enqueue(a);
+        ended = HIPOK(hipStreamEndCapture(st, &g));
+    }
     hipGraphExec_t ex = nullptr;
     const bool inst = ok && ended && g && HIPOK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     if (g) (void)hipGraphDestroy(g);
