@@ -934,8 +934,11 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
                                                        ok ? (Y0 + i - 9) * pitch : 0, STRIP_ST_POLICY);
                 // wait states before a VALU may overwrite the store's data VGPRs: the 16-byte
                 // store reads them after issue, and the compiler inserts none when soffset is
-                // an SGPR (measured: lanes 12-15 of each 16 stored the next step's v_perm)
-                __asm__ volatile("s_nop 4");
+                // an SGPR (measured: lanes 12-15 of each 16 stored the next step's v_perm); the
+                // operand keeps them allocated to the stored value until then (without it the
+                // scheduler may still put a VALU write of them between the store and the nop:
+                // a second band store measured wrong tiles at random, r6zb)
+                __asm__ volatile("s_nop 4" ::"v"(q));
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
         }
