@@ -708,7 +708,7 @@ def pick_dominant(gprof, steps):
     return max(cand, key=lambda k: cand[k][0] / max(steps, 1)) if cand else None
 
 
-def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv):
+def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv, ta_csv=None):
     """The headline `roofline` object.  `kernel` is the group that takes the most time in the
     run's one-stream pass (`sprof` over `ssteps` steps; the timed profile when the run has no
     such pass); `frac` is that group's algorithmic bytes per launch over its mean launch
@@ -752,7 +752,24 @@ def headline_roofline(prof, steps, sprof, ssteps, ext, B, traffic_csv, insts_csv
                                                              traffic_per_step(traffic_csv, tdom))["frac"]}
     for e in [roof] + list(roof["per_kernel"].values()):
         label_binding_roof(e)
+        # the texture addresser's busy fraction (the unit a patch-staging kernel can saturate
+        # below its VALU and HBM roofs: k_orient_desc), from the one-stream TA pass
+        t = ta_busy_from_csv(DEFAULT_TA if ta_csv is None else ta_csv, e["kernel"])
+        if t is not None:
+            e["ta_busy"] = t
     return roof
+
+
+DEFAULT_TA = os.path.join(HERE, "profiles", "r06_pmc_ta_b512.csv")
+
+
+def ta_busy_from_csv(paths, kernel):
+    """TA_BUSY_avr (cycles per texture addresser, averaged over the TAs) over the launch's
+    GRBM_GUI_ACTIVE / 8 cycles (GRBM counts over the 8 XCDs) from a rocprofv3 TA pass, per
+    dispatch, or None when the pass does not hold the kernel."""
+    busy = counter_from_csv(paths, kernel, "TA_BUSY_avr")
+    grbm = counter_from_csv(paths, kernel, "GRBM_GUI_ACTIVE")
+    return busy / (grbm / 8.0) if busy and grbm else None
 
 
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 1e12   # T SIMD issue cycles/s (1024 SIMDs at 2.4 GHz)

@@ -229,3 +229,14 @@ def test_headline_valu_entry_matches_committed_pmc():
     assert roof["valu"]["wave_instr_per_launch"] == pytest.approx(v)
     assert roof["valu"]["issue_rate"] == pytest.approx(v / (roof["avg_launch_ms"] / 1000.0) / 1e12)
     assert 0 < roof["valu"]["busy_frac"] <= 1.0
+
+
+def test_ta_busy_from_committed_pass():
+    """The per-kernel `ta_busy` of the headline roofline: TA_BUSY_avr over GRBM_GUI_ACTIVE / 8
+    from the committed one-stream TA pass.  k_orient_desc's patch staging keeps the texture
+    addresser the busiest unit of that kernel; a kernel absent from the pass has
+    none."""
+    b = _bench()
+    t = b.ta_busy_from_csv(b.DEFAULT_TA, "k_orient_desc")
+    assert t is not None and 0.5 < t <= 1.0
+    assert b.ta_busy_from_csv(b.DEFAULT_TA, "k_no_such_kernel") is None
