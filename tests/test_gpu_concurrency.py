@@ -242,3 +242,57 @@ def test_cpp_tracker_sessions_agree(orbx_lib, gpu, tmp_path):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["trackers"] == 4 and len(res["latency_ms"]) == 24
     assert len(set(res["digests"])) == 1, res["digests"]
+
+
+def test_capture_beside_cross_stream_wait(orbx_lib, gpu):
+    """The right handle's done event sits on the left handle's stream after
+    ComputeStereoMatches (orbx_stereo_match records it there); the right handle's next
+    extraction waits on it from its own stream while the left handle's thread re-captures its
+    graph (a new image size: new graph key).  The runtime refuses such a wait while the
+    event's stream is capturing, so the library orders the two (orbx_capi.hip
+    order_after_last / extract1_graph); every call must succeed and equal the serial result.
+    (The refusal was seen in test_facade_cpp's three-session facade bench, once in four runs;
+    this sweep of the right thread's start over the left thread's re-capture did not reproduce
+    it on the library without the ordering either, so it guards the scenario, not the timing.)"""
+    import my_orb_slam2_amd as m
+    mb = float(np.float32(MBF) / np.float32(FX))
+    sizes = [(1241, 376), (1226, 370)]
+    pairs = [synth.stereo_pair(760 + i, *sizes[i % 2]) for i in range(4)]
+    gl, gr = m.ORBextractor(2000, 1.2, 8, 20, 7), m.ORBextractor(2000, 1.2, 8, 20, 7)
+    ref = [(gl(L), gr(R)) for L, R in pairs]
+    errors = []
+    import time
+    for it in range(80):
+        L, R = pairs[it % 4]
+        gl(L)
+        gr(R)
+        m.compute_stereo_matches(gl, gr, MBF, mb)
+        nxt = (it + 1) % 4   # the other size: the left handle re-captures
+        out = {}
+
+        def left():
+            try:
+                out["l"] = gl(pairs[nxt][0])
+            except Exception as e:   # noqa: BLE001 -- reported below
+                errors.append(("left", it, repr(e)))
+
+        def right():
+            # the right thread's wait lands at a different point of the left thread's
+            # re-capture each iteration (0-9.75 ms after it starts: its workspace is rebuilt
+            # for the new size first)
+            time.sleep(2.5e-4 * (it % 40))
+            try:
+                out["r"] = gr(pairs[it % 4][1])
+            except Exception as e:   # noqa: BLE001
+                errors.append(("right", it, repr(e)))
+
+        ts = [threading.Thread(target=left), threading.Thread(target=right)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors
+        assert_kps_equal(out["l"][0], ref[nxt][0][0], f"left it {it}")
+        assert_bytes_equal(out["l"][1], ref[nxt][0][1], f"left desc it {it}")
+        assert_kps_equal(out["r"][0], ref[it % 4][1][0], f"right it {it}")
+        assert_bytes_equal(out["r"][1], ref[it % 4][1][1], f"right desc it {it}")
