@@ -268,9 +268,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
         // image): a wave-uniform row base per load plus one lane offset, no per-load VALU
         const uint8_t* src = pyr_b + L.off + (size_t)c.ini_y * L.pitch + (c.ini_x & ~3);
         const uint32_t lane_off = __umul24((uint32_t)lr2, (uint32_t)L.pitch) + 4u * (uint32_t)min(lc2, ndw - 1);
+        // buffer loads: the ROI base in the descriptor and row j's offset in soffset (scalar),
+        // so a load costs no 64-bit address add (10 per cell with flat loads)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
         for (int j = 0; j < FAST_PF2D; ++j)
-            pf[j] = *(const uint32_t*)(src + (size_t)(4 * j) * L.pitch + lane_off);
+            pf[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane_off, (uint32_t)(4 * j) * (uint32_t)L.pitch, 0);
         return true;
     };
     CellDesc cn = cells[c_first];
