@@ -653,6 +653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL_WPE))
 #define STRIP_NS0 7  // mode 0: load slots (1, 2 or 7)
 #define STRIP_PF0 6  // mode 0: rows in flight (<= STRIP_NS0)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 template <typename F, int... K>
 __device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, K...>) {
     (f(std::integral_constant<int, K>{}), ...);
@@ -710,6 +711,9 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
         src = pyr + (size_t)b * g->pyr_bytes + S.off;
         spitch = (size_t)S.pitch;
     }
+    // mode 3: the source level as a buffer (no range clamp: the row tables keep every read
+    // inside the level's rows and their padding, as the flat loads did)
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7FFFFFFF, 0x00020000);
     const uint32_t o0 = t0.x & 3u;         // mode 3: first tap's byte offset in its dword
     const uint32_t boff = t0.x & ~3u;      // mode 3: lane offset of the aligned dwords
     const uint32_t xoff4 = t0.x + 4u;      // mode 0: lane offset of its first byte
@@ -768,13 +772,13 @@ __device__ __forceinline__ void level_strip_wave(const Geometry* __restrict__ g,
             // t0.z + o in every byte (no carries: bytes <= 4 + 3): o replicated by one v_perm
             A[slot][2] = t0.z + __builtin_amdgcn_perm(0u, o, 0u);
         } else {
-            const uint8_t* ra = src + ri.x;
-            const uint8_t* rc = src + ri.y;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                A[slot][k] = *(const uint32_t*)(ra + boff + 4 * k);
-                C[slot][k] = *(const uint32_t*)(rc + boff + 4 * k);
-            }
+            // buffer loads: the source level in the descriptor, the row's byte offset in
+            // soffset (scalar) and the lane's in voffset, so a load costs no 64-bit address add
+            // (two per step with the flat dwordx3 loads the compiler merged the dwords into)
+            const v3u a3 = __builtin_bit_cast(v3u, __builtin_amdgcn_raw_buffer_load_b96(rsrc, boff, ri.x, 0));
+            const v3u c3 = __builtin_bit_cast(v3u, __builtin_amdgcn_raw_buffer_load_b96(rsrc, boff, ri.y, 0));
+            A[slot][0] = a3.x; A[slot][1] = a3.y; A[slot][2] = a3.z;
+            C[slot][0] = c3.x; C[slot][1] = c3.y; C[slot][2] = c3.z;
             RB[slot] = ri.z;
             RAo[slot] = ri.x;
             RCo[slot] = ri.y;
